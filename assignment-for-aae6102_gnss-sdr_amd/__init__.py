@@ -1,0 +1,15 @@
+"""MI355X-native GPS L1 C/A acquisition + conventional tracking (drop-in for
+acquisition.m / trackingCT.m of KangWelly/Assignment-for-AAE6102_GNSS-SDR).
+
+The compute path is the HIP C-ABI library lib/libgnss_mi355x.so (hand-written
+gfx950 kernels + rocFFT); this package is the host-side mirror of the
+reference's MATLAB interface. Import with
+``importlib.import_module("assignment-for-aae6102_gnss-sdr_amd")`` (the
+directory name is not a Python identifier).
+"""
+from . import abi, synth
+from .sdr import (Context, DeviceRecord, StructArray, TrackOutBuffers, acquisition, ca_code,
+                  default_context, initParameters, trackingCT)
+
+__all__ = ["abi", "synth", "Context", "DeviceRecord", "StructArray", "TrackOutBuffers",
+           "acquisition", "ca_code", "default_context", "initParameters", "trackingCT"]

@@ -1,0 +1,142 @@
+"""ctypes mirror of include/gnss_mi355x.h (the C-ABI drop-in boundary).
+
+The struct layouts here must match the header field for field; tests check the
+sizes against a tiny compiled probe. The product library is
+``lib/libgnss_mi355x.so`` next to this file (built in-tree by
+``__graft_entry__.build()``); if it is missing every entry point raises — there
+is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+MAX_SV = 64
+MAX_TAPS = 32
+
+OK, ENODATA, EIO, EARG, EDEVICE, EINDEX = 0, 1, 2, 3, 4, 5
+
+FIELDS = ["P_i", "P_q", "E_i", "E_q", "L_i", "L_q", "PLLdiscri", "DLLdiscri", "codedelay",
+          "remChip", "codeFreq", "carrierFreq", "remPhase", "remSample", "numSample",
+          "delayValue", "absoluteSample", "codedelay2"]
+NFIELDS = len(FIELDS)
+
+
+class GnssFile(C.Structure):
+    _fields_ = [("path", C.c_char_p), ("data", C.c_void_p), ("dev_data", C.c_void_p),
+                ("nbytes", C.c_uint64), ("skip", C.c_int64), ("dataType", C.c_int32),
+                ("dataPrecision", C.c_int32)]
+
+
+class GnssSignal(C.Structure):
+    _fields_ = [("IF", C.c_double), ("Fs", C.c_double), ("codeFreqBasis", C.c_double),
+                ("ms", C.c_double), ("Sample", C.c_int64), ("codelength", C.c_double)]
+
+
+class GnssAcq(C.Structure):
+    _fields_ = [("freqNum", C.c_int32), ("freqMin", C.c_double), ("freqStep", C.c_double),
+                ("datalen", C.c_int32), ("L", C.c_int32), ("n_prn", C.c_int32),
+                ("prn_list", C.POINTER(C.c_int32))]
+
+
+class GnssAcquired(C.Structure):
+    _fields_ = [("n", C.c_int32), ("sv", C.c_int32 * MAX_SV), ("SNR", C.c_double * MAX_SV),
+                ("Doppler", C.c_double * MAX_SV), ("codedelay", C.c_int32 * MAX_SV),
+                ("fineFreq", C.c_double * MAX_SV)]
+
+
+class GnssAcqDiag(C.Structure):
+    _fields_ = [("n", C.c_int32), ("prn", C.c_int32 * MAX_SV), ("SNR", C.c_double * MAX_SV),
+                ("fbin", C.c_int32 * MAX_SV), ("codePhase", C.c_int32 * MAX_SV),
+                ("peak", C.c_double * MAX_SV), ("peak2", C.c_double * MAX_SV)]
+
+
+class GnssTrack(C.Structure):
+    _fields_ = [("CorrelatorSpacing", C.c_double), ("DLLBW", C.c_double), ("DLLDamp", C.c_double),
+                ("DLLGain", C.c_double), ("PLLBW", C.c_double), ("PLLDamp", C.c_double),
+                ("PLLGain", C.c_double), ("msToProcessCT_1ms", C.c_int32),
+                ("msToProcessCT_10ms", C.c_int32), ("n_taps", C.c_int32),
+                ("tap_offsets", C.POINTER(C.c_double)), ("n_chan", C.c_int32),
+                ("chan", C.POINTER(C.c_int32))]
+
+
+class GnssTrackOut(C.Structure):
+    _fields_ = [("max_len", C.c_int64), ("rec", C.POINTER(C.c_double)),
+                ("taps", C.POINTER(C.c_double)), ("len", C.POINTER(C.c_int64)),
+                ("countinx", C.POINTER(C.c_int32)), ("CN0_Eph", C.POINTER(C.c_double)),
+                ("cn0_cap", C.c_int32), ("cn0_rows", C.c_int32)]
+
+
+class GnssTiming(C.Structure):
+    _fields_ = [("acq_ms", C.c_double), ("acq_corr_ms", C.c_double), ("acq_fine_ms", C.c_double),
+                ("track_ms", C.c_double), ("track_kernel_ms", C.c_double),
+                ("track_launches", C.c_int64), ("track_channel_samples", C.c_int64),
+                ("acq_hypothesis_samples", C.c_int64), ("h2d_ms", C.c_double)]
+
+
+class GnssSynthSv(C.Structure):
+    _fields_ = [("prn", C.c_int32), ("doppler_hz", C.c_double), ("code_phase0", C.c_double),
+                ("carr_phase0", C.c_double), ("cn0_dbhz", C.c_double), ("bit_seed", C.c_uint64),
+                ("bit_phase_chips", C.c_double)]
+
+
+class GnssSynth(C.Structure):
+    _fields_ = [("Fs", C.c_double), ("IF", C.c_double), ("noise_sigma", C.c_double),
+                ("seed", C.c_uint64), ("n_sv", C.c_int32), ("sv", GnssSynthSv * MAX_SV)]
+
+
+# exported symbols and their prototypes (checked by tests against the header)
+PROTOTYPES = {
+    "gnss_abi_version": (C.c_int, []),
+    "gnss_strerror": (C.c_char_p, [C.c_int]),
+    "gnss_ctx_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    "gnss_ctx_destroy": (None, [C.c_void_p]),
+    "gnss_last_error": (C.c_char_p, [C.c_void_p]),
+    "gnss_last_timing": (C.c_int, [C.c_void_p, C.POINTER(GnssTiming)]),
+    "gnss_ctx_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
+    "gnss_dev_alloc": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
+    "gnss_dev_free": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "gnss_dev_upload": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
+    "gnss_dev_download": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
+    "gnss_acquisition": (C.c_int, [C.c_void_p, C.POINTER(GnssFile), C.POINTER(GnssSignal),
+                                   C.POINTER(GnssAcq), C.POINTER(GnssAcquired),
+                                   C.POINTER(GnssAcqDiag)]),
+    "gnss_tracking_ct": (C.c_int, [C.c_void_p, C.POINTER(GnssFile), C.POINTER(GnssSignal),
+                                   C.POINTER(GnssTrack), C.POINTER(GnssAcquired),
+                                   C.POINTER(GnssTrackOut)]),
+    "gnss_ca_code": (C.c_int, [C.c_int, C.c_void_p]),
+    "gnss_correlate_step": (C.c_int, [C.c_void_p, C.POINTER(GnssFile), C.POINTER(GnssSignal),
+                                      C.c_int, C.c_int, C.c_double, C.c_double, C.c_double,
+                                      C.c_double, C.c_int64, C.c_int, C.POINTER(C.c_double),
+                                      C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
+    "gnss_synth_if_device": (C.c_int, [C.c_void_p, C.POINTER(GnssSynth), C.c_uint64, C.c_uint64,
+                                       C.c_void_p]),
+}
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libgnss_mi355x.so")
+_lib = None
+
+
+class GnssError(RuntimeError):
+    def __init__(self, status, msg=""):
+        self.status = status
+        super().__init__(f"gnss status {status}: {msg}")
+
+
+def load(path: str | None = None):
+    """Load the HIP C-ABI library (raises if it has not been built)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise ImportError(f"{p} missing: the HIP extension is not built "
+                          "(run `python -c 'import __graft_entry__ as g; g.build()'`)")
+    lib = C.CDLL(p)
+    for name, (res, args) in PROTOTYPES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib

@@ -1,0 +1,337 @@
+// acq.hip — acquisition.m parallel-code-phase search for gfx950 (MI355X).
+//
+// Reference: SDR_MATLAB-main/acqtckpos/acquisition.m. The reference recomputes
+// fft(replica) and the PRN-invariant signal FFT inside its PRN x ms x bin loop
+// (quirk A.2); here the signal spectra are computed once per (ms, bin) and the
+// code spectra once per PRN, both by batched rocFFT. The kernels below are the
+// parts around the transforms: carrier wipe, conj-product, |.|^2 non-coherent
+// accumulation (fixed ms order), and the two-level peak / SNR detector with
+// MATLAB's first-index semantics. Fine frequency uses an fp64 zero-padded FFT.
+#include "gnss_internal.h"
+
+namespace gnss {
+
+namespace {
+
+__device__ __forceinline__ float sin_rev(float x) { return __builtin_amdgcn_sinf(x); }
+__device__ __forceinline__ float cos_rev(float x) { return __builtin_amdgcn_cosf(x); }
+
+// temp1 = rawsignal(ms idx) .* carrier(freqband,:)  (acquisition.m:41-44,56)
+// carrier(b, n) = exp(1i*2*pi*(IF + freqMin + freqStep*(b-1))*n/Fs), n = 1..S
+__global__ void acq_wipe_kernel(const int8_t* __restrict__ iq, int64_t S, int datalen, int nbins,
+                                double IF, double freqMin, double freqStep, double Fs,
+                                float2* __restrict__ out)
+{
+    const int j = blockIdx.y;  // (idx, b) pair: j = idx*nbins + b
+    const int idx = j / nbins, b = j - idx * nbins;
+    const double f = (IF + (freqMin + freqStep * (double)b)) / Fs;  // cycles per sample
+    for (int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; n < S;
+         n += (int64_t)gridDim.x * blockDim.x) {
+        double cyc = f * (double)(n + 1);
+        cyc -= floor(cyc);
+        const float ph = (float)cyc;
+        const float c = cos_rev(ph), s = sin_rev(ph);
+        const char2 x = *reinterpret_cast<const char2*>(iq + 2 * ((int64_t)idx * S + n));
+        const float xr = (float)x.x, xi = (float)x.y;
+        out[(int64_t)j * S + n] = make_float2(xr * c - xi * s, xr * s + xi * c);
+    }
+}
+
+// scode = [CA CA](ceil(n*(codeFreqBasis/Fs))), n = 1..S  (acquisition.m:49-51)
+__global__ void acq_code_kernel(const float* __restrict__ ca, int nprn, int64_t S, double step,
+                                float2* __restrict__ out)
+{
+    const int p = blockIdx.y;
+    for (int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; n < S;
+         n += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t ci = (int64_t)ceil((double)(n + 1) * step);  // 1-based into [CA CA]
+        out[(int64_t)p * S + n] = make_float2(ca[(int64_t)p * 1023 + (ci - 1) % 1023], 0.f);
+    }
+}
+
+// temp3 .* conj(fft(temp1))  (acquisition.m:57-59): y[p][j][k] = C[p][k] * conj(X[j][k])
+__global__ void acq_mul_kernel(const float2* __restrict__ C, const float2* __restrict__ X,
+                               int nsig, int64_t S, float2* __restrict__ y)
+{
+    const int j = blockIdx.y, p = blockIdx.z;
+    const float2* c = C + (int64_t)p * S;
+    const float2* x = X + (int64_t)j * S;
+    float2* o = y + ((int64_t)p * nsig + j) * S;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < S;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const float2 a = c[k], b = x[k];
+        // (ar + i ai)(br - i bi)
+        o[k] = make_float2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
+    }
+}
+
+// correlation(b,:) = sum over ms of abs(ifft(.)).^2 (acquisition.m:53-61), ms order fixed
+__global__ void acq_power_kernel(const float2* __restrict__ y, int nbins, int datalen, int64_t S,
+                                 float scale, float* __restrict__ corr)
+{
+    const int b = blockIdx.y, p = blockIdx.z;
+    const int nsig = nbins * datalen;
+    for (int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; n < S;
+         n += (int64_t)gridDim.x * blockDim.x) {
+        float acc = 0.f;
+        for (int idx = 0; idx < datalen; idx++) {
+            const float2 v = y[((int64_t)p * nsig + (int64_t)idx * nbins + b) * S + n];
+            acc += (v.x * v.x + v.y * v.y) * scale;
+        }
+        corr[((int64_t)p * nbins + b) * S + n] = acc;
+    }
+}
+
+struct PeakPart {
+    float m;
+    int32_t bin, col, pad;
+};
+
+__device__ __forceinline__ void peak_merge(float& m, int& bin, int& col, float m2, int b2, int c2)
+{
+    if (m2 > m) { m = m2; bin = b2; col = c2; }
+    else if (m2 == m) { bin = min(bin, b2); col = min(col, c2); }
+}
+
+// [~,fbin] = max(max(corr')); [peak,codePhase] = max(max(corr)) (acquisition.m:62-63):
+// the global max; fbin = first bin holding it, codePhase = first column holding it.
+__global__ void acq_peak_part_kernel(const float* __restrict__ corr, int nbins, int64_t S,
+                                     int nblk, PeakPart* __restrict__ part)
+{
+    const int p = blockIdx.y, blk = blockIdx.x;
+    const float* c = corr + (int64_t)p * nbins * S;
+    float m = -1.f;
+    int bin = 0x7fffffff, col = 0x7fffffff;
+    for (int b = 0; b < nbins; b++)
+        for (int64_t k = (int64_t)blk * blockDim.x + threadIdx.x; k < S;
+             k += (int64_t)nblk * blockDim.x)
+            peak_merge(m, bin, col, c[(int64_t)b * S + k], b, (int)k);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float m2 = __shfl_xor(m, o, 64);
+        const int b2 = __shfl_xor(bin, o, 64), c2 = __shfl_xor(col, o, 64);
+        peak_merge(m, bin, col, m2, b2, c2);
+    }
+    __shared__ PeakPart s[16];
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) s[wv] = PeakPart{m, bin, col, 0};
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); w++) peak_merge(m, bin, col, s[w].m, s[w].bin, s[w].col);
+        part[(int64_t)p * nblk + blk] = PeakPart{m, bin, col, 0};
+    }
+}
+
+// Merge the partials, then SNR = 10*log10(peak^2 / mean(corr(fbin, off-peak).^2))
+// with the off-peak range [1:cp-cshift, cp+cshift:end] (acquisition.m:66-68).
+__global__ void acq_peak_final_kernel(const float* __restrict__ corr, int nbins, int64_t S,
+                                      int nblk, int cshift, const PeakPart* __restrict__ part,
+                                      AcqPeak* __restrict__ out)
+{
+    const int p = blockIdx.x;
+    __shared__ float s_m;
+    __shared__ int s_bin, s_col;
+    __shared__ double s_sum[16], s_cnt[16], s_mx[16];
+    if (threadIdx.x == 0) {
+        float m = -1.f;
+        int bin = 0x7fffffff, col = 0x7fffffff;
+        for (int k = 0; k < nblk; k++) {
+            const PeakPart q = part[(int64_t)p * nblk + k];
+            peak_merge(m, bin, col, q.m, q.bin, q.col);
+        }
+        s_m = m; s_bin = bin; s_col = col;
+    }
+    __syncthreads();
+    const int fbin = s_bin;
+    const int64_t cp1 = (int64_t)s_col + 1;  // 1-based codePhase
+    const float* row = corr + ((int64_t)p * nbins + fbin) * S;
+    double sum = 0, cnt = 0, mx = 0;
+    for (int64_t k = threadIdx.x + 1; k <= S; k += blockDim.x) {
+        if (k <= cp1 - cshift || k >= cp1 + cshift) {
+            const double v = (double)row[k - 1];
+            sum += v * v;
+            cnt += 1;
+            mx = fmax(mx, v);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        sum += __shfl_xor(sum, o, 64);
+        cnt += __shfl_xor(cnt, o, 64);
+        mx = fmax(mx, __shfl_xor(mx, o, 64));
+    }
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { s_sum[wv] = sum; s_cnt[wv] = cnt; s_mx[wv] = mx; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); w++) {
+            sum += s_sum[w]; cnt += s_cnt[w]; mx = fmax(mx, s_mx[w]);
+        }
+        const double pk = (double)s_m;
+        AcqPeak r;
+        r.peak = s_m;
+        r.fbin = fbin;
+        r.cp = s_col;
+        r.pad = 0;
+        r.snr = 10.0 * log10((pk * pk) / (sum / cnt));
+        r.peak2 = mx;
+        out[p] = r;
+    }
+}
+
+// CarrSignal = longrawsignal(S-cd : S-cd+L*S-1) .* longCaCode, zero-padded to N
+// (acquisition.m:103-108); fp64, code index floor((1/Fs*k)/(1/fc)) as the reference.
+__global__ void fine_build_kernel(const int8_t* __restrict__ iq, int64_t S, int L,
+                                  const int32_t* __restrict__ codedelay,
+                                  const float* __restrict__ ca, double invFs, double invFc,
+                                  double codelength, int64_t N, double2* __restrict__ out)
+{
+    const int s = blockIdx.y;
+    const int64_t Ls = (int64_t)L * S;
+    const int64_t base = S - codedelay[s] - 1;  // 0-based sample of k = 1
+    double2* o = out + (int64_t)s * N;
+    for (int64_t k0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k0 < N;
+         k0 += (int64_t)gridDim.x * blockDim.x) {
+        double2 v = make_double2(0.0, 0.0);
+        if (k0 < Ls) {
+            const double cvi = floor((invFs * (double)(k0 + 1)) / invFc);
+            const float code = ca[(int64_t)s * 1023 + (int64_t)fmod(cvi, codelength)];
+            const char2 x = *reinterpret_cast<const char2*>(iq + 2 * (base + k0));
+            v = make_double2((double)x.x * code, (double)x.y * code);
+        }
+        o[k0] = v;
+    }
+}
+
+struct FinePart {
+    double m;
+    int64_t i;
+};
+
+// first max of abs(fftshift(F)) (acquisition.m:110-116); shifted index i maps to
+// unshifted (i + N/2) mod N.
+__global__ void fine_argmax_part_kernel(const double2* __restrict__ F, int64_t N, int shifted,
+                                        int nblk, FinePart* __restrict__ part)
+{
+    const int s = blockIdx.y, blk = blockIdx.x;
+    const double2* f = F + (int64_t)s * N;
+    double m = -1.0;
+    int64_t bi = INT64_MAX;
+    const int64_t half = N / 2;
+    for (int64_t i = (int64_t)blk * blockDim.x + threadIdx.x; i < N;
+         i += (int64_t)nblk * blockDim.x) {
+        int64_t j = shifted ? i + half : i;
+        if (j >= N) j -= N;
+        const double2 v = f[j];
+        const double a = hypot(v.x, v.y);
+        if (a > m || (a == m && i < bi)) { m = a; bi = i; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double m2 = __shfl_xor(m, o, 64);
+        const int64_t i2 = __shfl_xor(bi, o, 64);
+        if (m2 > m || (m2 == m && i2 < bi)) { m = m2; bi = i2; }
+    }
+    __shared__ FinePart sp[16];
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) sp[wv] = FinePart{m, bi};
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); w++)
+            if (sp[w].m > m || (sp[w].m == m && sp[w].i < bi)) { m = sp[w].m; bi = sp[w].i; }
+        part[(int64_t)s * nblk + blk] = FinePart{m, bi};
+    }
+}
+
+__global__ void fine_argmax_final_kernel(const FinePart* __restrict__ part, int nblk,
+                                         int64_t* __restrict__ kbest)
+{
+    const int s = blockIdx.x;
+    if (threadIdx.x) return;
+    double m = -1.0;
+    int64_t bi = INT64_MAX;
+    for (int k = 0; k < nblk; k++) {
+        const FinePart q = part[(int64_t)s * nblk + k];
+        if (q.m > m || (q.m == m && q.i < bi)) { m = q.m; bi = q.i; }
+    }
+    kbest[s] = bi + 1;  // 1-based FreqPeakIndex
+}
+
+constexpr int kPeakBlocks = 128;
+constexpr int kFineBlocks = 512;
+
+}  // namespace
+
+hipError_t launch_acq_wipe(const int8_t* iq, int64_t S, int datalen, int nbins, double IF,
+                           double freqMin, double freqStep, double Fs, float2* out, hipStream_t s)
+{
+    dim3 grid((unsigned)((S + 255) / 256), (unsigned)(datalen * nbins));
+    hipLaunchKernelGGL(acq_wipe_kernel, grid, dim3(256), 0, s, iq, S, datalen, nbins, IF, freqMin,
+                       freqStep, Fs, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_acq_code(const float* ca, const int32_t* /*prn_slot*/, int nprn, int64_t S,
+                           double codeFreqBasis, double Fs, float2* out, hipStream_t s)
+{
+    dim3 grid((unsigned)((S + 255) / 256), (unsigned)nprn);
+    hipLaunchKernelGGL(acq_code_kernel, grid, dim3(256), 0, s, ca, nprn, S, codeFreqBasis / Fs, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_acq_mul(const float2* code_spec, const float2* sig_spec, int nprn, int nsig,
+                          int64_t S, float2* out, hipStream_t s)
+{
+    dim3 grid((unsigned)((S + 1023) / 1024), (unsigned)nsig, (unsigned)nprn);
+    hipLaunchKernelGGL(acq_mul_kernel, grid, dim3(256), 0, s, code_spec, sig_spec, nsig, S, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_acq_power(const float2* y, int nprn, int nbins, int datalen, int64_t S,
+                            int /*first_ms*/, float* corr, hipStream_t s)
+{
+    dim3 grid((unsigned)((S + 255) / 256), (unsigned)nbins, (unsigned)nprn);
+    const float scale = (float)(1.0 / ((double)S * (double)S));  // ifft's 1/N, squared
+    hipLaunchKernelGGL(acq_power_kernel, grid, dim3(256), 0, s, y, nbins, datalen, S, scale, corr);
+    return hipGetLastError();
+}
+
+hipError_t launch_acq_peak(const float* corr, int nprn, int nbins, int64_t S, int cshift,
+                           AcqPeak* out, void* scratch, hipStream_t s)
+{
+    PeakPart* part = reinterpret_cast<PeakPart*>(scratch);
+    hipLaunchKernelGGL(acq_peak_part_kernel, dim3(kPeakBlocks, nprn), dim3(256), 0, s, corr, nbins, S,
+                       kPeakBlocks, part);
+    hipLaunchKernelGGL(acq_peak_final_kernel, dim3(nprn), dim3(256), 0, s, corr, nbins, S,
+                       kPeakBlocks, cshift, part, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_fine_build(const int8_t* iq, int64_t S, int L, const int32_t* codedelay,
+                             const float* ca, int nsv, double Fs, double codeFreqBasis,
+                             double codelength, int64_t N, double2* out, hipStream_t s)
+{
+    dim3 grid(4096, (unsigned)nsv);
+    hipLaunchKernelGGL(fine_build_kernel, grid, dim3(256), 0, s, iq, S, L, codedelay, ca, 1 / Fs,
+                       1 / codeFreqBasis, codelength, N, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_fine_argmax(const double2* F, int nsv, int64_t N, int shifted, void* scratch,
+                              int64_t* kbest, hipStream_t s)
+{
+    FinePart* part = reinterpret_cast<FinePart*>(scratch);
+    hipLaunchKernelGGL(fine_argmax_part_kernel, dim3(kFineBlocks, nsv), dim3(256), 0, s, F, N,
+                       shifted, kFineBlocks, part);
+    hipLaunchKernelGGL(fine_argmax_final_kernel, dim3(nsv), dim3(64), 0, s, part, kFineBlocks, kbest);
+    return hipGetLastError();
+}
+
+size_t acq_scratch_bytes(int nprn, int nsv)
+{
+    size_t a = sizeof(PeakPart) * (size_t)kPeakBlocks * (size_t)nprn;
+    size_t b = sizeof(FinePart) * (size_t)kFineBlocks * (size_t)nsv;
+    return a > b ? a : b;
+}
+
+}  // namespace gnss

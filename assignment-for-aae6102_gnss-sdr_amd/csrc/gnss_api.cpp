@@ -1,0 +1,903 @@
+// gnss_api.cpp — host side of the C-ABI (include/gnss_mi355x.h).
+//
+// Owns the HIP stream, device buffers, rocFFT plans and step-graphs of one
+// device; stages the IF window into HBM once (or uses a caller-resident record)
+// and drives the kernels in track.hip / acq.hip. Orchestration mirrors the
+// reference's control flow:
+//   acquisition.m  : read block -> PRN search -> threshold -> fine frequency
+//   trackingCT.m   : phase A (1 ms) -> bit-edge search -> phase B (= A continued,
+//                    quirk A.9) -> phase C (10 ms) per channel, channels batched.
+#include <hip/hip_runtime.h>
+#include <rocfft/rocfft.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fcntl.h>
+#include <map>
+#include <string>
+#include <tuple>
+#include <unistd.h>
+#include <vector>
+
+#include "gnss_internal.h"
+
+using namespace gnss;
+
+struct gnss_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    gnss_timing timing{};
+    int profiling = 0;
+    std::map<std::tuple<size_t, size_t, int, int>, rocfft_plan> plans;
+    void* fft_work = nullptr;
+    size_t fft_work_size = 0;
+};
+
+namespace {
+
+int fail(gnss_ctx* ctx, int code, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
+int fail(gnss_ctx* ctx, int code, const char* fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (ctx) ctx->err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return fail(ctx, GNSS_EDEVICE, "%s:%d %s: %s", __FILE__, __LINE__, #expr,          \
+                        hipGetErrorString(e_));                                                \
+    } while (0)
+
+// RAII device buffer
+struct DevBuf {
+    void* p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    hipError_t alloc(size_t bytes)
+    {
+        if (p) { (void)hipFree(p); p = nullptr; }
+        n = bytes;
+        return hipMalloc(&p, bytes ? bytes : 16);
+    }
+    template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+struct Events {
+    hipEvent_t a = nullptr, b = nullptr;
+    Events() { (void)hipEventCreate(&a); (void)hipEventCreate(&b); }
+    ~Events() { (void)hipEventDestroy(a); (void)hipEventDestroy(b); }
+    double ms() const { float f = 0; (void)hipEventElapsedTime(&f, a, b); return f; }
+};
+
+int64_t file_length(const gnss_file* f)
+{
+    if (f->dev_data || f->data) return (int64_t)f->nbytes;
+    if (!f->path) return -1;
+    int fd = open(f->path, O_RDONLY);
+    if (fd < 0) return -1;
+    int64_t s = lseek(fd, 0, SEEK_END);
+    close(fd);
+    return s;
+}
+
+// The IF bytes [lo, hi) resident in HBM; base = file byte at ptr[0] (16-B aligned).
+struct IfWindow {
+    DevBuf own;
+    const int8_t* ptr = nullptr;
+    int64_t base = 0, len = 0;
+};
+
+int stage_window(gnss_ctx* ctx, const gnss_file* f, int64_t lo, int64_t hi, IfWindow& w)
+{
+    const int64_t flen = file_length(f);
+    if (flen < 0) return fail(ctx, GNSS_EIO, "cannot open IF record '%s'", f->path ? f->path : "");
+    lo = std::max<int64_t>(0, lo & ~(int64_t)15);
+    hi = std::min<int64_t>(hi, flen);
+    if (hi <= lo) { hi = lo; }
+    if (f->dev_data) {
+        w.ptr = static_cast<const int8_t*>(f->dev_data);
+        w.base = 0;
+        w.len = flen;
+        if ((reinterpret_cast<uintptr_t>(w.ptr) & 15) != 0)
+            return fail(ctx, GNSS_EARG, "dev_data must be 16-byte aligned");
+        return GNSS_OK;
+    }
+    const int64_t n = hi - lo;
+    HIP_TRY(w.own.alloc((size_t)n + 64));
+    Events ev;
+    HIP_TRY(hipEventRecord(ev.a, ctx->stream));
+    if (f->data) {
+        HIP_TRY(hipMemcpyAsync(w.own.p, f->data + lo, (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+    } else {
+        std::vector<int8_t> tmp((size_t)n);
+        int fd = open(f->path, O_RDONLY);
+        if (fd < 0) return fail(ctx, GNSS_EIO, "cannot open '%s'", f->path);
+        int64_t got = 0;
+        while (got < n) {
+            ssize_t r = pread(fd, tmp.data() + got, (size_t)(n - got), lo + got);
+            if (r <= 0) break;
+            got += r;
+        }
+        close(fd);
+        if (got != n) return fail(ctx, GNSS_EIO, "short read of '%s'", f->path);
+        HIP_TRY(hipMemcpyAsync(w.own.p, tmp.data(), (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+    }
+    HIP_TRY(hipEventRecord(ev.b, ctx->stream));
+    HIP_TRY(hipEventSynchronize(ev.b));
+    ctx->timing.h2d_ms += ev.ms();
+    w.ptr = w.own.as<int8_t>();
+    w.base = lo;
+    w.len = n;
+    return GNSS_OK;
+}
+
+int get_plan(gnss_ctx* ctx, size_t len, size_t batch, int dbl, int inverse, rocfft_plan* out)
+{
+    auto key = std::make_tuple(len, batch, dbl, inverse);
+    auto it = ctx->plans.find(key);
+    if (it != ctx->plans.end()) { *out = it->second; return GNSS_OK; }
+    rocfft_plan plan = nullptr;
+    rocfft_status st = rocfft_plan_create(
+        &plan, rocfft_placement_inplace,
+        inverse ? rocfft_transform_type_complex_inverse : rocfft_transform_type_complex_forward,
+        dbl ? rocfft_precision_double : rocfft_precision_single, 1, &len, batch, nullptr);
+    if (st != rocfft_status_success)
+        return fail(ctx, GNSS_EDEVICE, "rocfft_plan_create(len=%zu, batch=%zu) failed: %d", len, batch, (int)st);
+    size_t ws = 0;
+    rocfft_plan_get_work_buffer_size(plan, &ws);
+    if (ws > ctx->fft_work_size) {
+        if (ctx->fft_work) (void)hipFree(ctx->fft_work);
+        ctx->fft_work = nullptr;
+        HIP_TRY(hipMalloc(&ctx->fft_work, ws));
+        ctx->fft_work_size = ws;
+    }
+    ctx->plans[key] = plan;
+    *out = plan;
+    return GNSS_OK;
+}
+
+int run_fft(gnss_ctx* ctx, void* data, size_t len, size_t batch, int dbl, int inverse)
+{
+    rocfft_plan plan;
+    int st = get_plan(ctx, len, batch, dbl, inverse, &plan);
+    if (st) return st;
+    rocfft_execution_info info = nullptr;
+    rocfft_execution_info_create(&info);
+    rocfft_execution_info_set_stream(info, ctx->stream);
+    if (ctx->fft_work_size) rocfft_execution_info_set_work_buffer(info, ctx->fft_work, ctx->fft_work_size);
+    void* bufs[1] = {data};
+    rocfft_status rs = rocfft_execute(plan, bufs, nullptr, info);
+    rocfft_execution_info_destroy(info);
+    if (rs != rocfft_status_success) return fail(ctx, GNSS_EDEVICE, "rocfft_execute failed: %d", (int)rs);
+    return GNSS_OK;
+}
+
+// The kernels form CarrTime = k/Fs (trackingCT.m:104) as q = k*RN(1/Fs) corrected by
+// one FMA; that equals the IEEE quotient for every k we check here (exhaustive over
+// the step's sample range, cached per Fs). Otherwise they divide.
+int fast_div_exact(double Fs, int64_t kmax)
+{
+    static std::map<std::pair<double, int64_t>, int> cache;
+    auto key = std::make_pair(Fs, kmax);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    const double y = 1.0 / Fs;
+    int ok = 1;
+    for (int64_t k = 0; k <= kmax && ok; k++) {
+        const double a = (double)k;
+        const double q = a * y;
+        const double e = std::fma(-q, Fs, a);
+        if (std::fma(e, y, q) != a / Fs) ok = 0;
+    }
+    cache[key] = ok;
+    return ok;
+}
+
+// generateCAcode.m:16-64 (host copy; the oracle has its own independent one)
+void generate_ca(int prn, float* out)
+{
+    static const int g2s[51] = {5,   6,   7,   8,   17,  18,  139, 140, 141, 251, 252, 254, 255,
+                                256, 257, 258, 469, 470, 471, 472, 473, 474, 509, 512, 513, 514,
+                                515, 516, 859, 860, 861, 862, 145, 175, 52,  21,  237, 235, 886,
+                                657, 634, 762, 355, 1012, 176, 603, 130, 359, 595, 68,  386};
+    int g1[1023], g2[1023];
+    unsigned r1 = 0x3FF, r2 = 0x3FF;  // bit i = stage i+1, all stages start at "-1" (= 1 here)
+    for (int i = 0; i < 1023; i++) {
+        g1[i] = (r1 >> 9) & 1;
+        g2[i] = (r2 >> 9) & 1;
+        unsigned f1 = ((r1 >> 2) ^ (r1 >> 9)) & 1;
+        unsigned f2 = ((r2 >> 1) ^ (r2 >> 2) ^ (r2 >> 5) ^ (r2 >> 7) ^ (r2 >> 8) ^ (r2 >> 9)) & 1;
+        r1 = ((r1 << 1) | f1) & 0x3FF;
+        r2 = ((r2 << 1) | f2) & 0x3FF;
+    }
+    // +-1 product of "-1" states == XOR of bits; CA = -(g1 .* g2) -> +1 when bits differ... in
+    // the reference's -1 -> bit 1 mapping: value(x) = -1 if bit 1 else +1.
+    const int s = g2s[prn - 1];
+    for (int i = 0; i < 1023; i++) {
+        const int src = (i < s) ? (1023 - s + i) : (i - s);
+        const int v1 = g1[i] ? -1 : 1, v2 = g2[src] ? -1 : 1;
+        out[i] = (float)(-(v1 * v2));
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int gnss_abi_version(void) { return GNSS_ABI_VERSION; }
+
+const char* gnss_strerror(int s)
+{
+    switch (s) {
+    case GNSS_OK: return "ok";
+    case GNSS_ENODATA: return "no data (no satellites acquired / not enough raw data)";
+    case GNSS_EIO: return "I/O error or read past end of IF record";
+    case GNSS_EARG: return "invalid or unsupported argument";
+    case GNSS_EDEVICE: return "HIP/rocFFT device error";
+    case GNSS_EINDEX: return "index out of range (MATLAB would raise an error)";
+    default: return "unknown status";
+    }
+}
+
+int gnss_ctx_create(int device, gnss_ctx** out)
+{
+    if (!out) return GNSS_EARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return GNSS_EDEVICE;
+    if (device < 0 || device >= n) return GNSS_EARG;
+    if (hipSetDevice(device) != hipSuccess) return GNSS_EDEVICE;
+    gnss_ctx* ctx = new gnss_ctx();
+    ctx->device = device;
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return GNSS_EDEVICE;
+    }
+    rocfft_setup();
+    *out = ctx;
+    return GNSS_OK;
+}
+
+void gnss_ctx_destroy(gnss_ctx* ctx)
+{
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto& kv : ctx->plans) rocfft_plan_destroy(kv.second);
+    if (ctx->fft_work) (void)hipFree(ctx->fft_work);
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char* gnss_last_error(const gnss_ctx* ctx) { return ctx ? ctx->err.c_str() : "no context"; }
+
+int gnss_last_timing(const gnss_ctx* ctx, gnss_timing* out)
+{
+    if (!ctx || !out) return GNSS_EARG;
+    *out = ctx->timing;
+    return GNSS_OK;
+}
+
+int gnss_ctx_set_profiling(gnss_ctx* ctx, int enable)
+{
+    if (!ctx) return GNSS_EARG;
+    ctx->profiling = enable;
+    return GNSS_OK;
+}
+
+int gnss_dev_alloc(gnss_ctx* ctx, uint64_t nbytes, void** dev_ptr)
+{
+    if (!ctx || !dev_ptr) return GNSS_EARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipMalloc(dev_ptr, nbytes ? nbytes : 16));
+    return GNSS_OK;
+}
+
+int gnss_dev_free(gnss_ctx* ctx, void* p)
+{
+    if (!ctx) return GNSS_EARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipFree(p));
+    return GNSS_OK;
+}
+
+int gnss_dev_upload(gnss_ctx* ctx, void* dst, const void* src, uint64_t n)
+{
+    if (!ctx) return GNSS_EARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return GNSS_OK;
+}
+
+int gnss_dev_download(gnss_ctx* ctx, void* dst, const void* src, uint64_t n)
+{
+    if (!ctx) return GNSS_EARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return GNSS_OK;
+}
+
+// ---------------------------------------------------------------------------
+// acquisition.m
+// ---------------------------------------------------------------------------
+int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg,
+                     const gnss_acq* acq, gnss_acquired* out, gnss_acq_diag* diag)
+{
+    if (!ctx || !file || !sg || !acq || !out) return GNSS_EARG;
+    memset(out, 0, sizeof(*out));
+    if (diag) memset(diag, 0, sizeof(*diag));
+    ctx->timing = gnss_timing{};
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (file->dataPrecision != 1 || file->dataType != 2)
+        return fail(ctx, GNSS_EARG, "only int8 I/Q records (dataPrecision 1, dataType 2) are supported");
+    const int64_t S = sg->Sample;
+    const int nb = acq->freqNum, dl = acq->datalen, L = acq->L;
+    if (S <= 0 || nb <= 0 || dl <= 0 || L <= 0) return fail(ctx, GNSS_EARG, "bad acquisition sizes");
+
+    std::vector<int32_t> prns;
+    if (acq->n_prn > 0 && acq->prn_list) prns.assign(acq->prn_list, acq->prn_list + acq->n_prn);
+    else for (int i = 1; i <= 32; i++) prns.push_back(i);  // acquisition.m:47
+    if (prns.size() > GNSS_MAX_SV) return fail(ctx, GNSS_EARG, "too many PRNs");
+    for (int p : prns) if (p < 1 || p > 51) return fail(ctx, GNSS_EARG, "PRN %d out of range", p);
+    const int np = (int)prns.size();
+
+    const int64_t off = file->skip * S * file->dataPrecision * file->dataType;  // :27
+    const int64_t need = S * file->dataType * std::max<int64_t>(dl, L + 1);
+    const int64_t flen = file_length(file);
+    if (flen < off + S * file->dataType * dl) return fail(ctx, GNSS_EIO, "IF record too short for acquisition");
+    IfWindow w;
+    int st = stage_window(ctx, file, off, off + need, w);
+    if (st) return st;
+    const int8_t* blk = w.ptr + (off - w.base);
+
+    std::vector<float> cah((size_t)np * 1023);
+    for (int i = 0; i < np; i++) generate_ca(prns[i], &cah[(size_t)i * 1023]);
+    DevBuf ca, sig, code, y, corr, peaks, scratch;
+    HIP_TRY(ca.alloc(cah.size() * sizeof(float)));
+    HIP_TRY(hipMemcpyAsync(ca.p, cah.data(), cah.size() * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    const int nsig = dl * nb;
+    HIP_TRY(sig.alloc(sizeof(float2) * (size_t)nsig * S));
+    HIP_TRY(code.alloc(sizeof(float2) * (size_t)np * S));
+    HIP_TRY(corr.alloc(sizeof(float) * (size_t)np * nb * S));
+    HIP_TRY(peaks.alloc(sizeof(AcqPeak) * (size_t)np));
+    HIP_TRY(scratch.alloc(acq_scratch_bytes(np, np)));
+    // PRN chunk so the product/IFFT buffer stays <= ~4 GB
+    const size_t per_prn = sizeof(float2) * (size_t)nsig * S;
+    int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)np, ((size_t)4 << 30) / per_prn));
+    HIP_TRY(y.alloc(per_prn * (size_t)chunk));
+
+    // plans outside the timed region
+    rocfft_plan pl;
+    if ((st = get_plan(ctx, S, nsig, 0, 0, &pl))) return st;
+    if ((st = get_plan(ctx, S, np, 0, 0, &pl))) return st;
+    for (int p0 = 0; p0 < np; p0 += chunk) {
+        const int pc = std::min(chunk, np - p0);
+        if ((st = get_plan(ctx, S, (size_t)pc * nsig, 0, 1, &pl))) return st;
+    }
+
+    Events e_all, e_corr;  // e_corr.b marks the end of the PRN search
+    HIP_TRY(hipEventRecord(e_all.a, ctx->stream));
+    HIP_TRY(launch_acq_wipe(blk, S, dl, nb, sg->IF, acq->freqMin, acq->freqStep, sg->Fs, sig.as<float2>(), ctx->stream));
+    if ((st = run_fft(ctx, sig.p, S, nsig, 0, 0))) return st;
+    HIP_TRY(launch_acq_code(ca.as<float>(), nullptr, np, S, sg->codeFreqBasis, sg->Fs, code.as<float2>(), ctx->stream));
+    if ((st = run_fft(ctx, code.p, S, np, 0, 0))) return st;
+    for (int p0 = 0; p0 < np; p0 += chunk) {
+        const int pc = std::min(chunk, np - p0);
+        HIP_TRY(launch_acq_mul(code.as<float2>() + (size_t)p0 * S, sig.as<float2>(), pc, nsig, S, y.as<float2>(), ctx->stream));
+        if ((st = run_fft(ctx, y.p, S, (size_t)pc * nsig, 0, 1))) return st;
+        HIP_TRY(launch_acq_power(y.as<float2>(), pc, nb, dl, S, 0, corr.as<float>() + (size_t)p0 * nb * S, ctx->stream));
+    }
+    const int cshift = (int)std::ceil(sg->Fs / sg->codeFreqBasis);  // :66
+    HIP_TRY(launch_acq_peak(corr.as<float>(), np, nb, S, cshift, peaks.as<AcqPeak>(), scratch.p, ctx->stream));
+    HIP_TRY(hipEventRecord(e_corr.b, ctx->stream));
+    std::vector<AcqPeak> ph((size_t)np);
+    HIP_TRY(hipMemcpyAsync(ph.data(), peaks.p, sizeof(AcqPeak) * (size_t)np, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    ctx->timing.acq_hypothesis_samples = (int64_t)np * nb * dl * S;
+
+    std::vector<int> acq_idx;
+    for (int i = 0; i < np; i++) {
+        if (diag) {
+            int k = diag->n++;
+            diag->prn[k] = prns[i];
+            diag->SNR[k] = ph[i].snr;
+            diag->fbin[k] = ph[i].fbin + 1;
+            diag->codePhase[k] = ph[i].cp + 1;
+            diag->peak[k] = ph[i].peak;
+            diag->peak2[k] = ph[i].peak2;
+        }
+        if (ph[i].snr >= 12) {  // :70-74
+            int k = out->n++;
+            out->sv[k] = prns[i];
+            out->SNR[k] = ph[i].snr;
+            out->Doppler[k] = acq->freqMin + acq->freqStep * (double)ph[i].fbin;
+            out->codedelay[k] = ph[i].cp;  // codePhase - 1
+            acq_idx.push_back(i);
+        }
+    }
+    if (out->n == 0) {
+        HIP_TRY(hipEventRecord(e_all.b, ctx->stream));
+        HIP_TRY(hipEventSynchronize(e_all.b));
+        ctx->timing.acq_ms = e_all.ms();
+        ctx->timing.acq_corr_ms = ctx->timing.acq_ms;
+        return fail(ctx, GNSS_ENODATA, "No satellites acquired");  // :84-85
+    }
+
+    // fine frequency (:89-126)
+    if (flen < off + S * file->dataType * (L + 1)) return fail(ctx, GNSS_EIO, "IF record too short for fine search");
+    const int na = out->n;
+    const int64_t N = (int64_t)L * S * dl;  // :108
+    if (N % 2) return fail(ctx, GNSS_EINDEX, "odd fftlength: MATLAB indexes past the end (:116)");
+    std::vector<float> caf((size_t)na * 1023);
+    std::vector<int32_t> cdh((size_t)na);
+    for (int k = 0; k < na; k++) {
+        generate_ca(out->sv[k], &caf[(size_t)k * 1023]);
+        cdh[k] = out->codedelay[k];
+    }
+    DevBuf fca, fcd, fx, kb;
+    HIP_TRY(fca.alloc(caf.size() * sizeof(float)));
+    HIP_TRY(fcd.alloc(cdh.size() * sizeof(int32_t)));
+    HIP_TRY(fx.alloc(sizeof(double2) * (size_t)na * N));
+    HIP_TRY(kb.alloc(sizeof(int64_t) * (size_t)na));
+    HIP_TRY(hipMemcpyAsync(fca.p, caf.data(), caf.size() * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(fcd.p, cdh.data(), cdh.size() * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+    if ((st = get_plan(ctx, N, na, 1, 0, &pl))) return st;
+    Events e_fine;
+    HIP_TRY(hipEventRecord(e_fine.a, ctx->stream));
+    HIP_TRY(launch_fine_build(blk, S, L, fcd.as<int32_t>(), fca.as<float>(), na, sg->Fs, sg->codeFreqBasis,
+                              sg->codelength, N, fx.as<double2>(), ctx->stream));
+    if ((st = run_fft(ctx, fx.p, N, na, 1, 0))) return st;
+    DevBuf fscr;
+    HIP_TRY(fscr.alloc(acq_scratch_bytes(1, na)));
+    HIP_TRY(launch_fine_argmax(fx.as<double2>(), na, N, file->dataType == 2, fscr.p, kb.as<int64_t>(), ctx->stream));
+    HIP_TRY(hipEventRecord(e_fine.b, ctx->stream));
+    HIP_TRY(hipEventRecord(e_all.b, ctx->stream));
+    std::vector<int64_t> kh((size_t)na);
+    HIP_TRY(hipMemcpyAsync(kh.data(), kb.p, sizeof(int64_t) * (size_t)na, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    for (int k = 0; k < na; k++) {
+        const double K = (double)kh[k];
+        out->fineFreq[k] = (file->dataType == 2) ? (-K * (sg->Fs / (double)N) + sg->Fs / 2) : (K * (sg->Fs / (double)N));
+    }
+    {
+        float f = 0;
+        (void)hipEventElapsedTime(&f, e_all.a, e_corr.b);
+        ctx->timing.acq_corr_ms = f;
+    }
+    ctx->timing.acq_fine_ms = e_fine.ms();
+    ctx->timing.acq_ms = e_all.ms();
+    return GNSS_OK;
+}
+
+// ---------------------------------------------------------------------------
+// trackingCT.m
+// ---------------------------------------------------------------------------
+namespace {
+
+struct StepGraph {
+    hipGraphExec_t exec = nullptr;
+    hipGraph_t graph = nullptr;
+    int count = 0;
+    ~StepGraph()
+    {
+        if (exec) (void)hipGraphExecDestroy(exec);
+        if (graph) (void)hipGraphDestroy(graph);
+    }
+};
+
+}  // namespace
+
+int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg, const gnss_track* tr,
+                     const gnss_acquired* acq, gnss_track_out* out)
+{
+    if (!ctx || !file || !sg || !tr || !acq || !out) return GNSS_EARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    ctx->timing = gnss_timing{};
+    if (file->dataPrecision != 1 || file->dataType != 2)
+        return fail(ctx, GNSS_EARG, "only int8 I/Q records (dataPrecision 1, dataType 2) are supported");
+    const int nsv = acq->n;
+    if (nsv <= 0 || nsv > GNSS_MAX_SV) return fail(ctx, GNSS_EARG, "no channels");
+    const int64_t S = sg->Sample;
+    const int N1 = tr->msToProcessCT_1ms;
+    const int n10 = tr->msToProcessCT_10ms / 10;
+    if (N1 < 24) return fail(ctx, GNSS_EARG, "msToProcessCT_1ms must be >= 24 (bit-edge search window)");
+    if (out->max_len < (int64_t)N1 + 19 + (int64_t)tr->msToProcessCT_10ms) return fail(ctx, GNSS_EARG, "max_len too small");
+    if (8.0 * (sg->codeFreqBasis * 1.01) / sg->Fs >= 1.0)
+        return fail(ctx, GNSS_EARG, "Fs too low for the 8-sample lane groups (need Fs > 8.2 MHz)");
+
+    // taps (trackingCT.m:24; ACF taps per trackingCT_multiCorr-GIVEN.m:25)
+    TrkParams P{};
+    double taps3[3] = {-tr->CorrelatorSpacing, 0, tr->CorrelatorSpacing};
+    const double* taps = taps3;
+    int ntaps = 3;
+    if (tr->n_taps > 0) {
+        if (!tr->tap_offsets) return fail(ctx, GNSS_EARG, "tap_offsets missing");
+        ntaps = tr->n_taps;
+        taps = tr->tap_offsets;
+    }
+    if (ntaps != 3 && ntaps != 11) return fail(ctx, GNSS_EARG, "n_taps must be 3 or 11");
+    P.iE = P.iP = P.iL = -1;
+    for (int s = 0; s < ntaps; s++) {
+        P.taps[s] = taps[s];
+        if (taps[s] == -tr->CorrelatorSpacing && P.iE < 0) P.iE = s;
+        if (taps[s] == 0 && P.iP < 0) P.iP = s;
+        if (taps[s] == tr->CorrelatorSpacing && P.iL < 0) P.iL = s;
+    }
+    if (P.iE < 0 || P.iP < 0 || P.iL < 0) return fail(ctx, GNSS_EARG, "taps must contain -spacing, 0, +spacing");
+    P.ntaps = ntaps;
+
+    std::vector<int32_t> chans;
+    if (tr->chan && tr->n_chan > 0) chans.assign(tr->chan, tr->chan + tr->n_chan);
+    else for (int i = 0; i < nsv; i++) chans.push_back(i);
+    for (int c : chans) if (c < 0 || c >= nsv) return fail(ctx, GNSS_EARG, "channel index out of range");
+    const int nch = (int)chans.size();
+
+    // loop coefficients, calcLoopCoef.m:41-45 (trackingCT.m:26-27)
+    auto coef = [](double LBW, double zeta, double k, double& t1, double& t2) {
+        double Wn = LBW * 8 * zeta / (4 * (zeta * zeta) + 1);
+        t1 = k / (Wn * Wn);
+        t2 = 2.0 * zeta / Wn;
+    };
+    coef(tr->DLLBW, tr->DLLDamp, tr->DLLGain, P.tau1code, P.tau2code);
+    coef(tr->PLLBW, tr->PLLDamp, tr->PLLGain, P.tau1carr, P.tau2carr);
+    P.Fs = sg->Fs;
+    P.codeFreqBasis = sg->codeFreqBasis;
+    P.ms = sg->ms;
+    P.codelength = sg->codelength;
+    P.S = (double)S;
+    P.dataBytesPerSample = (double)(file->dataPrecision * file->dataType);
+    P.inv_Fs = 1.0 / sg->Fs;
+    P.exact_div = fast_div_exact(sg->Fs, (int64_t)(S * 10 * 1.02) + 64) ? 0 : 1;
+    P.nsv = nsv;
+    P.nch = nch;
+    P.rec_cap = N1 + 19 + n10;
+    P.cn0_cap = std::max(N1 + 19, n10) / 20 + 1;
+
+    // IF window resident in HBM: from the earliest channel start to the latest
+    // possible phase-C end (countinx <= 18, numSample within 1%)
+    const int64_t bps = file->dataPrecision * file->dataType;
+    int64_t lo = INT64_MAX, hi = 0;
+    for (int c : chans) {
+        const int64_t cd = acq->codedelay[c];
+        lo = std::min(lo, (S - cd + 1 + file->skip * S) * bps);
+        const int64_t c0 = (S - cd + 1 + (file->skip + N1 + 18) * S) * bps;
+        const int64_t a1 = (S - cd + 1 + file->skip * S) * bps + (int64_t)((N1 + 18) * S * 1.01 + 64) * bps;
+        hi = std::max(hi, std::max(c0 + (int64_t)(n10 * 10 * S * 1.01 + 4096) * bps, a1));
+    }
+    P.file_len = file_length(file);
+    if (P.file_len < 0) return fail(ctx, GNSS_EIO, "cannot open IF record");
+    IfWindow w;
+    int st = stage_window(ctx, file, lo, hi, w);
+    if (st) return st;
+    P.buf_base = w.base;
+    P.buf_len = w.len;
+
+    // geometry: 8 samples per lane, U lane-groups per thread
+    const int U1 = 1, U10 = 4;
+    auto bpc_for = [&](int pdi, int U) {
+        const double groups = (S * pdi * 1.01 + 64) / 8.0 + 2;
+        return (int)std::ceil(groups / (kTrkThreads * (double)U));
+    };
+    const int bpc1 = bpc_for(1, U1), bpc10 = bpc_for(10, U10);
+    if (bpc1 > kMaxBpc || bpc10 > kMaxBpc) return fail(ctx, GNSS_EARG, "Sample too large for the step geometry");
+
+    // device state
+    std::vector<TrkChan> ch0((size_t)nch);
+    std::vector<float> cah((size_t)nch * 1023);
+    for (int i = 0; i < nch; i++) {
+        const int c = chans[i];
+        TrkChan& t = ch0[i];
+        memset(&t, 0, sizeof(t));
+        t.codeFreq = sg->codeFreqBasis;  // trackingCT.m:56-58
+        t.carrierFreqBasis = acq->fineFreq[c];
+        t.carrierFreq = acq->fineFreq[c];
+        t.codedelay0 = acq->codedelay[c];
+        t.pos = (S - acq->codedelay[c] + 1 + file->skip * S) * bps;  // :63
+        t.snrIndex = 1;
+        t.sv1 = c + 1;
+        t.prn = acq->sv[c];
+        t.n1_target = N1;
+        if (acq->sv[c] < 1 || acq->sv[c] > 51) return fail(ctx, GNSS_EARG, "bad PRN");
+        generate_ca(acq->sv[c], &cah[(size_t)i * 1023]);
+    }
+    DevBuf d_chan, d_snap, d_ca, d_part, d_arrive, d_rec, d_taps, d_cn1, d_cn10, d_dv, d_pi;
+    HIP_TRY(d_chan.alloc(sizeof(TrkChan) * nch));
+    HIP_TRY(d_snap.alloc(sizeof(TrkChan) * nch));
+    HIP_TRY(d_ca.alloc(sizeof(float) * cah.size()));
+    HIP_TRY(d_part.alloc(sizeof(double) * (size_t)nch * kMaxBpc * 2 * ntaps));
+    HIP_TRY(d_arrive.alloc(sizeof(unsigned) * nch));
+    HIP_TRY(d_rec.alloc(sizeof(double) * (size_t)nch * P.rec_cap * GNSS_NFIELDS));
+    if (out->taps) HIP_TRY(d_taps.alloc(sizeof(double) * (size_t)nch * P.rec_cap * 2 * ntaps));
+    HIP_TRY(d_cn1.alloc(sizeof(double) * (size_t)nch * P.cn0_cap));
+    HIP_TRY(d_cn10.alloc(sizeof(double) * (size_t)nch * P.cn0_cap));
+    HIP_TRY(d_dv.alloc(sizeof(int64_t) * (size_t)nch * (P.rec_cap + 1)));
+    HIP_TRY(d_pi.alloc(sizeof(double) * (size_t)nch * N1));
+    HIP_TRY(hipMemcpyAsync(d_chan.p, ch0.data(), sizeof(TrkChan) * nch, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(d_ca.p, cah.data(), sizeof(float) * cah.size(), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemsetAsync(d_arrive.p, 0, sizeof(unsigned) * nch, ctx->stream));
+    HIP_TRY(hipMemsetAsync(d_cn1.p, 0, d_cn1.n, ctx->stream));
+    HIP_TRY(hipMemsetAsync(d_cn10.p, 0, d_cn10.n, ctx->stream));
+    HIP_TRY(hipMemsetAsync(d_dv.p, 0, d_dv.n, ctx->stream));
+    HIP_TRY(hipMemsetAsync(d_rec.p, 0, d_rec.n, ctx->stream));
+
+    TrkBuffers B{};
+    B.iq = w.ptr;
+    B.chan = d_chan.as<TrkChan>();
+    B.snap = d_snap.as<TrkChan>();
+    B.ca = d_ca.as<float>();
+    B.partial = d_part.as<double>();
+    B.arrive = d_arrive.as<unsigned>();
+    B.rec = d_rec.as<double>();
+    B.taps_rec = out->taps ? d_taps.as<double>() : nullptr;
+    B.cn0_1 = d_cn1.as<double>();
+    B.cn0_10 = d_cn10.as<double>();
+    B.dvpre = d_dv.as<int64_t>();
+    B.p_i_1ms = d_pi.as<double>();
+    B.n1 = N1;
+
+    // step launches: K-launch graphs replayed (no host launch cost per step); in
+    // profiling mode every launch is bracketed by events instead.
+    std::vector<hipEvent_t> pev;
+    int64_t launches = 0;
+    auto run_steps = [&](int pdi, int phaseC, int count) -> int {
+        const int bpc = pdi == 1 ? bpc1 : bpc10, U = pdi == 1 ? U1 : U10;
+        if (count <= 0) return GNSS_OK;
+        launches += count;
+        ctx->timing.track_channel_samples += (int64_t)count * nch * (int64_t)S * pdi;
+        if (ctx->profiling) {
+            for (int i = 0; i < count; i++) {
+                hipEvent_t a, b;
+                HIP_TRY(hipEventCreate(&a));
+                HIP_TRY(hipEventCreate(&b));
+                HIP_TRY(hipEventRecord(a, ctx->stream));
+                HIP_TRY(launch_track_step(P, B, pdi, phaseC, bpc, U, ctx->stream));
+                HIP_TRY(hipEventRecord(b, ctx->stream));
+                pev.push_back(a);
+                pev.push_back(b);
+            }
+            return GNSS_OK;
+        }
+        const int K = 50;
+        if (count >= K) {
+            StepGraph g;
+            HIP_TRY(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+            for (int i = 0; i < K; i++) {
+                hipError_t e = launch_track_step(P, B, pdi, phaseC, bpc, U, ctx->stream);
+                if (e != hipSuccess) {
+                    hipGraph_t junk;
+                    (void)hipStreamEndCapture(ctx->stream, &junk);
+                    if (junk) (void)hipGraphDestroy(junk);
+                    return fail(ctx, GNSS_EDEVICE, "capture: %s", hipGetErrorString(e));
+                }
+            }
+            HIP_TRY(hipStreamEndCapture(ctx->stream, &g.graph));
+            HIP_TRY(hipGraphInstantiate(&g.exec, g.graph, nullptr, nullptr, 0));
+            for (int r = 0; r < count / K; r++) HIP_TRY(hipGraphLaunch(g.exec, ctx->stream));
+            for (int i = 0; i < count % K; i++) HIP_TRY(launch_track_step(P, B, pdi, phaseC, bpc, U, ctx->stream));
+            HIP_TRY(hipStreamSynchronize(ctx->stream));  // graph objects die with this scope
+        } else {
+            for (int i = 0; i < count; i++) HIP_TRY(launch_track_step(P, B, pdi, phaseC, bpc, U, ctx->stream));
+        }
+        return GNSS_OK;
+    };
+
+    Events e_all;
+    HIP_TRY(hipEventRecord(e_all.a, ctx->stream));
+    // phase A: steps 1..N1-1, snapshot (for countinx = -1), step N1, bit-edge search
+    if ((st = run_steps(1, 0, N1 - 1))) return st;
+    HIP_TRY(launch_track_snapshot(P, B, ctx->stream));
+    if ((st = run_steps(1, 0, 1))) return st;
+    HIP_TRY(launch_track_bitedge(P, B, ctx->stream));
+    std::vector<TrkChan> chh((size_t)nch);
+    HIP_TRY(hipMemcpyAsync(chh.data(), d_chan.p, sizeof(TrkChan) * nch, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    int cxmax = 0;
+    for (auto& t : chh) cxmax = std::max(cxmax, t.countinx);
+    // phase B continues phase A up to 1000 + countinx (inactive channels skip)
+    if ((st = run_steps(1, 0, cxmax))) return st;
+    HIP_TRY(launch_track_phase_c_init(P, B, file->skip, ctx->stream));
+    // phase C
+    if ((st = run_steps(10, 1, n10))) return st;
+    HIP_TRY(hipEventRecord(e_all.b, ctx->stream));
+    HIP_TRY(hipEventSynchronize(e_all.b));
+    ctx->timing.track_ms = e_all.ms();
+    ctx->timing.track_launches = launches;
+    double ksum = 0;
+    for (size_t i = 0; i + 1 < pev.size(); i += 2) {
+        float f = 0;
+        (void)hipEventElapsedTime(&f, pev[i], pev[i + 1]);
+        ksum += f;
+    }
+    for (auto e : pev) (void)hipEventDestroy(e);
+    ctx->timing.track_kernel_ms = ksum;
+
+    // results
+    HIP_TRY(hipMemcpyAsync(chh.data(), d_chan.p, sizeof(TrkChan) * nch, hipMemcpyDeviceToHost, ctx->stream));
+    std::vector<double> rec((size_t)nch * P.rec_cap * GNSS_NFIELDS);
+    std::vector<double> tp(out->taps ? (size_t)nch * P.rec_cap * 2 * ntaps : 0);
+    std::vector<double> cn1((size_t)nch * P.cn0_cap), cn10((size_t)nch * P.cn0_cap);
+    HIP_TRY(hipMemcpyAsync(rec.data(), d_rec.p, rec.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    if (out->taps) HIP_TRY(hipMemcpyAsync(tp.data(), d_taps.p, tp.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(cn1.data(), d_cn1.p, cn1.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(cn10.data(), d_cn10.p, cn10.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+
+    int status = GNSS_OK;
+    for (auto& t : chh)
+        if (t.status && (status == GNSS_OK || t.status == GNSS_ENODATA)) status = t.status;
+    if (status != GNSS_OK) {
+        if (out->len) for (int c : chans) out->len[c] = 0;
+        return fail(ctx, status, status == GNSS_ENODATA ? "Not enough raw data" : "tracking failed: %s",
+                    gnss_strerror(status));
+    }
+
+    const int64_t ML = out->max_len;
+    int rows = N1 / 20;
+    for (int i = 0; i < nch; i++) {
+        const int c = chans[i];
+        const TrkChan& t = chh[i];
+        const int cx = t.countinx;
+        const int64_t n1 = N1 + cx;
+        const int64_t len = n1 + 10LL * n10;
+        if (out->len) out->len[c] = len;
+        if (out->countinx) out->countinx[c] = cx;
+        rows = std::max(rows, (int)(n1 / 20));
+        if (out->rec) {
+            for (int f = 0; f < GNSS_NFIELDS; f++) {
+                double* dst = out->rec + ((int64_t)c * GNSS_NFIELDS + f) * ML;
+                const double* src = rec.data() + (size_t)i * P.rec_cap * GNSS_NFIELDS + f;
+                for (int64_t k = 0; k < n1; k++) dst[k] = src[k * GNSS_NFIELDS];
+                for (int64_t s = 0; s < n10; s++) {
+                    const double v = src[(n1 + s) * GNSS_NFIELDS];
+                    for (int r = 0; r < 10; r++) dst[n1 + 10 * s + r] = v;
+                }
+            }
+        }
+        if (out->taps) {
+            for (int tq = 0; tq < 2 * ntaps; tq++) {
+                const int s = tq / 2, iq = tq % 2;
+                double* dst = out->taps + (((int64_t)c * 2 + iq) * ntaps + s) * ML;
+                const double* src = tp.data() + (size_t)i * P.rec_cap * 2 * ntaps + tq;
+                for (int64_t k = 0; k < n1; k++) dst[k] = src[k * 2 * ntaps];
+                for (int64_t q = 0; q < n10; q++) {
+                    const double v = src[(n1 + q) * 2 * ntaps];
+                    for (int r = 0; r < 10; r++) dst[n1 + 10 * q + r] = v;
+                }
+            }
+        }
+    }
+    rows = std::max(rows, n10 / 20);
+    out->cn0_rows = rows;
+    if (out->CN0_Eph) {
+        for (int i = 0; i < nch; i++) {
+            const int c = chans[i];
+            const int cx = chh[i].countinx;
+            const int r1 = std::max(N1, N1 + cx) / 20, r10 = n10 / 20;
+            for (int r = 0; r < out->cn0_cap; r++) {
+                double v = 0;
+                if (r < r10) v = cn10[(size_t)i * P.cn0_cap + r];
+                else if (r < r1) v = cn1[(size_t)i * P.cn0_cap + r];
+                out->CN0_Eph[(int64_t)r * nsv + c] = v;
+            }
+        }
+    }
+    return GNSS_OK;
+}
+
+int gnss_correlate_step(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg, int prn, int pdi,
+                        double remChip, double codeFreq, double carrierFreq, double remPhase,
+                        int64_t pos_bytes, int n_taps, const double* taps, double* sums_out,
+                        int64_t* numSample_out)
+{
+    if (!ctx || !file || !sg || !taps || !sums_out || (n_taps != 3 && n_taps != 11) || prn < 1 || prn > 51)
+        return GNSS_EARG;
+    if (pdi != 1 && pdi != 10) return GNSS_EARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    const int64_t S = sg->Sample;
+    TrkParams P{};
+    P.Fs = sg->Fs;
+    P.codeFreqBasis = sg->codeFreqBasis;
+    P.ms = sg->ms;
+    P.codelength = sg->codelength;
+    P.S = (double)S;
+    P.dataBytesPerSample = 2;
+    P.inv_Fs = 1.0 / sg->Fs;
+    P.exact_div = fast_div_exact(sg->Fs, (int64_t)(S * 10 * 1.02) + 64) ? 0 : 1;
+    P.ntaps = n_taps;
+    P.iE = 0; P.iP = n_taps / 2; P.iL = n_taps - 1;
+    for (int s = 0; s < n_taps; s++) P.taps[s] = taps[s];
+    P.nsv = P.nch = 1;
+    P.rec_cap = 1;
+    P.cn0_cap = 1;
+    P.file_len = file_length(file);
+    IfWindow w;
+    int st = stage_window(ctx, file, pos_bytes, pos_bytes + (int64_t)(2.1 * S * pdi) + 64, w);
+    if (st) return st;
+    P.buf_base = w.base;
+    P.buf_len = w.len;
+    TrkChan c{};
+    c.remChip = remChip;
+    c.codeFreq = codeFreq;
+    c.carrierFreq = carrierFreq;
+    c.remPhase = remPhase;
+    c.pos = pos_bytes;
+    c.n1_target = 1 << 30;
+    c.sv1 = 1;
+    c.prn = prn;
+    float ca[1023];
+    generate_ca(prn, ca);
+    const int U = pdi == 1 ? 1 : 4;
+    const int bpc = (int)std::ceil(((S * pdi * 1.01 + 64) / 8.0 + 2) / (kTrkThreads * (double)U));
+    DevBuf d_chan, d_ca, d_part, d_arrive, d_sums;
+    HIP_TRY(d_chan.alloc(sizeof(TrkChan)));
+    HIP_TRY(d_ca.alloc(sizeof(ca)));
+    HIP_TRY(d_part.alloc(sizeof(double) * kMaxBpc * 2 * n_taps));
+    HIP_TRY(d_arrive.alloc(sizeof(unsigned)));
+    HIP_TRY(d_sums.alloc(sizeof(double) * 2 * n_taps));
+    HIP_TRY(hipMemcpyAsync(d_chan.p, &c, sizeof c, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(d_ca.p, ca, sizeof ca, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemsetAsync(d_arrive.p, 0, sizeof(unsigned), ctx->stream));
+    TrkBuffers B{};
+    B.iq = w.ptr;
+    B.chan = d_chan.as<TrkChan>();
+    B.ca = d_ca.as<float>();
+    B.partial = d_part.as<double>();
+    B.arrive = d_arrive.as<unsigned>();
+    B.dbg_sums = d_sums.as<double>();
+    HIP_TRY(launch_track_step(P, B, pdi, 0, bpc, U, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(sums_out, d_sums.p, sizeof(double) * 2 * n_taps, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(&c, d_chan.p, sizeof c, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (c.status) return fail(ctx, c.status, "correlate step failed");
+    if (numSample_out) {
+        const double cps = codeFreq / sg->Fs;
+        *numSample_out = (int64_t)round((sg->codelength * pdi - remChip) / cps);
+    }
+    return GNSS_OK;
+}
+
+int gnss_ca_code(int prn, int8_t* out1023)
+{
+    if (prn < 1 || prn > 51 || !out1023) return GNSS_EARG;
+    float f[1023];
+    generate_ca(prn, f);
+    for (int i = 0; i < 1023; i++) out1023[i] = (int8_t)f[i];
+    return GNSS_OK;
+}
+
+int gnss_synth_if_device(gnss_ctx* ctx, const gnss_synth* cfg, uint64_t sample0, uint64_t nsamples,
+                         void* dev_dst)
+{
+    if (!ctx || !cfg || !dev_dst || cfg->n_sv < 0 || cfg->n_sv > GNSS_MAX_SV) return GNSS_EARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    std::vector<float> cah((size_t)std::max(1, cfg->n_sv) * 1023);
+    for (int i = 0; i < cfg->n_sv; i++) {
+        if (cfg->sv[i].prn < 1 || cfg->sv[i].prn > 51) return GNSS_EARG;
+        generate_ca(cfg->sv[i].prn, &cah[(size_t)i * 1023]);
+    }
+    DevBuf ca;
+    HIP_TRY(ca.alloc(cah.size() * sizeof(float)));
+    HIP_TRY(hipMemcpyAsync(ca.p, cah.data(), cah.size() * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(launch_synth_if(*cfg, ca.as<float>(), sample0, nsamples, static_cast<int8_t*>(dev_dst), ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return GNSS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,169 @@
+// gnss_internal.h — internal declarations shared by the C-ABI host code
+// (gnss_api.cpp) and the gfx950 kernels (track.hip, acq.hip, synth.hip).
+// Not part of the public boundary (that is include/gnss_mi355x.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/gnss_mi355x.h"
+
+#define GNSS_HD __host__ __device__ __forceinline__
+
+namespace gnss {
+
+// MATLAB colon a:d:b, MathWorks' published colonop construction (both ends toward
+// the midpoint). Evaluated in fp64 with contraction disabled (-ffp-contract=off for
+// every translation unit) so host, device and the CPU oracle agree bit for bit.
+struct Colon {
+    double a, d, c;
+    int64_t n;  // intervals; elements = n + 1
+};
+
+GNSS_HD Colon colon_make(double a, double d, double b)
+{
+    Colon r{a, d, b, -1};
+    if (!(a - a == 0) || !(d - d == 0) || !(b - b == 0)) return r;  // non-finite
+    if (d == 0 || (a < b && d < 0) || (b < a && d > 0)) return r;
+    double tol = 2.0 * 2.220446049250313e-16 * fmax(fabs(a), fabs(b));
+    double sig = d > 0 ? 1.0 : -1.0;
+    double n;
+    if (a == floor(a) && d == 1) {
+        n = floor(b) - a;
+    } else if (a == floor(a) && d == floor(d)) {
+        double q = floor(a / d);
+        double rr = a - q * d;
+        n = floor((b - rr) / d) - q;
+    } else {
+        n = round((b - a) / d);
+        if (sig * (a + n * d - b) > tol) n = n - 1;
+    }
+    double c = a + n * d;
+    if (sig * (c - b) > -tol) c = b;
+    r.c = c;
+    r.n = (int64_t)n;
+    return r;
+}
+
+GNSS_HD double colon_elem(const Colon& r, int64_t k)
+{
+    if (2 * k == r.n) return (r.a + r.c) / 2;
+    if (k <= r.n / 2) return r.a + (double)k * r.d;
+    return r.c - (double)(r.n - k) * r.d;
+}
+
+// Code = [CA(1023) repmat(CA,1,pdi) CA(1)]; Code(ceil(t)+1) = CA0[(ceil(t)+1022) % 1023]
+GNSS_HD int ca_index(int64_t chip)
+{
+    int64_t r = (chip + 1022) % 1023;
+    return (int)(r < 0 ? r + 1023 : r);
+}
+
+constexpr double kTwoPi = 2.0 * 3.14159265358979323846;  // MATLAB 2*pi
+constexpr double kTwoPiLo = 2.4492935982947064e-16;      // 2*pi - kTwoPi
+
+// ----------------------------------------------------------------------------
+// Tracking state (one per channel, fp64), lives in HBM across step launches.
+// ----------------------------------------------------------------------------
+struct TrkChan {
+    // NCO / loop-filter state (trackingCT.m:42-58)
+    double remChip, remPhase, remSample;
+    double carrier_outputLast, PLLdiscriLast, code_outputLast, DLLdiscriLast;
+    double codeFreq, carrierFreqBasis, carrierFreq;
+    double Zk[20];
+    int64_t numSample;  // numSample of the last executed step
+    int64_t pos;        // file position indicator (bytes) for the next read
+    int64_t Index;      // MATLAB Index after the last step
+    int64_t nstep;      // steps executed in the current phase (IndexSmall)
+    int64_t slot;       // compact record slot of the next step
+    int64_t n1_target;  // last 1-ms step to run (1000 + countinx)
+    int64_t codedelay0;
+    int32_t index_int, snrIndex;
+    int32_t sv1;        // global 1-based svindex (quirk A.11)
+    int32_t prn;
+    int32_t status;     // GNSS_* of this channel
+    int32_t countinx;
+};
+
+// Per-step compact record: the 18 TckResultCT fields of one step.
+struct TrkParams {
+    double Fs, codeFreqBasis, ms, codelength;
+    double S;                 // signal.Sample
+    double tau1code, tau2code, tau1carr, tau2carr;
+    double dataBytesPerSample;  // dataPrecision*dataType
+    double inv_Fs;            // RN(1/Fs)
+    int32_t exact_div;        // 1: FMA-corrected k/Fs not verified for this Fs -> divide
+    int64_t buf_base;         // file byte held at dev_if[0]
+    int64_t buf_len;          // bytes resident
+    int64_t file_len;         // bytes in the record (EOF)
+    int32_t ntaps, iE, iP, iL;
+    int32_t nsv;              // GLOBAL number of channels (quirk A.11)
+    int32_t nch;              // channels in this launch set
+    int32_t rec_cap;          // compact record slots per channel
+    int32_t cn0_cap;          // rows per channel per phase array
+    double taps[GNSS_MAX_TAPS];
+};
+
+struct TrkBuffers {
+    const int8_t* iq;         // IF bytes (dev)
+    TrkChan* chan;            // [nch]
+    TrkChan* snap;            // [nch] state after step msToProcessCT_1ms - 1
+    const float* ca;          // [nch][1023] +-1
+    double* partial;          // [nch][max_blocks][2*ntaps]
+    unsigned int* arrive;     // [nch] arrival counters
+    double* rec;              // [nch][rec_cap][GNSS_NFIELDS]
+    double* taps_rec;         // [nch][rec_cap][2*ntaps] or null
+    double* cn0_1;            // [nch][cn0_cap]
+    double* cn0_10;           // [nch][cn0_cap]
+    int64_t* dvpre;           // [nch][rec_cap+1] delayValue prefix sums of the current phase
+    double* p_i_1ms;          // [nch][n1] phase-A P_i for the bit-edge search
+    double* dbg_sums;         // if set: last arriver stores the raw sums [nch][2*ntaps], no finalize
+    int32_t n1;               // msToProcessCT_1ms
+};
+
+// Launch wrappers (track.hip)
+hipError_t launch_track_step(const TrkParams& p, const TrkBuffers& b, int pdi, int phaseC,
+                             int blocks_per_chan, int groups_per_thread, hipStream_t s);
+hipError_t launch_track_snapshot(const TrkParams& p, const TrkBuffers& b, hipStream_t s);
+hipError_t launch_track_bitedge(const TrkParams& p, const TrkBuffers& b, hipStream_t s);
+hipError_t launch_track_phase_c_init(const TrkParams& p, const TrkBuffers& b, int64_t skip,
+                                     hipStream_t s);
+
+constexpr int kTrkThreads = 256;
+constexpr int kMaxBpc = 128;  // blocks per channel per step (LDS partial buffer)
+
+// ----------------------------------------------------------------------------
+// Acquisition (acq.hip)
+// ----------------------------------------------------------------------------
+struct AcqPeak {           // per-PRN detector result
+    float peak;
+    int32_t fbin;          // 0-based
+    int32_t cp;            // 0-based code phase
+    int32_t pad;
+    double snr;
+    double peak2;
+};
+
+hipError_t launch_acq_wipe(const int8_t* iq, int64_t S, int datalen, int nbins, double IF,
+                           double freqMin, double freqStep, double Fs, float2* out, hipStream_t s);
+hipError_t launch_acq_code(const float* ca, const int32_t* prn_slot, int nprn, int64_t S,
+                           double codeFreqBasis, double Fs, float2* out, hipStream_t s);
+hipError_t launch_acq_mul(const float2* code_spec, const float2* sig_spec, int nprn, int nsig,
+                          int64_t S, float2* out, hipStream_t s);
+hipError_t launch_acq_power(const float2* y, int nprn, int nbins, int datalen, int64_t S,
+                            int first_ms, float* corr, hipStream_t s);
+hipError_t launch_acq_peak(const float* corr, int nprn, int nbins, int64_t S, int cshift,
+                           AcqPeak* out, void* scratch, hipStream_t s);
+hipError_t launch_fine_build(const int8_t* iq, int64_t S, int L, const int32_t* codedelay,
+                             const float* ca, int nsv, double Fs, double codeFreqBasis,
+                             double codelength, int64_t N, double2* out, hipStream_t s);
+hipError_t launch_fine_argmax(const double2* F, int nsv, int64_t N, int shifted, void* scratch,
+                              int64_t* kbest, hipStream_t s);
+
+size_t acq_scratch_bytes(int nprn, int nsv);
+
+// Synthetic IF (synth.hip)
+hipError_t launch_synth_if(const gnss_synth& cfg, const float* ca, uint64_t sample0,
+                           uint64_t nsamples, int8_t* dst, hipStream_t s);
+
+}  // namespace gnss

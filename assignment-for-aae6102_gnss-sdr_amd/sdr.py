@@ -1,0 +1,370 @@
+"""Host-side mirror of the reference's MATLAB interface for the hot path.
+
+    [file, signal, acq, track, solu, cmn] = initParameters()      initParameters.m:1-85
+    Acquired = acquisition(file, signal, acq)                      acquisition.m:1
+    [TckResultCT, CN0_Eph, countinx] = trackingCT(file, signal, track, Acquired)
+                                                                   trackingCT.m:1
+
+Same names, same struct fields, same argument meaning; the work happens in the
+HIP C-ABI library (abi.py). Differences forced by the language are documented
+per function. Errors follow the reference: nothing acquired -> empty Acquired
+(acquisition.m:84-85); "Not enough raw data" -> TckResultCT = [] (returned as
+an empty StructArray); conditions where MATLAB raises -> GnssError.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from types import SimpleNamespace
+
+import numpy as np
+
+from . import abi
+
+
+# ---------------------------------------------------------------------------
+# initParameters.m
+# ---------------------------------------------------------------------------
+def initParameters(fileRoute: str | None = None):
+    """Struct surface of initParameters.m:1-85 (Opensky defaults).
+
+    file.fid (a MATLAB file handle opened at :35) has no Python equivalent: the
+    core does positioned reads of file.fileRoute, or uses file.data (an int8
+    numpy record held in host memory) / file.dev (a DeviceRecord in HBM).
+    """
+    file = SimpleNamespace(fileName="Opensky", fileRoute=fileRoute, skip=5000, skiptimeVT=100,
+                           dataType=2, dataPrecision=1, data=None, dev=None)
+    signal = SimpleNamespace(IF=4.58e6, Fs=58e6, Fc=1575.42e6, codeFreqBasis=1.023e6, ms=1e-3)
+    signal.Sample = math.ceil(signal.Fs * signal.ms)
+    signal.codelength = signal.codeFreqBasis * signal.ms
+    acq = SimpleNamespace(prnList=list(range(1, 33)), freqStep=500, freqMin=-10000, datalen=20, L=10)
+    acq.freqNum = int(2 * abs(acq.freqMin) / acq.freqStep + 1)
+    track = SimpleNamespace(CorrelatorSpacing=0.5, DLLBW=2, DLLDamp=0.707, DLLGain=0.1, PLLBW=15,
+                            PLLDamp=0.707, PLLGain=0.25, msToProcessCT_1ms=1000,
+                            msToProcessCT_10ms=40000, ctPOS=3000, msToProcessVT=5000, pdi=1)
+    solu = SimpleNamespace(iniPos=[22.328444770087565 / 180 * math.pi,
+                                   114.1713630049711 / 180 * math.pi, 4],
+                           navSolPeriod=20, mode=2)
+    cmn = SimpleNamespace(doy=171, vtEnable=1, mltCorrON=[1, 0], cSpeed=299792458, equip="stereo")
+    return file, signal, acq, track, solu, cmn
+
+
+# ---------------------------------------------------------------------------
+# device context
+# ---------------------------------------------------------------------------
+class Context:
+    """One gnss_ctx on one HIP device (stream, rocFFT plans, device buffers)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = abi.load()
+        h = C.c_void_p()
+        st = self.lib.gnss_ctx_create(int(device), C.byref(h))
+        if st != abi.OK:
+            raise abi.GnssError(st, f"gnss_ctx_create(device={device}) failed")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.gnss_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self, st):
+        if st != abi.OK:
+            raise abi.GnssError(st, (self.lib.gnss_last_error(self.h) or b"").decode())
+        return st
+
+    def timing(self) -> dict:
+        t = abi.GnssTiming()
+        self.check(self.lib.gnss_last_timing(self.h, C.byref(t)))
+        return {f: getattr(t, f) for f, _ in abi.GnssTiming._fields_}
+
+    def set_profiling(self, on: bool):
+        self.check(self.lib.gnss_ctx_set_profiling(self.h, 1 if on else 0))
+
+
+class DeviceRecord:
+    """An IF record resident in this context's HBM (bytes = file bytes)."""
+
+    def __init__(self, ctx: Context, nbytes: int):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        p = C.c_void_p()
+        ctx.check(ctx.lib.gnss_dev_alloc(ctx.h, C.c_uint64(self.nbytes), C.byref(p)))
+        self.ptr = p
+
+    @classmethod
+    def from_host(cls, ctx: Context, data: np.ndarray):
+        data = np.ascontiguousarray(data, dtype=np.int8)
+        r = cls(ctx, data.nbytes)
+        ctx.check(ctx.lib.gnss_dev_upload(ctx.h, r.ptr, data.ctypes.data_as(C.c_void_p),
+                                          C.c_uint64(data.nbytes)))
+        return r
+
+    def download(self, offset: int = 0, nbytes: int | None = None) -> np.ndarray:
+        n = self.nbytes - offset if nbytes is None else int(nbytes)
+        out = np.empty(n, dtype=np.int8)
+        src = C.c_void_p(self.ptr.value + int(offset))
+        self.ctx.check(self.ctx.lib.gnss_dev_download(self.ctx.h, out.ctypes.data_as(C.c_void_p),
+                                                      src, C.c_uint64(n)))
+        return out
+
+    def free(self):
+        if self.ptr:
+            self.ctx.lib.gnss_dev_free(self.ctx.h, self.ptr)
+            self.ptr = None
+
+
+_default_ctx: Context | None = None
+
+
+def default_context() -> Context:
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(0)
+    return _default_ctx
+
+
+# ---------------------------------------------------------------------------
+# struct marshalling
+# ---------------------------------------------------------------------------
+def to_c_file(file):
+    f = abi.GnssFile()
+    keep = []
+    path = getattr(file, "fileRoute", None)
+    data = getattr(file, "data", None)
+    dev = getattr(file, "dev", None)
+    if dev is not None:
+        f.dev_data = dev.ptr
+        f.nbytes = dev.nbytes
+    elif data is not None:
+        arr = np.ascontiguousarray(data, dtype=np.int8)
+        keep.append(arr)
+        f.data = arr.ctypes.data
+        f.nbytes = arr.nbytes
+    elif path:
+        f.path = str(path).encode()
+    else:
+        raise abi.GnssError(abi.EARG, "file has no fileRoute, data or dev record")
+    f.skip = int(file.skip)
+    f.dataType = int(file.dataType)
+    f.dataPrecision = int(file.dataPrecision)
+    return f, keep
+
+
+def to_c_signal(signal):
+    s = abi.GnssSignal()
+    s.IF, s.Fs, s.codeFreqBasis, s.ms = signal.IF, signal.Fs, signal.codeFreqBasis, signal.ms
+    s.Sample = int(signal.Sample)
+    s.codelength = signal.codelength
+    return s
+
+
+def to_c_acq(acq, prn_list=None):
+    a = abi.GnssAcq()
+    a.freqNum, a.freqMin, a.freqStep = int(acq.freqNum), float(acq.freqMin), float(acq.freqStep)
+    a.datalen, a.L = int(acq.datalen), int(acq.L)
+    keep = []
+    if prn_list is not None:
+        arr = np.ascontiguousarray(prn_list, dtype=np.int32)
+        keep.append(arr)
+        a.n_prn = len(arr)
+        a.prn_list = arr.ctypes.data_as(C.POINTER(C.c_int32))
+    return a, keep
+
+
+def to_c_acquired(Acquired):
+    a = abi.GnssAcquired()
+    n = len(Acquired.sv)
+    a.n = n
+    for i in range(n):
+        a.sv[i] = int(Acquired.sv[i])
+        a.SNR[i] = float(Acquired.SNR[i])
+        a.Doppler[i] = float(Acquired.Doppler[i])
+        a.codedelay[i] = int(Acquired.codedelay[i])
+        a.fineFreq[i] = float(Acquired.fineFreq[i])
+    return a
+
+
+def from_c_acquired(a) -> SimpleNamespace:
+    n = a.n
+    return SimpleNamespace(sv=np.array(a.sv[:n], dtype=np.int64),
+                           SNR=np.array(a.SNR[:n]), Doppler=np.array(a.Doppler[:n]),
+                           codedelay=np.array(a.codedelay[:n], dtype=np.int64),
+                           fineFreq=np.array(a.fineFreq[:n]))
+
+
+def to_c_track(track, taps=None, channels=None):
+    t = abi.GnssTrack()
+    for f in ["CorrelatorSpacing", "DLLBW", "DLLDamp", "DLLGain", "PLLBW", "PLLDamp", "PLLGain"]:
+        setattr(t, f, float(getattr(track, f)))
+    t.msToProcessCT_1ms = int(track.msToProcessCT_1ms)
+    t.msToProcessCT_10ms = int(track.msToProcessCT_10ms)
+    keep = []
+    if taps is not None:
+        arr = np.ascontiguousarray(taps, dtype=np.float64)
+        keep.append(arr)
+        t.n_taps = len(arr)
+        t.tap_offsets = arr.ctypes.data_as(C.POINTER(C.c_double))
+    if channels is not None:
+        arr = np.ascontiguousarray(channels, dtype=np.int32)
+        keep.append(arr)
+        t.n_chan = len(arr)
+        t.chan = arr.ctypes.data_as(C.POINTER(C.c_int32))
+    return t, keep
+
+
+class TrackOutBuffers:
+    """Caller-allocated trackingCT outputs (see gnss_track_out in the header)."""
+
+    def __init__(self, nsv: int, track, ntaps: int = 0):
+        self.max_len = int(track.msToProcessCT_1ms) + 19 + int(track.msToProcessCT_10ms)
+        self.rec = np.zeros((nsv, abi.NFIELDS, self.max_len))
+        self.taps = np.zeros((nsv, 2, ntaps, self.max_len)) if ntaps else None
+        self.len = np.zeros(nsv, dtype=np.int64)
+        self.countinx = np.zeros(nsv, dtype=np.int32)
+        self.cn0_cap = max(int(track.msToProcessCT_1ms) + 19, int(track.msToProcessCT_10ms) // 10) // 20 + 1
+        self.CN0 = np.zeros((self.cn0_cap, nsv))
+        o = abi.GnssTrackOut()
+        o.max_len = self.max_len
+        o.rec = self.rec.ctypes.data_as(C.POINTER(C.c_double))
+        o.taps = self.taps.ctypes.data_as(C.POINTER(C.c_double)) if ntaps else None
+        o.len = self.len.ctypes.data_as(C.POINTER(C.c_int64))
+        o.countinx = self.countinx.ctypes.data_as(C.POINTER(C.c_int32))
+        o.CN0_Eph = self.CN0.ctypes.data_as(C.POINTER(C.c_double))
+        o.cn0_cap = self.cn0_cap
+        self.c = o
+
+
+class StructArray:
+    """MATLAB struct array indexed by PRN: TckResultCT(prn).P_i (trackingCT.m:153)."""
+
+    def __init__(self, entries: dict):
+        self._e = entries
+
+    def __call__(self, prn):
+        return self._e[int(prn)]
+
+    def __len__(self):
+        return max(self._e) if self._e else 0
+
+    def __bool__(self):
+        return bool(self._e)
+
+    def prns(self):
+        return sorted(self._e)
+
+
+def build_tck_result(Acquired, buf: TrackOutBuffers, channels=None) -> StructArray:
+    entries = {}
+    chans = range(len(Acquired.sv)) if channels is None else channels
+    for c in chans:
+        n = int(buf.len[c])
+        e = SimpleNamespace(**{f: buf.rec[c, k, :n].copy() for k, f in enumerate(abi.FIELDS)})
+        if buf.taps is not None:
+            e.taps_i = buf.taps[c, 0, :, :n].copy()
+            e.taps_q = buf.taps[c, 1, :, :n].copy()
+        entries[int(Acquired.sv[c])] = e
+    return StructArray(entries)
+
+
+# ---------------------------------------------------------------------------
+# acquisition.m / trackingCT.m
+# ---------------------------------------------------------------------------
+def acquisition(file, signal, acq, *, ctx: Context | None = None, prn_list=None,
+                diag: bool = False):
+    """acquisition.m:1-127 on the GPU.
+
+    Like the reference, acq.prnList is ignored (acquisition.m:47 hard-codes 1:32,
+    quirk A.1); `prn_list` selects PRNs explicitly (config 1: [3]; rank sharding).
+    Returns Acquired (fields sv, SNR, Doppler, codedelay, fineFreq as row vectors),
+    plus the per-PRN detector diagnostics when diag=True.
+    """
+    ctx = ctx or default_context()
+    f, k1 = to_c_file(file)
+    s = to_c_signal(signal)
+    a, k2 = to_c_acq(acq, prn_list)
+    out = abi.GnssAcquired()
+    dg = abi.GnssAcqDiag()
+    st = ctx.lib.gnss_acquisition(ctx.h, C.byref(f), C.byref(s), C.byref(a), C.byref(out),
+                                  C.byref(dg))
+    if st not in (abi.OK, abi.ENODATA):
+        ctx.check(st)
+    if st == abi.ENODATA:
+        print("No satellites acquired. Check parameter settings ... \n")
+    res = from_c_acquired(out)
+    if diag:
+        n = dg.n
+        d = SimpleNamespace(prn=np.array(dg.prn[:n]), SNR=np.array(dg.SNR[:n]),
+                            fbin=np.array(dg.fbin[:n]), codePhase=np.array(dg.codePhase[:n]),
+                            peak=np.array(dg.peak[:n]), peak2=np.array(dg.peak2[:n]))
+        return res, d
+    return res
+
+
+def trackingCT(file, signal, track, Acquired, *, ctx: Context | None = None, taps=None,
+               channels=None, save_countinx: str | None = None, raw: bool = False):
+    """trackingCT.m:1-530 on the GPU -> (TckResultCT, CN0_Eph, countinx).
+
+    TckResultCT is indexed by PRN (TckResultCT(prn).P_i), CN0_Eph is
+    cn0_rows x nsv, countinx is 1 x nsv. `taps` enables the multi-correlator ACF
+    taps (config 5); `channels` tracks a subset (multi-GPU shard). The side file
+    countinx.mat of trackingCT.m:530 is written only when save_countinx names it.
+    With raw=True the TrackOutBuffers are returned instead of the structs.
+    """
+    ctx = ctx or default_context()
+    nsv = len(Acquired.sv)
+    f, k1 = to_c_file(file)
+    s = to_c_signal(signal)
+    t, k2 = to_c_track(track, taps, channels)
+    a = to_c_acquired(Acquired)
+    buf = TrackOutBuffers(nsv, track, 0 if taps is None else len(taps))
+    st = ctx.lib.gnss_tracking_ct(ctx.h, C.byref(f), C.byref(s), C.byref(t), C.byref(a),
+                                  C.byref(buf.c))
+    if st == abi.ENODATA:
+        print("Not enough raw data  \n")
+        return StructArray({}), np.zeros((0, nsv)), buf.countinx.astype(np.int64)
+    ctx.check(st)
+    if raw:
+        return buf
+    countinx = buf.countinx.astype(np.int64)
+    if save_countinx:
+        import scipy.io as sio
+        sio.savemat(save_countinx, {"countinx": countinx.reshape(1, -1)})
+    cn0 = buf.CN0[: buf.c.cn0_rows].copy()
+    return build_tck_result(Acquired, buf, channels), cn0, countinx
+
+
+def ca_code(prn: int) -> np.ndarray:
+    """generateCAcode(PRN) as used by the kernels (1023 chips of +-1)."""
+    lib = abi.load()
+    out = np.zeros(1023, dtype=np.int8)
+    st = lib.gnss_ca_code(int(prn), out.ctypes.data_as(C.c_void_p))
+    if st != abi.OK:
+        raise abi.GnssError(st, "gnss_ca_code")
+    return out
+
+
+def correlate_step(file, signal, prn, pdi, remChip, codeFreq, carrierFreq, remPhase, pos_bytes,
+                   taps, *, ctx: Context | None = None):
+    """One trackingCT correlation step on the GPU at an arbitrary NCO state
+    (trackingCT.m:79-118 without negation / loop update). Returns (sums, numSample)
+    with sums = [I_0, Q_0, I_1, Q_1, ...] per tap."""
+    ctx = ctx or default_context()
+    f, k1 = to_c_file(file)
+    s = to_c_signal(signal)
+    taps = np.ascontiguousarray(taps, dtype=np.float64)
+    sums = np.zeros(2 * len(taps))
+    ns = C.c_int64()
+    ctx.check(ctx.lib.gnss_correlate_step(
+        ctx.h, C.byref(f), C.byref(s), int(prn), int(pdi), float(remChip), float(codeFreq),
+        float(carrierFreq), float(remPhase), int(pos_bytes), len(taps),
+        taps.ctypes.data_as(C.POINTER(C.c_double)), sums.ctypes.data_as(C.POINTER(C.c_double)),
+        C.byref(ns)))
+    return sums, ns.value

@@ -1,0 +1,247 @@
+/*
+ * gnss_mi355x.h — C-ABI drop-in boundary for the GPS L1 C/A acquisition +
+ * conventional-tracking hot path of KangWelly/Assignment-for-AAE6102_GNSS-SDR,
+ * implemented with hand-written CDNA4 (gfx950) HIP kernels.
+ *
+ * The reference boundary is two MATLAB function calls (no FFI of its own):
+ *
+ *   Acquired = acquisition(file, signal, acq)
+ *       SDR_MATLAB-main/acqtckpos/acquisition.m:1, called from SDR_main.m:22
+ *       and Plot_task_1.m:14
+ *   [TckResultCT, CN0_Eph, countinx] = trackingCT(file, signal, track, Acquired)
+ *       SDR_MATLAB-main/acqtckpos/trackingCT.m:1, called from SDR_main.m:38
+ *
+ * The structs below carry exactly the MATLAB struct fields those functions read
+ * (SDR_MATLAB-main/initParameters.m:20-70), as POD with fixed-width members.
+ * Everything is plain pointers and sizes; no torch / HIP types cross this line.
+ * The caller allocates every output; all lengths are known in advance.
+ *
+ * Threading: a gnss_ctx is bound to one HIP device and is not re-entrant
+ * (MATLAB calls the MEX from one thread; the ctypes harness follows that rule).
+ */
+#ifndef GNSS_MI355X_H
+#define GNSS_MI355X_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GNSS_ABI_VERSION 1
+
+/* ---- status codes (SURVEY §8b "Error conventions") --------------------- */
+#define GNSS_OK         0
+#define GNSS_ENODATA    1  /* reference's empty-result paths: "No satellites acquired"
+                              (acquisition.m:84-85) / "Not enough raw data" ->
+                              TckResultCT = [] (trackingCT.m:108-112, 302-306)          */
+#define GNSS_EIO        2  /* file cannot be opened/read, or phase-C read past EOF
+                              (trackingCT.m:442 has no check: MATLAB raises an error)  */
+#define GNSS_EARG       3  /* bad/unsupported argument                                  */
+#define GNSS_EDEVICE    4  /* HIP / rocFFT failure                                      */
+#define GNSS_EINDEX     5  /* an index MATLAB would reject (e.g. P_i(i+17) past the end
+                              in the bit-edge search, trackingCT.m:179-204)             */
+
+#define GNSS_MAX_SV     64   /* generateCAcode.m:16-27 knows 51 PRNs                     */
+#define GNSS_MAX_TAPS   32
+
+/* ---- config structs (initParameters.m) ---------------------------------- */
+
+/* file.* (initParameters.m:20-21,35-38). Exactly one of path / data / dev_data
+ * is used, in that order of preference reversed (dev_data, then data, then
+ * path). All seeks are absolute ('bof'), so positioned reads of `path` are
+ * equivalent to MATLAB's fseek/fread on file.fid (SURVEY §8b "File handle"). */
+typedef struct gnss_file {
+    const char   *path;          /* file.fileRoute, or NULL                          */
+    const int8_t *data;          /* host-resident IF record (byte 0 = file byte 0)   */
+    const void   *dev_data;      /* IF record already resident in this ctx's HBM     */
+    uint64_t      nbytes;        /* bytes in data / dev_data (ignored for path)      */
+    int64_t       skip;          /* file.skip, ms                                    */
+    int32_t       dataType;      /* file.dataType: 1 = I, 2 = IQ                     */
+    int32_t       dataPrecision; /* file.dataPrecision: 1 = int8, 2 = int16          */
+} gnss_file;
+
+/* signal.* (initParameters.m:41-48) */
+typedef struct gnss_signal {
+    double  IF;              /* Hz                                  */
+    double  Fs;              /* Hz                                  */
+    double  codeFreqBasis;   /* 1.023e6                             */
+    double  ms;              /* 1e-3                                */
+    int64_t Sample;          /* ceil(Fs*ms)                         */
+    double  codelength;      /* codeFreqBasis*ms                    */
+} gnss_signal;
+
+/* acq.* (initParameters.m:50-55) */
+typedef struct gnss_acq {
+    int32_t        freqNum;
+    double         freqMin;
+    double         freqStep;
+    int32_t        datalen;   /* ms of non-coherent 1-ms FFT correlations            */
+    int32_t        L;         /* ms used by the fine-frequency FFT                   */
+    int32_t        n_prn;     /* 0 -> PRNs 1..32, as acquisition.m:47 hard-codes     */
+    const int32_t *prn_list;  /* explicit PRN list (config 1: {3}; rank sharding)    */
+} gnss_acq;
+
+/* Acquired (acquisition.m:19-23,71-74,121): row vectors in ascending PRN order. */
+typedef struct gnss_acquired {
+    int32_t n;
+    int32_t sv[GNSS_MAX_SV];
+    double  SNR[GNSS_MAX_SV];
+    double  Doppler[GNSS_MAX_SV];
+    int32_t codedelay[GNSS_MAX_SV];
+    double  fineFreq[GNSS_MAX_SV];
+} gnss_acquired;
+
+/* Per-PRN detector diagnostics (not part of the reference struct): every tested
+ * PRN, acquired or not. peak2 = largest correlation value outside the peak's
+ * +-56-sample exclusion window of the peak bin (margin of the argmax). */
+typedef struct gnss_acq_diag {
+    int32_t n;
+    int32_t prn[GNSS_MAX_SV];
+    double  SNR[GNSS_MAX_SV];
+    int32_t fbin[GNSS_MAX_SV];        /* 1-based, as MATLAB                         */
+    int32_t codePhase[GNSS_MAX_SV];   /* 1-based                                    */
+    double  peak[GNSS_MAX_SV];
+    double  peak2[GNSS_MAX_SV];
+} gnss_acq_diag;
+
+/* track.* (initParameters.m:58-70) */
+typedef struct gnss_track {
+    double  CorrelatorSpacing;      /* chip                                         */
+    double  DLLBW, DLLDamp, DLLGain;
+    double  PLLBW, PLLDamp, PLLGain;
+    int32_t msToProcessCT_1ms;      /* the 1-ms phases A/B (trackingCT.m:29,221)    */
+    int32_t msToProcessCT_10ms;     /* the 10-ms phase C (trackingCT.m:384)         */
+    /* Multi-correlator ACF taps (config 5; semantics of
+     * trackingCT_multiCorr-GIVEN.m:25,92-143). n_taps = 0 -> the three E/P/L taps
+     * [-CorrelatorSpacing 0 +CorrelatorSpacing] (trackingCT.m:24). Otherwise
+     * tap_offsets[n_taps] (chips) must contain -CorrelatorSpacing, 0 and
+     * +CorrelatorSpacing, which feed the DLL/PLL exactly as E/P/L do.           */
+    int32_t        n_taps;
+    const double  *tap_offsets;
+    /* Channel shard (multi-GPU): process Acquired channels chan[0..n_chan-1]
+     * (0-based svindex) only; NULL -> every channel. Outputs of other channels
+     * are left untouched. The quirk of trackingCT.m:161 (linear indexing into an
+     * nsv x N matrix) uses the GLOBAL svindex and nsv, so shards stay bit-equal.  */
+    int32_t        n_chan;
+    const int32_t *chan;
+} gnss_track;
+
+/* Fields of one TckResultCT(prn) entry, in trackingCT.m:153-170 order. */
+enum gnss_track_field {
+    GNSS_F_P_i = 0, GNSS_F_P_q, GNSS_F_E_i, GNSS_F_E_q, GNSS_F_L_i, GNSS_F_L_q,
+    GNSS_F_PLLdiscri, GNSS_F_DLLdiscri, GNSS_F_codedelay, GNSS_F_remChip,
+    GNSS_F_codeFreq, GNSS_F_carrierFreq, GNSS_F_remPhase, GNSS_F_remSample,
+    GNSS_F_numSample, GNSS_F_delayValue, GNSS_F_absoluteSample, GNSS_F_codedelay2,
+    GNSS_NFIELDS
+};
+
+/* Outputs of trackingCT. Caller-allocated:
+ *   rec      [nsv][GNSS_NFIELDS][max_len]  TckResultCT series per channel
+ *            (series length 1000 + countinx + msToProcessCT_10ms, phase-C values
+ *            written 10x as trackingCT.m:507-524 does); may be NULL.
+ *   taps     [nsv][2][n_taps][max_len]     I then Q of every ACF tap; NULL unless
+ *            wanted (phase-C taps are negated like E/P/L, trackingCT.m:447-449).
+ *   len      [nsv]  series length per channel
+ *   countinx [nsv]  bit-edge result (trackingCT.m:207)
+ *   CN0_Eph  [cn0_cap][nsv] row-major (row = snrIndex-1); rows never written are 0
+ *   cn0_rows  out: rows of the MATLAB CN0_Eph matrix
+ * max_len must be >= msToProcessCT_1ms + 19 + msToProcessCT_10ms.             */
+typedef struct gnss_track_out {
+    int64_t  max_len;
+    double  *rec;
+    double  *taps;
+    int64_t *len;
+    int32_t *countinx;
+    double  *CN0_Eph;
+    int32_t  cn0_cap;
+    int32_t  cn0_rows;
+} gnss_track_out;
+
+/* Device-side timing of the last call (hipEvents on the ctx stream). */
+typedef struct gnss_timing {
+    double acq_ms;            /* whole acquisition, IF resident in HBM             */
+    double acq_corr_ms;       /* wipe + FFT correlation + power accumulation       */
+    double acq_fine_ms;       /* fine-frequency FFTs + argmax                      */
+    double track_ms;          /* whole trackingCT, IF resident in HBM              */
+    double track_kernel_ms;   /* sum of correlator-kernel durations                */
+    int64_t track_launches;   /* correlator-kernel launches                        */
+    int64_t track_channel_samples;   /* channel-samples correlated (all taps)      */
+    int64_t acq_hypothesis_samples;  /* PRN x bin x ms x Sample                     */
+    double h2d_ms;            /* host->HBM upload of the IF window, if any         */
+} gnss_timing;
+
+typedef struct gnss_ctx gnss_ctx;
+
+int         gnss_abi_version(void);
+const char *gnss_strerror(int status);
+
+/* Create a context bound to HIP device `device` (owns stream, device buffers,
+ * rocFFT plans). Replaces the MEX's persistent state (freed by mexAtExit). */
+int  gnss_ctx_create(int device, gnss_ctx **out);
+void gnss_ctx_destroy(gnss_ctx *ctx);
+const char *gnss_last_error(const gnss_ctx *ctx);
+int  gnss_last_timing(const gnss_ctx *ctx, gnss_timing *out);
+/* Profiling mode: every correlator-step launch is bracketed by hipEvents (no
+ * step graphs) so gnss_timing.track_kernel_ms is the sum of kernel durations. */
+int  gnss_ctx_set_profiling(gnss_ctx *ctx, int enable);
+
+/* Device memory owned by the ctx, for callers that keep an IF record resident
+ * in HBM (gnss_file.dev_data) across calls. */
+int  gnss_dev_alloc(gnss_ctx *ctx, uint64_t nbytes, void **dev_ptr);
+int  gnss_dev_free(gnss_ctx *ctx, void *dev_ptr);
+int  gnss_dev_upload(gnss_ctx *ctx, void *dev_dst, const void *host_src, uint64_t nbytes);
+int  gnss_dev_download(gnss_ctx *ctx, void *host_dst, const void *dev_src, uint64_t nbytes);
+
+/* acquisition.m replacement (acquisition.m:1-127). Returns GNSS_ENODATA with
+ * out->n == 0 when nothing is acquired (acquisition.m:84-85). diag may be NULL. */
+int gnss_acquisition(gnss_ctx *ctx, const gnss_file *file, const gnss_signal *signal,
+                     const gnss_acq *acq, gnss_acquired *out, gnss_acq_diag *diag);
+
+/* trackingCT.m replacement (trackingCT.m:1-530). The `countinx.mat` side file
+ * (trackingCT.m:530) is the wrapper's job (MEX / Python mirror). */
+int gnss_tracking_ct(gnss_ctx *ctx, const gnss_file *file, const gnss_signal *signal,
+                     const gnss_track *track, const gnss_acquired *acquired,
+                     gnss_track_out *out);
+
+/* Per-step parity hook: ONE trackingCT correlation step (trackingCT.m:79-118: numSample
+ * from remChip/codeFreq, E/P/L or ACF replicas, carrier wipe, sums; no negation, no
+ * loop update) at an arbitrary NCO state, on the same kernel the tracker launches.
+ * sums_out[2*n_taps] = (I, Q) per tap; taps as gnss_track.tap_offsets (3 or 11). */
+int gnss_correlate_step(gnss_ctx *ctx, const gnss_file *file, const gnss_signal *signal,
+                        int prn, int pdi, double remChip, double codeFreq, double carrierFreq,
+                        double remPhase, int64_t pos_bytes, int n_taps, const double *taps,
+                        double *sums_out, int64_t *numSample_out);
+
+/* generateCAcode.m:16-64: the 1023 +-1 chips of PRN 1..51 used by the kernels. */
+int gnss_ca_code(int prn, int8_t *out1023);
+
+/* ---- synthetic IF: deterministic int8 I/Q record ------------ */
+typedef struct gnss_synth_sv {
+    int32_t prn;
+    double  doppler_hz;     /* carrier Doppler; code Doppler = fd/1575.42e6      */
+    double  code_phase0;    /* chips at absolute sample 0 (unwrapped)            */
+    double  carr_phase0;    /* cycles at absolute sample 0                       */
+    double  cn0_dbhz;
+    uint64_t bit_seed;      /* 50 bps nav-bit stream seed                        */
+    double  bit_phase_chips;/* nav-bit edge offset, chips                        */
+} gnss_synth_sv;
+
+typedef struct gnss_synth {
+    double   Fs, IF;
+    double   noise_sigma;   /* per I/Q component, LSB                            */
+    uint64_t seed;
+    int32_t  n_sv;
+    gnss_synth_sv sv[GNSS_MAX_SV];
+} gnss_synth;
+
+/* Fill dev_dst (this ctx's HBM) with samples [sample0, sample0 + nsamples) of
+ * the record, 2 bytes per sample (I then Q). */
+int gnss_synth_if_device(gnss_ctx *ctx, const gnss_synth *cfg, uint64_t sample0,
+                         uint64_t nsamples, void *dev_dst);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GNSS_MI355X_H */

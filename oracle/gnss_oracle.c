@@ -1,0 +1,920 @@
+/*
+ * gnss_oracle.c — TEST INFRASTRUCTURE ONLY (see gnss_oracle.h).
+ *
+ * Plain-C fp64 restatement of the reference hot path, operation by operation,
+ * in MATLAB's evaluation order (left to right, no fused multiply-add: build
+ * with -ffp-contract=off). Citations are to /root/reference/SDR_MATLAB-main/.
+ */
+#define _GNU_SOURCE
+#include "gnss_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <fcntl.h>
+#include <unistd.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define TWO_PI (2.0 * M_PI) /* MATLAB's 2*pi evaluated first: 6.283185307179586 */
+
+/* ------------------------------------------------------------------------ */
+/* generateCAcode.m                                                          */
+/* ------------------------------------------------------------------------ */
+/* G2 delays, generateCAcode.m:16-27 (32 GPS + 19 SBAS). */
+static const int g2s[51] = {
+    5, 6, 7, 8, 17, 18, 139, 140, 141, 251, 252, 254, 255, 256, 257, 258, 469, 470, 471, 472,
+    473, 474, 509, 512, 513, 514, 515, 516, 859, 860, 861, 862, 145, 175, 52, 21, 237, 235, 886,
+    657, 634, 762, 355, 1012, 176, 603, 130, 359, 595, 68, 386};
+
+int or_generate_ca(int prn, int8_t *out)
+{
+    if (prn < 1 || prn > 51) return GNSS_EARG;
+    int g1[1023], g2[1023], reg[10];
+    /* G1: taps 3,10 in +-1 arithmetic (generateCAcode.m:34-42) */
+    for (int i = 0; i < 10; i++) reg[i] = -1;
+    for (int i = 0; i < 1023; i++) {
+        g1[i] = reg[9];
+        int save = reg[2] * reg[9];
+        for (int j = 9; j > 0; j--) reg[j] = reg[j - 1];
+        reg[0] = save;
+    }
+    /* G2: taps 2,3,6,8,9,10 (generateCAcode.m:49-57) */
+    for (int i = 0; i < 10; i++) reg[i] = -1;
+    for (int i = 0; i < 1023; i++) {
+        g2[i] = reg[9];
+        int save = reg[1] * reg[2] * reg[5] * reg[7] * reg[8] * reg[9];
+        for (int j = 9; j > 0; j--) reg[j] = reg[j - 1];
+        reg[0] = save;
+    }
+    /* g2 = [g2(1023-s+1:1023) g2(1:1023-s)] ; CA = -(g1.*g2) (:61,64) */
+    int s = g2s[prn - 1];
+    for (int i = 0; i < 1023; i++) {
+        int src = (i < s) ? (1023 - s + i) : (i - s);
+        out[i] = (int8_t)(-(g1[i] * g2[src]));
+    }
+    return GNSS_OK;
+}
+
+/* calcLoopCoef.m:41-45 */
+void or_calc_loop_coef(double LBW, double zeta, double k, double *tau1, double *tau2)
+{
+    double Wn = LBW * 8 * zeta / (4 * (zeta * zeta) + 1);
+    *tau1 = k / (Wn * Wn);
+    *tau2 = 2.0 * zeta / Wn;
+}
+
+/* ------------------------------------------------------------------------ */
+/* MATLAB scalar semantics                                                   */
+/* ------------------------------------------------------------------------ */
+double or_round(double x) { return round(x); } /* half away from zero */
+
+double or_mod(double a, double b)
+{
+    if (b == 0) return a;
+    double r = fmod(a, b);
+    if (r != 0 && ((r < 0) != (b < 0))) r += b;
+    return r;
+}
+
+/* Colon operator a:d:b following MathWorks' published colonop algorithm:
+ * n from round((b-a)/d) with a 2*eps tolerance, right end snapped to b, and the
+ * vector built from both ends toward the midpoint. */
+void or_colon_init(or_colon *r, double a, double d, double b)
+{
+    r->a = a; r->d = d; r->c = b; r->n = -1;
+    if (!isfinite(a) || !isfinite(d) || !isfinite(b)) return;
+    if (d == 0 || (a < b && d < 0) || (b < a && d > 0)) return;
+    double tol = 2.0 * DBL_EPSILON * fmax(fabs(a), fabs(b));
+    double sig = (d > 0) ? 1.0 : -1.0;
+    double n;
+    if (a == floor(a) && d == 1) {
+        n = floor(b) - a;
+    } else if (a == floor(a) && d == floor(d)) {
+        double q = floor(a / d);
+        double rr = a - q * d;
+        n = floor((b - rr) / d) - q;
+    } else {
+        n = round((b - a) / d);
+        if (sig * (a + n * d - b) > tol) n = n - 1;
+    }
+    double c = a + n * d;
+    if (sig * (c - b) > -tol) c = b;
+    r->c = c;
+    r->n = (int64_t)n;
+}
+
+double or_colon_elem(const or_colon *r, int64_t k)
+{
+    int64_t n = r->n;
+    if (2 * k == n) return (r->a + r->c) / 2;
+    if (k <= n / 2) return r->a + (double)k * r->d;
+    return r->c - (double)(n - k) * r->d;
+}
+
+int64_t or_colon_len(double a, double d, double b)
+{
+    or_colon r;
+    or_colon_init(&r, a, d, b);
+    return r.n + 1;
+}
+
+void or_colon_fill(double a, double d, double b, double *out, int64_t cap)
+{
+    or_colon r;
+    or_colon_init(&r, a, d, b);
+    for (int64_t k = 0; k <= r.n && k < cap; k++) out[k] = or_colon_elem(&r, k);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Mixed-radix complex FFT (decimation in time, recursive), fp64             */
+/* ------------------------------------------------------------------------ */
+typedef struct { double re, im; } cpx;
+
+typedef struct fftplan {
+    int64_t n;
+    int nf;
+    int64_t fac[2 * 64]; /* (p, m) pairs */
+    cpx *tw;             /* tw[k] = exp(-2*pi*i*k/n) */
+    int maxp;
+} fftplan;
+
+static int fft_plan_init(fftplan *pl, int64_t n)
+{
+    pl->n = n; pl->nf = 0; pl->maxp = 1;
+    int64_t m = n, p = 4;
+    while (m > 1) {
+        while (m % p) {
+            if (p == 4) p = 2;
+            else if (p == 2) p = 3;
+            else p += 2;
+            if (p * p > m) p = m;
+        }
+        m /= p;
+        pl->fac[2 * pl->nf] = p;
+        pl->fac[2 * pl->nf + 1] = m;
+        pl->nf++;
+        if (p > pl->maxp) pl->maxp = (int)p;
+    }
+    pl->tw = (cpx *)malloc(sizeof(cpx) * (size_t)(n ? n : 1));
+    if (!pl->tw) return -1;
+    for (int64_t k = 0; k < n; k++) {
+        double ang = -2.0 * M_PI * (double)k / (double)n;
+        pl->tw[k].re = cos(ang);
+        pl->tw[k].im = sin(ang);
+    }
+    return 0;
+}
+
+static void fft_plan_free(fftplan *pl) { free(pl->tw); pl->tw = NULL; }
+
+static inline cpx cmul(cpx a, cpx b)
+{
+    cpx r = {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
+    return r;
+}
+
+static void fft_work(cpx *out, const cpx *in, int64_t fstride, const int64_t *fac,
+                     const fftplan *pl, cpx *scratch)
+{
+    int64_t p = fac[0], m = fac[1];
+    if (m == 1) {
+        for (int64_t q = 0; q < p; q++) out[q] = in[q * fstride];
+    } else {
+        for (int64_t q = 0; q < p; q++)
+            fft_work(out + q * m, in + q * fstride, fstride * p, fac + 2, pl, scratch);
+    }
+    const int64_t N = pl->n;
+    const int64_t wp = N / p; /* W_p = tw[N/p] */
+    for (int64_t u = 0; u < m; u++) {
+        for (int64_t q = 0; q < p; q++) {
+            cpx v = out[u + q * m];
+            scratch[q] = (q == 0 || u == 0) ? v : cmul(v, pl->tw[fstride * q * u]);
+        }
+        if (p == 2) {
+            cpx a = scratch[0], b = scratch[1];
+            out[u].re = a.re + b.re; out[u].im = a.im + b.im;
+            out[u + m].re = a.re - b.re; out[u + m].im = a.im - b.im;
+            continue;
+        }
+        for (int64_t q1 = 0; q1 < p; q1++) {
+            cpx acc = scratch[0];
+            for (int64_t q = 1; q < p; q++) {
+                int64_t e = (q * q1) % p;
+                cpx t = e ? cmul(scratch[q], pl->tw[e * wp]) : scratch[q];
+                acc.re += t.re; acc.im += t.im;
+            }
+            out[u + q1 * m] = acc;
+        }
+    }
+}
+
+static int fft_exec(const fftplan *pl, cpx *data, int dir)
+{
+    int64_t n = pl->n;
+    if (n <= 1) return 0;
+    cpx *tmp = (cpx *)malloc(sizeof(cpx) * (size_t)n);
+    cpx *scratch = (cpx *)malloc(sizeof(cpx) * (size_t)pl->maxp);
+    if (!tmp || !scratch) { free(tmp); free(scratch); return -1; }
+    if (dir > 0)
+        for (int64_t k = 0; k < n; k++) data[k].im = -data[k].im;
+    memcpy(tmp, data, sizeof(cpx) * (size_t)n);
+    fft_work(data, tmp, 1, pl->fac, pl, scratch);
+    if (dir > 0) {
+        double s = 1.0 / (double)n;
+        for (int64_t k = 0; k < n; k++) { data[k].re *= s; data[k].im = -data[k].im * s; }
+    }
+    free(tmp); free(scratch);
+    return 0;
+}
+
+int or_fft(double *inout, int64_t n, int dir)
+{
+    fftplan pl;
+    if (fft_plan_init(&pl, n)) return GNSS_EARG;
+    int r = fft_exec(&pl, (cpx *)inout, dir);
+    fft_plan_free(&pl);
+    return r ? GNSS_EARG : GNSS_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* IF record access (fseek 'bof' + fread of int8)                            */
+/* ------------------------------------------------------------------------ */
+/* Copies up to `count` bytes at absolute byte `off` into dst; returns bytes
+ * read (fread semantics: short at EOF). */
+static int64_t rd_bytes(const gnss_file *f, int64_t off, int64_t count, int8_t *dst)
+{
+    if (off < 0 || count <= 0) return 0;
+    if (f->data) {
+        if ((uint64_t)off >= f->nbytes) return 0;
+        int64_t avail = (int64_t)f->nbytes - off;
+        int64_t n = count < avail ? count : avail;
+        memcpy(dst, f->data + off, (size_t)n);
+        return n;
+    }
+    if (!f->path) return -1;
+    int fd = open(f->path, O_RDONLY);
+    if (fd < 0) return -1;
+    int64_t got = 0;
+    while (got < count) {
+        ssize_t r = pread(fd, dst + got, (size_t)(count - got), off + got);
+        if (r <= 0) break;
+        got += r;
+    }
+    close(fd);
+    return got;
+}
+
+static int64_t file_size(const gnss_file *f)
+{
+    if (f->data) return (int64_t)f->nbytes;
+    if (!f->path) return -1;
+    int fd = open(f->path, O_RDONLY);
+    if (fd < 0) return -1;
+    int64_t s = lseek(fd, 0, SEEK_END);
+    close(fd);
+    return s;
+}
+
+/* ------------------------------------------------------------------------ */
+/* acquisition.m                                                             */
+/* ------------------------------------------------------------------------ */
+static int nthreads_of(int n)
+{
+#ifdef _OPENMP
+    return n > 0 ? n : omp_get_max_threads();
+#else
+    (void)n;
+    return 1;
+#endif
+}
+
+int or_acquisition(const gnss_file *file, const gnss_signal *sg, const gnss_acq *acq,
+                   gnss_acquired *out, gnss_acq_diag *diag, int nthreads)
+{
+    memset(out, 0, sizeof(*out));
+    if (diag) memset(diag, 0, sizeof(*diag));
+    if (file->dataPrecision != 1 || file->dataType != 2) return GNSS_EARG; /* int16/I-only: next */
+    const int64_t S = sg->Sample;
+    const int nb = acq->freqNum, dl = acq->datalen;
+    if (S <= 0 || nb <= 0 || dl <= 0 || acq->L <= 0) return GNSS_EARG;
+
+    int prns[GNSS_MAX_SV], np = 0;
+    if (acq->n_prn > 0 && acq->prn_list) {
+        for (int i = 0; i < acq->n_prn && i < GNSS_MAX_SV; i++) prns[np++] = acq->prn_list[i];
+    } else {
+        for (int i = 1; i <= 32; i++) prns[np++] = i; /* acquisition.m:47 */
+    }
+
+    /* read data (acquisition.m:27,34-37) */
+    const int64_t off = file->skip * S * file->dataPrecision * file->dataType;
+    const int64_t nbytes = S * file->dataType * dl;
+    int8_t *raw8 = (int8_t *)malloc((size_t)nbytes);
+    if (!raw8) return GNSS_EIO;
+    if (rd_bytes(file, off, nbytes, raw8) != nbytes) { free(raw8); return GNSS_EIO; }
+
+    /* carrier(freqband,:) = exp(1i*2*pi*(IF+dopplershift)*sampleindex./Fs) (:41-44) */
+    cpx *carrier = (cpx *)malloc(sizeof(cpx) * (size_t)(nb * S));
+    for (int b = 0; b < nb; b++) {
+        double ds = acq->freqMin + acq->freqStep * (double)b;
+        double w = TWO_PI * (sg->IF + ds);
+        for (int64_t n = 1; n <= S; n++) {
+            double th = (w * (double)n) / sg->Fs;
+            carrier[b * S + n - 1].re = cos(th);
+            carrier[b * S + n - 1].im = sin(th);
+        }
+    }
+
+    fftplan pl;
+    fft_plan_init(&pl, S);
+
+    /* conj(fft(temp1)) is PRN-invariant (quirk A.2): computed once per (ms, bin). */
+    cpx *Xc = (cpx *)malloc(sizeof(cpx) * (size_t)(dl * nb * S));
+    int nt = nthreads_of(nthreads);
+#pragma omp parallel for num_threads(nt) schedule(dynamic)
+    for (int j = 0; j < dl * nb; j++) {
+        int idx = j / nb, b = j % nb;
+        cpx *x = Xc + (int64_t)j * S;
+        for (int64_t n = 0; n < S; n++) {
+            double xr = raw8[2 * (idx * S + n)], xi = raw8[2 * (idx * S + n) + 1];
+            cpx c = carrier[b * S + n];
+            x[n].re = xr * c.re - xi * c.im;
+            x[n].im = xr * c.im + xi * c.re;
+        }
+        fft_exec(&pl, x, -1);
+        for (int64_t n = 0; n < S; n++) x[n].im = -x[n].im;
+    }
+
+    const int64_t cshift = (int64_t)ceil(sg->Fs / sg->codeFreqBasis); /* :66 */
+    double res_snr[GNSS_MAX_SV], res_peak[GNSS_MAX_SV], res_peak2[GNSS_MAX_SV];
+    int res_fbin[GNSS_MAX_SV], res_cp[GNSS_MAX_SV];
+
+#pragma omp parallel for num_threads(nt) schedule(dynamic)
+    for (int ip = 0; ip < np; ip++) {
+        int8_t ca[1023];
+        or_generate_ca(prns[ip], ca);
+        cpx *C = (cpx *)malloc(sizeof(cpx) * (size_t)S);
+        cpx *y = (cpx *)malloc(sizeof(cpx) * (size_t)S);
+        double *corr = (double *)calloc((size_t)(nb * S), sizeof(double));
+        /* scode = [CA CA](ceil(sampleindex.*(codeFreqBasis/Fs))) (:50-51) */
+        double step = sg->codeFreqBasis / sg->Fs;
+        for (int64_t n = 1; n <= S; n++) {
+            int64_t ci = (int64_t)ceil((double)n * step); /* 1-based into [CA CA] */
+            C[n - 1].re = ca[(ci - 1) % 1023];
+            C[n - 1].im = 0;
+        }
+        fft_exec(&pl, C, -1); /* temp3 = fft(replica) (:58) */
+        for (int idx = 0; idx < dl; idx++) {
+            for (int b = 0; b < nb; b++) {
+                const cpx *x = Xc + ((int64_t)idx * nb + b) * S;
+                for (int64_t k = 0; k < S; k++) y[k] = cmul(C[k], x[k]);
+                fft_exec(&pl, y, +1);
+                double *row = corr + (int64_t)b * S;
+                for (int64_t k = 0; k < S; k++) { /* abs(...).^2 accumulated (:59) */
+                    double a = hypot(y[k].re, y[k].im);
+                    row[k] = row[k] + a * a;
+                }
+            }
+        }
+        /* [~, fbin] = max(max(abs(correlation'))); [peak, codePhase] = max(max(...)) (:62-63) */
+        double peak = -INFINITY;
+        for (int64_t i = 0; i < nb * S; i++)
+            if (corr[i] > peak) peak = corr[i];
+        int fbin = 0;
+        int64_t cp = 0;
+        for (int b = 0; b < nb && !fbin; b++)
+            for (int64_t k = 0; k < S; k++)
+                if (corr[b * S + k] == peak) { fbin = b + 1; break; }
+        for (int64_t k = 0; k < S && !cp; k++)
+            for (int b = 0; b < nb; b++)
+                if (corr[b * S + k] == peak) { cp = k + 1; break; }
+        /* SNR over corr(fbin, [1:cp-cshift cp+cshift:end]) (:66-68) */
+        const double *row = corr + (int64_t)(fbin - 1) * S;
+        double ss = 0, p2 = 0;
+        int64_t cnt = 0;
+        for (int64_t k = 1; k <= cp - cshift; k++) { ss += row[k - 1] * row[k - 1]; cnt++; if (row[k - 1] > p2) p2 = row[k - 1]; }
+        for (int64_t k = cp + cshift; k <= S; k++) { ss += row[k - 1] * row[k - 1]; cnt++; if (row[k - 1] > p2) p2 = row[k - 1]; }
+        double snr = 10.0 * log10((peak * peak) / (ss / (double)cnt));
+        res_snr[ip] = snr; res_peak[ip] = peak; res_peak2[ip] = p2;
+        res_fbin[ip] = fbin; res_cp[ip] = (int)cp;
+        free(C); free(y); free(corr);
+    }
+
+    for (int ip = 0; ip < np; ip++) {
+        if (diag) {
+            int k = diag->n++;
+            diag->prn[k] = prns[ip]; diag->SNR[k] = res_snr[ip]; diag->fbin[k] = res_fbin[ip];
+            diag->codePhase[k] = res_cp[ip]; diag->peak[k] = res_peak[ip]; diag->peak2[k] = res_peak2[ip];
+        }
+        if (res_snr[ip] >= 12) { /* :70-74 */
+            int k = out->n++;
+            out->sv[k] = prns[ip];
+            out->SNR[k] = res_snr[ip];
+            out->Doppler[k] = acq->freqMin + acq->freqStep * (double)(res_fbin[ip] - 1);
+            out->codedelay[k] = res_cp[ip] - 1;
+        }
+    }
+    free(Xc); free(carrier); free(raw8);
+    fft_plan_free(&pl);
+
+    if (out->n == 0) return GNSS_ENODATA; /* :84-85 */
+
+    /* fine frequency (:89-126) */
+    const int64_t Ls = (int64_t)acq->L * S;
+    const int64_t lbytes = S * file->dataType * (acq->L + 1);
+    int8_t *lraw = (int8_t *)malloc((size_t)lbytes);
+    if (rd_bytes(file, off, lbytes, lraw) != lbytes) { free(lraw); return GNSS_EIO; }
+    const int64_t N = Ls * dl; /* fftlength = length(CarrSignal)*acq.datalen (:108) */
+    fftplan fp;
+    fft_plan_init(&fp, N);
+    const double invFs = 1 / sg->Fs, invFc = 1 / sg->codeFreqBasis;
+    int status = GNSS_OK;
+#pragma omp parallel for num_threads(nt < out->n ? nt : out->n) schedule(dynamic)
+    for (int s = 0; s < out->n; s++) {
+        int8_t ca[1023];
+        or_generate_ca(out->sv[s], ca);
+        cpx *x = (cpx *)calloc((size_t)N, sizeof(cpx));
+        int64_t start = S - out->codedelay[s]; /* 1-based (:106) */
+        for (int64_t k = 1; k <= Ls; k++) {
+            double cvi = floor((invFs * (double)k) / invFc);      /* :104 */
+            int8_t code = ca[(int64_t)fmod(cvi, sg->codelength)]; /* :105 rem(.,1023)+1 */
+            int64_t j = start + k - 1;                            /* 1-based sample */
+            x[k - 1].re = (double)lraw[2 * (j - 1)] * code;
+            x[k - 1].im = (double)lraw[2 * (j - 1) + 1] * code;
+        }
+        fft_exec(&fp, x, -1);
+        /* abs(fftshift(.)); max over 1:halffftlength*2 -> first index (:110-116) */
+        int64_t half = (N + 1) / 2;
+        double best = -1;
+        int64_t kbest = 0;
+        for (int64_t i = 0; i < 2 * half && i < N; i++) {
+            int64_t j = (i + N / 2) % N; /* fftshift: shifted[i] = F[(i + floor(N/2)) mod N] */
+            double a = hypot(x[j].re, x[j].im);
+            if (a > best) { best = a; kbest = i + 1; }
+        }
+        if (2 * half > N) {
+#pragma omp atomic write
+            status = GNSS_EINDEX; /* odd fftlength: MATLAB indexes past the end */
+        }
+        out->fineFreq[s] = -(double)kbest * (sg->Fs / (double)N) + sg->Fs / 2; /* :119 */
+        free(x);
+    }
+    fft_plan_free(&fp);
+    free(lraw);
+    return status;
+}
+
+/* ------------------------------------------------------------------------ */
+/* trackingCT.m                                                              */
+/* ------------------------------------------------------------------------ */
+/* Code(ceil(t)+1) with Code = [CA(1023) repmat(CA,1,pdi) CA(1)] (trackingCT.m:68,413):
+ * chip c = ceil(t) maps to CA((c-1) mod 1023 + 1). */
+static inline int chip_ok(int64_t c, int pdi) { return c >= 0 && c <= 1023 * (int64_t)pdi + 1; }
+static inline int ca_index(int64_t c) { return (int)((c + 1022) % 1023); }
+
+void or_correlate_step(const int8_t *iq, int64_t n, double remChip, double codeFreq, double Fs,
+                       double carrierFreq, double remPhase, const int8_t *ca, int pdi, int ntaps,
+                       const double *taps, double *sums)
+{
+    (void)pdi;
+    const double d = codeFreq / Fs;
+    or_colon col[GNSS_MAX_TAPS];
+    /* sum(Code.*InphaseSignal): the order of MATLAB's summation is not published;
+     * accumulate in extended precision so the oracle is the (near-)exact sum. */
+    long double acc[2 * GNSS_MAX_TAPS];
+    for (int s = 0; s < ntaps; s++) {
+        /* t = (0 + Spacing(s) + remChip) : d : ((numSample-1)*d + Spacing(s) + remChip) */
+        double a = (0 + taps[s]) + remChip;
+        double b = ((double)(n - 1) * d + taps[s]) + remChip;
+        or_colon_init(&col[s], a, d, b);
+        acc[2 * s] = 0;
+        acc[2 * s + 1] = 0;
+    }
+    for (int64_t k = 0; k < n; k++) {
+        /* CarrTime = (0:numSample)./Fs; Wave = (2*pi*(carrierFreq.*CarrTime)) + remPhase */
+        double W = TWO_PI * (carrierFreq * ((double)k / Fs)) + remPhase;
+        double cw = cos(W), sw = sin(W);
+        double xr = iq[2 * k], xi = iq[2 * k + 1];
+        double I = xr * sw + xi * cw; /* imag(raw.*carrsig) */
+        double Q = xr * cw - xi * sw; /* real(raw.*carrsig) */
+        for (int s = 0; s < ntaps; s++) {
+            double t = or_colon_elem(&col[s], k);
+            double code = ca[ca_index((int64_t)ceil(t))];
+            acc[2 * s] += code * I;
+            acc[2 * s + 1] += code * Q;
+        }
+    }
+    for (int s = 0; s < 2 * ntaps; s++) sums[s] = (double)acc[s];
+}
+
+int or_bit_edge(const double *P, int64_t len, int *status)
+{
+    *status = GNSS_OK;
+#define SGN(x) (((x) > 0) - ((x) < 0))
+    for (int64_t i = 7; i <= len - 1; i++) { /* 1-based i (trackingCT.m:179) */
+        int si = SGN(P[i - 1]);
+        int ok = 1;
+        for (int j = 6; j >= 1 && ok; j--) ok = SGN(P[i - j - 1]) != si;
+        for (int j = 1; j <= 17 && ok; j++) {
+            if (i + j > len) { *status = GNSS_EINDEX; return 0; }
+            ok = SGN(P[i + j - 1]) == si;
+        }
+        if (ok && i >= 600) return (int)(or_mod((double)i, 20) - 1); /* :207 */
+    }
+#undef SGN
+    return 0;
+}
+
+void or_nco_replay(double remChip, double codeFreq, double carrFreq, double remCarrPhase,
+                   double Fs, double codelength, int pdi, int use_ceil, int64_t *numSample,
+                   double *remChipNext, double *remCarrPhaseNext)
+{
+    double cps = codeFreq / Fs;
+    double ns = (codelength * pdi - remChip) / cps;
+    int64_t n = (int64_t)(use_ceil ? ceil(ns) : round(ns));
+    *numSample = n;
+    /* remChip = t_CodePrompt(numSample) + cps - codelength*pdi, last colon element = b */
+    double a = (0 + 0.0) + remChip;
+    double b = ((double)(n - 1) * cps + 0.0) + remChip;
+    or_colon col;
+    or_colon_init(&col, a, cps, b);
+    *remChipNext = (or_colon_elem(&col, n - 1) + cps) - codelength * pdi;
+    double W = TWO_PI * (carrFreq * ((double)n / Fs)) + remCarrPhase;
+    *remCarrPhaseNext = fmod(W, TWO_PI);
+}
+
+double or_loop_filter(double outLast, double discri, double discriLast, double tau1, double tau2,
+                      double T)
+{
+    /* code_output = code_outputLast + (tau2/tau1)*(d - dLast) + d*(T/tau1) (trackingCT.m:140) */
+    return outLast + (tau2 / tau1) * (discri - discriLast) + discri * (T / tau1);
+}
+
+typedef struct chan_state {
+    double remChip, remPhase, remSample;
+    double carrier_output, carrier_outputLast, PLLdiscriLast;
+    double code_output, code_outputLast, DLLdiscriLast;
+    double codeFreq, carrierFreqBasis, carrierFreq;
+    int64_t numSample;
+    int64_t pos; /* file position indicator, bytes */
+    int index_int, snrIndex;
+    double Zk[20];
+} chan_state;
+
+typedef struct trk_ctx {
+    const gnss_file *file;
+    const gnss_signal *sg;
+    const gnss_track *tr;
+    int64_t fsize;
+    int ntaps, iE, iP, iL;
+    const double *taps;
+    double tau1code, tau2code, tau1carr, tau2carr;
+    int nsv;
+    gnss_track_out *out;
+} trk_ctx;
+
+static void chan_init(chan_state *c, const trk_ctx *t, const gnss_acquired *acq, int sv)
+{
+    memset(c, 0, sizeof(*c));
+    c->codeFreq = t->sg->codeFreqBasis;
+    c->carrierFreqBasis = acq->fineFreq[sv];
+    c->carrierFreq = acq->fineFreq[sv];
+    c->snrIndex = 1;
+}
+
+/* record one value into rec[ch][field][i0..i1) */
+static inline void rec_put(const trk_ctx *t, int ch, int f, int64_t i0, int64_t i1, double v)
+{
+    if (!t->out->rec) return;
+    double *r = t->out->rec + ((int64_t)ch * GNSS_NFIELDS + f) * t->out->max_len;
+    for (int64_t i = i0; i < i1 && i < t->out->max_len; i++) r[i] = v;
+}
+
+static inline void taps_put(const trk_ctx *t, int ch, int64_t i0, int64_t i1, const double *sums)
+{
+    if (!t->out->taps) return;
+    for (int s = 0; s < t->ntaps; s++)
+        for (int iq = 0; iq < 2; iq++) {
+            double *r = t->out->taps + (((int64_t)ch * 2 + iq) * t->ntaps + s) * t->out->max_len;
+            for (int64_t i = i0; i < i1 && i < t->out->max_len; i++) r[i] = sums[2 * s + iq];
+        }
+}
+
+/* sum(delayValue(1:Index)) for an nsv x N matrix whose only non-zero row is sv
+ * (1-based) holding dv[0..filled-1] (trackingCT.m:161,359,515, quirk A.11). */
+static double dv_linear_sum(const int64_t *dv, int64_t filled, int64_t Index, int sv, int nsv)
+{
+    if (Index < sv) return 0;
+    int64_t cols = (Index - sv) / nsv + 1;
+    if (cols > filled) cols = filled;
+    double s = 0;
+    for (int64_t c = 0; c < cols; c++) s += (double)dv[c];
+    return s;
+}
+
+/* One tracking step (body of trackingCT.m:79-170 / 407-524). Returns status. */
+static int trk_step(const trk_ctx *t, chan_state *c, int ch, int sv1, int pdi, int phaseC,
+                    int64_t Index, int64_t *dv, int64_t dv_col, double *cn0, int8_t *buf,
+                    const int8_t *ca, int64_t codedelay0, double *p_i_log)
+{
+    const gnss_signal *sg = t->sg;
+    const double S = (double)sg->Sample;
+    int64_t delayValue;
+    if (phaseC) {
+        delayValue = c->numSample - (int64_t)(S * pdi); /* :411 uses previous numSample */
+        c->remSample = (sg->codelength * pdi - c->remChip) / (c->codeFreq / sg->Fs); /* :414 */
+        c->numSample = (int64_t)or_round((sg->codelength * pdi - c->remChip) / (c->codeFreq / sg->Fs));
+    } else {
+        c->remSample = (sg->codelength - c->remChip) / (c->codeFreq / sg->Fs); /* :79 */
+        c->numSample = (int64_t)or_round((sg->codelength * pdi - c->remChip) / (c->codeFreq / sg->Fs));
+        delayValue = c->numSample - (int64_t)(S * pdi); /* :82 */
+    }
+    dv[dv_col] = delayValue;
+    const int64_t n = c->numSample;
+    int64_t got = rd_bytes(t->file, c->pos, 2 * n, buf);
+    if (got < 0) return GNSS_EIO;
+    if (got != 2 * n) return phaseC ? GNSS_EIO : GNSS_ENODATA; /* :108-112 / :442 */
+    c->pos += got; /* ftell */
+
+    /* code range check: MATLAB would raise an index error */
+    {
+        const double d = c->codeFreq / sg->Fs;
+        for (int s = 0; s < t->ntaps; s++) {
+            double a = (0 + t->taps[s]) + c->remChip;
+            double b = ((double)(n - 1) * d + t->taps[s]) + c->remChip;
+            or_colon col;
+            or_colon_init(&col, a, d, b);
+            if (col.n != n - 1) return GNSS_EINDEX;
+            if (!chip_ok((int64_t)ceil(or_colon_elem(&col, 0)), pdi) ||
+                !chip_ok((int64_t)ceil(or_colon_elem(&col, n - 1)), pdi))
+                return GNSS_EINDEX;
+        }
+    }
+
+    double sums[2 * GNSS_MAX_TAPS];
+    or_correlate_step(buf, n, c->remChip, c->codeFreq, sg->Fs, c->carrierFreq, c->remPhase, ca, pdi,
+                      t->ntaps, t->taps, sums);
+    if (phaseC)
+        for (int s = 0; s < 2 * t->ntaps; s++) sums[s] = -sums[s]; /* :447-449 */
+
+    /* remChip = (t_CodePrompt(numSample) + codeFreq/Fs) - codeFreqBasis*ms*pdi (:102) */
+    {
+        const double d = c->codeFreq / sg->Fs;
+        double a = (0 + t->taps[t->iP]) + c->remChip;
+        double b = ((double)(n - 1) * d + t->taps[t->iP]) + c->remChip;
+        or_colon col;
+        or_colon_init(&col, a, d, b);
+        c->remChip = (or_colon_elem(&col, n - 1) + c->codeFreq / sg->Fs) -
+                     sg->codeFreqBasis * sg->ms * pdi;
+    }
+    /* remPhase = rem(Wave(numSample+1), 2*pi) (:104-106) */
+    c->remPhase = fmod(TWO_PI * (c->carrierFreq * ((double)n / sg->Fs)) + c->remPhase, TWO_PI);
+
+    const double E_i = sums[2 * t->iE], E_q = sums[2 * t->iE + 1];
+    const double P_i = sums[2 * t->iP], P_q = sums[2 * t->iP + 1];
+    const double L_i = sums[2 * t->iL], L_q = sums[2 * t->iL + 1];
+    if (p_i_log) p_i_log[Index - 1] = P_i;
+
+    /* C/N0 every K = 20 steps (:120-134) */
+    c->index_int += 1;
+    c->Zk[c->index_int - 1] = P_i * P_i + P_q * P_q;
+    if (c->index_int % 20 == 0) {
+        double mean = 0;
+        for (int k = 0; k < 20; k++) mean += c->Zk[k];
+        mean = mean / 20;
+        double var = 0;
+        for (int k = 0; k < 20; k++) var += (c->Zk[k] - mean) * (c->Zk[k] - mean);
+        var = var / 19;
+        double m2v = mean * mean - var;
+        double cn;
+        double scale = 1 / (1 * sg->ms * pdi);
+        if (m2v >= 0) {
+            double NA2 = sqrt(m2v);
+            double varIQ = 0.5 * (mean - NA2);
+            cn = fabs(10 * log10(scale * NA2 / (2 * varIQ)));
+        } else { /* sqrt of a negative: complex NA2 = i*y; abs(10*log10(z)) */
+            double y = sqrt(-m2v);
+            /* z = (scale * (i*y)) / (2 * 0.5*(mean - i*y)) */
+            double nr = 0, ni = scale * y;
+            double dr = 2 * (0.5 * mean), di = 2 * (0.5 * -y);
+            double den = dr * dr + di * di;
+            double zr = (nr * dr + ni * di) / den, zi = (ni * dr - nr * di) / den;
+            double lr = 10 * (log(hypot(zr, zi)) / log(10.0));
+            double li = 10 * (atan2(zi, zr) / log(10.0));
+            cn = hypot(lr, li);
+        }
+        if (cn0 && c->snrIndex <= t->out->cn0_cap)
+            cn0[(int64_t)(c->snrIndex - 1) * t->nsv + ch] = cn;
+        c->index_int = 0;
+        c->snrIndex += 1;
+    }
+
+    /* DLL (:136-143); phase C keeps T = 0.001 (:473) */
+    double E = sqrt(E_i * E_i + E_q * E_q);
+    double L = sqrt(L_i * L_i + L_q * L_q);
+    double DLLdiscri = 0.5 * (E - L) / (E + L);
+    double Tc = phaseC ? 0.001 : (0.001 * pdi);
+    c->code_output = or_loop_filter(c->code_outputLast, DLLdiscri, c->DLLdiscriLast, t->tau1code,
+                                    t->tau2code, Tc);
+    c->DLLdiscriLast = DLLdiscri;
+    c->code_outputLast = c->code_output;
+    c->codeFreq = sg->codeFreqBasis - c->code_output;
+    /* PLL (:145-150) */
+    double PLLdiscri = atan(P_q / P_i) / TWO_PI;
+    c->carrier_output = or_loop_filter(c->carrier_outputLast, PLLdiscri, c->PLLdiscriLast,
+                                       t->tau1carr, t->tau2carr, Tc);
+    c->carrier_outputLast = c->carrier_output;
+    c->PLLdiscriLast = PLLdiscri;
+    c->carrierFreq = c->carrierFreqBasis + c->carrier_output;
+
+    /* record (:153-170; phase C writes Index-9:Index, :507-524) */
+    int64_t i1 = Index, i0 = phaseC ? Index - 10 : Index - 1; /* 0-based half-open */
+    double absS = (double)c->pos;
+    double cd = (double)codedelay0 + dv_linear_sum(dv, dv_col + 1, Index, sv1, t->nsv);
+    double vals[GNSS_NFIELDS] = {P_i, P_q, E_i, E_q, L_i, L_q, PLLdiscri, DLLdiscri, cd,
+                                 c->remChip, c->codeFreq, c->carrierFreq, c->remPhase,
+                                 c->remSample, (double)n, (double)delayValue, absS,
+                                 or_mod(absS / (t->file->dataPrecision * t->file->dataType),
+                                        sg->Fs * sg->ms)};
+    for (int f = 0; f < GNSS_NFIELDS; f++) rec_put(t, ch, f, i0, i1, vals[f]);
+    taps_put(t, ch, i0, i1, sums);
+    return GNSS_OK;
+}
+
+static int track_channel(const trk_ctx *t, const gnss_acquired *acq, int ch, double *cn0,
+                         int *countinx_out)
+{
+    const gnss_signal *sg = t->sg;
+    const gnss_file *f = t->file;
+    const int64_t S = sg->Sample;
+    const int sv1 = ch + 1;
+    const int64_t N1 = t->tr->msToProcessCT_1ms, N10 = t->tr->msToProcessCT_10ms;
+    const int64_t cd0 = acq->codedelay[ch];
+    int8_t ca[1023];
+    if (or_generate_ca(acq->sv[ch], ca)) return GNSS_EARG;
+    int8_t *buf = (int8_t *)malloc((size_t)(2 * (S * 10 + 4096)));
+    int64_t *dv = (int64_t *)calloc((size_t)(N1 + 32 + N10), sizeof(int64_t));
+    double *plog = (double *)calloc((size_t)(N1 + 1), sizeof(double));
+    chan_state c;
+    int st = GNSS_OK;
+
+    /* phase A (:22-171) */
+    chan_init(&c, t, acq, ch);
+    c.pos = (S - cd0 + 1 + f->skip * S) * f->dataPrecision * f->dataType; /* :63 */
+    for (int64_t i = 1; i <= N1 && st == GNSS_OK; i++)
+        st = trk_step(t, &c, ch, sv1, 1, 0, i, dv, i - 1, cn0, buf, ca, cd0, plog);
+    if (st) goto done;
+
+    /* bit transition (:178-213) on the phase-A P_i (length N1) */
+    int cx = or_bit_edge(plog, N1, &st);
+    if (st) goto done;
+    *countinx_out = cx;
+
+    /* phase B (:215-369): identical re-run for N1 + countinx steps */
+    chan_init(&c, t, acq, ch);
+    memset(dv, 0, sizeof(int64_t) * (size_t)(N1 + 32 + N10));
+    c.pos = (S - cd0 + 1 + f->skip * S) * f->dataPrecision * f->dataType; /* :258 */
+    int64_t Index = 0;
+    for (int64_t i = 1; i <= N1 + cx && st == GNSS_OK; i++) {
+        Index++;
+        st = trk_step(t, &c, ch, sv1, 1, 0, Index, dv, i - 1, cn0, buf, ca, cd0, NULL);
+    }
+    if (st) goto done;
+
+    /* phase C (:377-525) */
+    memset(dv, 0, sizeof(int64_t) * (size_t)(N1 + 32 + N10));
+    c.index_int = 0;
+    c.snrIndex = 1;
+    c.pos = (S - cd0 + 1 + (f->skip + N1 + cx) * S) * f->dataPrecision * f->dataType; /* :403 */
+    for (int64_t is = 1; is <= N10 / 10 && st == GNSS_OK; is++) {
+        Index += 10;
+        st = trk_step(t, &c, ch, sv1, 10, 1, Index, dv, is - 1, cn0, buf, ca, cd0, NULL);
+    }
+    if (!st && t->out->len) t->out->len[ch] = Index;
+done:
+    free(buf);
+    free(dv);
+    free(plog);
+    return st;
+}
+
+int or_tracking_ct(const gnss_file *file, const gnss_signal *sg, const gnss_track *tr,
+                   const gnss_acquired *acq, gnss_track_out *out, int nthreads)
+{
+    if (file->dataPrecision != 1 || file->dataType != 2) return GNSS_EARG;
+    trk_ctx t;
+    memset(&t, 0, sizeof(t));
+    t.file = file; t.sg = sg; t.tr = tr; t.out = out; t.nsv = acq->n;
+    t.fsize = file_size(file);
+    double taps3[3] = {-tr->CorrelatorSpacing, 0, tr->CorrelatorSpacing}; /* :24 */
+    if (tr->n_taps > 0) {
+        if (tr->n_taps > GNSS_MAX_TAPS || !tr->tap_offsets) return GNSS_EARG;
+        t.ntaps = tr->n_taps; t.taps = tr->tap_offsets;
+    } else {
+        t.ntaps = 3; t.taps = taps3;
+    }
+    t.iE = t.iP = t.iL = -1;
+    for (int s = 0; s < t.ntaps; s++) {
+        if (t.taps[s] == -tr->CorrelatorSpacing && t.iE < 0) t.iE = s;
+        if (t.taps[s] == 0 && t.iP < 0) t.iP = s;
+        if (t.taps[s] == tr->CorrelatorSpacing && t.iL < 0) t.iL = s;
+    }
+    if (t.iE < 0 || t.iP < 0 || t.iL < 0) return GNSS_EARG;
+    if (out->max_len < (int64_t)tr->msToProcessCT_1ms + 19 + tr->msToProcessCT_10ms) return GNSS_EARG;
+    or_calc_loop_coef(tr->DLLBW, tr->DLLDamp, tr->DLLGain, &t.tau1code, &t.tau2code); /* :26-27 */
+    or_calc_loop_coef(tr->PLLBW, tr->PLLDamp, tr->PLLGain, &t.tau1carr, &t.tau2carr);
+
+    int nch = tr->chan ? tr->n_chan : acq->n;
+    int nt = nthreads_of(nthreads);
+    int status = GNSS_OK;
+    if (out->CN0_Eph) memset(out->CN0_Eph, 0, sizeof(double) * (size_t)out->cn0_cap * (size_t)acq->n);
+#pragma omp parallel for num_threads(nt) schedule(dynamic)
+    for (int i = 0; i < nch; i++) {
+        int ch = tr->chan ? tr->chan[i] : i;
+        int cx = 0;
+        int st = track_channel(&t, acq, ch, out->CN0_Eph, &cx);
+        if (out->countinx) out->countinx[ch] = cx;
+#pragma omp critical
+        {
+            /* the reference aborts the whole call on the first failing channel;
+             * ENODATA dominates (TckResultCT = []), then the hard errors */
+            if (st && (status == GNSS_OK || st == GNSS_ENODATA)) status = st;
+        }
+    }
+    /* CN0_Eph rows = max rows written by any phase (quirk A.16) */
+    int rows = 0;
+    int r1 = tr->msToProcessCT_1ms / 20;
+    for (int i = 0; i < nch; i++) {
+        int ch = tr->chan ? tr->chan[i] : i;
+        int cx = out->countinx ? out->countinx[ch] : 0;
+        int rb = (int)((tr->msToProcessCT_1ms + cx) / 20);
+        if (rb > rows) rows = rb;
+    }
+    if (r1 > rows) rows = r1;
+    if (tr->msToProcessCT_10ms / 10 / 20 > rows) rows = tr->msToProcessCT_10ms / 10 / 20;
+    out->cn0_rows = rows;
+    return status;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Synthetic IF                                                 */
+/* ------------------------------------------------------------------------ */
+static inline uint64_t mix64(uint64_t z)
+{
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+void or_synth_if(const gnss_synth *cfg, uint64_t sample0, uint64_t nsamples, int8_t *dst,
+                 int nthreads)
+{
+    const double fL1 = 1575.42e6, fc = 1.023e6;
+    int8_t ca[GNSS_MAX_SV][1023];
+    double amp[GNSS_MAX_SV], crate[GNSS_MAX_SV], frate[GNSS_MAX_SV];
+    for (int s = 0; s < cfg->n_sv; s++) {
+        or_generate_ca(cfg->sv[s].prn, ca[s]);
+        double snr_lin = pow(10.0, cfg->sv[s].cn0_dbhz / 10.0);
+        amp[s] = sqrt(2.0 * cfg->noise_sigma * cfg->noise_sigma * snr_lin / cfg->Fs);
+        crate[s] = fc * (1.0 + cfg->sv[s].doppler_hz / fL1) / cfg->Fs;
+        frate[s] = (cfg->IF + cfg->sv[s].doppler_hz) / cfg->Fs;
+    }
+    int nt = nthreads_of(nthreads);
+#pragma omp parallel for num_threads(nt) schedule(static)
+    for (int64_t i = 0; i < (int64_t)nsamples; i++) {
+        uint64_t n = sample0 + (uint64_t)i;
+        double re = 0, im = 0;
+        for (int s = 0; s < cfg->n_sv; s++) {
+            const gnss_synth_sv *v = &cfg->sv[s];
+            double th = v->code_phase0 + (double)n * crate[s];
+            double chipf = floor(th);
+            int64_t chip = (int64_t)chipf % 1023;
+            if (chip < 0) chip += 1023;
+            double bitf = floor((th + v->bit_phase_chips) / 20460.0);
+            uint64_t bh = mix64(v->bit_seed ^ (uint64_t)(int64_t)bitf);
+            double D = (bh & 1) ? 1.0 : -1.0;
+            double ph = v->carr_phase0 - (double)n * frate[s]; /* received at -(IF+fd) */
+            ph -= floor(ph);
+            double a = amp[s] * D * ca[s][chip];
+            re += a * cos(TWO_PI * ph);
+            im += a * sin(TWO_PI * ph);
+        }
+        uint64_t h1 = mix64(cfg->seed ^ (n * 0xD1B54A32D192ED03ULL));
+        uint64_t h2 = mix64(h1 ^ 0x8CB92BA72F3D8DD7ULL);
+        double u1 = ((double)(h1 >> 11) + 1.0) * (1.0 / 9007199254740992.0);
+        double u2 = (double)(h2 >> 11) * (1.0 / 9007199254740992.0);
+        double r = sqrt(-2.0 * log(u1)) * cfg->noise_sigma;
+        double vi = rint(re + r * cos(TWO_PI * u2));
+        double vq = rint(im + r * sin(TWO_PI * u2));
+        if (vi > 127) vi = 127;
+        if (vi < -128) vi = -128;
+        if (vq > 127) vq = 127;
+        if (vq < -128) vq = -128;
+        dst[2 * i] = (int8_t)vi;
+        dst[2 * i + 1] = (int8_t)vq;
+    }
+}

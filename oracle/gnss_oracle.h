@@ -1,0 +1,81 @@
+/*
+ * gnss_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU fp64 restatement of the reference hot path (acquisition.m, trackingCT.m,
+ * generateCAcode.m, calcLoopCoef.m of KangWelly/Assignment-for-AAE6102_GNSS-SDR)
+ * used as the parity checker for the HIP product path. Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.
+ * The product library never links or calls it.
+ *
+ * Parity pinning: C/A codes against the IS-GPS-200
+ * first-10-chip table; the NCO / loop-filter arithmetic against the bit-exact
+ * replay of SDR_MATLAB-main/tckRstCT_10ms_Opensky.mat; output structure against
+ * countinx.mat / Acquired_Opensky_5000.mat. Correlator sums and FFT values
+ * against MATLAB itself are UNPINNED (the IF recordings are absent).
+ */
+#ifndef GNSS_ORACLE_H
+#define GNSS_ORACLE_H
+#include "../include/gnss_mi355x.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* generateCAcode.m:16-64 — 1023 chips of +-1 for PRN 1..51 */
+int  or_generate_ca(int prn, int8_t *out1023);
+/* calcLoopCoef.m:41-45 */
+void or_calc_loop_coef(double LBW, double zeta, double k, double *tau1, double *tau2);
+
+/* MATLAB colon a:d:b (MathWorks' published colonop algorithm). n = number of
+ * intervals (elements = n+1); n < 0 -> empty. */
+typedef struct or_colon { double a, d, c; int64_t n; } or_colon;
+void   or_colon_init(or_colon *r, double a, double d, double b);
+double or_colon_elem(const or_colon *r, int64_t k);
+int64_t or_colon_len(double a, double d, double b);
+void   or_colon_fill(double a, double d, double b, double *out, int64_t cap);
+
+/* Complex FFT (any length, mixed radix), fp64, interleaved re/im.
+ * dir = -1 forward (MATLAB fft), +1 inverse with 1/N scale (MATLAB ifft). */
+int or_fft(double *inout, int64_t n, int dir);
+
+/* MATLAB round (half away from zero), mod(a,b), rem(a,b) */
+double or_round(double x);
+double or_mod(double a, double b);
+
+/* acquisition.m:1-127 */
+int or_acquisition(const gnss_file *file, const gnss_signal *signal, const gnss_acq *acq,
+                   gnss_acquired *out, gnss_acq_diag *diag, int nthreads);
+
+/* trackingCT.m:1-530 (phase B literally re-runs phase A). */
+int or_tracking_ct(const gnss_file *file, const gnss_signal *signal, const gnss_track *track,
+                   const gnss_acquired *acquired, gnss_track_out *out, int nthreads);
+
+/* One trackingCT-style correlation step on host bytes (the body of
+ * trackingCT.m:96-118 / :429-449 without the negation): sums[2*ntaps] =
+ * (I, Q) per tap. Exposed for per-step parity tests. */
+void or_correlate_step(const int8_t *iq, int64_t numSample, double remChip, double codeFreq,
+                       double Fs, double carrierFreq, double remPhase, const int8_t *ca1023,
+                       int pdi, int ntaps, const double *taps, double *sums);
+
+/* trackingCT.m:178-213: returns countinx (0 if not found), *status = GNSS_EINDEX
+ * where MATLAB would raise an index error. */
+int or_bit_edge(const double *P_i, int64_t len, int *status);
+
+/* Sibling NCO replay (trackingCT_POS_updated.m:186-262 conventions) for the
+ * tckRstCT_10ms_Opensky.mat KAT: given the previous state, produce next
+ * numSample (ceil), remChip and remCarrPhase. */
+void or_nco_replay(double remChip, double codeFreq, double carrFreq, double remCarrPhase,
+                   double Fs, double codelength, int pdi, int use_ceil,
+                   int64_t *numSample, double *remChipNext, double *remCarrPhaseNext);
+/* trackingCT.m:136-150 loop filter, one update: returns the new output. */
+double or_loop_filter(double outLast, double discri, double discriLast, double tau1, double tau2,
+                      double T);
+
+/* Synthetic IF — CPU twin of the HIP generator. */
+void or_synth_if(const gnss_synth *cfg, uint64_t sample0, uint64_t nsamples, int8_t *dst,
+                 int nthreads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
