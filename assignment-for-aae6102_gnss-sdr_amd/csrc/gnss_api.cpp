@@ -15,6 +15,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <fcntl.h>
 #include <map>
 #include <string>
@@ -206,6 +207,19 @@ int fast_div_exact(double Fs, int64_t kmax)
     }
     cache[key] = ok;
     return ok;
+}
+
+void generate_ca(int prn, float* out);
+
+// C/A chips as 32 words of bits (bit i set <-> chip i is -1), read by the kernels
+// through lane shuffles
+void ca_bits(int prn, unsigned* out32)
+{
+    float f[1023];
+    generate_ca(prn, f);
+    for (int w = 0; w < 32; w++) out32[w] = 0;
+    for (int i = 0; i < 1023; i++)
+        if (f[i] < 0) out32[i >> 5] |= 1u << (i & 31);
 }
 
 // generateCAcode.m:16-64 (host copy; the oracle has its own independent one)
@@ -589,18 +603,28 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     P.buf_base = w.base;
     P.buf_len = w.len;
 
-    // geometry: 8 samples per lane, U lane-groups per thread
-    const int U1 = 1, U10 = 4;
-    auto bpc_for = [&](int pdi, int U) {
-        const double groups = (S * pdi * 1.01 + 64) / 8.0 + 2;
-        return (int)std::ceil(groups / (kTrkThreads * (double)U));
+    // geometry: SUB x 8 contiguous samples per lane, 256 lanes per block, bpc blocks per
+    // channel; SUB grows with the step's total work (more per-lane amortisation once the
+    // grid fills the chip)
+    auto sub_for = [&](int pdi) {
+        const double lanes8 = (double)nch * S * pdi / 8.0;
+        return lanes8 >= 4.0 * 256 * 2048 ? 4 : lanes8 >= 2.0 * 256 * 1024 ? 2 : 1;
     };
-    const int bpc1 = bpc_for(1, U1), bpc10 = bpc_for(10, U10);
-    if (bpc1 > kMaxBpc || bpc10 > kMaxBpc) return fail(ctx, GNSS_EARG, "Sample too large for the step geometry");
+    int sub1 = sub_for(1), sub10 = sub_for(10);
+    if (const char* fs = getenv("GNSS_FORCE_SUB")) {  // test hook: exercise every kernel variant
+        const int v = atoi(fs);
+        if (v == 1 || v == 2 || v == 4) sub1 = sub10 = v;
+    }
+    auto bpc_for = [&](int pdi, int sub) {
+        const double groups = (S * pdi * 1.01 + 64) / 8.0 + 2;
+        return (int)std::ceil(groups / ((double)kTrkThreads * sub));
+    };
+    const int bpc1 = bpc_for(1, sub1), bpc10 = bpc_for(10, sub10);
+    if (bpc10 > kMaxBpc) return fail(ctx, GNSS_EARG, "Sample too large for the step geometry");
 
     // device state
     std::vector<TrkChan> ch0((size_t)nch);
-    std::vector<float> cah((size_t)nch * 1023);
+    std::vector<unsigned> cab((size_t)nch * 32);
     for (int i = 0; i < nch; i++) {
         const int c = chans[i];
         TrkChan& t = ch0[i];
@@ -615,12 +639,13 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         t.prn = acq->sv[c];
         t.n1_target = N1;
         if (acq->sv[c] < 1 || acq->sv[c] > 51) return fail(ctx, GNSS_EARG, "bad PRN");
-        generate_ca(acq->sv[c], &cah[(size_t)i * 1023]);
+        ca_bits(acq->sv[c], &cab[(size_t)i * 32]);
     }
-    DevBuf d_chan, d_snap, d_ca, d_part, d_arrive, d_rec, d_taps, d_cn1, d_cn10, d_dv, d_pi;
+    DevBuf d_chan, d_snap, d_desc, d_ca, d_part, d_arrive, d_rec, d_taps, d_cn1, d_cn10, d_dv, d_pi;
     HIP_TRY(d_chan.alloc(sizeof(TrkChan) * nch));
     HIP_TRY(d_snap.alloc(sizeof(TrkChan) * nch));
-    HIP_TRY(d_ca.alloc(sizeof(float) * cah.size()));
+    HIP_TRY(d_desc.alloc(sizeof(StepDesc) * nch));
+    HIP_TRY(d_ca.alloc(sizeof(unsigned) * cab.size()));
     HIP_TRY(d_part.alloc(sizeof(double) * (size_t)nch * kMaxBpc * 2 * ntaps));
     HIP_TRY(d_arrive.alloc(sizeof(unsigned) * nch));
     HIP_TRY(d_rec.alloc(sizeof(double) * (size_t)nch * P.rec_cap * GNSS_NFIELDS));
@@ -630,7 +655,7 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     HIP_TRY(d_dv.alloc(sizeof(int64_t) * (size_t)nch * (P.rec_cap + 1)));
     HIP_TRY(d_pi.alloc(sizeof(double) * (size_t)nch * N1));
     HIP_TRY(hipMemcpyAsync(d_chan.p, ch0.data(), sizeof(TrkChan) * nch, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(hipMemcpyAsync(d_ca.p, cah.data(), sizeof(float) * cah.size(), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(d_ca.p, cab.data(), sizeof(unsigned) * cab.size(), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemsetAsync(d_arrive.p, 0, sizeof(unsigned) * nch, ctx->stream));
     HIP_TRY(hipMemsetAsync(d_cn1.p, 0, d_cn1.n, ctx->stream));
     HIP_TRY(hipMemsetAsync(d_cn10.p, 0, d_cn10.n, ctx->stream));
@@ -641,7 +666,8 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     B.iq = w.ptr;
     B.chan = d_chan.as<TrkChan>();
     B.snap = d_snap.as<TrkChan>();
-    B.ca = d_ca.as<float>();
+    B.desc = d_desc.as<StepDesc>();
+    B.ca_bits = d_ca.as<unsigned>();
     B.partial = d_part.as<double>();
     B.arrive = d_arrive.as<unsigned>();
     B.rec = d_rec.as<double>();
@@ -656,8 +682,8 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     // profiling mode every launch is bracketed by events instead.
     std::vector<hipEvent_t> pev;
     int64_t launches = 0;
-    auto run_steps = [&](int pdi, int phaseC, int count) -> int {
-        const int bpc = pdi == 1 ? bpc1 : bpc10, U = pdi == 1 ? U1 : U10;
+    auto run_steps = [&](int pdi, int count) -> int {
+        const int bpc = pdi == 1 ? bpc1 : bpc10, sub = pdi == 1 ? sub1 : sub10;
         if (count <= 0) return GNSS_OK;
         launches += count;
         ctx->timing.track_channel_samples += (int64_t)count * nch * (int64_t)S * pdi;
@@ -667,7 +693,7 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
                 HIP_TRY(hipEventCreate(&a));
                 HIP_TRY(hipEventCreate(&b));
                 HIP_TRY(hipEventRecord(a, ctx->stream));
-                HIP_TRY(launch_track_step(P, B, pdi, phaseC, bpc, U, ctx->stream));
+                HIP_TRY(launch_track_step(P, B, bpc, sub, ctx->stream));
                 HIP_TRY(hipEventRecord(b, ctx->stream));
                 pev.push_back(a);
                 pev.push_back(b);
@@ -679,7 +705,7 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
             StepGraph g;
             HIP_TRY(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
             for (int i = 0; i < K; i++) {
-                hipError_t e = launch_track_step(P, B, pdi, phaseC, bpc, U, ctx->stream);
+                hipError_t e = launch_track_step(P, B, bpc, sub, ctx->stream);
                 if (e != hipSuccess) {
                     hipGraph_t junk;
                     (void)hipStreamEndCapture(ctx->stream, &junk);
@@ -690,10 +716,10 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
             HIP_TRY(hipStreamEndCapture(ctx->stream, &g.graph));
             HIP_TRY(hipGraphInstantiate(&g.exec, g.graph, nullptr, nullptr, 0));
             for (int r = 0; r < count / K; r++) HIP_TRY(hipGraphLaunch(g.exec, ctx->stream));
-            for (int i = 0; i < count % K; i++) HIP_TRY(launch_track_step(P, B, pdi, phaseC, bpc, U, ctx->stream));
+            for (int i = 0; i < count % K; i++) HIP_TRY(launch_track_step(P, B, bpc, sub, ctx->stream));
             HIP_TRY(hipStreamSynchronize(ctx->stream));  // graph objects die with this scope
         } else {
-            for (int i = 0; i < count; i++) HIP_TRY(launch_track_step(P, B, pdi, phaseC, bpc, U, ctx->stream));
+            for (int i = 0; i < count; i++) HIP_TRY(launch_track_step(P, B, bpc, sub, ctx->stream));
         }
         return GNSS_OK;
     };
@@ -701,9 +727,10 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     Events e_all;
     HIP_TRY(hipEventRecord(e_all.a, ctx->stream));
     // phase A: steps 1..N1-1, snapshot (for countinx = -1), step N1, bit-edge search
-    if ((st = run_steps(1, 0, N1 - 1))) return st;
+    HIP_TRY(launch_track_prepare(P, B, 1, 0, ctx->stream));
+    if ((st = run_steps(1, N1 - 1))) return st;
     HIP_TRY(launch_track_snapshot(P, B, ctx->stream));
-    if ((st = run_steps(1, 0, 1))) return st;
+    if ((st = run_steps(1, 1))) return st;
     HIP_TRY(launch_track_bitedge(P, B, ctx->stream));
     std::vector<TrkChan> chh((size_t)nch);
     HIP_TRY(hipMemcpyAsync(chh.data(), d_chan.p, sizeof(TrkChan) * nch, hipMemcpyDeviceToHost, ctx->stream));
@@ -711,10 +738,10 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     int cxmax = 0;
     for (auto& t : chh) cxmax = std::max(cxmax, t.countinx);
     // phase B continues phase A up to 1000 + countinx (inactive channels skip)
-    if ((st = run_steps(1, 0, cxmax))) return st;
+    if ((st = run_steps(1, cxmax))) return st;
     HIP_TRY(launch_track_phase_c_init(P, B, file->skip, ctx->stream));
     // phase C
-    if ((st = run_steps(10, 1, n10))) return st;
+    if ((st = run_steps(10, n10))) return st;
     HIP_TRY(hipEventRecord(e_all.b, ctx->stream));
     HIP_TRY(hipEventSynchronize(e_all.b));
     ctx->timing.track_ms = e_all.ms();
@@ -841,27 +868,34 @@ int gnss_correlate_step(gnss_ctx* ctx, const gnss_file* file, const gnss_signal*
     c.n1_target = 1 << 30;
     c.sv1 = 1;
     c.prn = prn;
-    float ca[1023];
-    generate_ca(prn, ca);
-    const int U = pdi == 1 ? 1 : 4;
-    const int bpc = (int)std::ceil(((S * pdi * 1.01 + 64) / 8.0 + 2) / (kTrkThreads * (double)U));
-    DevBuf d_chan, d_ca, d_part, d_arrive, d_sums;
+    unsigned cab[32];
+    ca_bits(prn, cab);
+    int sub = 1;
+    if (const char* fs = getenv("GNSS_FORCE_SUB")) {
+        const int v = atoi(fs);
+        if (v == 1 || v == 2 || v == 4) sub = v;
+    }
+    const int bpc = (int)std::ceil(((S * pdi * 1.01 + 64) / 8.0 + 2) / ((double)kTrkThreads * sub));
+    DevBuf d_chan, d_desc, d_ca, d_part, d_arrive, d_sums;
     HIP_TRY(d_chan.alloc(sizeof(TrkChan)));
-    HIP_TRY(d_ca.alloc(sizeof(ca)));
+    HIP_TRY(d_desc.alloc(sizeof(StepDesc)));
+    HIP_TRY(d_ca.alloc(sizeof(cab)));
     HIP_TRY(d_part.alloc(sizeof(double) * kMaxBpc * 2 * n_taps));
     HIP_TRY(d_arrive.alloc(sizeof(unsigned)));
     HIP_TRY(d_sums.alloc(sizeof(double) * 2 * n_taps));
     HIP_TRY(hipMemcpyAsync(d_chan.p, &c, sizeof c, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(hipMemcpyAsync(d_ca.p, ca, sizeof ca, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(d_ca.p, cab, sizeof cab, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemsetAsync(d_arrive.p, 0, sizeof(unsigned), ctx->stream));
     TrkBuffers B{};
     B.iq = w.ptr;
     B.chan = d_chan.as<TrkChan>();
-    B.ca = d_ca.as<float>();
+    B.desc = d_desc.as<StepDesc>();
+    B.ca_bits = d_ca.as<unsigned>();
     B.partial = d_part.as<double>();
     B.arrive = d_arrive.as<unsigned>();
     B.dbg_sums = d_sums.as<double>();
-    HIP_TRY(launch_track_step(P, B, pdi, 0, bpc, U, ctx->stream));
+    HIP_TRY(launch_track_prepare(P, B, pdi, 0, ctx->stream));
+    HIP_TRY(launch_track_step(P, B, bpc, sub, ctx->stream));
     HIP_TRY(hipMemcpyAsync(sums_out, d_sums.p, sizeof(double) * 2 * n_taps, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipMemcpyAsync(&c, d_chan.p, sizeof c, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));

@@ -104,11 +104,22 @@ struct TrkParams {
     double taps[GNSS_MAX_TAPS];
 };
 
+// Everything the blocks of one step need, prepared by the previous step's last
+// block (or a prepare kernel at a phase start) so a block prologue is scalar loads.
+struct StepDesc {
+    int64_t n, delayValue, A, g_first, g_last, Index;
+    double remSample, d, inv_d, f, phi0, dhi, dlo, remChip_next, remPhase_next;
+    double rc[9], rs[9];                                // e^{i m delta}, m = 0..8
+    double tap_a[GNSS_MAX_TAPS], tap_c[GNSS_MAX_TAPS];  // colon start / end per tap
+    int32_t pdi, phaseC, bad, pad;
+};
+
 struct TrkBuffers {
     const int8_t* iq;         // IF bytes (dev)
     TrkChan* chan;            // [nch]
     TrkChan* snap;            // [nch] state after step msToProcessCT_1ms - 1
-    const float* ca;          // [nch][1023] +-1
+    StepDesc* desc;           // [nch] next step of each channel
+    const unsigned* ca_bits;  // [nch][32] C/A chips, bit set = -1
     double* partial;          // [nch][max_blocks][2*ntaps]
     unsigned int* arrive;     // [nch] arrival counters
     double* rec;              // [nch][rec_cap][GNSS_NFIELDS]
@@ -122,15 +133,17 @@ struct TrkBuffers {
 };
 
 // Launch wrappers (track.hip)
-hipError_t launch_track_step(const TrkParams& p, const TrkBuffers& b, int pdi, int phaseC,
-                             int blocks_per_chan, int groups_per_thread, hipStream_t s);
+hipError_t launch_track_step(const TrkParams& p, const TrkBuffers& b, int blocks_per_chan,
+                             int sub, hipStream_t s);
+hipError_t launch_track_prepare(const TrkParams& p, const TrkBuffers& b, int pdi, int phaseC,
+                                hipStream_t s);
 hipError_t launch_track_snapshot(const TrkParams& p, const TrkBuffers& b, hipStream_t s);
 hipError_t launch_track_bitedge(const TrkParams& p, const TrkBuffers& b, hipStream_t s);
 hipError_t launch_track_phase_c_init(const TrkParams& p, const TrkBuffers& b, int64_t skip,
                                      hipStream_t s);
 
 constexpr int kTrkThreads = 256;
-constexpr int kMaxBpc = 128;  // blocks per channel per step (LDS partial buffer)
+constexpr int kMaxBpc = 1024; // blocks per channel per step (partial buffer)
 
 // ----------------------------------------------------------------------------
 // Acquisition (acq.hip)
