@@ -1,0 +1,76 @@
+"""Multi-GPU sharding of the hot path (one process per GPU, torch.distributed).
+
+trackingCT.m's channels are independent (the `for svindex` loop re-initialises
+everything, trackingCT.m:22-528) and acquisition.m's PRNs too
+(acquisition.m:47-80), so the path shards with no per-step communication:
+
+  * acquisition: PRNs round-robin over ranks; each rank searches its PRNs on its
+    GPU; one all-gather of the fixed-size per-PRN records assembles the
+    reference's ascending-PRN Acquired struct on every rank;
+  * trackingCT: channels round-robin over ranks (the GLOBAL svindex/nsv are kept
+    for the linear-indexing quirk of trackingCT.m:161); per-channel series are
+    gathered to rank 0 (or all ranks) at the end.
+
+The collective backend is whatever the process group uses: "nccl" (= RCCL over
+xGMI on MI355X) on the GPU box, "gloo" for the CPU tests.
+"""
+from __future__ import annotations
+
+from types import SimpleNamespace
+
+import numpy as np
+
+
+def shard(n: int, world: int, rank: int) -> list[int]:
+    """Round-robin indices of `n` units owned by `rank`."""
+    return list(range(rank, n, world))
+
+
+def _all_gather_array(arr: np.ndarray, group=None, device=None) -> list[np.ndarray]:
+    import torch
+    import torch.distributed as dist
+    t = torch.from_numpy(np.ascontiguousarray(arr))
+    if device is not None:
+        t = t.to(device)
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(out, t, group=group)
+    return [o.cpu().numpy() for o in out]
+
+
+def gather_acquired(local, prns_local, world_prns, group=None, device=None):
+    """Merge per-rank Acquired structs into the reference's ascending-PRN struct.
+
+    local: Acquired of this rank's PRNs (sv, SNR, Doppler, codedelay, fineFreq).
+    Each rank packs a fixed-size record table (one row per PRN of the whole search,
+    NaN where not acquired here) and one all-gather merges them.
+    """
+    allp = sorted(world_prns)
+    tab = np.full((len(allp), 5), np.nan)
+    pos = {p: i for i, p in enumerate(allp)}
+    for k, sv in enumerate(local.sv):
+        tab[pos[int(sv)]] = [sv, local.SNR[k], local.Doppler[k], local.codedelay[k], local.fineFreq[k]]
+    parts = _all_gather_array(tab, group, device)
+    merged = np.full_like(tab, np.nan)
+    for t in parts:
+        have = ~np.isnan(t[:, 0])
+        merged[have] = t[have]
+    rows = merged[~np.isnan(merged[:, 0])]
+    return SimpleNamespace(sv=rows[:, 0].astype(np.int64), SNR=rows[:, 1], Doppler=rows[:, 2],
+                           codedelay=rows[:, 3].astype(np.int64), fineFreq=rows[:, 4])
+
+
+def gather_tracking(buf, nsv: int, group=None, device=None):
+    """All-gather the channel rows each rank filled in its TrackOutBuffers.
+
+    Every rank owns disjoint channels (rows of rec / taps / len / countinx /
+    CN0 columns); rows a rank did not track are zero there, so the element-wise
+    sum of the gathered buffers is the full result.
+    """
+    rec = sum(_all_gather_array(buf.rec, group, device))
+    length = sum(_all_gather_array(buf.len, group, device))
+    cx = sum(_all_gather_array(buf.countinx.astype(np.int64), group, device))
+    cn0 = sum(_all_gather_array(buf.CN0, group, device))
+    taps = sum(_all_gather_array(buf.taps, group, device)) if buf.taps is not None else None
+    rows = int(max(_all_gather_array(np.array([buf.c.cn0_rows]), group, device))[0])
+    return SimpleNamespace(rec=rec, len=length, countinx=cx, CN0=cn0[:rows], taps=taps,
+                           cn0_rows=rows)

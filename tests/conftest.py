@@ -1,0 +1,60 @@
+"""Shared fixtures. `-m gpu` tests need an MI355X; everything else runs on CPU."""
+import importlib
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device)")
+
+
+@pytest.fixture(scope="session")
+def pkg():
+    return importlib.import_module("assignment-for-aae6102_gnss-sdr_amd")
+
+
+@pytest.fixture(scope="session")
+def po():
+    import pyoracle
+    pyoracle.load()
+    return pyoracle
+
+
+@pytest.fixture(scope="session")
+def ctx(pkg):
+    c = pkg.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="session")
+def opensky_short(pkg, po):
+    """A 3-s synthetic Opensky record (skip 5 ms) shared by the parity tests."""
+    skip = 5
+    cfg = pkg.synth.opensky(skip_ms=skip)
+    n_ms = skip + 1000 + 19 + 1000 + 4
+    data = po.synth_if(cfg, 0, n_ms * 58000)
+    return skip, cfg, data
+
+
+def params(pkg, skip, data):
+    file, signal, acq, track, _, _ = pkg.initParameters()
+    file.skip, file.data = skip, data
+    return file, signal, acq, track
+
+
+def acquired_of(svs, codedelay, finefreq):
+    from types import SimpleNamespace
+    n = len(svs)
+    return SimpleNamespace(sv=np.array(svs), SNR=np.full(n, 20.0), Doppler=np.zeros(n),
+                           codedelay=np.array(codedelay), fineFreq=np.array(finefreq, dtype=float))

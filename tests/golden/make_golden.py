@@ -1,0 +1,80 @@
+"""Generate the synthetic golden vectors under tests/golden/ (run in the build
+container; the outputs are committed and read by CPU and GPU tests).
+
+The reference's own IF recordings are absent, so these vectors are produced by the
+CPU oracle (oracle/, fp64 restatement of acquisition.m / trackingCT.m) on seeded
+synthetic IF (assignment-for-aae6102_gnss-sdr_amd/synth.py), and co-signed where
+feasible by the independent numpy twin (tests/numpy_twin.py).
+"""
+import importlib
+import os
+import sys
+from types import SimpleNamespace
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
+import numpy_twin as tw  # noqa: E402
+import pyoracle as po  # noqa: E402
+
+pkg = importlib.import_module("assignment-for-aae6102_gnss-sdr_amd")
+
+SKIP = 2
+N1, N10 = 100, 60
+
+
+def record():
+    cfg = pkg.synth.opensky(skip_ms=SKIP)
+    return po.synth_if(cfg, 0, (SKIP + N1 + 19 + N10 + 4) * 58000)
+
+
+def main():
+    data = record()
+    file, signal, acq, track, _, _ = pkg.initParameters()
+    file.skip, file.data = SKIP, data
+
+    # trackingCT, 2 channels, 100 x 1 ms + 6 x 10 ms
+    A = SimpleNamespace(sv=np.array([3, 16]), SNR=np.array([20.0, 26.0]),
+                        Doppler=np.array([1000.0, 0.0]), codedelay=np.array([3683, 26051]),
+                        fineFreq=np.array([4580990.0, 4579695.0]))
+    track.msToProcessCT_1ms, track.msToProcessCT_10ms = N1, N10
+    buf = po.trackingCT(file, signal, track, A, raw=True)
+    assert buf.status == 0
+    L = int(buf.len.max())
+    np.savez_compressed(os.path.join(HERE, "golden_track_small.npz"), rec=buf.rec[:, :, :L],
+                        len=buf.len, countinx=buf.countinx, CN0=buf.CN0[: buf.c.cn0_rows],
+                        sv=A.sv, codedelay=A.codedelay, fineFreq=A.fineFreq, skip=SKIP, N1=N1, N10=N10)
+
+    # single correlation steps at fixed NCO states (co-signed by the numpy twin)
+    rng = np.random.default_rng(2024)
+    states, sums = [], []
+    for k in range(6):
+        pdi = 10 if k % 3 == 2 else 1
+        prn = [3, 16, 22][k % 3]
+        rc, cf = float(rng.uniform(-0.009, 0.009)), 1.023e6 + float(rng.normal(0, 3))
+        f, ph = 4.58e6 + float(rng.uniform(-4000, 4000)), float(rng.uniform(0, 2 * np.pi))
+        pos = 2 * int(rng.integers(0, 40 * 58000))
+        n = int(np.round((1023.0 * pdi - rc) / (cf / 58e6)))
+        taps = po.colon(-0.5, 0.1, 0.5) if k % 2 else np.array([-0.5, 0.0, 0.5])
+        s = po.correlate_step(data[pos:pos + 2 * n], n, rc, cf, 58e6, f, ph, po.generate_ca(prn),
+                              pdi, taps)
+        t = tw.correlate_step(data[pos:pos + 2 * n], n, rc, cf, 58e6, f, ph, po.generate_ca(prn), taps)
+        assert np.max(np.abs(s - t)) / np.sqrt(np.mean(t ** 2)) < 1e-12
+        states.append([prn, pdi, rc, cf, f, ph, pos, n, len(taps)])
+        sums.append(np.pad(s, (0, 22 - len(s))))
+    np.savez_compressed(os.path.join(HERE, "golden_steps.npz"), states=np.array(states),
+                        sums=np.array(sums))
+
+    # acquisition, PRNs 3 / 7 / 16, 21 bins (+-5 kHz), 4 ms, fine FFT over L = 10 ms
+    acq.freqMin, acq.freqNum, acq.datalen = -5000, 21, 4
+    Aq, d = po.acquisition(file, signal, acq, prn_list=[3, 7, 16], diag=True)
+    np.savez_compressed(os.path.join(HERE, "golden_acq_small.npz"), prn=d.prn, SNR=d.SNR,
+                        fbin=d.fbin, codePhase=d.codePhase, sv=Aq.sv, codedelay=Aq.codedelay,
+                        Doppler=Aq.Doppler, fineFreq=Aq.fineFreq)
+    print("golden vectors written:", Aq.sv, Aq.codedelay, Aq.fineFreq - 4.58e6, buf.countinx)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,90 @@
+"""GPU parity for acquisition.m (through the C-ABI) against the CPU oracle:
+acquired PRN set, Doppler bin, code-phase index and fine frequency bit-exact;
+SNR within 1e-3 dB (fp32 FFT correlation on the GPU vs fp64 in the oracle;
+every case also reports the detector's peak margin)."""
+import os
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, params
+
+pytestmark = pytest.mark.gpu
+
+
+def compare(g, gd, r, rd):
+    assert np.array_equal(gd.prn, rd.prn)
+    assert np.array_equal(gd.fbin, rd.fbin), (gd.fbin, rd.fbin)
+    assert np.array_equal(gd.codePhase, rd.codePhase)
+    assert np.max(np.abs(gd.SNR - rd.SNR)) < 1e-3
+    assert np.array_equal(g.sv, r.sv)
+    assert np.array_equal(g.codedelay, r.codedelay)
+    assert np.array_equal(g.Doppler, r.Doppler)
+    assert np.array_equal(g.fineFreq, r.fineFreq)
+
+
+def test_config1_prn3_acquisition(pkg, po, ctx, opensky_short):
+    """BASELINE config 1: PRN 3, +-5 kHz / 500 Hz (21 bins), 20 x 1 ms, fine FFT L = 10."""
+    skip, cfg, data = opensky_short
+    file, signal, acq, track = params(pkg, skip, data)
+    acq.freqMin, acq.freqNum, acq.freqStep, acq.datalen, acq.L = -5000, 21, 500, 20, 10
+    g, gd = pkg.acquisition(file, signal, acq, ctx=ctx, prn_list=[3], diag=True)
+    r, rd = po.acquisition(file, signal, acq, prn_list=[3], diag=True)
+    compare(g, gd, r, rd)
+    assert list(g.sv) == [3]
+    # fine frequency on the 5 Hz grid (Fs / (L*S*datalen)), near the true 990 Hz
+    assert abs(g.fineFreq[0] - 4.58e6 - 990) <= 5
+
+
+def test_32prn_acquisition(pkg, po, ctx, opensky_short):
+    """BASELINE config 2 grid (32 PRNs, +-7 kHz / 500 Hz); 8 ms non-coherent to bound
+    the oracle's CPU time."""
+    skip, cfg, data = opensky_short
+    file, signal, acq, track = params(pkg, skip, data)
+    acq.freqMin, acq.freqNum, acq.freqStep, acq.datalen, acq.L = -7000, 29, 500, 8, 10
+    g, gd = pkg.acquisition(file, signal, acq, ctx=ctx, diag=True)
+    r, rd = po.acquisition(file, signal, acq, diag=True)
+    compare(g, gd, r, rd)
+    assert set(pkg.synth.OPENSKY_SV) <= set(g.sv)
+
+
+def test_no_satellites_acquired(pkg, po, ctx):
+    """acquisition.m:84-85: nothing above 12 dB -> empty Acquired."""
+    cfg = pkg.synth.scenario([], [], [], [], skip_ms=0)
+    data = po.synth_if(cfg, 0, 30 * 58000)
+    file, signal, acq, track = params(pkg, 0, data)
+    acq.freqMin, acq.freqNum, acq.datalen = -3000, 13, 20
+    g = pkg.acquisition(file, signal, acq, ctx=ctx, prn_list=[1, 2, 3, 4])
+    assert len(g.sv) == 0 and len(g.fineFreq) == 0
+
+
+def test_urban_parameters(pkg, po, ctx):
+    """BASELINE config 4 shape: IF = 0, Fs = 26 MHz (assumed), +-10 kHz / 250 Hz (81 bins),
+    10 ms; PRN subset to bound the oracle's CPU time."""
+    skip = 3
+    cfg = pkg.synth.urban(skip_ms=skip)
+    S = 26000
+    data = po.synth_if(cfg, 0, (skip + 14) * S)
+    file = SimpleNamespace(skip=skip, dataType=2, dataPrecision=1, data=data, fileRoute=None, dev=None)
+    signal = SimpleNamespace(IF=0.0, Fs=26e6, codeFreqBasis=1.023e6, ms=1e-3, Sample=S,
+                             codelength=1023.0)
+    acq = SimpleNamespace(freqNum=81, freqMin=-10000, freqStep=250, datalen=10, L=10)
+    prns = [1, 3, 5, 7]
+    g, gd = pkg.acquisition(file, signal, acq, ctx=ctx, prn_list=prns, diag=True)
+    r, rd = po.acquisition(file, signal, acq, prn_list=prns, diag=True)
+    compare(g, gd, r, rd)
+    assert {1, 3, 7} <= set(g.sv)
+
+
+def test_acquisition_matches_golden_vectors(pkg, po, ctx):
+    from test_golden_oracle import golden_record
+    z = np.load(os.path.join(GOLDEN, "golden_acq_small.npz"))
+    g, data = golden_record(pkg, po)
+    file, signal, acq, track = params(pkg, int(g["skip"]), data)
+    acq.freqMin, acq.freqNum, acq.datalen = -5000, 21, 4
+    A, d = pkg.acquisition(file, signal, acq, ctx=ctx, prn_list=[3, 7, 16], diag=True)
+    assert np.array_equal(d.fbin, z["fbin"]) and np.array_equal(d.codePhase, z["codePhase"])
+    assert np.max(np.abs(d.SNR - z["SNR"])) < 1e-3
+    assert np.array_equal(A.sv, z["sv"]) and np.array_equal(A.codedelay, z["codedelay"])
+    assert np.array_equal(A.fineFreq, z["fineFreq"])
