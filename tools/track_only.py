@@ -1,0 +1,29 @@
+"""Tracking-only driver for profiling: cfg3-shape (8 channels) with a short 1-ms
+phase so the 10-ms correlator kernel dominates. Args: N1 N10 [ntaps] [nch]."""
+import importlib, os, sys, time
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+pkg = importlib.import_module("assignment-for-aae6102_gnss-sdr_amd")
+N1 = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+N10 = int(sys.argv[2]) if len(sys.argv) > 2 else 4000
+ntaps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+nch = int(sys.argv[4]) if len(sys.argv) > 4 else 8
+ctx = pkg.Context(0)
+file, signal, acq, track, _, _ = pkg.initParameters()
+skip = 0
+cfg = pkg.synth.opensky(skip_ms=skip) if nch <= 8 else pkg.synth.all_prn(nch, skip_ms=skip)
+dev = pkg.DeviceRecord(ctx, (skip + N1 + 19 + N10 + 3) * 58000 * 2)
+pkg.synth.generate_device(ctx, cfg, dev)
+file.skip, file.dev = skip, dev
+from types import SimpleNamespace
+S = 58000
+cds = [int(round((cfg.sv[i].code_phase0 * -1) % 1023 / (1.023e6 / 58e6))) % S for i in range(cfg.n_sv)]
+A = SimpleNamespace(sv=np.array([cfg.sv[i].prn for i in range(nch)]), SNR=np.zeros(nch), Doppler=np.zeros(nch),
+                    codedelay=np.array(cds[:nch]), fineFreq=np.array([4.58e6 + cfg.sv[i].doppler_hz for i in range(nch)]))
+track.msToProcessCT_1ms, track.msToProcessCT_10ms = N1, N10
+taps = None if ntaps == 3 else np.array([-0.5, -0.4, -0.3, -0.2, -0.1, 0.0, 0.1, 0.2, 0.3, 0.4, 0.5])
+for it in range(2):
+    t = time.perf_counter()
+    buf = pkg.trackingCT(file, signal, track, A, ctx=ctx, taps=taps, raw=True)
+    print("track wall", time.perf_counter() - t, ctx.timing(), flush=True)
