@@ -606,15 +606,23 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     // geometry: SUB x 8 contiguous samples per lane, 256 lanes per block, bpc blocks per
     // channel; SUB grows with the step's total work (more per-lane amortisation once the
     // grid fills the chip)
+    // a lane's 8*SUB samples may hold at most one chip boundary per tap: 8*SUB*codeFreq/Fs
+    // < 1 with margin for the DLL's excursions (the kernel flags a violating step)
+    const double cps_max = 1.1 * sg->codeFreqBasis / sg->Fs;
+    auto sub_ok = [&](int sub) { return 8.0 * sub * cps_max < 1.0 && (sub == 1 || !P.exact_div); };
+    // (measured on MI355X, 8 channels: 1-ms steps are latency-bound -> the shortest lanes;
+    // 10-ms steps -> the longest, fewest blocks)
     auto sub_for = [&](int pdi) {
-        const double lanes8 = (double)nch * S * pdi / 8.0;
-        return lanes8 >= 4.0 * 256 * 2048 ? 4 : lanes8 >= 2.0 * 256 * 1024 ? 2 : 1;
+        int sub = pdi >= 10 ? 4 : 1;
+        while (sub > 1 && !sub_ok(sub)) sub /= 2;
+        return sub;
     };
     int sub1 = sub_for(1), sub10 = sub_for(10);
     if (const char* fs = getenv("GNSS_FORCE_SUB")) {  // test hook: exercise every kernel variant
         const int v = atoi(fs);
-        if (v == 1 || v == 2 || v == 4) sub1 = sub10 = v;
+        if ((v == 1 || v == 2 || v == 4) && sub_ok(v)) sub1 = sub10 = v;
     }
+    if (const char* pr = getenv("GNSS_PROBE")) P.probe = atoi(pr);
     auto bpc_for = [&](int pdi, int sub) {
         const double groups = (S * pdi * 1.01 + 64) / 8.0 + 2;
         return (int)std::ceil(groups / ((double)kTrkThreads * sub));
@@ -647,7 +655,8 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     HIP_TRY(d_desc.alloc(sizeof(StepDesc) * nch));
     HIP_TRY(d_ca.alloc(sizeof(unsigned) * cab.size()));
     HIP_TRY(d_part.alloc(sizeof(double) * (size_t)nch * kMaxBpc * 2 * ntaps));
-    HIP_TRY(d_arrive.alloc(sizeof(unsigned) * nch));
+    const size_t arrive_bytes = sizeof(unsigned) * kArrivePerChan * kArriveStride * nch;
+    HIP_TRY(d_arrive.alloc(arrive_bytes));
     HIP_TRY(d_rec.alloc(sizeof(double) * (size_t)nch * P.rec_cap * GNSS_NFIELDS));
     if (out->taps) HIP_TRY(d_taps.alloc(sizeof(double) * (size_t)nch * P.rec_cap * 2 * ntaps));
     HIP_TRY(d_cn1.alloc(sizeof(double) * (size_t)nch * P.cn0_cap));
@@ -656,7 +665,7 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     HIP_TRY(d_pi.alloc(sizeof(double) * (size_t)nch * N1));
     HIP_TRY(hipMemcpyAsync(d_chan.p, ch0.data(), sizeof(TrkChan) * nch, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(d_ca.p, cab.data(), sizeof(unsigned) * cab.size(), hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(hipMemsetAsync(d_arrive.p, 0, sizeof(unsigned) * nch, ctx->stream));
+    HIP_TRY(hipMemsetAsync(d_arrive.p, 0, arrive_bytes, ctx->stream));
     HIP_TRY(hipMemsetAsync(d_cn1.p, 0, d_cn1.n, ctx->stream));
     HIP_TRY(hipMemsetAsync(d_cn10.p, 0, d_cn10.n, ctx->stream));
     HIP_TRY(hipMemsetAsync(d_dv.p, 0, d_dv.n, ctx->stream));
@@ -677,6 +686,14 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     B.dvpre = d_dv.as<int64_t>();
     B.p_i_1ms = d_pi.as<double>();
     B.n1 = N1;
+
+    DevBuf d_stamps;  // timing probe: per-launch wall-clock stamps of channel 0
+    const char* stamp_path = getenv("GNSS_STAMPS");
+    if (stamp_path) {
+        HIP_TRY(d_stamps.alloc(sizeof(unsigned long long) * ((size_t)kStampSlots * (8 + 3 * kMaxBpc) + 1)));
+        HIP_TRY(hipMemsetAsync(d_stamps.p, 0, d_stamps.n, ctx->stream));
+        B.stamps = d_stamps.as<unsigned long long>();
+    }
 
     // step launches: K-launch graphs replayed (no host launch cost per step); in
     // profiling mode every launch is bracketed by events instead.
@@ -754,6 +771,14 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     }
     for (auto e : pev) (void)hipEventDestroy(e);
     ctx->timing.track_kernel_ms = ksum;
+    if (stamp_path) {
+        std::vector<unsigned long long> st(d_stamps.n / sizeof(unsigned long long));
+        HIP_TRY(hipMemcpy(st.data(), d_stamps.p, d_stamps.n, hipMemcpyDeviceToHost));
+        if (FILE* fp = fopen(stamp_path, "wb")) {
+            fwrite(st.data(), sizeof(unsigned long long), st.size(), fp);
+            fclose(fp);
+        }
+    }
 
     // results
     HIP_TRY(hipMemcpyAsync(chh.data(), d_chan.p, sizeof(TrkChan) * nch, hipMemcpyDeviceToHost, ctx->stream));
@@ -873,7 +898,7 @@ int gnss_correlate_step(gnss_ctx* ctx, const gnss_file* file, const gnss_signal*
     int sub = 1;
     if (const char* fs = getenv("GNSS_FORCE_SUB")) {
         const int v = atoi(fs);
-        if (v == 1 || v == 2 || v == 4) sub = v;
+        if ((v == 2 || v == 4) && !P.exact_div && 8.0 * v * codeFreq / sg->Fs < 1.0) sub = v;
     }
     const int bpc = (int)std::ceil(((S * pdi * 1.01 + 64) / 8.0 + 2) / ((double)kTrkThreads * sub));
     DevBuf d_chan, d_desc, d_ca, d_part, d_arrive, d_sums;
@@ -881,11 +906,11 @@ int gnss_correlate_step(gnss_ctx* ctx, const gnss_file* file, const gnss_signal*
     HIP_TRY(d_desc.alloc(sizeof(StepDesc)));
     HIP_TRY(d_ca.alloc(sizeof(cab)));
     HIP_TRY(d_part.alloc(sizeof(double) * kMaxBpc * 2 * n_taps));
-    HIP_TRY(d_arrive.alloc(sizeof(unsigned)));
+    HIP_TRY(d_arrive.alloc(sizeof(unsigned) * kArrivePerChan * kArriveStride));
     HIP_TRY(d_sums.alloc(sizeof(double) * 2 * n_taps));
     HIP_TRY(hipMemcpyAsync(d_chan.p, &c, sizeof c, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(d_ca.p, cab, sizeof cab, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(hipMemsetAsync(d_arrive.p, 0, sizeof(unsigned), ctx->stream));
+    HIP_TRY(hipMemsetAsync(d_arrive.p, 0, sizeof(unsigned) * kArrivePerChan * kArriveStride, ctx->stream));
     TrkBuffers B{};
     B.iq = w.ptr;
     B.chan = d_chan.as<TrkChan>();

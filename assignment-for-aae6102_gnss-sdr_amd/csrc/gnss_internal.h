@@ -45,6 +45,25 @@ GNSS_HD Colon colon_make(double a, double d, double b)
     return r;
 }
 
+// colon_make when the caller knows the interval count to expect (b = a + hint*d up to
+// rounding): if fl(b - a) is within 0.4*d of hint*d, round(fl(b - a)/d) == hint
+// and the division is skipped; otherwise the general construction runs.
+GNSS_HD Colon colon_make_hint(double a, double d, double b, int64_t hint)
+{
+    const double X = b - a;
+    const double r = fma(-(double)hint, d, X);
+    if (!(d > 0) || !(fabs(r) < 0.4 * d) || a == floor(a)) return colon_make(a, d, b);
+    Colon o{a, d, b, hint};
+    const double tol = 2.0 * 2.220446049250313e-16 * fmax(fabs(a), fabs(b));
+    double n = (double)hint;
+    if (a + n * d - b > tol) n = n - 1;
+    double c = a + n * d;
+    if (c - b > -tol) c = b;
+    o.c = c;
+    o.n = (int64_t)n;
+    return o;
+}
+
 GNSS_HD double colon_elem(const Colon& r, int64_t k)
 {
     if (2 * k == r.n) return (r.a + r.c) / 2;
@@ -57,6 +76,13 @@ GNSS_HD int ca_index(int64_t chip)
 {
     int64_t r = (chip + 1022) % 1023;
     return (int)(r < 0 ? r + 1023 : r);
+}
+
+// The same for chip >= -1022 (every chip a step can address, ceil(t) in [-1, 1023*pdi+1]):
+// one 32-bit unsigned division by a constant.
+GNSS_HD unsigned ca_index32(int chip)
+{
+    return (unsigned)(chip + 1022) % 1023u;
 }
 
 constexpr double kTwoPi = 2.0 * 3.14159265358979323846;  // MATLAB 2*pi
@@ -101,15 +127,21 @@ struct TrkParams {
     int32_t nch;              // channels in this launch set
     int32_t rec_cap;          // compact record slots per channel
     int32_t cn0_cap;          // rows per channel per phase array
+    int32_t probe;            // timing probe (GNSS_PROBE): 1 = skip the scalar loop update
     double taps[GNSS_MAX_TAPS];
 };
+
+// Samples per lane of the step kernel: 8 * SUB, SUB <= 4.
+constexpr int kLaneMax = 32;
 
 // Everything the blocks of one step need, prepared by the previous step's last
 // block (or a prepare kernel at a phase start) so a block prologue is scalar loads.
 struct StepDesc {
     int64_t n, delayValue, A, g_first, g_last, Index;
     double remSample, d, inv_d, f, phi0, dhi, dlo, remChip_next, remPhase_next;
-    double rc[9], rs[9];                                // e^{i m delta}, m = 0..8
+    // carrier rotation of lane sample m against the lane's first sample:
+    // phi[m] = RN(m*dhi + m*dlo) ~ m * 2*pi*f/Fs, (rc, rs)[m] = (cos, sin)(phi[m])
+    double phi[kLaneMax], rc[kLaneMax], rs[kLaneMax];
     double tap_a[GNSS_MAX_TAPS], tap_c[GNSS_MAX_TAPS];  // colon start / end per tap
     int32_t pdi, phaseC, bad, pad;
 };
@@ -121,7 +153,7 @@ struct TrkBuffers {
     StepDesc* desc;           // [nch] next step of each channel
     const unsigned* ca_bits;  // [nch][32] C/A chips, bit set = -1
     double* partial;          // [nch][max_blocks][2*ntaps]
-    unsigned int* arrive;     // [nch] arrival counters
+    unsigned int* arrive;     // [nch][kArrivePerChan][kArriveStride] arrival counters
     double* rec;              // [nch][rec_cap][GNSS_NFIELDS]
     double* taps_rec;         // [nch][rec_cap][2*ntaps] or null
     double* cn0_1;            // [nch][cn0_cap]
@@ -129,6 +161,7 @@ struct TrkBuffers {
     int64_t* dvpre;           // [nch][rec_cap+1] delayValue prefix sums of the current phase
     double* p_i_1ms;          // [nch][n1] phase-A P_i for the bit-edge search
     double* dbg_sums;         // if set: last arriver stores the raw sums [nch][2*ntaps], no finalize
+    unsigned long long* stamps;  // timing probe (GNSS_STAMPS): [kStampSlots][8] wall clock + counter
     int32_t n1;               // msToProcessCT_1ms
 };
 
@@ -143,6 +176,9 @@ hipError_t launch_track_phase_c_init(const TrkParams& p, const TrkBuffers& b, in
                                      hipStream_t s);
 
 constexpr int kTrkThreads = 256;
+constexpr int kArriveStride = 64;   // words: one 256-B line per counter
+constexpr int kArrivePerChan = 9;   // 8 XCD-group counters + the channel counter
+constexpr int kStampSlots = 2200;
 constexpr int kMaxBpc = 1024; // blocks per channel per step (partial buffer)
 
 // ----------------------------------------------------------------------------

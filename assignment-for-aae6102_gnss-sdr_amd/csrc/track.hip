@@ -7,7 +7,7 @@
 //   * the previous step's last block prepares a StepDesc (numSample, colon
 //     ranges per tap, carrier constants, end-of-step NCO values) so a block's
 //     prologue is a handful of scalar loads;
-//   * every lane owns 8 consecutive samples (one 16-B load of int8 I/Q issued
+//   * every lane owns 8*SUB consecutive samples (16-B loads of int8 I/Q issued
 //     first thing), generates the E/P/L (or ACF) replica from exact fp64 colon
 //     arithmetic and the carrier from the reference's own fp64 Wave rounding,
 //     and accumulates fp64 partial correlations;
@@ -22,11 +22,21 @@ namespace gnss {
 
 namespace {
 
-__device__ __forceinline__ double wave_sum(double v)
+// Timing probe (GNSS_STAMPS): per-launch wall-clock stamps (100 MHz) of channel 0,
+// row = [8 tail marks][kMaxBpc block starts][kMaxBpc computed][kMaxBpc tickets]; plain
+// stores, one writer per word (atomics on shared words would queue behind each other).
+constexpr int kStampRow = 8 + 3 * kMaxBpc;
+
+__device__ __forceinline__ unsigned long long* stamp_row(const TrkBuffers& b)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    const unsigned long long cnt = __hip_atomic_load(b.stamps + (size_t)kStampSlots * kStampRow,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return b.stamps + (cnt % kStampSlots) * kStampRow;
+}
+
+__device__ __forceinline__ void stamp_max(unsigned long long* row, int k, unsigned long long v)
+{
+    row[k] = v;
 }
 
 __device__ __forceinline__ double ld_sc1(const double* ptr)
@@ -41,67 +51,129 @@ __device__ __forceinline__ void st_sc1(double* ptr, double v)
 
 // CarrTime = k/Fs (trackingCT.m:104) as the IEEE quotient: one FMA-corrected
 // reciprocal (host-verified exact for this Fs and k range) or a true division.
-__device__ __forceinline__ double carr_time(double kd, double Fs, double rFs, bool exact_div)
+template <bool DIVIDE>
+__device__ __forceinline__ double carr_time(double kd, double Fs, double rFs)
 {
-    if (exact_div) return kd / Fs;
+    if constexpr (DIVIDE) return kd / Fs;
     const double q = kd * rFs;
     const double e = __builtin_fma(-q, Fs, kd);
     return __builtin_fma(e, rFs, q);
 }
 
 // Wave(k) = (2*pi*(carrierFreq .* CarrTime)) + remPhase with the reference's roundings
-__device__ __forceinline__ double wave_at(double kd, double f, double phi0, double Fs, double rFs,
-                                          bool exact_div)
+template <bool DIVIDE>
+__device__ __forceinline__ double wave_at(double kd, double f, double phi0, double Fs, double rFs)
 {
-    const double t = carr_time(kd, Fs, rFs, exact_div);
+    const double t = carr_time<DIVIDE>(kd, Fs, rFs);
     const double x = f * t;
     const double y = kTwoPi * x;
     return y + phi0;
 }
 
-// Prepare the descriptor of the step that follows state `c` (trackingCT.m:79-107 /
-// :411-441), executed by the 64 lanes of one wave: lanes < ntaps build the colon of
-// their tap, lanes < 8 the carrier rotations e^{i m delta}, lane 0 the scalars.
-__device__ void prepare_desc(const TrkParams& p, const TrkChan& c, int pdi, int phaseC, int lane,
-                             StepDesc* d)
+// The NCO state a step is prepared from.
+struct NcoState {
+    double remChip, remPhase, codeFreq, carrierFreq;
+    int64_t numSample, pos, Index;
+};
+
+__device__ __forceinline__ NcoState nco_of(const TrkChan& c)
 {
-    const double cps = c.codeFreq / p.Fs;
-    int64_t n, dv;
-    double remSample;
-    if (phaseC) {
-        dv = c.numSample - (int64_t)(p.S * pdi);                      // :411
-        remSample = (p.codelength * pdi - c.remChip) / cps;            // :414
-        n = (int64_t)round((p.codelength * pdi - c.remChip) / cps);    // :415
+    return NcoState{c.remChip, c.remPhase, c.codeFreq, c.carrierFreq, c.numSample, c.pos, c.Index};
+}
+
+// rem(x, 2*pi) (trackingCT.m:106), exact like C fmod: |x| < 2^52 * 2*pi, the quotient
+// is exact or one too large, and x - q*2*pi is then representable (a multiple of 2^-50
+// below 8 in magnitude), so the FMA and the correction are exact.
+__device__ __forceinline__ double rem_2pi(double x)
+{
+    const double q = trunc(x / kTwoPi);
+    double r = __builtin_fma(-q, kTwoPi, x);
+    if (x >= 0) {
+        if (r < 0) r += kTwoPi;
     } else {
-        remSample = (p.codelength - c.remChip) / cps;                  // :79
-        n = (int64_t)round((p.codelength * pdi - c.remChip) / cps);    // :80
-        dv = n - (int64_t)(p.S * pdi);                                 // :82
+        if (r > 0) r -= kTwoPi;
+    }
+    return r;
+}
+
+// numSample / remSample / delayValue of the step that follows state `c`
+// (trackingCT.m:79-82 / :411-415).
+struct StepSize {
+    double cps, remSample;
+    int64_t n, dv;
+};
+
+__device__ __forceinline__ StepSize step_size(const TrkParams& p, const NcoState& c, int pdi, int phaseC)
+{
+    StepSize z;
+    z.cps = c.codeFreq / p.Fs;
+    if (phaseC) {
+        z.dv = c.numSample - (int64_t)(p.S * pdi);                      // :411
+        z.remSample = (p.codelength * pdi - c.remChip) / z.cps;          // :414
+        z.n = (int64_t)round((p.codelength * pdi - c.remChip) / z.cps);  // :415
+    } else {
+        z.remSample = (p.codelength - c.remChip) / z.cps;                // :79
+        z.n = (int64_t)round((p.codelength * pdi - c.remChip) / z.cps);  // :80
+        z.dv = z.n - (int64_t)(p.S * pdi);                               // :82
+    }
+    return z;
+}
+
+// Prepare the descriptor of the step that follows state `c` (trackingCT.m:79-107 /
+// :411-441). Two waves work on it side by side:
+//   role 0 (code): lanes < ntaps build the colon of their tap, lane 0 the scalars;
+//   role 1 (carrier): lanes < 32 the rotation table e^{i phi_m}, lane 63 remPhase.
+__device__ void prepare_desc(const TrkParams& p, const NcoState& c, int pdi, int phaseC, int role,
+                             int lane, StepDesc* d)
+{
+    const StepSize z = step_size(p, c, pdi, phaseC);
+    const int64_t n = z.n;
+    const double cps = z.cps;
+    if (role == 1) {
+        // carrier increment delta = 2*pi*f/Fs as a double-double; dhi has 48 bits so
+        // m*dhi (m < 32) is exact
+        const double f = c.carrierFreq;
+        double dhi, dlo;
+        {
+            const double p0 = kTwoPi * f;
+            double pe = __builtin_fma(kTwoPi, f, -p0);
+            pe = pe + kTwoPiLo * f;
+            const double q = p0 / p.Fs;
+            const double r = __builtin_fma(-q, p.Fs, p0);
+            const double ql = (r + pe) / p.Fs;
+            dhi = __longlong_as_double(__double_as_longlong(q) & ~0x1FLL);
+            dlo = (q - dhi) + ql;
+        }
+        if (lane < kLaneMax) {
+            // phi[m] rounds once (m*dhi is exact)
+            const double ph = (double)lane * dhi + (double)lane * dlo;
+            double sn, cs;
+            sincos(ph, &sn, &cs);
+            d->phi[lane] = ph;
+            d->rc[lane] = cs;
+            d->rs[lane] = sn;
+            if (lane == 0) {
+                d->f = f;
+                d->phi0 = c.remPhase;
+                d->dhi = dhi;
+                d->dlo = dlo;
+            }
+        } else if (lane == 63) {
+            // remPhase = rem(Wave(numSample+1), 2*pi) (:104-106)
+            d->remPhase_next = rem_2pi(kTwoPi * (f * ((double)n / p.Fs)) + c.remPhase);
+        }
+        return;
     }
     const int64_t A = c.pos / 2;
     int bad = GNSS_OK;
     if (n <= 0 || n > (int64_t)(p.S * pdi * 1.01) + 64) bad = GNSS_EINDEX;
     else if (2 * (A + n) > p.file_len) bad = phaseC ? GNSS_EIO : GNSS_ENODATA;  // :108-112 / :442
     else if (2 * A < p.buf_base || 2 * (A + n) > p.buf_base + p.buf_len) bad = GNSS_EIO;
-
-    // carrier increment delta = 2*pi*f/Fs as a double-double; dhi has 48 bits so
-    // m*dhi (m < 8) is exact
-    const double f = c.carrierFreq;
-    double dhi, dlo;
-    {
-        const double p0 = kTwoPi * f;
-        double pe = __builtin_fma(kTwoPi, f, -p0);
-        pe = pe + kTwoPiLo * f;
-        const double q = p0 / p.Fs;
-        const double r = __builtin_fma(-q, p.Fs, p0);
-        const double ql = (r + pe) / p.Fs;
-        dhi = __longlong_as_double(__double_as_longlong(q) & ~0x1FLL);
-        dlo = (q - dhi) + ql;
-    }
     if (lane < p.ntaps) {
         // t = (0 + Spacing + remChip) : cps : ((numSample-1)*cps + Spacing + remChip) (:96-98)
         const double a = (0 + p.taps[lane]) + c.remChip;
         const double bb = ((double)(n - 1) * cps + p.taps[lane]) + c.remChip;
-        const Colon col = colon_make(a, cps, bb);
+        const Colon col = colon_make_hint(a, cps, bb, n - 1);
         d->tap_a[lane] = col.a;
         d->tap_c[lane] = col.c;
         const int64_t c0 = (int64_t)ceil(colon_elem(col, 0));
@@ -114,68 +186,121 @@ __device__ void prepare_desc(const TrkParams& p, const TrkChan& c, int pdi, int 
         }
         if (tb != GNSS_OK && bad == GNSS_OK) bad = tb;
     }
-    if (lane < 9) {
-        double sn, cs;
-        sincos((double)lane * dhi + (double)lane * dlo, &sn, &cs);
-        d->rc[lane] = cs;
-        d->rs[lane] = sn;
-    }
-    if (lane == 9) {
-        // remPhase = rem(Wave(numSample+1), 2*pi) (:104-106)
-        d->remPhase_next = fmod(kTwoPi * (f * ((double)n / p.Fs)) + c.remPhase, kTwoPi);
-    }
     // any lane's failure wins (bitwise-or of the positive codes is enough to flag)
     int badw = bad;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) badw = max(badw, __shfl_xor(badw, o, 64));
     if (lane == 0) {
         d->n = n;
-        d->delayValue = dv;
+        d->delayValue = z.dv;
         d->A = A;
         d->g_first = A >> 3;
         d->g_last = (A + n - 1) >> 3;
         d->Index = c.Index;
-        d->remSample = remSample;
+        d->remSample = z.remSample;
         d->d = cps;
         d->inv_d = 1.0 / cps;
-        d->f = f;
-        d->phi0 = c.remPhase;
-        d->dhi = dhi;
-        d->dlo = dlo;
         d->pdi = pdi;
         d->phaseC = phaseC;
         d->bad = badw;
     }
 }
 
-// The scalar end of a step (trackingCT.m:102-170 / :435-524), fp64, same operation
-// order as the reference. Returns the updated state in `c`.
-__device__ void finalize_step(const TrkParams& p, const TrkBuffers& b, int ch, const StepDesc& d,
-                              const double* sums, TrkChan& c)
+// The DLL / PLL update of one step (trackingCT.m:136-150 / :469-483), fp64, same
+// operation order as the reference; phase C keeps T = 0.001 (:473,480). Every lane
+// that calls it computes the same values.
+struct LoopUpd {
+    double DLLdiscri, code_output, codeFreq, PLLdiscri, carrier_output, carrierFreq;
+};
+
+__device__ __forceinline__ LoopUpd loop_update(const TrkParams& p, const TrkChan& c, double E_i,
+                                               double E_q, double P_i, double P_q, double L_i,
+                                               double L_q, int pdi, int phaseC)
 {
-    const int64_t n = d.n;
-    const int pdi = d.pdi, phaseC = d.phaseC;
-    const int nt = p.ntaps;
-    const double* s = sums;  // already negated for phase C (:447-449)
+    LoopUpd u;
+    const double E = sqrt(E_i * E_i + E_q * E_q);
+    const double L = sqrt(L_i * L_i + L_q * L_q);
+    u.DLLdiscri = 0.5 * (E - L) / (E + L);
+    const double T = phaseC ? 0.001 : (0.001 * pdi);
+    u.code_output = c.code_outputLast + (p.tau2code / p.tau1code) * (u.DLLdiscri - c.DLLdiscriLast) +
+                    u.DLLdiscri * (T / p.tau1code);
+    u.codeFreq = p.codeFreqBasis - u.code_output;
+    u.PLLdiscri = atan(P_q / P_i) / kTwoPi;
+    u.carrier_output = c.carrier_outputLast +
+                       (p.tau2carr / p.tau1carr) * (u.PLLdiscri - c.PLLdiscriLast) +
+                       u.PLLdiscri * (T / p.tau1carr);
+    u.carrierFreq = c.carrierFreqBasis + u.carrier_output;
+    return u;
+}
 
-    c.remChip = d.remChip_next;
-    c.remPhase = d.remPhase_next;
-    const double E_i = s[2 * p.iE], E_q = s[2 * p.iE + 1];
+// Per-step values of the finished step the side writers need (read before the
+// next descriptor overwrites the current one).
+struct StepOut {
+    int64_t n, delayValue;
+    double remSample, remChip, remPhase;
+    int pdi, phaseC;
+};
+
+// TckResultCT fields of the step (trackingCT.m:153-170 / :507-524) and the phase-A
+// P_i kept for the bit-edge search. `s` = the step's (negated in phase C) sums.
+__device__ void write_record(const TrkParams& p, const TrkBuffers& b, int ch, const TrkChan& c,
+                             const StepOut& o, const LoopUpd& u, const double* s)
+{
     const double P_i = s[2 * p.iP], P_q = s[2 * p.iP + 1];
-    const double L_i = s[2 * p.iL], L_q = s[2 * p.iL + 1];
+    const int64_t pos = c.pos + 2 * o.n;  // ftell after fread
+    const int64_t Index = c.Index + (o.phaseC ? 10 : 1);
+    const int64_t col = c.nstep;          // 0-based IndexSmall - 1
+    int64_t* dvpre = b.dvpre + (int64_t)ch * (p.rec_cap + 1);
+    const int64_t dvsum = dvpre[col] + o.delayValue;
+    dvpre[col + 1] = dvsum;
+    const int64_t nstep = col + 1;
+    // sum(delayValue(1:Index)) over an nsv x N matrix (column-major, quirk A.11)
+    int64_t cols = 0;
+    if (Index >= c.sv1) cols = (Index - c.sv1) / p.nsv + 1;
+    if (cols > nstep) cols = nstep;
+    const double codedelay = (double)c.codedelay0 + (double)(cols == nstep ? dvsum : dvpre[cols]);
+    const double absS = (double)pos;
+    const double m = fmod(absS / p.dataBytesPerSample, p.Fs * p.ms);  // mod() of positives
+    const int64_t slot = c.slot;
+    if (slot < p.rec_cap) {
+        double* r = b.rec + ((int64_t)ch * p.rec_cap + slot) * GNSS_NFIELDS;
+        r[GNSS_F_P_i] = P_i;                     r[GNSS_F_P_q] = P_q;
+        r[GNSS_F_E_i] = s[2 * p.iE];             r[GNSS_F_E_q] = s[2 * p.iE + 1];
+        r[GNSS_F_L_i] = s[2 * p.iL];             r[GNSS_F_L_q] = s[2 * p.iL + 1];
+        r[GNSS_F_PLLdiscri] = u.PLLdiscri;       r[GNSS_F_DLLdiscri] = u.DLLdiscri;
+        r[GNSS_F_codedelay] = codedelay;         r[GNSS_F_remChip] = o.remChip;
+        r[GNSS_F_codeFreq] = u.codeFreq;         r[GNSS_F_carrierFreq] = u.carrierFreq;
+        r[GNSS_F_remPhase] = o.remPhase;         r[GNSS_F_remSample] = o.remSample;
+        r[GNSS_F_numSample] = (double)o.n;       r[GNSS_F_delayValue] = (double)o.delayValue;
+        r[GNSS_F_absoluteSample] = absS;         r[GNSS_F_codedelay2] = m;
+    }
+    if (!o.phaseC && slot < b.n1) b.p_i_1ms[(int64_t)ch * b.n1 + slot] = P_i;
+}
 
-    // C/N0 (:120-134)
-    c.index_int += 1;
-    c.Zk[c.index_int - 1] = P_i * P_i + P_q * P_q;
-    if (c.index_int % 20 == 0) {
+// The channel state after the step, with the C/N0 estimator (trackingCT.m:120-134).
+__device__ void write_state(const TrkParams& p, const TrkBuffers& b, int ch, const TrkChan& c,
+                            const StepOut& o, const LoopUpd& u, const double* s)
+{
+    TrkChan* g = b.chan + ch;
+    const double P_i = s[2 * p.iP], P_q = s[2 * p.iP + 1];
+    int index_int = c.index_int + 1;
+    int snrIndex = c.snrIndex;
+    const double zk = P_i * P_i + P_q * P_q;
+    g->Zk[index_int - 1] = zk;
+    if (index_int % 20 == 0) {
+        double Z[20];
+#pragma unroll
+        for (int k = 0; k < 20; k++) Z[k] = k == index_int - 1 ? zk : c.Zk[k];
         double mean = 0;
-        for (int k = 0; k < 20; k++) mean += c.Zk[k];
+#pragma unroll
+        for (int k = 0; k < 20; k++) mean += Z[k];
         mean = mean / 20;
         double var = 0;
-        for (int k = 0; k < 20; k++) var += (c.Zk[k] - mean) * (c.Zk[k] - mean);
+#pragma unroll
+        for (int k = 0; k < 20; k++) var += (Z[k] - mean) * (Z[k] - mean);
         var = var / 19;
         const double m2v = mean * mean - var;
-        const double scale = 1 / (1 * p.ms * pdi);
+        const double scale = 1 / (1 * p.ms * o.pdi);
         double cn;
         if (m2v >= 0) {
             const double NA2 = sqrt(m2v);
@@ -191,95 +316,73 @@ __device__ void finalize_step(const TrkParams& p, const TrkBuffers& b, int ch, c
             const double li = 10 * (atan2(zi, zr) / log(10.0));
             cn = hypot(lr, li);
         }
-        double* cn0 = phaseC ? b.cn0_10 : b.cn0_1;
-        if (c.snrIndex <= p.cn0_cap) cn0[(int64_t)ch * p.cn0_cap + c.snrIndex - 1] = cn;
-        c.index_int = 0;
-        c.snrIndex += 1;
+        double* cn0 = o.phaseC ? b.cn0_10 : b.cn0_1;
+        if (snrIndex <= p.cn0_cap) cn0[(int64_t)ch * p.cn0_cap + snrIndex - 1] = cn;
+        index_int = 0;
+        snrIndex += 1;
     }
-
-    // DLL (:136-143), PLL (:145-150); phase C keeps T = 0.001 (:473,480)
-    const double E = sqrt(E_i * E_i + E_q * E_q);
-    const double L = sqrt(L_i * L_i + L_q * L_q);
-    const double DLLdiscri = 0.5 * (E - L) / (E + L);
-    const double T = phaseC ? 0.001 : (0.001 * pdi);
-    const double code_output = c.code_outputLast +
-                               (p.tau2code / p.tau1code) * (DLLdiscri - c.DLLdiscriLast) +
-                               DLLdiscri * (T / p.tau1code);
-    c.DLLdiscriLast = DLLdiscri;
-    c.code_outputLast = code_output;
-    c.codeFreq = p.codeFreqBasis - code_output;
-    const double PLLdiscri = atan(P_q / P_i) / kTwoPi;
-    const double carrier_output = c.carrier_outputLast +
-                                  (p.tau2carr / p.tau1carr) * (PLLdiscri - c.PLLdiscriLast) +
-                                  PLLdiscri * (T / p.tau1carr);
-    c.carrier_outputLast = carrier_output;
-    c.PLLdiscriLast = PLLdiscri;
-    c.carrierFreq = c.carrierFreqBasis + carrier_output;
-
-    // bookkeeping + record (:153-170 / :507-524)
-    c.numSample = n;
-    c.remSample = d.remSample;
-    c.pos += 2 * n;  // ftell after fread
-    c.Index += phaseC ? 10 : 1;
-    const int64_t col = c.nstep;  // 0-based IndexSmall - 1
-    int64_t* dvpre = b.dvpre + (int64_t)ch * (p.rec_cap + 1);
-    const int64_t dvsum = dvpre[col] + d.delayValue;
-    dvpre[col + 1] = dvsum;
-    c.nstep = col + 1;
-    // sum(delayValue(1:Index)) over an nsv x N matrix (column-major, quirk A.11)
-    int64_t cols = 0;
-    if (c.Index >= c.sv1) cols = (c.Index - c.sv1) / p.nsv + 1;
-    if (cols > c.nstep) cols = c.nstep;
-    const double codedelay = (double)c.codedelay0 + (double)(cols == c.nstep ? dvsum : dvpre[cols]);
-    const double absS = (double)c.pos;
-    const double m = fmod(absS / p.dataBytesPerSample, p.Fs * p.ms);  // mod() of positives
-    const int64_t slot = c.slot;
-    if (slot < p.rec_cap) {
-        double* r = b.rec + ((int64_t)ch * p.rec_cap + slot) * GNSS_NFIELDS;
-        r[GNSS_F_P_i] = P_i;             r[GNSS_F_P_q] = P_q;
-        r[GNSS_F_E_i] = E_i;             r[GNSS_F_E_q] = E_q;
-        r[GNSS_F_L_i] = L_i;             r[GNSS_F_L_q] = L_q;
-        r[GNSS_F_PLLdiscri] = PLLdiscri; r[GNSS_F_DLLdiscri] = DLLdiscri;
-        r[GNSS_F_codedelay] = codedelay; r[GNSS_F_remChip] = c.remChip;
-        r[GNSS_F_codeFreq] = c.codeFreq; r[GNSS_F_carrierFreq] = c.carrierFreq;
-        r[GNSS_F_remPhase] = c.remPhase; r[GNSS_F_remSample] = d.remSample;
-        r[GNSS_F_numSample] = (double)n; r[GNSS_F_delayValue] = (double)d.delayValue;
-        r[GNSS_F_absoluteSample] = absS; r[GNSS_F_codedelay2] = m;
-        if (b.taps_rec) {
-            double* tr = b.taps_rec + ((int64_t)ch * p.rec_cap + slot) * (2 * nt);
-            for (int v = 0; v < 2 * nt; v++) tr[v] = s[v];
-        }
-    }
-    if (!phaseC && slot < b.n1) b.p_i_1ms[(int64_t)ch * b.n1 + slot] = P_i;
-    c.slot = slot + 1;
+    g->remChip = o.remChip;
+    g->remPhase = o.remPhase;
+    g->remSample = o.remSample;
+    g->carrier_outputLast = u.carrier_output;
+    g->PLLdiscriLast = u.PLLdiscri;
+    g->code_outputLast = u.code_output;
+    g->DLLdiscriLast = u.DLLdiscri;
+    g->codeFreq = u.codeFreq;
+    g->carrierFreq = u.carrierFreq;
+    g->numSample = o.n;
+    g->pos = c.pos + 2 * o.n;
+    g->Index = c.Index + (o.phaseC ? 10 : 1);
+    g->nstep = c.nstep + 1;
+    g->slot = c.slot + 1;
+    g->index_int = index_int;
+    g->snrIndex = snrIndex;
 }
 
 }  // namespace
 
 // ---------------------------------------------------------------------------
 // The correlator step kernel. NT = taps (3: E/P/L, 11: ACF), SUB = 8-sample
-// sub-groups per lane (contiguous), both compile-time so the accumulators stay
-// in VGPRs. Grid: nch x bpc blocks; block b of a channel owns the 256*SUB
-// consecutive 8-sample groups starting at g_first + 256*SUB*b.
+// groups per lane (M = 8*SUB contiguous samples), both compile-time so the
+// accumulators stay in VGPRs. Grid: nch x bpc blocks; block b of a channel owns
+// the 256*SUB consecutive 8-sample groups starting at g_first + 256*SUB*b.
+//
+// Per lane (trackingCT.m:96-118):
+//   * carrier: w_m = x_m * e^{i(Wave(k_m) - Wave(k_0))} in the frame of the lane's
+//     first sample, Wave(k) rounded exactly as the reference rounds it; the
+//     rotation is the table e^{i phi_m} plus the first-order residue
+//     eta = (Wave(k_m) - Wave(k_0)) - phi_m (|eta| ~ 1e-10). One sincos per lane
+//     rotates the lane's sums back at the end;
+//   * code: M * codeFreq/Fs < 1, so every tap's replica Code(ceil(t)+1) changes
+//     at most once in the lane, at sample p (exact colon arithmetic at the lane
+//     start, exact re-evaluation within 1e-6 sample of a boundary). With the
+//     running sum of w in LDS, the tap sum is v1*Sum + (v0 - v1)*Prefix(p).
 // ---------------------------------------------------------------------------
-template <int NT, int SUB>
+template <int NT, int SUB, bool DIVIDE>
 __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(TrkParams p, TrkBuffers b, int bpc)
 {
+    constexpr int M = 8 * SUB;
+    constexpr int NV = 2 * NT;
+    constexpr int T = kTrkThreads;
+    static_assert(M <= kLaneMax, "lane span exceeds the rotation table");
     const int ch = blockIdx.x / bpc;
     const int blk = blockIdx.x - ch * bpc;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    constexpr int NV = 2 * NT;
-    constexpr int J = kTrkThreads / NV;
 
-    __shared__ double s_red[kTrkThreads / 64][NV];
-    __shared__ double s_tmp[J * NV];
+    // LDS: running sums slot[9][T] (slot 8 stays zero), then the block reduction
+    constexpr int kSlot = 9 * T * 2;
+    constexpr int kRed = NV * (T + 32);
+    __shared__ __attribute__((aligned(16))) double s_mem[kSlot > kRed ? kSlot : kRed];
     __shared__ double s_fin[NV];
     __shared__ int s_last;
+    __shared__ TrkChan s_c;
 
     const StepDesc* dp = b.desc + ch;
     const TrkChan* cp = b.chan + ch;
+    unsigned long long* srow = b.stamps && ch == 0 ? stamp_row(b) : nullptr;
+    if (srow && tid == 0) stamp_max(srow, 8 + blk, wall_clock64());  // block start
     const int64_t g_first = dp->g_first, g_last = dp->g_last;
-    const int64_t g0 = g_first + ((int64_t)blk * kTrkThreads + tid) * SUB;  // first group of the lane
+    const int64_t g0 = g_first + ((int64_t)blk * T + tid) * SUB;  // first group of the lane
     // issue the IF loads first (clamped so every lane loads something valid)
     const int8_t* iq = b.iq - p.buf_base;  // absolute-byte addressing
     const int bad = dp->bad;
@@ -290,151 +393,190 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(TrkParams p, Tr
         raw[j] = bad ? make_int4(0, 0, 0, 0) : *reinterpret_cast<const int4*>(iq + 16 * gj);
     }
     const unsigned cabits = lane < 32 ? b.ca_bits[ch * 32 + lane] : 0u;
+    // the channel state, for whichever block arrives last
+    constexpr int kChanWords = (int)(sizeof(TrkChan) / 8);
+    if (tid < kChanWords)
+        reinterpret_cast<uint64_t*>(&s_c)[tid] = reinterpret_cast<const uint64_t*>(cp)[tid];
 
     if (cp->status != GNSS_OK) return;
     if (!dp->phaseC && dp->Index + 1 > cp->n1_target) return;  // 1-ms run of this channel done
-    if (bad) {
-        if (blk == 0 && tid == 0) b.chan[ch].status = bad;
-        return;
-    }
-
     const int64_t n = dp->n, A = dp->A;
     const double d = dp->d, inv_d = dp->inv_d;
-    const double f = dp->f, phi0 = dp->phi0, dhi = dp->dhi, dlo = dp->dlo;
-    const double Fs = p.Fs, rFs = p.inv_Fs;
-    const bool exact_div = p.exact_div != 0;
-
-    const int64_t ks = 8 * g0 - A;  // relative index of the lane's first sample
-    const int mlo = ks < 0 ? (int)(-ks) : 0;  // only the window's first lane has ks < 0
-    const int64_t kf = ks + mlo < n - 1 ? ks + mlo : n - 1;
-
-    // ---- code replica per tap: chip ic at the sub-group's first sample and the
-    // distance R (samples) from that sample to the next chip boundary; the boundary
-    // falls at m = floor(R) + 1 (at most one per 8 samples since 8*cps < 1). Exact
-    // fp64 colon values at the lane start, then R -= 8 / += 1/cps per sub-group; an
-    // ambiguous boundary (|R - round R| < 1e-6) takes the per-sample exact path.
-    int64_t ic[NT];
-    double R[NT];
-#pragma unroll
-    for (int s = 0; s < NT; s++) {
-        const Colon col{dp->tap_a[s], d, dp->tap_c[s], n - 1};
-        const double t0 = colon_elem(col, kf);
-        const double c0 = ceil(t0);
-        ic[s] = (int64_t)c0;
-        R[s] = (double)(kf - ks) + (c0 - t0) * inv_d;
+    if (bad || d * M >= 1.0) {  // (a code rate beyond Fs/M breaks the one-boundary lane)
+        if (blk == 0 && tid == 0) b.chan[ch].status = bad ? bad : GNSS_EINDEX;
+        return;
     }
+    const double f = dp->f, phi0 = dp->phi0;
+    const double Fs = p.Fs, rFs = p.inv_Fs;
 
-    // ---- carrier: Wave(k) exactly as the reference rounds it (trackingCT.m:104-107);
-    // one sincos per lane, every other sample rotated by e^{i m delta} and corrected
-    // by eta = (Wave(k) - Wave(kb)) - m*delta, the rounding residue of Wave.
-    double kb = (double)ks;
-    double Wb = wave_at(kb, f, phi0, Fs, rFs, exact_div);
-    double sb, cb;
-    sincos(Wb, &sb, &cb);
-
-    double accI[NT], accQ[NT];
-#pragma unroll
-    for (int s = 0; s < NT; s++) { accI[s] = 0.0; accQ[s] = 0.0; }
-
+    // ---- valid samples of the lane: [lo, hi) (only the window's two end lanes are partial)
+    const int64_t ks = 8 * g0 - A;  // window-relative index of the lane's first sample
+    const int lo = ks < 0 ? (int)(-ks < M ? -ks : M) : 0;
+    const int hi = n - ks < M ? (n - ks > 0 ? (int)(n - ks) : 0) : M;
+    unsigned wd[SUB][4];
 #pragma unroll
     for (int j = 0; j < SUB; j++) {
-        const int64_t kj = ks + 8 * j;
-        const int lo = j == 0 ? mlo : 0;
-        const int hi = (n - kj) < 8 ? (int)(n - kj) : 8;  // valid m in [lo, hi)
-        double v0[NT], v1[NT];
-        unsigned sel[NT];
+        wd[j][0] = raw[j].x; wd[j][1] = raw[j].y; wd[j][2] = raw[j].z; wd[j][3] = raw[j].w;
+    }
+    if (lo > 0 || hi < M) {
 #pragma unroll
-        for (int s = 0; s < NT; s++) {
-            const int i0 = ca_index(ic[s]), i1 = ca_index(ic[s] + 1);
-            const unsigned w0 = __shfl(cabits, i0 >> 5, 64), w1 = __shfl(cabits, i1 >> 5, 64);
-            v0[s] = ((w0 >> (i0 & 31)) & 1u) ? -1.0 : 1.0;
-            v1[s] = ((w1 >> (i1 & 31)) & 1u) ? -1.0 : 1.0;
-            const double rr = rint(R[s]);
-            unsigned m = 0;
-            if (fabs(R[s] - rr) < 1e-6 && rr < 8.0 && hi > 0) {
-                // exact per-sample chips, then an exact restart at the next sub-group
-                const Colon col{dp->tap_a[s], d, dp->tap_c[s], n - 1};
-                // the lane's first valid sample has chip ic by construction; later
-                // sub-groups may already start past the boundary (R <= 0)
-                for (int q = j == 0 ? lo + 1 : 0; q < hi; q++)
-                    if ((int64_t)ceil(colon_elem(col, kj + q)) != ic[s]) m |= 1u << q;
-                const int64_t kn = kj + 8 < n - 1 ? kj + 8 : n - 1;
-                const double tn = colon_elem(col, kn);
-                const double cn = ceil(tn);
-                ic[s] = (int64_t)cn;
-                R[s] = (double)(kn - (kj + 8)) + (cn - tn) * inv_d;
-            } else {
-                const double fl = floor(R[s]);
-                const int pb = (int)fl + 1;
-                m = pb >= 8 ? 0u : (0xFFu << pb) & 0xFFu;
-                if (pb < 8) { ic[s] += 1; R[s] += inv_d; }
-                R[s] -= 8.0;
+        for (int j = 0; j < SUB; j++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int m0 = 8 * j + 2 * q;
+                const unsigned k0 = (m0 >= lo && m0 < hi) ? 0x0000FFFFu : 0u;
+                const unsigned k1 = (m0 + 1 >= lo && m0 + 1 < hi) ? 0xFFFF0000u : 0u;
+                wd[j][q] &= k0 | k1;
             }
-            sel[s] = m;
+    }
+
+    double oI[NT], oQ[NT];
+    if (p.probe & 2) {  // timing probe: no correlation (loads, reduction and hand-off only)
+#pragma unroll
+        for (int s = 0; s < NT; s++) { oI[s] = (double)(int)wd[0][s & 3]; oQ[s] = 0.0; }
+    } else {
+        // ---- code replica per tap: chip c0 at the first valid sample, the sample p of the
+        // lane's (single) chip boundary, and the two code values around it
+        const int64_t kf0 = ks + lo;
+        const int64_t kf = kf0 < 0 ? 0 : (kf0 > n - 1 ? n - 1 : kf0);
+        int cap[NT];
+        double v1[NT], dv[NT];
+    #pragma unroll
+        for (int s = 0; s < NT; s++) {
+            const Colon col{dp->tap_a[s], d, dp->tap_c[s], n - 1};
+            const double t0 = colon_elem(col, kf);
+            const double c0 = ceil(t0);
+            const double R = (double)(kf - ks) + (c0 - t0) * inv_d;  // samples to the boundary
+            const double rr = rint(R);
+            int pb = (int)floor(R) + 1;
+            if (fabs(R - rr) < 1e-6) {  // too close to call in floating point: exact colon value
+                const int ms = (int)rr;
+                pb = ms;
+                const int64_t kx = ks + ms;
+                if (ms >= 0 && ms < M && kx >= 0 && kx <= n - 1)
+                    pb = ceil(colon_elem(col, kx)) > c0 ? ms : ms + 1;
+            }
+            cap[s] = (pb < M ? pb : M) - 1;  // Prefix(p) = running sum through sample p-1
+            const unsigned i0 = ca_index32((int)c0);
+            const unsigned i1 = i0 == 1022u ? 0u : i0 + 1u;
+            const unsigned w0 = __shfl(cabits, (int)(i0 >> 5), 64);
+            const unsigned w1 = __shfl(cabits, (int)(i1 >> 5), 64);
+            const double a0 = ((w0 >> (i0 & 31)) & 1u) ? -1.0 : 1.0;
+            const double a1 = ((w1 >> (i1 & 31)) & 1u) ? -1.0 : 1.0;
+            v1[s] = a1;
+            dv[s] = a0 - a1;
         }
 
-        const int w[4] = {raw[j].x, raw[j].y, raw[j].z, raw[j].w};
-#pragma unroll
-        for (int m = 0; m < 8; m++) {
-            const int word = w[m >> 1];
-            const int sh = (m & 1) * 16;
-            double xr = (double)(int8_t)((word >> sh) & 0xFF);
-            double xi = (double)(int8_t)((word >> (sh + 8)) & 0xFF);
-            if (m < lo || m >= hi) { xr = 0.0; xi = 0.0; }
-            double cw = cb, sw = sb;
-            if (m > 0) {
-                const double dm = wave_at(kb + (double)m, f, phi0, Fs, rFs, exact_div) - Wb;
-                const double eta = (dm - (double)m * dhi) - (double)m * dlo;
-                const double rcm = dp->rc[m], rsm = dp->rs[m];
-                const double cm = __builtin_fma(cb, rcm, -(sb * rsm));
-                const double sm = __builtin_fma(sb, rcm, cb * rsm);
-                cw = __builtin_fma(-eta, sm, cm);
-                sw = __builtin_fma(eta, cm, sm);
+        // ---- carrier base of the lane
+        const double kb = (double)ks;
+        const double Wb = wave_at<DIVIDE>(kb, f, phi0, Fs, rFs);
+        double sb, cb;
+        sincos(Wb, &sb, &cb);
+
+        double2* myslot = reinterpret_cast<double2*>(s_mem) + tid;  // slot m at myslot[m * T]
+        myslot[8 * T] = make_double2(0.0, 0.0);
+        double run_r = 0.0, run_i = 0.0;
+        double pre_r[NT], pre_i[NT];
+    #pragma unroll
+        for (int s = 0; s < NT; s++) { pre_r[s] = 0.0; pre_i[s] = 0.0; }
+
+    #pragma unroll
+        for (int j = 0; j < SUB; j++) {
+    #pragma unroll
+            for (int mm = 0; mm < 8; mm++) {
+                const int m = 8 * j + mm;
+                const unsigned word = wd[j][mm >> 1];
+                const int sh = (mm & 1) * 16;
+                const double xr = (double)(int8_t)((word >> sh) & 0xFF);
+                const double xi = (double)(int8_t)((word >> (sh + 8)) & 0xFF);
+                double wr = xr, wi = xi;
+                if (m > 0) {
+                    const double W = wave_at<DIVIDE>(kb + (double)m, f, phi0, Fs, rFs);
+                    const double eta = (W - Wb) - dp->phi[m];
+                    const double rc = dp->rc[m], rs = dp->rs[m];
+                    const double yr = __builtin_fma(xr, rc, -(xi * rs));
+                    const double yi = __builtin_fma(xr, rs, xi * rc);
+                    wr = __builtin_fma(-eta, yi, yr);
+                    wi = __builtin_fma(eta, yr, yi);
+                }
+                run_r += wr;
+                run_i += wi;
+                myslot[mm * T] = make_double2(run_r, run_i);
             }
-            const double I = __builtin_fma(xr, sw, xi * cw);     // imag(raw.*carrsig)
-            const double Q = __builtin_fma(xr, cw, -(xi * sw));  // real(raw.*carrsig)
-#pragma unroll
+    #pragma unroll
             for (int s = 0; s < NT; s++) {
-                const double code = ((sel[s] >> m) & 1u) ? v1[s] : v0[s];
-                accI[s] = __builtin_fma(code, I, accI[s]);
-                accQ[s] = __builtin_fma(code, Q, accQ[s]);
+                const unsigned idx = (unsigned)(cap[s] - 8 * j);
+                const double2 v = myslot[(idx < 8u ? idx : 8u) * T];
+                pre_r[s] += v.x;
+                pre_i[s] += v.y;
             }
         }
-        if (j + 1 < SUB) {  // chain the base phasor to the next sub-group, exactly
-            const double Wn = wave_at(kb + 8.0, f, phi0, Fs, rFs, exact_div);
-            const double eta = ((Wn - Wb) - 8.0 * dhi) - 8.0 * dlo;
-            const double rc8 = dp->rc[8], rs8 = dp->rs[8];
-            const double cm = __builtin_fma(cb, rc8, -(sb * rs8));
-            const double sm = __builtin_fma(sb, rc8, cb * rs8);
-            cb = __builtin_fma(-eta, sm, cm);
-            sb = __builtin_fma(eta, cm, sm);
-            Wb = Wn;
-            kb += 8.0;
+
+        // ---- tap sums of the lane, rotated back by e^{i Wave(k_0)}:
+        // I = imag(raw .* carrsig), Q = real(raw .* carrsig) (trackingCT.m:107-118)
+    #pragma unroll
+        for (int s = 0; s < NT; s++) {
+            const double ur = __builtin_fma(dv[s], pre_r[s], v1[s] * run_r);
+            const double ui = __builtin_fma(dv[s], pre_i[s], v1[s] * run_i);
+            oI[s] = __builtin_fma(cb, ui, sb * ur);
+            oQ[s] = __builtin_fma(cb, ur, -(sb * ui));
         }
     }
 
     // ---- block reduction (fixed order), then hand the partial to the last arriver
+    __syncthreads();  // every wave is done with its slots
+    if (srow && tid == 0) stamp_max(srow, 8 + kMaxBpc + blk, wall_clock64());  // block computed
+    double* red = s_mem;             // [NV][T]
+    double* red2 = s_mem + NV * T;   // [NV][32]
 #pragma unroll
     for (int s = 0; s < NT; s++) {
-        const double si = wave_sum(accI[s]);
-        const double sq = wave_sum(accQ[s]);
-        if (lane == 0) { s_red[wv][2 * s] = si; s_red[wv][2 * s + 1] = sq; }
+        red[(2 * s) * T + tid] = oI[s];
+        red[(2 * s + 1) * T + tid] = oQ[s];
+    }
+    __syncthreads();
+    for (int e = tid; e < NV * 32; e += T) {
+        const int v = e >> 5, g = e & 31;
+        const double* r = red + v * T + g * 8;
+        double a = r[0];
+#pragma unroll
+        for (int k = 1; k < 8; k++) a += r[k];
+        red2[e] = a;
     }
     __syncthreads();
     double* allp = b.partial + (int64_t)ch * bpc * NV;
     if (wv == 0) {
         if (lane < NV) {
-            double v = 0;
-#pragma unroll
-            for (int k = 0; k < kTrkThreads / 64; k++) v += s_red[k][lane];
-            st_sc1(allp + (int64_t)blk * NV + lane, v);  // write-through
+            double a = red2[lane * 32];
+            for (int k = 1; k < 32; k++) a += red2[lane * 32 + k];
+            st_sc1(allp + (int64_t)blk * NV + lane, a);  // write-through
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the storing wave drains
-        int last = 0;
         if (lane == 0) {
-            const unsigned old = __hip_atomic_fetch_add(b.arrive + ch, 1u, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT);
-            last = (old == (unsigned)(bpc - 1));
+            // two-level ticket: the blocks of the channel in this XCD group, then the
+            // last of each group on the channel's counter (every counter on its own line)
+            const int g = blockIdx.x & 7;
+            const int first = ((g - (ch * bpc) % 8) % 8 + 8) % 8;  // first blk of group g
+            const unsigned cnt = first < bpc ? (unsigned)((bpc - 1 - first) / 8 + 1) : 0u;
+            unsigned* sub = b.arrive + (ch * kArrivePerChan + g) * kArriveStride;
+            unsigned* top = b.arrive + (ch * kArrivePerChan + 8) * kArriveStride;
+            if (srow) stamp_max(srow, 8 + 2 * kMaxBpc + blk, wall_clock64());  // last ticket issued
+            int last = 0;
+            if (bpc <= 32) {  // few arrivals: one level
+                if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                    (unsigned)bpc - 1) {
+                    __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    last = 1;
+                }
+            } else if (__hip_atomic_fetch_add(sub, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                       cnt - 1) {
+                __hip_atomic_store(sub, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned ngroups = bpc < 8 ? (unsigned)bpc : 8u;
+                if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                    ngroups - 1) {
+                    __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    last = 1;
+                }
+            }
             s_last = last;
         }
     }
@@ -442,6 +584,9 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(TrkParams p, Tr
     if (!s_last) return;
 
     // ---- last arriver: deterministic reduction of all block partials (sc1 loads)
+    if (srow && tid == 0) stamp_max(srow, 3, wall_clock64());
+    constexpr int J = T / NV;
+    double* s_tmp = s_mem;  // [J][NV]
     if (tid < J * NV) {
         const int v = tid % NV, j = tid / NV;
         double a = 0;
@@ -456,32 +601,79 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(TrkParams p, Tr
         for (; k < bpc; k += J) a += ld_sc1(allp + (int64_t)k * NV + v);
         s_tmp[j * NV + v] = a;
     }
+    // the step's values the writers need, read before the next descriptor replaces them
+    StepOut o;
+    o.n = dp->n;
+    o.delayValue = dp->delayValue;
+    o.remSample = dp->remSample;
+    o.remChip = dp->remChip_next;
+    o.remPhase = dp->remPhase_next;
+    o.pdi = dp->pdi;
+    o.phaseC = dp->phaseC;
+    const bool dbg = b.dbg_sums || (p.probe & 1);
     __syncthreads();
     if (tid < NV) {
         double a = 0;
         for (int j = 0; j < J; j++) a += s_tmp[j * NV + tid];
-        s_fin[tid] = a;
+        if (dbg) {
+            if (b.dbg_sums) b.dbg_sums[ch * NV + tid] = a;
+        } else {
+            s_fin[tid] = o.phaseC ? -a : a;  // :447-449
+        }
     }
+    if (dbg) return;
     __syncthreads();
-    if (wv != 0) return;
-    const StepDesc dd = *dp;
-    if (b.dbg_sums) {
-        if (lane < NV) b.dbg_sums[ch * NV + lane] = s_fin[lane];
-        if (lane == 0) b.arrive[ch] = 0;
+    if (srow && tid == 0) stamp_max(srow, 4, wall_clock64());  // sums final
+    // every wave computes the loop update (same values in every lane); then wave 0
+    // prepares the next step while waves 1 and 2 write the record and the state
+    const LoopUpd u = loop_update(p, s_c, s_fin[2 * p.iE], s_fin[2 * p.iE + 1], s_fin[2 * p.iP],
+                                  s_fin[2 * p.iP + 1], s_fin[2 * p.iL], s_fin[2 * p.iL + 1], o.pdi,
+                                  o.phaseC);
+    if (wv == 0 || wv == 3) {
+        if (p.probe & 8) return;
+        NcoState nx;
+        nx.remChip = o.remChip;
+        nx.remPhase = o.remPhase;
+        nx.codeFreq = u.codeFreq;
+        nx.carrierFreq = u.carrierFreq;
+        nx.numSample = o.n;
+        nx.pos = s_c.pos + 2 * o.n;
+        nx.Index = s_c.Index + (o.phaseC ? 10 : 1);
+        if (srow && wv == 0 && lane == 0) stamp_max(srow, 5, wall_clock64());  // loop updated
+        prepare_desc(p, nx, o.pdi, o.phaseC, wv == 0 ? 0 : 1, lane, b.desc + ch);
+        if (srow && wv == 0 && lane == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            stamp_max(srow, 6, wall_clock64());  // next descriptor stored
+        }
+        if (srow && wv == 0 && (p.probe & 32)) {  // the same again with a warm instruction cache
+            if (lane == 0) stamp_max(srow, 0, wall_clock64());
+            const LoopUpd u2 = loop_update(p, s_c, s_fin[2 * p.iE], s_fin[2 * p.iE + 1],
+                                           s_fin[2 * p.iP], s_fin[2 * p.iP + 1], s_fin[2 * p.iL],
+                                           s_fin[2 * p.iL + 1], o.pdi, o.phaseC);
+            nx.codeFreq = u2.codeFreq;
+            nx.carrierFreq = u2.carrierFreq;
+            if (lane == 0) stamp_max(srow, 1, wall_clock64());
+            prepare_desc(p, nx, o.pdi, o.phaseC, 0, lane, b.desc + ch);
+            if (lane == 0) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                stamp_max(srow, 2, wall_clock64());
+            }
+        }
+    } else if (p.probe & 4) {
         return;
+    } else if (wv == 1) {
+        if (lane == 0) write_record(p, b, ch, s_c, o, u, s_fin);
+        if (b.taps_rec && lane < NV && s_c.slot < p.rec_cap)
+            b.taps_rec[((int64_t)ch * p.rec_cap + s_c.slot) * NV + lane] = s_fin[lane];
+    } else if (lane == 0) {
+        write_state(p, b, ch, s_c, o, u, s_fin);
+        if (srow) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            stamp_max(srow, 7, wall_clock64());  // state stored
+            __hip_atomic_fetch_add(b.stamps + (size_t)kStampSlots * kStampRow, 1ull, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
-    __shared__ TrkChan s_c;
-    if (dd.phaseC && lane < NV) s_fin[lane] = -s_fin[lane];  // :447-449
-    if (lane == 0) {
-        b.arrive[ch] = 0;
-        s_c = *cp;
-        finalize_step(p, b, ch, dd, s_fin, s_c);
-        b.chan[ch] = s_c;
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): lane 0's LDS store is visible
-    __builtin_amdgcn_wave_barrier();
-    const TrkChan cn = s_c;
-    prepare_desc(p, cn, dd.pdi, dd.phaseC, lane, b.desc + ch);
 }
 
 // Prepare the StepDesc of every channel from its current state (start of a phase).
@@ -489,7 +681,7 @@ __global__ void track_prepare_kernel(TrkParams p, TrkBuffers b, int pdi, int pha
 {
     const int ch = blockIdx.x;
     const TrkChan c = b.chan[ch];
-    prepare_desc(p, c, pdi, phaseC, threadIdx.x, b.desc + ch);
+    prepare_desc(p, nco_of(c), pdi, phaseC, threadIdx.x >> 6, threadIdx.x & 63, b.desc + ch);
 }
 
 __global__ void track_snapshot_kernel(TrkBuffers b, int nch)
@@ -558,20 +750,21 @@ __global__ void track_phase_c_init_kernel(TrkParams p, TrkBuffers b, int64_t ski
     }
     __syncthreads();
     const TrkChan c = s_c;
-    if (c.status == GNSS_OK) prepare_desc(p, c, 10, 1, threadIdx.x, b.desc + ch);
+    if (c.status == GNSS_OK) prepare_desc(p, nco_of(c), 10, 1, threadIdx.x >> 6, threadIdx.x & 63, b.desc + ch);
 }
 
 hipError_t launch_track_step(const TrkParams& p, const TrkBuffers& b, int bpc, int sub,
                              hipStream_t s)
 {
     dim3 grid(p.nch * bpc), block(kTrkThreads);
-#define GNSS_STEP(NT_, SUB_)                                                                   \
-    if (p.ntaps == NT_ && sub == SUB_) {                                                       \
-        hipLaunchKernelGGL((track_step_kernel<NT_, SUB_>), grid, block, 0, s, p, b, bpc);      \
+#define GNSS_STEP(NT_, SUB_, DIV_)                                                             \
+    if (p.ntaps == NT_ && sub == SUB_ && (p.exact_div != 0) == DIV_) {                         \
+        hipLaunchKernelGGL((track_step_kernel<NT_, SUB_, DIV_>), grid, block, 0, s, p, b, bpc); \
         return hipGetLastError();                                                              \
     }
-    GNSS_STEP(3, 1) GNSS_STEP(3, 2) GNSS_STEP(3, 4)
-    GNSS_STEP(11, 1) GNSS_STEP(11, 2) GNSS_STEP(11, 4)
+    GNSS_STEP(3, 1, false) GNSS_STEP(3, 2, false) GNSS_STEP(3, 4, false)
+    GNSS_STEP(11, 1, false) GNSS_STEP(11, 2, false) GNSS_STEP(11, 4, false)
+    GNSS_STEP(3, 1, true) GNSS_STEP(11, 1, true)
 #undef GNSS_STEP
     return hipErrorInvalidValue;
 }
@@ -579,7 +772,7 @@ hipError_t launch_track_step(const TrkParams& p, const TrkBuffers& b, int bpc, i
 hipError_t launch_track_prepare(const TrkParams& p, const TrkBuffers& b, int pdi, int phaseC,
                                 hipStream_t s)
 {
-    hipLaunchKernelGGL(track_prepare_kernel, dim3(p.nch), dim3(64), 0, s, p, b, pdi, phaseC);
+    hipLaunchKernelGGL(track_prepare_kernel, dim3(p.nch), dim3(128), 0, s, p, b, pdi, phaseC);
     return hipGetLastError();
 }
 
@@ -598,7 +791,7 @@ hipError_t launch_track_bitedge(const TrkParams& p, const TrkBuffers& b, hipStre
 hipError_t launch_track_phase_c_init(const TrkParams& p, const TrkBuffers& b, int64_t skip,
                                      hipStream_t s)
 {
-    hipLaunchKernelGGL(track_phase_c_init_kernel, dim3(p.nch), dim3(64), 0, s, p, b, skip);
+    hipLaunchKernelGGL(track_phase_c_init_kernel, dim3(p.nch), dim3(128), 0, s, p, b, skip);
     return hipGetLastError();
 }
 

@@ -1,0 +1,22 @@
+"""Host-side checks of helpers the kernels share with the host (compiled with hipcc,
+host code only; no GPU needed)."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+HIPCC = "/opt/rocm/bin/hipcc"
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_colon_make_hint_equals_colonop(tmp_path):
+    src = os.path.join(ROOT, "tests", "native", "colon_hint.cpp")
+    exe = tmp_path / "colon_hint"
+    subprocess.run([HIPCC, "-O2", "-std=c++17", "-ffp-contract=off", "-o", str(exe), src],
+                   check=True, capture_output=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches 0" in r.stdout
