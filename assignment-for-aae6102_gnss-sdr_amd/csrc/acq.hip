@@ -95,8 +95,20 @@ __device__ __forceinline__ void peak_merge(float& m, int& bin, int& col, float m
 
 // [~,fbin] = max(max(corr')); [peak,codePhase] = max(max(corr)) (acquisition.m:62-63):
 // the global max; fbin = first bin holding it, codePhase = first column holding it.
+// perm = P: the surface is stored tau2-major (acq_fft.hip), storage k -> column
+// k / 2000 + P * (k % 2000); perm = 0: natural order.
+__device__ __forceinline__ int64_t natural_col(int64_t k, int perm)
+{
+    return perm ? k / 2000 + (int64_t)perm * (k % 2000) : k;
+}
+
+__device__ __forceinline__ int64_t storage_of(int64_t col, int perm)
+{
+    return perm ? (col % perm) * 2000 + col / perm : col;
+}
+
 __global__ void acq_peak_part_kernel(const float* __restrict__ corr, int nbins, int64_t S,
-                                     int nblk, PeakPart* __restrict__ part)
+                                     int nblk, int perm, PeakPart* __restrict__ part)
 {
     const int p = blockIdx.y, blk = blockIdx.x;
     const float* c = corr + (int64_t)p * nbins * S;
@@ -105,7 +117,7 @@ __global__ void acq_peak_part_kernel(const float* __restrict__ corr, int nbins, 
     for (int b = 0; b < nbins; b++)
         for (int64_t k = (int64_t)blk * blockDim.x + threadIdx.x; k < S;
              k += (int64_t)nblk * blockDim.x)
-            peak_merge(m, bin, col, c[(int64_t)b * S + k], b, (int)k);
+            peak_merge(m, bin, col, c[(int64_t)b * S + k], b, (int)natural_col(k, perm));
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const float m2 = __shfl_xor(m, o, 64);
@@ -125,7 +137,7 @@ __global__ void acq_peak_part_kernel(const float* __restrict__ corr, int nbins, 
 // Merge the partials, then SNR = 10*log10(peak^2 / mean(corr(fbin, off-peak).^2))
 // with the off-peak range [1:cp-cshift, cp+cshift:end] (acquisition.m:66-68).
 __global__ void acq_peak_final_kernel(const float* __restrict__ corr, int nbins, int64_t S,
-                                      int nblk, int cshift, const PeakPart* __restrict__ part,
+                                      int nblk, int cshift, int perm, const PeakPart* __restrict__ part,
                                       AcqPeak* __restrict__ out)
 {
     const int p = blockIdx.x;
@@ -148,7 +160,7 @@ __global__ void acq_peak_final_kernel(const float* __restrict__ corr, int nbins,
     double sum = 0, cnt = 0, mx = 0;
     for (int64_t k = threadIdx.x + 1; k <= S; k += blockDim.x) {
         if (k <= cp1 - cshift || k >= cp1 + cshift) {
-            const double v = (double)row[k - 1];
+            const double v = (double)row[storage_of(k - 1, perm)];
             sum += v * v;
             cnt += 1;
             mx = fmax(mx, v);
@@ -297,13 +309,13 @@ hipError_t launch_acq_power(const float2* y, int nprn, int nbins, int datalen, i
 }
 
 hipError_t launch_acq_peak(const float* corr, int nprn, int nbins, int64_t S, int cshift,
-                           AcqPeak* out, void* scratch, hipStream_t s)
+                           int perm, AcqPeak* out, void* scratch, hipStream_t s)
 {
     PeakPart* part = reinterpret_cast<PeakPart*>(scratch);
     hipLaunchKernelGGL(acq_peak_part_kernel, dim3(kPeakBlocks, nprn), dim3(256), 0, s, corr, nbins, S,
-                       kPeakBlocks, part);
+                       kPeakBlocks, perm, part);
     hipLaunchKernelGGL(acq_peak_final_kernel, dim3(nprn), dim3(256), 0, s, corr, nbins, S,
-                       kPeakBlocks, cshift, part, out);
+                       kPeakBlocks, cshift, perm, part, out);
     return hipGetLastError();
 }
 

@@ -1,0 +1,649 @@
+// acq_fft.hip — acquisition.m's FFT work for gfx950 without rocFFT's Bluestein path:
+//  (1) the parallel-code-phase search (acquisition.m:47-61) as a two-pass mixed-radix FFT
+//      correlator in fp32 for S = P * 2000 with P prime (Opensky 58000 = 29 * 2000,
+//      Urban 26000 = 13 * 2000);
+//  (2) the fine-frequency search (acquisition.m:103-116) in fp64: the zero-padded
+//      N = L*S*datalen point FFT of the 10-ms code-wiped block, split into datalen
+//      transforms of M = L*S points (X[datalen*q + r] = DFT_M(x .* w_N^(-n*r))[q]),
+//      each a three-level FFT (P x L x 2000), reduced to the first fftshift-ed argmax
+//      without storing the spectrum.
+//
+// A length-S transform does not fit one CU's LDS (464 KB of complex fp32), so every
+// transform is a four-step FFT: P-point DFTs down the columns of a P x 2000 view (in
+// registers, one column per lane) and 2000-point DFTs along the rows (Stockham in
+// LDS, radices 5 5 5 16), with the four-step twiddle folded into the neighbouring pass.
+// Correlator passes, loads and epilogues fused:
+//   forward  F1: rows  x[P*n1 + n2] (carrier wipe / code replica built on the fly)
+//                -> B[n2][k1] * w_S^(-n2*k1)
+//            F2: cols  DFT_P over n2 -> X[k1 + 2000*k2] (natural order)
+//   inverse  I1: cols  Z[k] = C_p[k] * conj(X_{ms,bin}[k]) (acquisition.m:57-59),
+//                DFT_P over k2, * w_S^(+k1*tau2) -> A[tau2][k1]
+//            I2: rows  DFT_2000 over k1 -> y[tau2 + P*tau1]; |y|^2 / S^2 summed over
+//                the ms in order (acquisition.m:53-61) in registers -> corr[tau2][tau1]
+// The correlation surface is stored tau2-major ("permuted"); the detector maps
+// storage index s = tau2*2000 + tau1 to the code phase tau = tau2 + P*tau1.
+#include "gnss_internal.h"
+
+// FFT values need no bit-for-bit replay of the reference: let the compiler fuse.
+#pragma clang fp contract(fast)
+
+namespace gnss {
+
+namespace {
+
+constexpr int kRow = 2000;      // row length, 5*5*5*16
+constexpr int kRowThreads = 256;
+constexpr int kColThreads = 256;
+
+// cos/sin(2*pi*m/P) (tools/gen_dft_consts.py 13 29); the fp32 kernels round them
+template <int P> struct PrimeTab;
+template <> struct PrimeTab<13> {
+    static constexpr double c[13] = {1.0, 0.8854560256532099, 0.5680647467311559, 0.120536680255323, -0.35460488704253545, -0.7485107481711012, -0.970941817426052, -0.9709418174260521, -0.7485107481711013, -0.3546048870425359, 0.1205366802553232, 0.5680647467311548, 0.88545602565321};
+    static constexpr double s[13] = {0.0, 0.4647231720437685, 0.8229838658936564, 0.992708874098054, 0.9350162426854148, 0.6631226582407952, 0.23931566428755768, -0.23931566428755743, -0.663122658240795, -0.9350162426854147, -0.992708874098054, -0.822983865893657, -0.4647231720437684};
+};
+template <> struct PrimeTab<29> {
+    static constexpr double c[29] = {1.0, 0.9766205557100867, 0.907575419670957, 0.7960930657056438, 0.6473862847818277, 0.46840844069979015, 0.26752833852922075, 0.05413890858541761, -0.16178199655276473, -0.37013815533991423, -0.5611870653623823, -0.7259954919231306, -0.8568571761675893, -0.9476531711828025, -0.9941379571543596, -0.9941379571543597, -0.9476531711828025, -0.8568571761675892, -0.7259954919231311, -0.5611870653623825, -0.37013815533991445, -0.16178199655276476, 0.0541389085854167, 0.2675283385292201, 0.4684084406997903, 0.6473862847818279, 0.796093065705644, 0.9075754196709569, 0.9766205557100867};
+    static constexpr double s[29] = {0.0, 0.21497044021102407, 0.4198891015602646, 0.6051742151937652, 0.7621620551276365, 0.8835120444460229, 0.963549992519223, 0.9985334138511238, 0.9868265225415261, 0.9289767198167915, 0.8276889981568906, 0.6876994588534235, 0.5155538571770216, 0.3193015301359798, 0.10811901842394192, -0.10811901842394124, -0.31930153013597995, -0.5155538571770218, -0.6876994588534231, -0.8276889981568905, -0.9289767198167914, -0.9868265225415261, -0.9985334138511239, -0.9635499925192231, -0.8835120444460228, -0.7621620551276362, -0.6051742151937649, -0.41988910156026493, -0.21497044021102438};
+};
+
+template <class V> struct RealOf;
+template <> struct RealOf<float2> { using T = float; };
+template <> struct RealOf<double2> { using T = double; };
+template <class V> using Re = typename RealOf<V>::T;
+
+template <class V> __device__ __forceinline__ V mk(Re<V> x, Re<V> y)
+{
+    V r;
+    r.x = x;
+    r.y = y;
+    return r;
+}
+template <class V> __device__ __forceinline__ V cadd(V a, V b) { return mk<V>(a.x + b.x, a.y + b.y); }
+template <class V> __device__ __forceinline__ V csub(V a, V b) { return mk<V>(a.x - b.x, a.y - b.y); }
+template <class V> __device__ __forceinline__ V cmul(V a, V b)
+{
+    return mk<V>(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+template <class V> __device__ __forceinline__ V cmulc(V a, V b)  // a * conj(b)
+{
+    return mk<V>(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
+}
+// multiply by -j (DIR = -1, forward) or +j (DIR = +1, inverse)
+template <int DIR, class V> __device__ __forceinline__ V mul_dj(V a)
+{
+    return DIR < 0 ? mk<V>(a.y, -a.x) : mk<V>(-a.y, a.x);
+}
+// multiply by tw (forward) or conj(tw) (inverse); tables hold e^{-j...}
+template <int DIR, class V> __device__ __forceinline__ V twid(V a, V tw)
+{
+    return DIR < 0 ? cmul(a, tw) : cmulc(a, tw);
+}
+
+// ---- small DFTs in registers; DIR = -1: X[k] = sum x[n] e^{-j2pi nk/N}, +1: e^{+j..}
+template <int DIR, class V> __device__ __forceinline__ void dft4(V& a, V& b, V& c, V& d)
+{
+    const V t0 = cadd(a, c), t1 = csub(a, c), t2 = cadd(b, d), t3 = mul_dj<DIR>(csub(b, d));
+    a = cadd(t0, t2);
+    c = csub(t0, t2);
+    b = cadd(t1, t3);
+    d = csub(t1, t3);
+}
+
+template <int DIR, class V> __device__ __forceinline__ void dft5(V (&v)[5])
+{
+    using R = Re<V>;
+    constexpr R c1 = (R)0.30901699437494745, c2 = (R)-0.8090169943749475;  // cos(2pi/5), cos(4pi/5)
+    constexpr R s1 = (R)0.9510565162951535, s2 = (R)0.5877852522924731;    // sin(2pi/5), sin(4pi/5)
+    const V t1 = cadd(v[1], v[4]), t2 = cadd(v[2], v[3]);
+    const V t3 = csub(v[1], v[4]), t4 = csub(v[2], v[3]);
+    const V b1 = mk<V>(v[0].x + c1 * t1.x + c2 * t2.x, v[0].y + c1 * t1.y + c2 * t2.y);
+    const V b2 = mk<V>(v[0].x + c2 * t1.x + c1 * t2.x, v[0].y + c2 * t1.y + c1 * t2.y);
+    const V e1 = mul_dj<DIR>(mk<V>(s1 * t3.x + s2 * t4.x, s1 * t3.y + s2 * t4.y));
+    const V e2 = mul_dj<DIR>(mk<V>(s2 * t3.x - s1 * t4.x, s2 * t3.y - s1 * t4.y));
+    v[0] = mk<V>(v[0].x + t1.x + t2.x, v[0].y + t1.y + t2.y);
+    v[1] = cadd(b1, e1);
+    v[4] = csub(b1, e1);
+    v[2] = cadd(b2, e2);
+    v[3] = csub(b2, e2);
+}
+
+// 10 = 2 x 5: even/odd 5-point DFTs and one radix-2 combine
+template <int DIR, class V> __device__ __forceinline__ void dft10(V (&v)[10])
+{
+    using R = Re<V>;
+    constexpr R c[5] = {(R)1.0, (R)0.8090169943749475, (R)0.30901699437494745, (R)-0.30901699437494745,
+                        (R)-0.8090169943749475};  // cos(2 pi k/10)
+    constexpr R s[5] = {(R)0.0, (R)0.5877852522924731, (R)0.9510565162951535, (R)0.9510565162951535,
+                        (R)0.5877852522924731};   // sin(2 pi k/10)
+    V e[5] = {v[0], v[2], v[4], v[6], v[8]}, o[5] = {v[1], v[3], v[5], v[7], v[9]};
+    dft5<DIR>(e);
+    dft5<DIR>(o);
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        const V t = cmul(o[k], mk<V>(c[k], DIR < 0 ? -s[k] : s[k]));
+        v[k] = cadd(e[k], t);
+        v[k + 5] = csub(e[k], t);
+    }
+}
+
+constexpr double kC16 = 0.9238795325112867, kS16 = 0.3826834323650898, kR2 = 0.7071067811865476;
+constexpr double kTc16[10] = {1., kC16, kR2, kS16, 0., -kS16, -kR2, -kC16, -1., -kC16};  // cos(2 pi m/16)
+constexpr double kTs16[10] = {0., kS16, kR2, kC16, 1., kC16, kR2, kS16, 0., -kS16};    // sin(2 pi m/16)
+
+// 16 = 4 x 4: x index n = 4*n1 + n2, output k = k1 + 4*k2, natural order in v
+template <int DIR, class V> __device__ __forceinline__ void dft16(V (&v)[16])
+{
+    using R = Re<V>;
+#pragma unroll
+    for (int n2 = 0; n2 < 4; n2++) dft4<DIR>(v[n2], v[4 + n2], v[8 + n2], v[12 + n2]);
+    // y[n2][k1] sits in v[4*k1 + n2]; twiddle w16^(n2*k1)
+#pragma unroll
+    for (int k1 = 1; k1 < 4; k1++)
+#pragma unroll
+        for (int n2 = 1; n2 < 4; n2++) {
+            const int m = n2 * k1;  // <= 9
+            const V w = mk<V>((R)kTc16[m], DIR < 0 ? (R)-kTs16[m] : (R)kTs16[m]);
+            v[4 * k1 + n2] = cmul(v[4 * k1 + n2], w);
+        }
+    V o[16];
+#pragma unroll
+    for (int k1 = 0; k1 < 4; k1++) {
+        V a = v[4 * k1], b = v[4 * k1 + 1], c = v[4 * k1 + 2], d = v[4 * k1 + 3];
+        dft4<DIR>(a, b, c, d);
+        o[k1] = a; o[k1 + 4] = b; o[k1 + 8] = c; o[k1 + 12] = d;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; i++) v[i] = o[i];
+}
+
+// P-point DFT (P odd prime) by conjugate-pair symmetry: 4*((P-1)/2)^2 FMAs. The pairs
+// a_n = x_n + x_{P-n}, d_n = x_n - x_{P-n} overwrite v; outputs go through `put(k, X_k)`.
+template <int P, int DIR, class V, class Put>
+__device__ __forceinline__ void dft_prime(V (&v)[P], Put put)
+{
+    using R = Re<V>;
+    constexpr int H = (P - 1) / 2;
+    using T = PrimeTab<P>;
+    const V x0 = v[0];
+    V sum = x0;
+#pragma unroll
+    for (int n = 1; n <= H; n++) {
+        const V a = cadd(v[n], v[P - n]), d = csub(v[n], v[P - n]);
+        v[n] = a;
+        v[P - n] = d;
+        sum = cadd(sum, a);
+    }
+    put(0, sum);
+#pragma unroll
+    for (int k = 1; k <= H; k++) {
+        R re = x0.x, im = x0.y, sr = 0, si = 0;
+#pragma unroll
+        for (int n = 1; n <= H; n++) {
+            const int m = (n * k) % P;
+            re += v[n].x * (R)T::c[m];
+            im += v[n].y * (R)T::c[m];
+            sr += v[P - n].y * (R)T::s[m];
+            si += v[P - n].x * (R)T::s[m];
+        }
+        // sum_n d_n * (-+ j sin): forward (e^{-j}) adds (+sr, -si)
+        if (DIR < 0) {
+            put(k, mk<V>(re + sr, im - si));
+            put(P - k, mk<V>(re - sr, im + si));
+        } else {
+            put(k, mk<V>(re - sr, im + si));
+            put(P - k, mk<V>(re + sr, im - si));
+        }
+    }
+}
+
+// ---- 2000-point Stockham in LDS (one buffer: every stage reads to registers, syncs,
+// writes): radices 5, 5, 5, 16 (Ns = 1, 5, 25, 125), natural order at the end.
+// tw[m] = e^{-j 2 pi m / 2000}. Callers sync after filling `a`.
+template <int DIR, int NS, class V>
+__device__ __forceinline__ void stage5(V* a, const V* tw, int tid)
+{
+    constexpr int NB = kRow / 5, PER = (NB + kRowThreads - 1) / kRowThreads;
+    V v[PER][5];
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int j0 = tid + q * kRowThreads, j = j0 < NB ? j0 : NB - 1;
+        const int k = j % NS;
+#pragma unroll
+        for (int i = 0; i < 5; i++) v[q][i] = a[j + i * NB];
+        if (NS > 1) {
+#pragma unroll
+            for (int i = 1; i < 5; i++) v[q][i] = twid<DIR>(v[q][i], tw[i * k * (kRow / (NS * 5))]);
+        }
+        dft5<DIR>(v[q]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int j = tid + q * kRowThreads;
+        if (j < NB) {
+            const int k = j % NS, d = (j / NS) * NS * 5 + k;
+#pragma unroll
+            for (int i = 0; i < 5; i++) a[d + i * NS] = v[q][i];
+        }
+    }
+    __syncthreads();
+}
+
+template <int DIR, class V>
+__device__ __forceinline__ void fft2000(V* a, const V* tw, int tid)
+{
+    stage5<DIR, 1>(a, tw, tid);
+    stage5<DIR, 5>(a, tw, tid);
+    stage5<DIR, 25>(a, tw, tid);
+    constexpr int NB = kRow / 16;  // radix 16, Ns = 125: k = j
+    const int j = tid < NB ? tid : NB - 1;
+    V v[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) v[i] = a[j + i * NB];
+#pragma unroll
+    for (int i = 1; i < 16; i++) v[i] = twid<DIR>(v[i], tw[i * j]);
+    dft16<DIR>(v);
+    __syncthreads();
+    if (tid < NB) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) a[tid + i * NB] = v[i];
+    }
+    __syncthreads();
+}
+
+template <class V>
+__device__ __forceinline__ void load_row_tw(V* s_tw, const V* tw_row, int tid)
+{
+    for (int i = tid; i < kRow; i += kRowThreads) s_tw[i] = tw_row[i];
+}
+
+// ============================== correlator (fp32) =================================
+
+// ---- F1: forward rows. Transform s < nsig: rawsignal(ms) .* carrier(bin) (acquisition.m:41-44,56);
+// s >= nsig: the code replica of PRN s - nsig (acquisition.m:49-51). Row n2 holds
+// x[P*n1 + n2]; output B[s][n2][k1] * w_S^(-n2*k1).
+template <int P>
+__global__ __launch_bounds__(kRowThreads) void fwd_rows_kernel(
+    const int8_t* __restrict__ iq, int nbins, int nsig, double IF, double freqMin, double freqStep,
+    double Fs, const float* __restrict__ ca, double code_step, const float2* __restrict__ tw_row,
+    const float2* __restrict__ tw_col, float2* __restrict__ B)
+{
+    constexpr int64_t S = (int64_t)P * kRow;
+    __shared__ float2 s_a[kRow], s_tw[kRow];
+    const int n2 = blockIdx.x, s = blockIdx.y, tid = threadIdx.x;
+    load_row_tw(s_tw, tw_row, tid);
+    if (s < nsig) {
+        const int idx = s / nbins, bin = s - idx * nbins;
+        const double f = (IF + (freqMin + freqStep * (double)bin)) / Fs;  // cycles per sample
+        const int8_t* x = iq + 2 * (int64_t)idx * S;
+        for (int n1 = tid; n1 < kRow; n1 += kRowThreads) {
+            const int64_t n = (int64_t)P * n1 + n2;
+            double cyc = f * (double)(n + 1);  // n is 1-based in the reference
+            cyc -= floor(cyc);
+            const float ph = (float)cyc;
+            const float c = __builtin_amdgcn_cosf(ph), sn = __builtin_amdgcn_sinf(ph);
+            const char2 r = *reinterpret_cast<const char2*>(x + 2 * n);
+            const float xr = (float)r.x, xi = (float)r.y;
+            s_a[n1] = make_float2(xr * c - xi * sn, xr * sn + xi * c);
+        }
+    } else {
+        const float* cp = ca + (int64_t)(s - nsig) * 1023;
+        for (int n1 = tid; n1 < kRow; n1 += kRowThreads) {
+            const int64_t n = (int64_t)P * n1 + n2;
+            const int64_t ci = (int64_t)ceil((double)(n + 1) * code_step);  // 1-based into [CA CA]
+            s_a[n1] = make_float2(cp[(ci - 1) % 1023], 0.f);
+        }
+    }
+    __syncthreads();
+    fft2000<-1>(s_a, s_tw, tid);
+    float2* o = B + ((int64_t)s * P + n2) * kRow;
+    const float2* twc = tw_col + (int64_t)n2 * kRow;
+    for (int k1 = tid; k1 < kRow; k1 += kRowThreads) o[k1] = cmul(s_a[k1], twc[k1]);
+}
+
+// ---- F2: forward columns: X[s][k1 + 2000*k2] = DFT_P over n2 of B[s][n2][k1]
+template <int P>
+__global__ __launch_bounds__(kColThreads) void fwd_cols_kernel(const float2* __restrict__ B,
+                                                              float2* __restrict__ X)
+{
+    const int k1 = blockIdx.x * kColThreads + threadIdx.x, s = blockIdx.y;
+    if (k1 >= kRow) return;
+    const float2* b = B + (int64_t)s * P * kRow + k1;
+    float2 v[P];
+#pragma unroll
+    for (int i = 0; i < P; i++) v[i] = b[(int64_t)i * kRow];
+    float2* x = X + (int64_t)s * P * kRow + k1;
+    dft_prime<P, -1>(v, [&](int k, float2 y) { x[(int64_t)k * kRow] = y; });
+}
+
+// ---- I1: inverse columns of Z = C_p .* conj(X_{ms,bin}) for transform t = (pair, ms)
+// of this batch; pair q = first_pair + t / datalen -> bin = q / nprn, p = q % nprn.
+template <int P>
+__global__ __launch_bounds__(kColThreads) void inv_cols_kernel(
+    const float2* __restrict__ C, const float2* __restrict__ X, int nbins, int nprn, int datalen,
+    int first_pair, const float2* __restrict__ tw_col, float2* __restrict__ A)
+{
+    const int k1 = blockIdx.x * kColThreads + threadIdx.x, t = blockIdx.y;
+    if (k1 >= kRow) return;
+    const int q = first_pair + t / datalen, idx = t % datalen;
+    const int bin = q / nprn, p = q - bin * nprn;
+    const float2* c = C + (int64_t)p * P * kRow + k1;
+    const float2* x = X + ((int64_t)idx * nbins + bin) * P * kRow + k1;
+    float2 v[P];
+#pragma unroll
+    for (int i = 0; i < P; i++) v[i] = cmulc(c[(int64_t)i * kRow], x[(int64_t)i * kRow]);
+    float2* a = A + (int64_t)t * P * kRow + k1;
+    const float2* tw = tw_col + k1;
+    dft_prime<P, 1>(v, [&](int k, float2 y) {
+        a[(int64_t)k * kRow] = cmulc(y, tw[(int64_t)k * kRow]);
+    });
+}
+
+// ---- I2: inverse rows, |.|^2/S^2 summed over the ms in order, stored tau2-major.
+template <int P>
+__global__ __launch_bounds__(kRowThreads) void inv_rows_kernel(
+    const float2* __restrict__ A, int nprn, int datalen, int first_pair, float scale,
+    const float2* __restrict__ tw_row, float* __restrict__ corr, int nbins)
+{
+    constexpr int Q = (kRow + kRowThreads - 1) / kRowThreads;
+    constexpr int V4 = kRow / 2;  // float4 = two complex
+    constexpr int QV = (V4 + kRowThreads - 1) / kRowThreads;
+    static_assert(QV == 4, "row copy is written for 4 float4 per lane");
+    // s_a is padded to QV*256 float4 so the row copy needs no bounds test
+    __shared__ float4 s_a4[QV * kRowThreads];
+    __shared__ float2 s_tw[kRow];
+    float2* s_a = reinterpret_cast<float2*>(s_a4);
+    const int tau2 = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
+    load_row_tw(s_tw, tw_row, tid);
+    float acc[Q];
+#pragma unroll
+    for (int i = 0; i < Q; i++) acc[i] = 0.f;
+    const float4* src = reinterpret_cast<const float4*>(A + ((int64_t)g * datalen * P + tau2) * kRow);
+    // clamped: every lane loads, only e < V4 is used (named registers: an array here
+    // ends up in scratch)
+    auto ld = [&](const float4* p, int i) {
+        const int e = tid + i * kRowThreads;
+        return p[e < V4 ? e : V4 - 1];
+    };
+    float4 n0 = ld(src, 0), n1 = ld(src, 1), n2 = ld(src, 2), n3 = ld(src, 3);
+    for (int idx = 0; idx < datalen; idx++) {
+        s_a4[tid] = n0;
+        s_a4[tid + kRowThreads] = n1;
+        s_a4[tid + 2 * kRowThreads] = n2;
+        s_a4[tid + 3 * kRowThreads] = n3;
+        if (idx + 1 < datalen) {  // prefetch the next ms while this one transforms
+            const float4* s2 = src + (int64_t)(idx + 1) * P * V4;
+            n0 = ld(s2, 0); n1 = ld(s2, 1); n2 = ld(s2, 2); n3 = ld(s2, 3);
+        }
+        __syncthreads();
+        fft2000<1>(s_a, s_tw, tid);
+#pragma unroll
+        for (int i = 0; i < Q; i++) {
+            const int t1 = tid + i * kRowThreads;
+            const float2 v = s_a[t1 < kRow ? t1 : kRow - 1];
+            acc[i] += (v.x * v.x + v.y * v.y) * scale;
+        }
+        __syncthreads();
+    }
+    const int q = first_pair + g;
+    const int bin = q / nprn, p = q - bin * nprn;
+    float* o = corr + (((int64_t)p * nbins + bin) * P + tau2) * kRow;
+#pragma unroll
+    for (int i = 0; i < Q; i++) {
+        const int t1 = tid + i * kRowThreads;
+        if (t1 < kRow) o[t1] = acc[i];
+    }
+}
+
+// ============================== fine frequency (fp64) =============================
+// x[n] = longrawsignal(S-cd + n) .* CA(rem(floor((n+1)/Fs*fc), 1023)+1), n < M = L*S
+// (acquisition.m:103-106); X[k] = DFT_N of x zero-padded to N = M*D (:108), D = datalen.
+// X[D*q + r] = DFT_M(y_r)[q], y_r[n] = x[n] w_N^(-n r). M = P*T*R (T = L = 10, R = 2000):
+//   n = P*T*m1 + P*m2 + n2, q = j1 + R*j2 + T*R*k2.
+// FR (rows): DFT_R over m1 of y_r[P*T*m1 + P*m2 + n2] (w_N^(-n r) = w_{R*D}^(-m1 r) *
+//            w_N^(-(P*m2 + n2) r), the second factor applied after the DFT), * w_{T*R}^(-m2*j1)
+//            -> E[r][n2][m2][j1]
+// FC (cols): per (n2, j1) DFT_T over m2, * w_M^(-n2*(j1 + R*j2)); per (j1, j2) DFT_P over n2
+//            -> |X| and the first maximum in fftshift order (:110-116)
+
+constexpr int kFineT = 10;
+constexpr int kFineJC = 8;  // j1 columns per FC block
+
+__global__ void fine_twiddle_kernel(double2* __restrict__ t, int64_t len)
+{
+    const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= len) return;
+    double s, c;
+    sincospi(-2.0 * (double)m / (double)len, &s, &c);
+    t[m] = make_double2(c, s);
+}
+
+template <int P>
+__global__ __launch_bounds__(kRowThreads) void fine_rows_kernel(
+    const int8_t* __restrict__ iq, int64_t base, const float* __restrict__ ca, double invFs,
+    double invFc, double codelength, int D, int64_t N, const double2* __restrict__ tw_row,
+    const double2* __restrict__ tabA, const double2* __restrict__ tabB, double2* __restrict__ E)
+{
+    constexpr int T = kFineT;
+    __shared__ double2 s_a[kRow], s_tw[kRow];
+    const int rho = blockIdx.x, r = blockIdx.y, tid = threadIdx.x;
+    const int m2 = rho / P, n2 = rho - m2 * P;
+    load_row_tw(s_tw, tw_row, tid);
+    const int64_t RD = (int64_t)kRow * D;
+    for (int m1 = tid; m1 < kRow; m1 += kRowThreads) {
+        const int64_t n = (int64_t)P * T * m1 + (int64_t)P * m2 + n2;
+        const double cvi = floor((invFs * (double)(n + 1)) / invFc);
+        const double code = (double)ca[(int64_t)fmod(cvi, codelength)];
+        const char2 raw = *reinterpret_cast<const char2*>(iq + 2 * (base + n));
+        const double2 x = make_double2((double)raw.x * code, (double)raw.y * code);
+        s_a[m1] = cmul(x, tabA[((int64_t)m1 * r) % RD]);
+    }
+    __syncthreads();
+    fft2000<-1>(s_a, s_tw, tid);
+    double sn, cs;
+    const int64_t e = ((int64_t)(P * m2 + n2) * r) % N;
+    sincospi(-2.0 * (double)e / (double)N, &sn, &cs);
+    const double2 cb = make_double2(cs, sn);
+    double2* o = E + (((int64_t)r * P + n2) * T + m2) * kRow;
+    for (int j1 = tid; j1 < kRow; j1 += kRowThreads)
+        o[j1] = cmul(cmul(s_a[j1], cb), tabB[((int64_t)m2 * j1) % ((int64_t)T * kRow)]);
+}
+
+struct FineBest {
+    double m;
+    int64_t i;
+};
+
+__device__ __forceinline__ void best_merge(double& m, int64_t& i, double m2, int64_t i2)
+{
+    if (m2 > m || (m2 == m && i2 < i)) { m = m2; i = i2; }
+}
+
+template <int P>
+__global__ __launch_bounds__(kColThreads) void fine_cols_kernel(
+    const double2* __restrict__ E, int D, int64_t N, int shifted, const double2* __restrict__ tabM,
+    FineBest* __restrict__ part)
+{
+    constexpr int T = kFineT, JC = kFineJC;
+    constexpr int64_t M = (int64_t)P * T * kRow;
+    __shared__ double2 s_e[P * T * JC];  // [n2][m2 -> j2][jj]
+    __shared__ FineBest s_b[kColThreads / 64];
+    const int r = blockIdx.y, j10 = blockIdx.x * JC, tid = threadIdx.x;
+    for (int e = tid; e < P * T * JC; e += kColThreads) {
+        const int jj = e % JC, nm = e / JC;  // nm = n2*T + m2
+        s_e[e] = E[((int64_t)r * P * T + nm) * kRow + j10 + jj];
+    }
+    __syncthreads();
+    // DFT_T over m2 for each (n2, jj), twiddle w_M^(-n2*k1)
+    for (int pr = tid; pr < P * JC; pr += kColThreads) {
+        const int n2 = pr / JC, jj = pr - n2 * JC;
+        double2 v[T];
+#pragma unroll
+        for (int m2 = 0; m2 < T; m2++) v[m2] = s_e[(n2 * T + m2) * JC + jj];
+        dft10<-1>(v);
+#pragma unroll
+        for (int j2 = 0; j2 < T; j2++) {
+            const int64_t k1 = j10 + jj + (int64_t)kRow * j2;
+            s_e[(n2 * T + j2) * JC + jj] = cmul(v[j2], tabM[((int64_t)n2 * k1) % M]);
+        }
+    }
+    __syncthreads();
+    double bm = -1.0;
+    int64_t bi = INT64_MAX;
+    const int64_t half = N / 2;
+    for (int pr = tid; pr < T * JC; pr += kColThreads) {
+        const int j2 = pr / JC, jj = pr - j2 * JC;
+        double2 v[P];
+#pragma unroll
+        for (int n2 = 0; n2 < P; n2++) v[n2] = s_e[(n2 * T + j2) * JC + jj];
+        const int64_t k1 = j10 + jj + (int64_t)kRow * j2;
+        dft_prime<P, -1>(v, [&](int k2, double2 y) {
+            const int64_t q = k1 + (int64_t)T * kRow * k2;
+            const int64_t k = (int64_t)D * q + r;  // natural bin of the N-point FFT
+            int64_t i = k;
+            if (shifted) { i = k + half; if (i >= N) i -= N; }
+            best_merge(bm, bi, hypot(y.x, y.y), i);
+        });
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double m2 = __shfl_xor(bm, o, 64);
+        const int64_t i2 = __shfl_xor(bi, o, 64);
+        best_merge(bm, bi, m2, i2);
+    }
+    if ((tid & 63) == 0) s_b[tid >> 6] = FineBest{bm, bi};
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < kColThreads / 64; w++) best_merge(bm, bi, s_b[w].m, s_b[w].i);
+        part[(int64_t)r * gridDim.x + blockIdx.x] = FineBest{bm, bi};
+    }
+}
+
+__global__ void fine_best_final_kernel(const FineBest* __restrict__ part, int nblk,
+                                       int64_t* __restrict__ kbest)
+{
+    double bm = -1.0;
+    int64_t bi = INT64_MAX;
+    for (int k = threadIdx.x; k < nblk; k += blockDim.x) best_merge(bm, bi, part[k].m, part[k].i);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double m2 = __shfl_xor(bm, o, 64);
+        const int64_t i2 = __shfl_xor(bi, o, 64);
+        best_merge(bm, bi, m2, i2);
+    }
+    __shared__ FineBest s_b[4];
+    if ((threadIdx.x & 63) == 0) s_b[threadIdx.x >> 6] = FineBest{bm, bi};
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); w++) best_merge(bm, bi, s_b[w].m, s_b[w].i);
+        *kbest = bi + 1;  // 1-based FreqPeakIndex
+    }
+}
+
+}  // namespace
+
+bool acq_fft_supported(int64_t S) { return S == 13 * kRow || S == 29 * kRow; }
+
+// The forward spectra: X[s] for s < nsig ((ms, bin) signals, s = ms*nbins + bin) and the
+// code spectra C[p] (stored after them: X + nsig*S).
+hipError_t launch_acq_fft_forward(const int8_t* iq, int64_t S, int datalen, int nbins, double IF,
+                                  double freqMin, double freqStep, double Fs, const float* ca,
+                                  int nprn, double codeFreqBasis, const float2* tw_row,
+                                  const float2* tw_col, float2* B, float2* X, hipStream_t s)
+{
+    const int nsig = datalen * nbins, ntr = nsig + nprn;
+    const double step = codeFreqBasis / Fs;
+#define GNSS_FWD(P_)                                                                            \
+    if (S == (int64_t)P_ * kRow) {                                                              \
+        hipLaunchKernelGGL(fwd_rows_kernel<P_>, dim3(P_, ntr), dim3(kRowThreads), 0, s, iq, nbins, \
+                           nsig, IF, freqMin, freqStep, Fs, ca, step, tw_row, tw_col, B);       \
+        hipLaunchKernelGGL(fwd_cols_kernel<P_>, dim3((kRow + kColThreads - 1) / kColThreads, ntr), \
+                           dim3(kColThreads), 0, s, B, X);                                      \
+        return hipGetLastError();                                                               \
+    }
+    GNSS_FWD(13) GNSS_FWD(29)
+#undef GNSS_FWD
+    return hipErrorInvalidValue;
+}
+
+// Correlation of (bin, PRN) pairs [first_pair, first_pair + npair) (pair = bin*nprn + p)
+// over every ms: corr[p][bin] (tau2-major) = sum_ms |ifft(C_p .* conj(X_{ms,bin}))|^2.
+hipError_t launch_acq_fft_correlate(const float2* C, const float2* X, int64_t S, int datalen,
+                                    int nbins, int nprn, int first_pair, int npair,
+                                    const float2* tw_row, const float2* tw_col, float2* A,
+                                    float* corr, hipStream_t s)
+{
+    const float scale = (float)(1.0 / ((double)S * (double)S));  // ifft's 1/N, squared
+#define GNSS_INV(P_)                                                                            \
+    if (S == (int64_t)P_ * kRow) {                                                              \
+        hipLaunchKernelGGL(inv_cols_kernel<P_>,                                                 \
+                           dim3((kRow + kColThreads - 1) / kColThreads, npair * datalen),       \
+                           dim3(kColThreads), 0, s, C, X, nbins, nprn, datalen, first_pair,     \
+                           tw_col, A);                                                          \
+        hipLaunchKernelGGL(inv_rows_kernel<P_>, dim3(P_, npair), dim3(kRowThreads), 0, s, A, nprn, \
+                           datalen, first_pair, scale, tw_row, corr, nbins);                    \
+        return hipGetLastError();                                                               \
+    }
+    GNSS_INV(13) GNSS_INV(29)
+#undef GNSS_INV
+    return hipErrorInvalidValue;
+}
+
+bool fine_fft_supported(int64_t S, int L) { return acq_fft_supported(S) && L == kFineT; }
+
+size_t fine_fft_scratch_bytes(int64_t S, int L, int datalen)
+{
+    const int64_t M = (int64_t)L * S;
+    return sizeof(double2) * (size_t)(M * datalen + kRow + (int64_t)kRow * datalen +
+                                      (int64_t)kFineT * kRow + M) +
+           sizeof(FineBest) * (size_t)datalen * (kRow / kFineJC);
+}
+
+// Twiddle tables of the fine search, once per call: w_2000, w_{2000*D}, w_{T*2000}, w_M.
+hipError_t launch_fine_fft_tables(int64_t S, int L, int datalen, void* scratch, hipStream_t s)
+{
+    const int64_t M = (int64_t)L * S;
+    double2* E = static_cast<double2*>(scratch);
+    double2* tw_row = E + M * datalen;
+    double2* tabA = tw_row + kRow;
+    double2* tabB = tabA + (int64_t)kRow * datalen;
+    double2* tabM = tabB + (int64_t)kFineT * kRow;
+    const int64_t lens[4] = {kRow, (int64_t)kRow * datalen, (int64_t)kFineT * kRow, M};
+    double2* tabs[4] = {tw_row, tabA, tabB, tabM};
+    for (int t = 0; t < 4; t++)
+        hipLaunchKernelGGL(fine_twiddle_kernel, dim3((unsigned)((lens[t] + 255) / 256)), dim3(256), 0,
+                           s, tabs[t], lens[t]);
+    return hipGetLastError();
+}
+
+// First fftshift-ed argmax (1-based) of |fft(CarrSignal, N)| for one SV (acquisition.m:103-116).
+hipError_t launch_fine_fft_argmax(const int8_t* iq, int64_t S, int L, int datalen, int64_t base,
+                                  const float* ca, double Fs, double codeFreqBasis,
+                                  double codelength, int shifted, void* scratch, int64_t* kbest,
+                                  hipStream_t s)
+{
+    const int64_t M = (int64_t)L * S, N = M * datalen;
+    double2* E = static_cast<double2*>(scratch);
+    double2* tw_row = E + M * datalen;
+    double2* tabA = tw_row + kRow;
+    double2* tabB = tabA + (int64_t)kRow * datalen;
+    double2* tabM = tabB + (int64_t)kFineT * kRow;
+    FineBest* part = reinterpret_cast<FineBest*>(tabM + M);
+    const int nblk = kRow / kFineJC;
+#define GNSS_FINE(P_)                                                                           \
+    if (S == (int64_t)P_ * kRow) {                                                              \
+        hipLaunchKernelGGL(fine_rows_kernel<P_>, dim3(P_ * kFineT, datalen), dim3(kRowThreads), 0, s, \
+                           iq, base, ca, 1 / Fs, 1 / codeFreqBasis, codelength, datalen, N,     \
+                           tw_row, tabA, tabB, E);                                              \
+        hipLaunchKernelGGL(fine_cols_kernel<P_>, dim3(nblk, datalen), dim3(kColThreads), 0, s, E, \
+                           datalen, N, shifted, tabM, part);                                    \
+        hipLaunchKernelGGL(fine_best_final_kernel, dim3(1), dim3(256), 0, s, part, nblk * datalen, \
+                           kbest);                                                              \
+        return hipGetLastError();                                                               \
+    }
+    GNSS_FINE(13) GNSS_FINE(29)
+#undef GNSS_FINE
+    return hipErrorInvalidValue;
+}
+
+}  // namespace gnss

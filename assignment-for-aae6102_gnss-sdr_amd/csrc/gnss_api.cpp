@@ -384,14 +384,57 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     std::vector<float> cah((size_t)np * 1023);
     for (int i = 0; i < np; i++) generate_ca(prns[i], &cah[(size_t)i * 1023]);
     DevBuf ca, sig, code, y, corr, peaks, scratch;
+    DevBuf d_twr, d_twc, B, X, A;  // own FFT correlator buffers (freed after the stream drains)
     HIP_TRY(ca.alloc(cah.size() * sizeof(float)));
     HIP_TRY(hipMemcpyAsync(ca.p, cah.data(), cah.size() * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
     const int nsig = dl * nb;
-    HIP_TRY(sig.alloc(sizeof(float2) * (size_t)nsig * S));
-    HIP_TRY(code.alloc(sizeof(float2) * (size_t)np * S));
     HIP_TRY(corr.alloc(sizeof(float) * (size_t)np * nb * S));
     HIP_TRY(peaks.alloc(sizeof(AcqPeak) * (size_t)np));
     HIP_TRY(scratch.alloc(acq_scratch_bytes(np, np)));
+    const bool own_fft = acq_fft_supported(S) && !getenv("GNSS_ACQ_ROCFFT");
+    int perm = 0;
+    Events e_all, e_corr;  // e_corr.b marks the end of the PRN search
+    if (own_fft) {
+        // two-pass FFT correlator (acq_fft.hip): S = P * 2000
+        const int P = (int)(S / 2000);
+        perm = P;
+        std::vector<float2> twr(2000), twc((size_t)P * 2000);
+        for (int m = 0; m < 2000; m++) {
+            const double a = -2.0 * M_PI * (double)m / 2000.0;
+            twr[m] = make_float2((float)std::cos(a), (float)std::sin(a));
+        }
+        for (int m = 0; m < P; m++)
+            for (int k = 0; k < 2000; k++) {
+                const double a = -2.0 * M_PI * (double)((int64_t)m * k % S) / (double)S;
+                twc[(size_t)m * 2000 + k] = make_float2((float)std::cos(a), (float)std::sin(a));
+            }
+        HIP_TRY(d_twr.alloc(twr.size() * sizeof(float2)));
+        HIP_TRY(d_twc.alloc(twc.size() * sizeof(float2)));
+        HIP_TRY(hipMemcpyAsync(d_twr.p, twr.data(), twr.size() * sizeof(float2), hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(d_twc.p, twc.data(), twc.size() * sizeof(float2), hipMemcpyHostToDevice, ctx->stream));
+        const size_t ntr = (size_t)nsig + np;
+        HIP_TRY(B.alloc(sizeof(float2) * ntr * S));
+        HIP_TRY(X.alloc(sizeof(float2) * ntr * S));
+        const int npairs = nb * np;
+        // (bin, PRN) pairs per batch: the inverse intermediate stays ~256 MB (Infinity Cache)
+        int batch = (int)std::max<int64_t>(1, ((int64_t)256 << 20) / ((int64_t)dl * S * 8));
+        if (const char* e = getenv("GNSS_ACQ_BATCH")) batch = std::max(1, atoi(e));
+        batch = std::min(batch, npairs);
+        HIP_TRY(A.alloc(sizeof(float2) * (size_t)batch * dl * S));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        HIP_TRY(hipEventRecord(e_all.a, ctx->stream));
+        HIP_TRY(launch_acq_fft_forward(blk, S, dl, nb, sg->IF, acq->freqMin, acq->freqStep, sg->Fs,
+                                       ca.as<float>(), np, sg->codeFreqBasis, d_twr.as<float2>(),
+                                       d_twc.as<float2>(), B.as<float2>(), X.as<float2>(), ctx->stream));
+        const float2* C = X.as<float2>() + (size_t)nsig * S;
+        for (int q0 = 0; q0 < npairs; q0 += batch) {
+            const int nq = std::min(batch, npairs - q0);
+            HIP_TRY(launch_acq_fft_correlate(C, X.as<float2>(), S, dl, nb, np, q0, nq, d_twr.as<float2>(),
+                                             d_twc.as<float2>(), A.as<float2>(), corr.as<float>(), ctx->stream));
+        }
+    } else {
+    HIP_TRY(sig.alloc(sizeof(float2) * (size_t)nsig * S));
+    HIP_TRY(code.alloc(sizeof(float2) * (size_t)np * S));
     // PRN chunk so the product/IFFT buffer stays <= ~4 GB
     const size_t per_prn = sizeof(float2) * (size_t)nsig * S;
     int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)np, ((size_t)4 << 30) / per_prn));
@@ -406,7 +449,6 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         if ((st = get_plan(ctx, S, (size_t)pc * nsig, 0, 1, &pl))) return st;
     }
 
-    Events e_all, e_corr;  // e_corr.b marks the end of the PRN search
     HIP_TRY(hipEventRecord(e_all.a, ctx->stream));
     HIP_TRY(launch_acq_wipe(blk, S, dl, nb, sg->IF, acq->freqMin, acq->freqStep, sg->Fs, sig.as<float2>(), ctx->stream));
     if ((st = run_fft(ctx, sig.p, S, nsig, 0, 0))) return st;
@@ -418,8 +460,9 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         if ((st = run_fft(ctx, y.p, S, (size_t)pc * nsig, 0, 1))) return st;
         HIP_TRY(launch_acq_power(y.as<float2>(), pc, nb, dl, S, 0, corr.as<float>() + (size_t)p0 * nb * S, ctx->stream));
     }
+    }
     const int cshift = (int)std::ceil(sg->Fs / sg->codeFreqBasis);  // :66
-    HIP_TRY(launch_acq_peak(corr.as<float>(), np, nb, S, cshift, peaks.as<AcqPeak>(), scratch.p, ctx->stream));
+    HIP_TRY(launch_acq_peak(corr.as<float>(), np, nb, S, cshift, perm, peaks.as<AcqPeak>(), scratch.p, ctx->stream));
     HIP_TRY(hipEventRecord(e_corr.b, ctx->stream));
     std::vector<AcqPeak> ph((size_t)np);
     HIP_TRY(hipMemcpyAsync(ph.data(), peaks.p, sizeof(AcqPeak) * (size_t)np, hipMemcpyDeviceToHost, ctx->stream));
@@ -468,19 +511,34 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     DevBuf fca, fcd, fx, kb;
     HIP_TRY(fca.alloc(caf.size() * sizeof(float)));
     HIP_TRY(fcd.alloc(cdh.size() * sizeof(int32_t)));
-    HIP_TRY(fx.alloc(sizeof(double2) * (size_t)na * N));
     HIP_TRY(kb.alloc(sizeof(int64_t) * (size_t)na));
     HIP_TRY(hipMemcpyAsync(fca.p, caf.data(), caf.size() * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(fcd.p, cdh.data(), cdh.size() * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
-    if ((st = get_plan(ctx, N, na, 1, 0, &pl))) return st;
+    const bool own_fine = fine_fft_supported(S, L) && !getenv("GNSS_FINE_ROCFFT");
     Events e_fine;
-    HIP_TRY(hipEventRecord(e_fine.a, ctx->stream));
-    HIP_TRY(launch_fine_build(blk, S, L, fcd.as<int32_t>(), fca.as<float>(), na, sg->Fs, sg->codeFreqBasis,
-                              sg->codelength, N, fx.as<double2>(), ctx->stream));
-    if ((st = run_fft(ctx, fx.p, N, na, 1, 0))) return st;
-    DevBuf fscr;
-    HIP_TRY(fscr.alloc(acq_scratch_bytes(1, na)));
-    HIP_TRY(launch_fine_argmax(fx.as<double2>(), na, N, file->dataType == 2, fscr.p, kb.as<int64_t>(), ctx->stream));
+    if (own_fine) {
+        // per-SV zero-padded FFT as datalen three-level transforms (acq_fft.hip)
+        HIP_TRY(fx.alloc(fine_fft_scratch_bytes(S, L, dl)));
+        HIP_TRY(hipEventRecord(e_fine.a, ctx->stream));
+        HIP_TRY(launch_fine_fft_tables(S, L, dl, fx.p, ctx->stream));
+        for (int k = 0; k < na; k++) {
+            const int64_t base = S - cdh[k] - 1;  // 0-based sample of CarrSignal(1) (:105)
+            HIP_TRY(launch_fine_fft_argmax(blk, S, L, dl, base, fca.as<float>() + (size_t)k * 1023, sg->Fs,
+                                           sg->codeFreqBasis, sg->codelength, file->dataType == 2, fx.p,
+                                           kb.as<int64_t>() + k, ctx->stream));
+        }
+    } else {
+        HIP_TRY(fx.alloc(sizeof(double2) * (size_t)na * N));
+        rocfft_plan pl;
+        if ((st = get_plan(ctx, N, na, 1, 0, &pl))) return st;
+        HIP_TRY(hipEventRecord(e_fine.a, ctx->stream));
+        HIP_TRY(launch_fine_build(blk, S, L, fcd.as<int32_t>(), fca.as<float>(), na, sg->Fs, sg->codeFreqBasis,
+                                  sg->codelength, N, fx.as<double2>(), ctx->stream));
+        if ((st = run_fft(ctx, fx.p, N, na, 1, 0))) return st;
+        DevBuf fscr;
+        HIP_TRY(fscr.alloc(acq_scratch_bytes(1, na)));
+        HIP_TRY(launch_fine_argmax(fx.as<double2>(), na, N, file->dataType == 2, fscr.p, kb.as<int64_t>(), ctx->stream));
+    }
     HIP_TRY(hipEventRecord(e_fine.b, ctx->stream));
     HIP_TRY(hipEventRecord(e_all.b, ctx->stream));
     std::vector<int64_t> kh((size_t)na);

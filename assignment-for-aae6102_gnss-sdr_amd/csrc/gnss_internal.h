@@ -202,7 +202,25 @@ hipError_t launch_acq_mul(const float2* code_spec, const float2* sig_spec, int n
 hipError_t launch_acq_power(const float2* y, int nprn, int nbins, int datalen, int64_t S,
                             int first_ms, float* corr, hipStream_t s);
 hipError_t launch_acq_peak(const float* corr, int nprn, int nbins, int64_t S, int cshift,
-                           AcqPeak* out, void* scratch, hipStream_t s);
+                           int perm, AcqPeak* out, void* scratch, hipStream_t s);
+
+// Two-pass FFT correlator for S = P * 2000 (acq_fft.hip)
+bool acq_fft_supported(int64_t S);
+hipError_t launch_acq_fft_forward(const int8_t* iq, int64_t S, int datalen, int nbins, double IF,
+                                  double freqMin, double freqStep, double Fs, const float* ca,
+                                  int nprn, double codeFreqBasis, const float2* tw_row,
+                                  const float2* tw_col, float2* B, float2* X, hipStream_t s);
+hipError_t launch_acq_fft_correlate(const float2* C, const float2* X, int64_t S, int datalen,
+                                    int nbins, int nprn, int first_pair, int npair,
+                                    const float2* tw_row, const float2* tw_col, float2* A,
+                                    float* corr, hipStream_t s);
+bool fine_fft_supported(int64_t S, int L);
+size_t fine_fft_scratch_bytes(int64_t S, int L, int datalen);
+hipError_t launch_fine_fft_tables(int64_t S, int L, int datalen, void* scratch, hipStream_t s);
+hipError_t launch_fine_fft_argmax(const int8_t* iq, int64_t S, int L, int datalen, int64_t base,
+                                  const float* ca, double Fs, double codeFreqBasis,
+                                  double codelength, int shifted, void* scratch, int64_t* kbest,
+                                  hipStream_t s);
 hipError_t launch_fine_build(const int8_t* iq, int64_t S, int L, const int32_t* codedelay,
                              const float* ca, int nsv, double Fs, double codeFreqBasis,
                              double codelength, int64_t N, double2* out, hipStream_t s);

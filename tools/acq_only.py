@@ -1,0 +1,24 @@
+"""Acquisition-only driver for profiling: BASELINE config 2 (32 PRNs, +-7 kHz / 500 Hz,
+20 ms) on a device-resident synthetic Opensky record. Args: [datalen] [freqNum]."""
+import importlib, os, sys, time
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+pkg = importlib.import_module("assignment-for-aae6102_gnss-sdr_amd")
+dl = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+nb = int(sys.argv[2]) if len(sys.argv) > 2 else 29
+ctx = pkg.Context(0)
+file, signal, acq, track, _, _ = pkg.initParameters()
+skip = 5000
+cfg = pkg.synth.opensky(skip_ms=skip)
+dev = pkg.DeviceRecord(ctx, (skip + 40) * 58000 * 2)
+pkg.synth.generate_device(ctx, cfg, dev)
+file.skip, file.dev = skip, dev
+acq.freqMin, acq.freqNum, acq.datalen = -(nb // 2) * 500, nb, dl
+for it in range(3):
+    t = time.perf_counter()
+    A, d = pkg.acquisition(file, signal, acq, ctx=ctx, diag=True)
+    print("acq wall", time.perf_counter() - t, ctx.timing(), flush=True)
+print("sv", list(A.sv), "cd", list(A.codedelay), "ff", list(A.fineFreq))
+print("fbin", list(d.fbin), "cp", list(d.codePhase))
+print("snr", [round(x, 4) for x in d.SNR])
