@@ -71,7 +71,9 @@ class GnssTiming(C.Structure):
     _fields_ = [("acq_ms", C.c_double), ("acq_corr_ms", C.c_double), ("acq_fine_ms", C.c_double),
                 ("track_ms", C.c_double), ("track_kernel_ms", C.c_double),
                 ("track_launches", C.c_int64), ("track_channel_samples", C.c_int64),
-                ("acq_hypothesis_samples", C.c_int64), ("h2d_ms", C.c_double)]
+                ("acq_hypothesis_samples", C.c_int64), ("h2d_ms", C.c_double),
+                ("track10_kernel_ms", C.c_double), ("track10_launches", C.c_int64),
+                ("track10_channel_samples", C.c_int64)]
 
 
 class GnssSynthSv(C.Structure):

@@ -756,6 +756,7 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     // step launches: K-launch graphs replayed (no host launch cost per step); in
     // profiling mode every launch is bracketed by events instead.
     std::vector<hipEvent_t> pev;
+    std::vector<char> pev10;  // launch of the 10-ms phase
     int64_t launches = 0;
     auto run_steps = [&](int pdi, int count) -> int {
         const int bpc = pdi == 1 ? bpc1 : bpc10, sub = pdi == 1 ? sub1 : sub10;
@@ -772,6 +773,11 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
                 HIP_TRY(hipEventRecord(b, ctx->stream));
                 pev.push_back(a);
                 pev.push_back(b);
+                pev10.push_back(pdi == 10);
+            }
+            if (pdi == 10) {
+                ctx->timing.track10_launches += count;
+                ctx->timing.track10_channel_samples += (int64_t)count * nch * (int64_t)S * pdi;
             }
             return GNSS_OK;
         }
@@ -821,12 +827,14 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     HIP_TRY(hipEventSynchronize(e_all.b));
     ctx->timing.track_ms = e_all.ms();
     ctx->timing.track_launches = launches;
-    double ksum = 0;
+    double ksum = 0, ksum10 = 0;
     for (size_t i = 0; i + 1 < pev.size(); i += 2) {
         float f = 0;
         (void)hipEventElapsedTime(&f, pev[i], pev[i + 1]);
         ksum += f;
+        if (pev10[i / 2]) ksum10 += f;
     }
+    ctx->timing.track10_kernel_ms = ksum10;
     for (auto e : pev) (void)hipEventDestroy(e);
     ctx->timing.track_kernel_ms = ksum;
     if (stamp_path) {

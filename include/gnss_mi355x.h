@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define GNSS_ABI_VERSION 1
+#define GNSS_ABI_VERSION 2
 
 /* ---- status codes (SURVEY §8b "Error conventions") --------------------- */
 #define GNSS_OK         0
@@ -170,6 +170,11 @@ typedef struct gnss_timing {
     int64_t track_channel_samples;   /* channel-samples correlated (all taps)      */
     int64_t acq_hypothesis_samples;  /* PRN x bin x ms x Sample                     */
     double h2d_ms;            /* host->HBM upload of the IF window, if any         */
+    /* profiling mode, the 10-ms phase (trackingCT.m:377-525) alone: the dominant
+     * correlator kernel                                                           */
+    double  track10_kernel_ms;
+    int64_t track10_launches;
+    int64_t track10_channel_samples;
 } gnss_timing;
 
 typedef struct gnss_ctx gnss_ctx;
