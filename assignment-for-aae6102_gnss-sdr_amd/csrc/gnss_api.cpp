@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
+#include <functional>
 #include <fcntl.h>
 #include <map>
 #include <string>
@@ -753,23 +754,90 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         B.stamps = d_stamps.as<unsigned long long>();
     }
 
-    // step launches: K-launch graphs replayed (no host launch cost per step); in
-    // profiling mode every launch is bracketed by events instead.
+    // Persistent step loop (track_run_kernel) when every block of its grid can be
+    // resident: one launch per phase run. Residency from the occupancy query; the kernel's
+    // own census confirms it (the query can over-report, guide section 1) and a launch
+    // that finds a block missing changes nothing and is re-run one launch per step, as
+    // is everything with GNSS_NO_PERSIST.
+    int cus = 0;
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    auto persistent_ok = [&](int bpc, int sub) {
+        if (getenv("GNSS_NO_PERSIST") || bpc > kMaxBpcRun) return false;
+        const int occ = std::min(track_run_blocks_per_cu(P, sub), 4);
+        return occ >= 1 && (int64_t)nch * bpc <= (int64_t)occ * cus;
+    };
+    bool persist1 = persistent_ok(bpc1, sub1), persist10 = persistent_ok(bpc10, sub10);
+    DevBuf d_pgran, d_err;
+    if (persist1 || persist10) {
+        HIP_TRY(d_pgran.alloc(sizeof(unsigned long long) * (size_t)nch * 2 * kMaxBpcRun * 4 * ntaps));
+        HIP_TRY(d_err.alloc(16));
+        HIP_TRY(hipMemsetAsync(d_pgran.p, 0, d_pgran.n, ctx->stream));
+        HIP_TRY(hipMemsetAsync(d_err.p, 0, 16, ctx->stream));
+        B.pgran = d_pgran.as<unsigned long long>();
+        B.run_err = d_err.as<unsigned>();
+    }
+    unsigned tag = 0;  // hand-off tags grow across the launches of this call
+
+    DevBuf d_args;  // the kernels' TrkParams / TrkBuffers
+    HIP_TRY(d_args.alloc(sizeof(TrkParams) + sizeof(TrkBuffers)));
+    HIP_TRY(hipMemcpyAsync(d_args.p, &P, sizeof(TrkParams), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(static_cast<char*>(d_args.p) + sizeof(TrkParams), &B, sizeof(TrkBuffers),
+                           hipMemcpyHostToDevice, ctx->stream));
+    const TrkDev TD{d_args.as<TrkParams>(),
+                    reinterpret_cast<const TrkBuffers*>(static_cast<char*>(d_args.p) + sizeof(TrkParams))};
+
+
+    // step launches: one persistent launch per phase run, else K-launch graphs replayed
+    // (no host launch cost per step); in profiling mode every launch is bracketed by events.
     std::vector<hipEvent_t> pev;
     std::vector<char> pev10;  // launch of the 10-ms phase
     int64_t launches = 0;
+    std::function<int(int, int)> run_steps_ref;
     auto run_steps = [&](int pdi, int count) -> int {
         const int bpc = pdi == 1 ? bpc1 : bpc10, sub = pdi == 1 ? sub1 : sub10;
         if (count <= 0) return GNSS_OK;
-        launches += count;
         ctx->timing.track_channel_samples += (int64_t)count * nch * (int64_t)S * pdi;
+        if (pdi == 1 ? persist1 : persist10) {
+            hipEvent_t a = nullptr, b = nullptr;
+            if (ctx->profiling) {
+                HIP_TRY(hipEventCreate(&a));
+                HIP_TRY(hipEventCreate(&b));
+                HIP_TRY(hipEventRecord(a, ctx->stream));
+            }
+            HIP_TRY(hipMemsetAsync(d_err.p, 0, 16, ctx->stream));  // timeout word + census
+            HIP_TRY(launch_track_run(P, B, TD, bpc, sub, count, tag, ctx->stream));
+            tag += (unsigned)count + 1;
+            unsigned err[3] = {0, 0, 0};
+            HIP_TRY(hipMemcpyAsync(err, d_err.p, sizeof err, hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(hipStreamSynchronize(ctx->stream));
+            if (err[0] == 2) {  // census: not every block was resident -> one launch per step
+                (pdi == 1 ? persist1 : persist10) = false;
+                if (a) (void)hipEventDestroy(a);
+                ctx->timing.track_channel_samples -= (int64_t)count * nch * (int64_t)S * pdi;
+                return run_steps_ref(pdi, count);
+            }
+            if (err[0]) return fail(ctx, GNSS_EDEVICE, "persistent tracking kernel: a hand-off wait timed out");
+            launches += 1;
+            if (ctx->profiling) {
+                HIP_TRY(hipEventRecord(b, ctx->stream));
+                pev.push_back(a);
+                pev.push_back(b);
+                pev10.push_back(pdi == 10);
+                if (pdi == 10) {
+                    ctx->timing.track10_launches += 1;
+                    ctx->timing.track10_channel_samples += (int64_t)count * nch * (int64_t)S * pdi;
+                }
+            }
+            return GNSS_OK;
+        }
+        launches += count;
         if (ctx->profiling) {
             for (int i = 0; i < count; i++) {
                 hipEvent_t a, b;
                 HIP_TRY(hipEventCreate(&a));
                 HIP_TRY(hipEventCreate(&b));
                 HIP_TRY(hipEventRecord(a, ctx->stream));
-                HIP_TRY(launch_track_step(P, B, bpc, sub, ctx->stream));
+                HIP_TRY(launch_track_step(P, B, TD, bpc, sub, ctx->stream));
                 HIP_TRY(hipEventRecord(b, ctx->stream));
                 pev.push_back(a);
                 pev.push_back(b);
@@ -786,7 +854,7 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
             StepGraph g;
             HIP_TRY(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
             for (int i = 0; i < K; i++) {
-                hipError_t e = launch_track_step(P, B, bpc, sub, ctx->stream);
+                hipError_t e = launch_track_step(P, B, TD, bpc, sub, ctx->stream);
                 if (e != hipSuccess) {
                     hipGraph_t junk;
                     (void)hipStreamEndCapture(ctx->stream, &junk);
@@ -797,22 +865,23 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
             HIP_TRY(hipStreamEndCapture(ctx->stream, &g.graph));
             HIP_TRY(hipGraphInstantiate(&g.exec, g.graph, nullptr, nullptr, 0));
             for (int r = 0; r < count / K; r++) HIP_TRY(hipGraphLaunch(g.exec, ctx->stream));
-            for (int i = 0; i < count % K; i++) HIP_TRY(launch_track_step(P, B, bpc, sub, ctx->stream));
+            for (int i = 0; i < count % K; i++) HIP_TRY(launch_track_step(P, B, TD, bpc, sub, ctx->stream));
             HIP_TRY(hipStreamSynchronize(ctx->stream));  // graph objects die with this scope
         } else {
-            for (int i = 0; i < count; i++) HIP_TRY(launch_track_step(P, B, bpc, sub, ctx->stream));
+            for (int i = 0; i < count; i++) HIP_TRY(launch_track_step(P, B, TD, bpc, sub, ctx->stream));
         }
         return GNSS_OK;
     };
+    run_steps_ref = run_steps;
 
     Events e_all;
     HIP_TRY(hipEventRecord(e_all.a, ctx->stream));
     // phase A: steps 1..N1-1, snapshot (for countinx = -1), step N1, bit-edge search
-    HIP_TRY(launch_track_prepare(P, B, 1, 0, ctx->stream));
+    HIP_TRY(launch_track_prepare(P, B, TD, 1, 0, ctx->stream));
     if ((st = run_steps(1, N1 - 1))) return st;
-    HIP_TRY(launch_track_snapshot(P, B, ctx->stream));
+    HIP_TRY(launch_track_snapshot(P, B, TD, ctx->stream));
     if ((st = run_steps(1, 1))) return st;
-    HIP_TRY(launch_track_bitedge(P, B, ctx->stream));
+    HIP_TRY(launch_track_bitedge(P, B, TD, ctx->stream));
     std::vector<TrkChan> chh((size_t)nch);
     HIP_TRY(hipMemcpyAsync(chh.data(), d_chan.p, sizeof(TrkChan) * nch, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
@@ -820,12 +889,13 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     for (auto& t : chh) cxmax = std::max(cxmax, t.countinx);
     // phase B continues phase A up to 1000 + countinx (inactive channels skip)
     if ((st = run_steps(1, cxmax))) return st;
-    HIP_TRY(launch_track_phase_c_init(P, B, file->skip, ctx->stream));
+    HIP_TRY(launch_track_phase_c_init(P, B, TD, file->skip, ctx->stream));
     // phase C
     if ((st = run_steps(10, n10))) return st;
     HIP_TRY(hipEventRecord(e_all.b, ctx->stream));
     HIP_TRY(hipEventSynchronize(e_all.b));
     ctx->timing.track_ms = e_all.ms();
+
     ctx->timing.track_launches = launches;
     double ksum = 0, ksum10 = 0;
     for (size_t i = 0; i + 1 < pev.size(); i += 2) {
@@ -985,8 +1055,16 @@ int gnss_correlate_step(gnss_ctx* ctx, const gnss_file* file, const gnss_signal*
     B.partial = d_part.as<double>();
     B.arrive = d_arrive.as<unsigned>();
     B.dbg_sums = d_sums.as<double>();
-    HIP_TRY(launch_track_prepare(P, B, pdi, 0, ctx->stream));
-    HIP_TRY(launch_track_step(P, B, bpc, sub, ctx->stream));
+    DevBuf d_args;  // the kernels' TrkParams / TrkBuffers
+    HIP_TRY(d_args.alloc(sizeof(TrkParams) + sizeof(TrkBuffers)));
+    HIP_TRY(hipMemcpyAsync(d_args.p, &P, sizeof(TrkParams), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(static_cast<char*>(d_args.p) + sizeof(TrkParams), &B, sizeof(TrkBuffers),
+                           hipMemcpyHostToDevice, ctx->stream));
+    const TrkDev TD{d_args.as<TrkParams>(),
+                    reinterpret_cast<const TrkBuffers*>(static_cast<char*>(d_args.p) + sizeof(TrkParams))};
+
+    HIP_TRY(launch_track_prepare(P, B, TD, pdi, 0, ctx->stream));
+    HIP_TRY(launch_track_step(P, B, TD, bpc, sub, ctx->stream));
     HIP_TRY(hipMemcpyAsync(sums_out, d_sums.p, sizeof(double) * 2 * n_taps, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipMemcpyAsync(&c, d_chan.p, sizeof c, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));

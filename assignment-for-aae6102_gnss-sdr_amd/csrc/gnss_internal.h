@@ -140,8 +140,9 @@ struct StepDesc {
     int64_t n, delayValue, A, g_first, g_last, Index;
     double remSample, d, inv_d, f, phi0, dhi, dlo, remChip_next, remPhase_next;
     // carrier rotation of lane sample m against the lane's first sample:
-    // phi[m] = RN(m*dhi + m*dlo) ~ m * 2*pi*f/Fs, (rc, rs)[m] = (cos, sin)(phi[m])
-    double phi[kLaneMax], rc[kLaneMax], rs[kLaneMax];
+    // phi[m] = RN(m*dhi + m*dlo) ~ m * 2*pi*f/Fs, rcs[m] = (cos, sin)(phi[m])
+    double phi[kLaneMax];
+    double2 rcs[kLaneMax];
     double tap_a[GNSS_MAX_TAPS], tap_c[GNSS_MAX_TAPS];  // colon start / end per tap
     int32_t pdi, phaseC, bad, pad;
 };
@@ -162,24 +163,44 @@ struct TrkBuffers {
     double* p_i_1ms;          // [nch][n1] phase-A P_i for the bit-edge search
     double* dbg_sums;         // if set: last arriver stores the raw sums [nch][2*ntaps], no finalize
     unsigned long long* stamps;  // timing probe (GNSS_STAMPS): [kStampSlots][8] wall clock + counter
+    // persistent step loop (track_run_kernel): R2 hand-off granules {tag:32 | word:32}
+    unsigned long long* pgran;   // [nch][2 (step parity)][kMaxBpcRun][4*ntaps] block partials
+    unsigned* run_err;           // set when a hand-off wait times out
     int32_t n1;               // msToProcessCT_1ms
 };
 
-// Launch wrappers (track.hip)
-hipError_t launch_track_step(const TrkParams& p, const TrkBuffers& b, int blocks_per_chan,
-                             int sub, hipStream_t s);
-hipError_t launch_track_prepare(const TrkParams& p, const TrkBuffers& b, int pdi, int phaseC,
-                                hipStream_t s);
-hipError_t launch_track_snapshot(const TrkParams& p, const TrkBuffers& b, hipStream_t s);
-hipError_t launch_track_bitedge(const TrkParams& p, const TrkBuffers& b, hipStream_t s);
-hipError_t launch_track_phase_c_init(const TrkParams& p, const TrkBuffers& b, int64_t skip,
-                                     hipStream_t s);
+// Device copies of one call's TrkParams / TrkBuffers: the kernels take pointers (a
+// by-value aggregate whose address reaches a non-inlined function is copied to scratch
+// by every lane).
+struct TrkDev {
+    const TrkParams* p;
+    const TrkBuffers* b;
+};
+
+// Launch wrappers (track.hip); p / b are the host copies (grid sizes, dispatch)
+hipError_t launch_track_step(const TrkParams& p, const TrkBuffers& b, const TrkDev& d,
+                             int blocks_per_chan, int sub, hipStream_t s);
+// Persistent form: `nsteps` steps of every channel in one launch (all nch*bpc blocks
+// resident); tags of this launch's hand-offs are tag0 + 1 .. tag0 + nsteps.
+hipError_t launch_track_run(const TrkParams& p, const TrkBuffers& b, const TrkDev& d,
+                            int blocks_per_chan, int sub, int nsteps, unsigned tag0, hipStream_t s);
+// blocks of the persistent kernel one CU can hold (occupancy query), for the host's
+// residency check
+int track_run_blocks_per_cu(const TrkParams& p, int sub);
+hipError_t launch_track_prepare(const TrkParams& p, const TrkBuffers& b, const TrkDev& d, int pdi,
+                                int phaseC, hipStream_t s);
+hipError_t launch_track_snapshot(const TrkParams& p, const TrkBuffers& b, const TrkDev& d, hipStream_t s);
+hipError_t launch_track_bitedge(const TrkParams& p, const TrkBuffers& b, const TrkDev& d, hipStream_t s);
+hipError_t launch_track_phase_c_init(const TrkParams& p, const TrkBuffers& b, const TrkDev& d,
+                                     int64_t skip, hipStream_t s);
 
 constexpr int kTrkThreads = 256;
 constexpr int kArriveStride = 64;   // words: one 256-B line per counter
 constexpr int kArrivePerChan = 9;   // 8 XCD-group counters + the channel counter
 constexpr int kStampSlots = 2200;
 constexpr int kMaxBpc = 1024; // blocks per channel per step (partial buffer)
+constexpr int kMaxBpcRun = 256;  // blocks per channel of the persistent kernel
+constexpr int kDescWords = (int)(sizeof(StepDesc) / 4);
 
 // ----------------------------------------------------------------------------
 // Acquisition (acq.hip)

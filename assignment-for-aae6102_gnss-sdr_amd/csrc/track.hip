@@ -39,14 +39,61 @@ __device__ __forceinline__ void stamp_max(unsigned long long* row, int k, unsign
     row[k] = v;
 }
 
+// A wave-uniform value read from LDS into SGPRs (keeps it out of the VGPR budget).
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int64_t uni(int64_t v)
+{
+    const int lo = __builtin_amdgcn_readfirstlane((int)v);
+    const int hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ double uni(double v) { return __longlong_as_double(uni((int64_t)__double_as_longlong(v))); }
+
+// Global-address-space views (pointers held in TrkBuffers would otherwise be flat:
+// flat loads count on lgkmcnt too, so every LDS wait would also wait for them).
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const i32x4 g_i32x4;
+typedef __attribute__((address_space(1))) double g_dbl;
+typedef __attribute__((address_space(1))) unsigned g_u32;
+typedef __attribute__((address_space(1))) unsigned long long g_u64;
+typedef __attribute__((address_space(1))) const StepDesc g_desc;
+typedef __attribute__((address_space(1))) const TrkChan g_chan;
+typedef __attribute__((address_space(1))) const unsigned g_cu32;
+
+__device__ __forceinline__ int4 ld_g16(const int8_t* p)
+{
+    const i32x4 v = *(g_i32x4*)p;
+    return make_int4(v.x, v.y, v.z, v.w);
+}
+
 __device__ __forceinline__ double ld_sc1(const double* ptr)
 {
-    return __hip_atomic_load(ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load((g_dbl*)ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ void st_sc1(double* ptr, double v)
 {
-    __hip_atomic_store(ptr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((g_dbl*)ptr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ unsigned atomic_add_agent(unsigned* p, unsigned v)
+{
+    return __hip_atomic_fetch_add((g_u32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void store_agent(unsigned* p, unsigned v)
+{
+    __hip_atomic_store((g_u32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void store_agent(unsigned long long* p, unsigned long long v)
+{
+    __hip_atomic_store((g_u64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ unsigned long long load_agent(const unsigned long long* p)
+{
+    return __hip_atomic_load((g_u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // CarrTime = k/Fs (trackingCT.m:104) as the IEEE quotient: one FMA-corrected
@@ -123,7 +170,7 @@ __device__ __forceinline__ StepSize step_size(const TrkParams& p, const NcoState
 // :411-441). Two waves work on it side by side:
 //   role 0 (code): lanes < ntaps build the colon of their tap, lane 0 the scalars;
 //   role 1 (carrier): lanes < 32 the rotation table e^{i phi_m}, lane 63 remPhase.
-__device__ void prepare_desc(const TrkParams& p, const NcoState& c, int pdi, int phaseC, int role,
+__device__ __forceinline__ void prepare_desc_i(const TrkParams& p, const NcoState& c, int pdi, int phaseC, int role,
                              int lane, StepDesc* d)
 {
     const StepSize z = step_size(p, c, pdi, phaseC);
@@ -150,8 +197,7 @@ __device__ void prepare_desc(const TrkParams& p, const NcoState& c, int pdi, int
             double sn, cs;
             sincos(ph, &sn, &cs);
             d->phi[lane] = ph;
-            d->rc[lane] = cs;
-            d->rs[lane] = sn;
+            d->rcs[lane] = make_double2(cs, sn);
             if (lane == 0) {
                 d->f = f;
                 d->phi0 = c.remPhase;
@@ -205,6 +251,56 @@ __device__ void prepare_desc(const TrkParams& p, const NcoState& c, int pdi, int
         d->bad = badw;
     }
 }
+// out-of-line copy for the persistent kernel (keeps its register budget)
+__device__ __noinline__ void prepare_desc(const TrkParams& p, const NcoState& c, int pdi, int phaseC, int role, int lane, StepDesc* d)
+{
+    prepare_desc_i(p, c, pdi, phaseC, role, lane, d);
+}
+
+
+// atan for the PLL discriminator. The classic four-interval reduction with an
+// 11-term odd polynomial (error < 1 ulp); its constants are read through a pointer the
+// compiler cannot see through, so inlined into the persistent step loop they are not
+// hoisted into registers that would stay live over the correlator (+40 VGPRs with the
+// library atan).
+__device__ const double kAtanTab[19] = {
+    4.63647609000806093515e-01, 7.85398163397448278999e-01, 9.82793723247329054082e-01,
+    1.57079632679489655800e+00,  // atan(0.5), atan(1), atan(1.5), atan(inf): high parts
+    2.26987774529616870924e-17, 3.06161699786838301793e-17, 1.39033110312309984516e-17,
+    6.12323399573676603587e-17,  // low parts
+    3.33333333333329318027e-01, -1.99999999998764832476e-01, 1.42857142725034663711e-01,
+    -1.11111104054623557880e-01, 9.09088713343650656196e-02, -7.69187620504482999495e-02,
+    6.66107313738753120669e-02, -5.83357013379057348645e-02, 4.97687799461593236017e-02,
+    -3.65315727442169155270e-02, 1.62858201153657823623e-02};
+
+__device__ __forceinline__ double atan_tab(double x)
+{
+    const double* t = kAtanTab;
+    asm volatile("" : "+s"(t));
+    const double ax = fabs(x);
+    if (!(ax < 0x1p66)) return x != x ? x : copysign(t[3] + t[7], x);
+    int id;
+    double y;
+    if (ax < 0.4375) {
+        if (ax < 0x1p-27) return x;
+        id = -1;
+        y = x;
+    } else if (ax < 1.1875) {
+        if (ax < 0.6875) { id = 0; y = (2.0 * ax - 1.0) / (2.0 + ax); }
+        else { id = 1; y = (ax - 1.0) / (ax + 1.0); }
+    } else if (ax < 2.4375) {
+        id = 2; y = (ax - 1.5) / (1.0 + 1.5 * ax);
+    } else {
+        id = 3; y = -1.0 / ax;
+    }
+    const double z = y * y, w = z * z;
+    const double* a = t + 8;
+    const double s1 = z * (a[0] + w * (a[2] + w * (a[4] + w * (a[6] + w * (a[8] + w * a[10])))));
+    const double s2 = w * (a[1] + w * (a[3] + w * (a[5] + w * (a[7] + w * a[9]))));
+    if (id < 0) return y - y * (s1 + s2);
+    const double r = t[id] - ((y * (s1 + s2) - t[4 + id]) - y);
+    return x < 0 ? -r : r;
+}
 
 // The DLL / PLL update of one step (trackingCT.m:136-150 / :469-483), fp64, same
 // operation order as the reference; phase C keeps T = 0.001 (:473,480). Every lane
@@ -213,7 +309,7 @@ struct LoopUpd {
     double DLLdiscri, code_output, codeFreq, PLLdiscri, carrier_output, carrierFreq;
 };
 
-__device__ __forceinline__ LoopUpd loop_update(const TrkParams& p, const TrkChan& c, double E_i,
+__device__ __forceinline__ LoopUpd loop_update_i(const TrkParams& p, const TrkChan& c, double E_i,
                                                double E_q, double P_i, double P_q, double L_i,
                                                double L_q, int pdi, int phaseC)
 {
@@ -225,13 +321,19 @@ __device__ __forceinline__ LoopUpd loop_update(const TrkParams& p, const TrkChan
     u.code_output = c.code_outputLast + (p.tau2code / p.tau1code) * (u.DLLdiscri - c.DLLdiscriLast) +
                     u.DLLdiscri * (T / p.tau1code);
     u.codeFreq = p.codeFreqBasis - u.code_output;
-    u.PLLdiscri = atan(P_q / P_i) / kTwoPi;
+    u.PLLdiscri = atan_tab(P_q / P_i) / kTwoPi;
     u.carrier_output = c.carrier_outputLast +
                        (p.tau2carr / p.tau1carr) * (u.PLLdiscri - c.PLLdiscriLast) +
                        u.PLLdiscri * (T / p.tau1carr);
     u.carrierFreq = c.carrierFreqBasis + u.carrier_output;
     return u;
 }
+// out-of-line copy for the persistent kernel (keeps its register budget)
+__device__ __noinline__ LoopUpd loop_update(const TrkParams& p, const TrkChan& c, double E_i, double E_q, double P_i, double P_q, double L_i, double L_q, int pdi, int phaseC)
+{
+    return loop_update_i(p, c, E_i, E_q, P_i, P_q, L_i, L_q, pdi, phaseC);
+}
+
 
 // Per-step values of the finished step the side writers need (read before the
 // next descriptor overwrites the current one).
@@ -243,7 +345,7 @@ struct StepOut {
 
 // TckResultCT fields of the step (trackingCT.m:153-170 / :507-524) and the phase-A
 // P_i kept for the bit-edge search. `s` = the step's (negated in phase C) sums.
-__device__ void write_record(const TrkParams& p, const TrkBuffers& b, int ch, const TrkChan& c,
+__device__ __forceinline__ void write_record_i(const TrkParams& p, const TrkBuffers& b, int ch, const TrkChan& c,
                              const StepOut& o, const LoopUpd& u, const double* s)
 {
     const double P_i = s[2 * p.iP], P_q = s[2 * p.iP + 1];
@@ -276,48 +378,64 @@ __device__ void write_record(const TrkParams& p, const TrkBuffers& b, int ch, co
     }
     if (!o.phaseC && slot < b.n1) b.p_i_1ms[(int64_t)ch * b.n1 + slot] = P_i;
 }
+// out-of-line copy for the persistent kernel (keeps its register budget)
+__device__ __noinline__ void write_record(const TrkParams& p, const TrkBuffers& b, int ch, const TrkChan& c, const StepOut& o, const LoopUpd& u, const double* s)
+{
+    write_record_i(p, b, ch, c, o, u, s);
+}
+
+
+// C/N0 of one 20-sample window of |P|^2 (trackingCT.m:124-131; moment method), out of
+// line: it runs once every 20 steps and its log/hypot/atan2 would otherwise sit in the
+// registers of the persistent step loop.
+__device__ __noinline__ double cn0_estimate(const double (&Z)[20], double T)
+{
+    double mean = 0;
+#pragma unroll
+    for (int k = 0; k < 20; k++) mean += Z[k];
+    mean = mean / 20;
+    double var = 0;
+#pragma unroll
+    for (int k = 0; k < 20; k++) var += (Z[k] - mean) * (Z[k] - mean);
+    var = var / 19;
+    const double m2v = mean * mean - var;
+    const double scale = 1 / T;
+    if (m2v >= 0) {
+        const double NA2 = sqrt(m2v);
+        const double varIQ = 0.5 * (mean - NA2);
+        return fabs(10 * log10(scale * NA2 / (2 * varIQ)));
+    }
+    // complex sqrt branch of MATLAB (quirk A.16)
+    const double y = sqrt(-m2v);
+    const double nr = 0, ni = scale * y;
+    const double dr = 2 * (0.5 * mean), di = 2 * (0.5 * -y);
+    const double den = dr * dr + di * di;
+    const double zr = (nr * dr + ni * di) / den, zi = (ni * dr - nr * di) / den;
+    const double lr = 10 * (log(hypot(zr, zi)) / log(10.0));
+    const double li = 10 * (atan2(zi, zr) / log(10.0));
+    return hypot(lr, li);
+}
 
 // The channel state after the step, with the C/N0 estimator (trackingCT.m:120-134).
-__device__ void write_state(const TrkParams& p, const TrkBuffers& b, int ch, const TrkChan& c,
-                            const StepOut& o, const LoopUpd& u, const double* s)
+__device__ __forceinline__ void write_state_i(const TrkParams& p, const TrkBuffers& b, int ch, TrkChan* g,
+                            const TrkChan& c, const StepOut& o, const LoopUpd& u, const double* s,
+                            bool io = true)
 {
-    TrkChan* g = b.chan + ch;
     const double P_i = s[2 * p.iP], P_q = s[2 * p.iP + 1];
     int index_int = c.index_int + 1;
     int snrIndex = c.snrIndex;
     const double zk = P_i * P_i + P_q * P_q;
-    g->Zk[index_int - 1] = zk;
-    if (index_int % 20 == 0) {
+    for (int k = 0; k < 20; k++) g->Zk[k] = k == index_int - 1 ? zk : c.Zk[k];
+    if (index_int % 20 == 0 && io) {
         double Z[20];
 #pragma unroll
         for (int k = 0; k < 20; k++) Z[k] = k == index_int - 1 ? zk : c.Zk[k];
-        double mean = 0;
-#pragma unroll
-        for (int k = 0; k < 20; k++) mean += Z[k];
-        mean = mean / 20;
-        double var = 0;
-#pragma unroll
-        for (int k = 0; k < 20; k++) var += (Z[k] - mean) * (Z[k] - mean);
-        var = var / 19;
-        const double m2v = mean * mean - var;
-        const double scale = 1 / (1 * p.ms * o.pdi);
-        double cn;
-        if (m2v >= 0) {
-            const double NA2 = sqrt(m2v);
-            const double varIQ = 0.5 * (mean - NA2);
-            cn = fabs(10 * log10(scale * NA2 / (2 * varIQ)));
-        } else {  // complex sqrt branch of MATLAB (quirk A.16)
-            const double y = sqrt(-m2v);
-            const double nr = 0, ni = scale * y;
-            const double dr = 2 * (0.5 * mean), di = 2 * (0.5 * -y);
-            const double den = dr * dr + di * di;
-            const double zr = (nr * dr + ni * di) / den, zi = (ni * dr - nr * di) / den;
-            const double lr = 10 * (log(hypot(zr, zi)) / log(10.0));
-            const double li = 10 * (atan2(zi, zr) / log(10.0));
-            cn = hypot(lr, li);
-        }
+        const double cn = cn0_estimate(Z, 1 * p.ms * o.pdi);
         double* cn0 = o.phaseC ? b.cn0_10 : b.cn0_1;
         if (snrIndex <= p.cn0_cap) cn0[(int64_t)ch * p.cn0_cap + snrIndex - 1] = cn;
+        index_int = 0;
+        snrIndex += 1;
+    } else if (index_int % 20 == 0) {  // (a replica of the state: counters only)
         index_int = 0;
         snrIndex += 1;
     }
@@ -338,196 +456,186 @@ __device__ void write_state(const TrkParams& p, const TrkBuffers& b, int ch, con
     g->index_int = index_int;
     g->snrIndex = snrIndex;
 }
+// out-of-line copy for the persistent kernel (keeps its register budget)
+__device__ __noinline__ void write_state(const TrkParams& p, const TrkBuffers& b, int ch, TrkChan* g, const TrkChan& c, const StepOut& o, const LoopUpd& u, const double* s, bool io)
+{
+    write_state_i(p, b, ch, g, c, o, u, s, io);
+}
+
 
 }  // namespace
 
-// ---------------------------------------------------------------------------
-// The correlator step kernel. NT = taps (3: E/P/L, 11: ACF), SUB = 8-sample
-// groups per lane (M = 8*SUB contiguous samples), both compile-time so the
-// accumulators stay in VGPRs. Grid: nch x bpc blocks; block b of a channel owns
-// the 256*SUB consecutive 8-sample groups starting at g_first + 256*SUB*b.
-//
-// Per lane (trackingCT.m:96-118):
+// One lane's 8*SUB samples starting at window-relative sample ks of the step described
+// by `dp` (trackingCT.m:96-118): the lane's NT tap sums, I = imag(raw .* carrsig) in oI,
+// Q = real(raw .* carrsig) in oQ. `raw` = the lane's 16-B IF groups, `myslot` = this
+// lane's column of the LDS running-sum slots (slot m at myslot[m * kTrkThreads]),
+// `zero` = an LDS double2 holding 0 (read when a tap's boundary is outside the subgroup).
+// RELOAD (descriptor in LDS): read the rotation table where it is used rather than
+// letting the compiler hoist all 96 values into VGPRs.
 //   * carrier: w_m = x_m * e^{i(Wave(k_m) - Wave(k_0))} in the frame of the lane's
-//     first sample, Wave(k) rounded exactly as the reference rounds it; the
-//     rotation is the table e^{i phi_m} plus the first-order residue
-//     eta = (Wave(k_m) - Wave(k_0)) - phi_m (|eta| ~ 1e-10). One sincos per lane
-//     rotates the lane's sums back at the end;
-//   * code: M * codeFreq/Fs < 1, so every tap's replica Code(ceil(t)+1) changes
-//     at most once in the lane, at sample p (exact colon arithmetic at the lane
-//     start, exact re-evaluation within 1e-6 sample of a boundary). With the
-//     running sum of w in LDS, the tap sum is v1*Sum + (v0 - v1)*Prefix(p).
-// ---------------------------------------------------------------------------
-template <int NT, int SUB, bool DIVIDE>
-__global__ __launch_bounds__(kTrkThreads) void track_step_kernel(TrkParams p, TrkBuffers b, int bpc)
+//     first sample, Wave(k) rounded exactly as the reference rounds it; the rotation
+//     is the table e^{i phi_m} plus the first-order residue eta = (Wave(k_m) - Wave(k_0))
+//     - phi_m (|eta| ~ 1e-10). One sincos per lane rotates the lane's sums back;
+//   * code: M * codeFreq/Fs < 1, so every tap's replica Code(ceil(t)+1) changes at most
+//     once in the lane, at sample p (exact colon arithmetic at the lane start, exact
+//     re-evaluation within 1e-6 sample of a boundary). With the running sum of w in
+//     LDS, the tap sum is v1*Sum + (v0 - v1)*Prefix(p).
+// The lane's 16-B IF groups: in registers (step kernel) or staged in LDS (persistent loop)
+__device__ __forceinline__ double2 ld_rcs(const StepDesc* d, int m) { return d->rcs[m]; }
+__device__ __forceinline__ double2 ld_rcs(g_desc* d, int m)
+{
+    typedef __attribute__((address_space(1))) const double g_cdbl;
+    g_cdbl* q = (g_cdbl*)&d->rcs[m];
+    return make_double2(q[0], q[1]);
+}
+
+template <int SUB> struct RegRaw {
+    const int4 (&r)[SUB];
+    __device__ __forceinline__ int4 get(int j) const { return r[j]; }
+};
+struct LdsRaw {
+    const int4* p;  // this lane's group j at p[j * kTrkThreads]
+    __device__ __forceinline__ int4 get(int j) const { return p[j * kTrkThreads]; }
+};
+
+template <int NT, int SUB, bool DIVIDE, bool RELOAD, class Desc, class Raw>
+__device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* dp, const Raw& raw,
+                                               int64_t ks, unsigned cabits, double2* myslot,
+                                               const double2* zero, double (&oI)[NT], double (&oQ)[NT])
 {
     constexpr int M = 8 * SUB;
-    constexpr int NV = 2 * NT;
     constexpr int T = kTrkThreads;
-    static_assert(M <= kLaneMax, "lane span exceeds the rotation table");
-    const int ch = blockIdx.x / bpc;
-    const int blk = blockIdx.x - ch * bpc;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-
-    // LDS: running sums slot[9][T] (slot 8 stays zero), then the block reduction
-    constexpr int kSlot = 9 * T * 2;
-    constexpr int kRed = NV * (T + 32);
-    __shared__ __attribute__((aligned(16))) double s_mem[kSlot > kRed ? kSlot : kRed];
-    __shared__ double s_fin[NV];
-    __shared__ int s_last;
-    __shared__ TrkChan s_c;
-
-    const StepDesc* dp = b.desc + ch;
-    const TrkChan* cp = b.chan + ch;
-    unsigned long long* srow = b.stamps && ch == 0 ? stamp_row(b) : nullptr;
-    if (srow && tid == 0) stamp_max(srow, 8 + blk, wall_clock64());  // block start
-    const int64_t g_first = dp->g_first, g_last = dp->g_last;
-    const int64_t g0 = g_first + ((int64_t)blk * T + tid) * SUB;  // first group of the lane
-    // issue the IF loads first (clamped so every lane loads something valid)
-    const int8_t* iq = b.iq - p.buf_base;  // absolute-byte addressing
-    const int bad = dp->bad;
-    int4 raw[SUB];
-#pragma unroll
-    for (int j = 0; j < SUB; j++) {
-        const int64_t gj = g0 + j <= g_last ? g0 + j : g_last;
-        raw[j] = bad ? make_int4(0, 0, 0, 0) : *reinterpret_cast<const int4*>(iq + 16 * gj);
-    }
-    const unsigned cabits = lane < 32 ? b.ca_bits[ch * 32 + lane] : 0u;
-    // the channel state, for whichever block arrives last
-    constexpr int kChanWords = (int)(sizeof(TrkChan) / 8);
-    if (tid < kChanWords)
-        reinterpret_cast<uint64_t*>(&s_c)[tid] = reinterpret_cast<const uint64_t*>(cp)[tid];
-
-    if (cp->status != GNSS_OK) return;
-    if (!dp->phaseC && dp->Index + 1 > cp->n1_target) return;  // 1-ms run of this channel done
-    const int64_t n = dp->n, A = dp->A;
-    const double d = dp->d, inv_d = dp->inv_d;
-    if (bad || d * M >= 1.0) {  // (a code rate beyond Fs/M breaks the one-boundary lane)
-        if (blk == 0 && tid == 0) b.chan[ch].status = bad ? bad : GNSS_EINDEX;
-        return;
-    }
-    const double f = dp->f, phi0 = dp->phi0;
+    const int64_t n = uni(dp->n);
+    const double d = uni(dp->d), inv_d = uni(dp->inv_d);
+    const double f = uni(dp->f), phi0 = uni(dp->phi0);
     const double Fs = p.Fs, rFs = p.inv_Fs;
 
     // ---- valid samples of the lane: [lo, hi) (only the window's two end lanes are partial)
-    const int64_t ks = 8 * g0 - A;  // window-relative index of the lane's first sample
     const int lo = ks < 0 ? (int)(-ks < M ? -ks : M) : 0;
     const int hi = n - ks < M ? (n - ks > 0 ? (int)(n - ks) : 0) : M;
-    unsigned wd[SUB][4];
+
+    // ---- code replica per tap: chip c0 at the first valid sample, the sample p of the
+    // lane's (single) chip boundary, and the two code values around it
+    const int64_t kf0 = ks + lo;
+    const int64_t kf = kf0 < 0 ? 0 : (kf0 > n - 1 ? n - 1 : kf0);
+    int cap[NT];
+    double v1[NT], dv[NT];
 #pragma unroll
-    for (int j = 0; j < SUB; j++) {
-        wd[j][0] = raw[j].x; wd[j][1] = raw[j].y; wd[j][2] = raw[j].z; wd[j][3] = raw[j].w;
+    for (int s = 0; s < NT; s++) {
+        const Colon col{uni(dp->tap_a[s]), d, uni(dp->tap_c[s]), n - 1};
+        const double t0 = colon_elem(col, kf);
+        const double c0 = ceil(t0);
+        const double R = (double)(kf - ks) + (c0 - t0) * inv_d;  // samples to the boundary
+        const double rr = rint(R);
+        int pb = (int)floor(R) + 1;
+        if (fabs(R - rr) < 1e-6) {  // too close to call in floating point: exact colon value
+            const int ms = (int)rr;
+            pb = ms;
+            const int64_t kx = ks + ms;
+            if (ms >= 0 && ms < M && kx >= 0 && kx <= n - 1)
+                pb = ceil(colon_elem(col, kx)) > c0 ? ms : ms + 1;
+        }
+        cap[s] = (pb < M ? pb : M) - 1;  // Prefix(p) = running sum through sample p-1
+        const unsigned i0 = ca_index32((int)c0);
+        const unsigned i1 = i0 == 1022u ? 0u : i0 + 1u;
+        const unsigned w0 = __shfl(cabits, (int)(i0 >> 5), 64);
+        const unsigned w1 = __shfl(cabits, (int)(i1 >> 5), 64);
+        const double a0 = ((w0 >> (i0 & 31)) & 1u) ? -1.0 : 1.0;
+        const double a1 = ((w1 >> (i1 & 31)) & 1u) ? -1.0 : 1.0;
+        v1[s] = a1;
+        dv[s] = a0 - a1;
     }
-    if (lo > 0 || hi < M) {
+
+    // ---- carrier base of the lane
+    const double kb = (double)ks;
+    const double Wb = wave_at<DIVIDE>(kb, f, phi0, Fs, rFs);
+    double sb, cb;
+    sincos(Wb, &sb, &cb);
+
+    double run_r = 0.0, run_i = 0.0;
+    double pre_r[NT], pre_i[NT];
 #pragma unroll
-        for (int j = 0; j < SUB; j++)
+    for (int s = 0; s < NT; s++) { pre_r[s] = 0.0; pre_i[s] = 0.0; }
+
+    // one 8-sample subgroup: running sums into the LDS slots, tap prefixes captured
+    auto subgroup = [&](const int j) {
+        const int4 rj = raw.get(j);
+        unsigned wd[4] = {(unsigned)rj.x, (unsigned)rj.y, (unsigned)rj.z, (unsigned)rj.w};
+        if (lo > 8 * j || hi < 8 * j + 8) {
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 const int m0 = 8 * j + 2 * q;
                 const unsigned k0 = (m0 >= lo && m0 < hi) ? 0x0000FFFFu : 0u;
                 const unsigned k1 = (m0 + 1 >= lo && m0 + 1 < hi) ? 0xFFFF0000u : 0u;
-                wd[j][q] &= k0 | k1;
+                wd[q] &= k0 | k1;
             }
-    }
-
-    double oI[NT], oQ[NT];
-    if (p.probe & 2) {  // timing probe: no correlation (loads, reduction and hand-off only)
+        }
+        const double kbj = kb + (double)(8 * j);
 #pragma unroll
-        for (int s = 0; s < NT; s++) { oI[s] = (double)(int)wd[0][s & 3]; oQ[s] = 0.0; }
+        for (int mm = 0; mm < 8; mm++) {
+            const int m = 8 * j + mm;
+            const unsigned word = wd[mm >> 1];
+            const int sh = (mm & 1) * 16;
+            const double xr = (double)(int8_t)((word >> sh) & 0xFF);
+            const double xi = (double)(int8_t)((word >> (sh + 8)) & 0xFF);
+            double wr = xr, wi = xi;
+            // m = 0: W = Wb, phi = 0, rcs = (1, 0) -> w = x exactly; skipped when known
+            if (RELOAD || m > 0) {
+                const double W = wave_at<DIVIDE>(kbj + (double)mm, f, phi0, Fs, rFs);
+                const double eta = (W - Wb) - dp->phi[m];
+                const double2 rcs = ld_rcs(dp, m);
+                const double rc = rcs.x, rs = rcs.y;
+                const double yr = __builtin_fma(xr, rc, -(xi * rs));
+                const double yi = __builtin_fma(xr, rs, xi * rc);
+                wr = __builtin_fma(-eta, yi, yr);
+                wi = __builtin_fma(eta, yr, yi);
+            }
+            run_r += wr;
+            run_i += wi;
+            myslot[mm * T] = make_double2(run_r, run_i);
+            // RELOAD: at most two samples' table values in flight (VGPR budget of 3 waves/SIMD)
+            if (RELOAD && (mm & 1)) __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int s = 0; s < NT; s++) {
+            const unsigned idx = (unsigned)(cap[s] - 8 * j);
+            const double2 v = *(idx < 8u ? myslot + idx * T : zero);
+            pre_r[s] += v.x;
+            pre_i[s] += v.y;
+        }
+    };
+    if constexpr (RELOAD) {
+        // descriptor in LDS: one subgroup at a time (unrolled, the compiler would keep
+        // every subgroup's table values live)
+#pragma unroll 1
+        for (int j = 0; j < SUB; j++) subgroup(j);
     } else {
-        // ---- code replica per tap: chip c0 at the first valid sample, the sample p of the
-        // lane's (single) chip boundary, and the two code values around it
-        const int64_t kf0 = ks + lo;
-        const int64_t kf = kf0 < 0 ? 0 : (kf0 > n - 1 ? n - 1 : kf0);
-        int cap[NT];
-        double v1[NT], dv[NT];
-    #pragma unroll
-        for (int s = 0; s < NT; s++) {
-            const Colon col{dp->tap_a[s], d, dp->tap_c[s], n - 1};
-            const double t0 = colon_elem(col, kf);
-            const double c0 = ceil(t0);
-            const double R = (double)(kf - ks) + (c0 - t0) * inv_d;  // samples to the boundary
-            const double rr = rint(R);
-            int pb = (int)floor(R) + 1;
-            if (fabs(R - rr) < 1e-6) {  // too close to call in floating point: exact colon value
-                const int ms = (int)rr;
-                pb = ms;
-                const int64_t kx = ks + ms;
-                if (ms >= 0 && ms < M && kx >= 0 && kx <= n - 1)
-                    pb = ceil(colon_elem(col, kx)) > c0 ? ms : ms + 1;
-            }
-            cap[s] = (pb < M ? pb : M) - 1;  // Prefix(p) = running sum through sample p-1
-            const unsigned i0 = ca_index32((int)c0);
-            const unsigned i1 = i0 == 1022u ? 0u : i0 + 1u;
-            const unsigned w0 = __shfl(cabits, (int)(i0 >> 5), 64);
-            const unsigned w1 = __shfl(cabits, (int)(i1 >> 5), 64);
-            const double a0 = ((w0 >> (i0 & 31)) & 1u) ? -1.0 : 1.0;
-            const double a1 = ((w1 >> (i1 & 31)) & 1u) ? -1.0 : 1.0;
-            v1[s] = a1;
-            dv[s] = a0 - a1;
-        }
-
-        // ---- carrier base of the lane
-        const double kb = (double)ks;
-        const double Wb = wave_at<DIVIDE>(kb, f, phi0, Fs, rFs);
-        double sb, cb;
-        sincos(Wb, &sb, &cb);
-
-        double2* myslot = reinterpret_cast<double2*>(s_mem) + tid;  // slot m at myslot[m * T]
-        myslot[8 * T] = make_double2(0.0, 0.0);
-        double run_r = 0.0, run_i = 0.0;
-        double pre_r[NT], pre_i[NT];
-    #pragma unroll
-        for (int s = 0; s < NT; s++) { pre_r[s] = 0.0; pre_i[s] = 0.0; }
-
-    #pragma unroll
-        for (int j = 0; j < SUB; j++) {
-    #pragma unroll
-            for (int mm = 0; mm < 8; mm++) {
-                const int m = 8 * j + mm;
-                const unsigned word = wd[j][mm >> 1];
-                const int sh = (mm & 1) * 16;
-                const double xr = (double)(int8_t)((word >> sh) & 0xFF);
-                const double xi = (double)(int8_t)((word >> (sh + 8)) & 0xFF);
-                double wr = xr, wi = xi;
-                if (m > 0) {
-                    const double W = wave_at<DIVIDE>(kb + (double)m, f, phi0, Fs, rFs);
-                    const double eta = (W - Wb) - dp->phi[m];
-                    const double rc = dp->rc[m], rs = dp->rs[m];
-                    const double yr = __builtin_fma(xr, rc, -(xi * rs));
-                    const double yi = __builtin_fma(xr, rs, xi * rc);
-                    wr = __builtin_fma(-eta, yi, yr);
-                    wi = __builtin_fma(eta, yr, yi);
-                }
-                run_r += wr;
-                run_i += wi;
-                myslot[mm * T] = make_double2(run_r, run_i);
-            }
-    #pragma unroll
-            for (int s = 0; s < NT; s++) {
-                const unsigned idx = (unsigned)(cap[s] - 8 * j);
-                const double2 v = myslot[(idx < 8u ? idx : 8u) * T];
-                pre_r[s] += v.x;
-                pre_i[s] += v.y;
-            }
-        }
-
-        // ---- tap sums of the lane, rotated back by e^{i Wave(k_0)}:
-        // I = imag(raw .* carrsig), Q = real(raw .* carrsig) (trackingCT.m:107-118)
-    #pragma unroll
-        for (int s = 0; s < NT; s++) {
-            const double ur = __builtin_fma(dv[s], pre_r[s], v1[s] * run_r);
-            const double ui = __builtin_fma(dv[s], pre_i[s], v1[s] * run_i);
-            oI[s] = __builtin_fma(cb, ui, sb * ur);
-            oQ[s] = __builtin_fma(cb, ur, -(sb * ui));
-        }
+#pragma unroll
+        for (int j = 0; j < SUB; j++) subgroup(j);
     }
 
-    // ---- block reduction (fixed order), then hand the partial to the last arriver
-    __syncthreads();  // every wave is done with its slots
-    if (srow && tid == 0) stamp_max(srow, 8 + kMaxBpc + blk, wall_clock64());  // block computed
-    double* red = s_mem;             // [NV][T]
-    double* red2 = s_mem + NV * T;   // [NV][32]
+    // ---- tap sums of the lane, rotated back by e^{i Wave(k_0)}:
+    // I = imag(raw .* carrsig), Q = real(raw .* carrsig) (trackingCT.m:107-118)
+#pragma unroll
+    for (int s = 0; s < NT; s++) {
+        const double ur = __builtin_fma(dv[s], pre_r[s], v1[s] * run_r);
+        const double ui = __builtin_fma(dv[s], pre_i[s], v1[s] * run_i);
+        oI[s] = __builtin_fma(cb, ui, sb * ur);
+        oQ[s] = __builtin_fma(cb, ur, -(sb * ui));
+    }
+}
+
+// Block-level sum of the lanes' tap sums in a fixed order (bit-reproducible). On return
+// thread v < 2*NT holds block sum v (I of tap v/2 for even v, Q for odd); s_mem is
+// free again for the caller. s_mem: [2NT][T] + [2NT][32] doubles.
+template <int NT>
+__device__ __forceinline__ double block_partial(double* s_mem, const double (&oI)[NT],
+                                                const double (&oQ)[NT], int tid)
+{
+    constexpr int NV = 2 * NT, T = kTrkThreads;
+    __syncthreads();  // every wave is done with the slots
+    double* red = s_mem;            // [NV][T]
+    double* red2 = s_mem + NV * T;  // [NV][32]
 #pragma unroll
     for (int s = 0; s < NT; s++) {
         red[(2 * s) * T + tid] = oI[s];
@@ -543,13 +651,90 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(TrkParams p, Tr
         red2[e] = a;
     }
     __syncthreads();
+    double a = 0.0;
+    if (tid < NV) {
+        a = red2[tid * 32];
+        for (int k = 1; k < 32; k++) a += red2[tid * 32 + k];
+    }
+    __syncthreads();
+    return a;
+}
+
+// ---------------------------------------------------------------------------
+// The correlator step kernel: one launch per tracking step of every channel (the
+// fallback when the persistent loop below cannot keep its grid resident, and the
+// per-step parity hook). NT = taps (3: E/P/L, 11: ACF), SUB = 8-sample groups per
+// lane (M = 8*SUB contiguous samples), both compile-time so the accumulators stay in
+// VGPRs. Grid: nch x bpc blocks; block b of a channel owns the 256*SUB consecutive
+// 8-sample groups starting at g_first + 256*SUB*b.
+// ---------------------------------------------------------------------------
+template <int NT, int SUB, bool DIVIDE>
+__global__ __launch_bounds__(kTrkThreads) void track_step_kernel(const TrkParams* __restrict__ pp,
+                                                                const TrkBuffers* __restrict__ bp, int bpc)
+{
+    const TrkParams& p = *pp;  // (in device memory: the tail's calls take them by reference)
+    const TrkBuffers& b = *bp;
+    constexpr int M = 8 * SUB;
+    constexpr int NV = 2 * NT;
+    constexpr int T = kTrkThreads;
+    static_assert(M <= kLaneMax, "lane span exceeds the rotation table");
+    const int ch = blockIdx.x / bpc;
+    const int blk = blockIdx.x - ch * bpc;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+
+    // LDS: running sums slot[8][T], then the block reduction
+    constexpr int kSlot = 8 * T * 2;
+    constexpr int kRed = NV * (T + 32);
+    __shared__ __attribute__((aligned(16))) double s_mem[kSlot > kRed ? kSlot : kRed];
+    __shared__ double s_fin[NV];
+    __shared__ int s_last;
+    __shared__ TrkChan s_c;
+    __shared__ double2 s_zero;
+
+    g_desc* dp = (g_desc*)(b.desc + ch);  // global views: scalar loads, no flat waits
+    g_chan* cp = (g_chan*)(b.chan + ch);
+    unsigned long long* srow = b.stamps && ch == 0 ? stamp_row(b) : nullptr;
+    if (srow && tid == 0) stamp_max(srow, 8 + blk, wall_clock64());  // block start
+    const int64_t g_first = dp->g_first, g_last = dp->g_last;
+    const int64_t g0 = g_first + ((int64_t)blk * T + tid) * SUB;  // first group of the lane
+    // issue the IF loads first (clamped so every lane loads something valid)
+    const int8_t* iq = b.iq - p.buf_base;  // absolute-byte addressing
+    const int bad = dp->bad;
+    int4 raw[SUB];
+#pragma unroll
+    for (int j = 0; j < SUB; j++) {
+        const int64_t gj = g0 + j <= g_last ? g0 + j : g_last;
+        raw[j] = bad ? make_int4(0, 0, 0, 0) : ld_g16(iq + 16 * gj);
+    }
+    const unsigned cabits = lane < 32 ? ((g_cu32*)b.ca_bits)[ch * 32 + lane] : 0u;
+    // the channel state, for whichever block arrives last
+    constexpr int kChanWords = (int)(sizeof(TrkChan) / 8);
+    if (tid < kChanWords)
+        reinterpret_cast<uint64_t*>(&s_c)[tid] = ((const g_u64*)cp)[tid];
+
+    if (cp->status != GNSS_OK) return;
+    if (!dp->phaseC && dp->Index + 1 > cp->n1_target) return;  // 1-ms run of this channel done
+    if (bad || dp->d * M >= 1.0) {  // (a code rate beyond Fs/M breaks the one-boundary lane)
+        if (blk == 0 && tid == 0) b.chan[ch].status = bad ? bad : GNSS_EINDEX;
+        return;
+    }
+    double oI[NT], oQ[NT];
+    if (p.probe & 2) {  // timing probe: no correlation (loads, reduction and hand-off only)
+#pragma unroll
+        for (int s = 0; s < NT; s++) { oI[s] = (double)raw[0].x; oQ[s] = 0.0; }
+    } else {
+        if (tid == 0) s_zero = make_double2(0.0, 0.0);
+        __syncthreads();
+        lane_correlate<NT, SUB, DIVIDE, false>(p, dp, RegRaw<SUB>{raw}, 8 * g0 - dp->A, cabits,
+                                        reinterpret_cast<double2*>(s_mem) + tid, &s_zero, oI, oQ);
+    }
+
+    // ---- block reduction (fixed order), then hand the partial to the last arriver
+    const double bsum = block_partial<NT>(s_mem, oI, oQ, tid);
+    if (srow && tid == 0) stamp_max(srow, 8 + kMaxBpc + blk, wall_clock64());  // block computed
     double* allp = b.partial + (int64_t)ch * bpc * NV;
     if (wv == 0) {
-        if (lane < NV) {
-            double a = red2[lane * 32];
-            for (int k = 1; k < 32; k++) a += red2[lane * 32 + k];
-            st_sc1(allp + (int64_t)blk * NV + lane, a);  // write-through
-        }
+        if (lane < NV) st_sc1(allp + (int64_t)blk * NV + lane, bsum);  // write-through
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the storing wave drains
         if (lane == 0) {
             // two-level ticket: the blocks of the channel in this XCD group, then the
@@ -562,18 +747,18 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(TrkParams p, Tr
             if (srow) stamp_max(srow, 8 + 2 * kMaxBpc + blk, wall_clock64());  // last ticket issued
             int last = 0;
             if (bpc <= 32) {  // few arrivals: one level
-                if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                if (atomic_add_agent(top, 1u) ==
                     (unsigned)bpc - 1) {
-                    __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    store_agent(top, 0u);
                     last = 1;
                 }
-            } else if (__hip_atomic_fetch_add(sub, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            } else if (atomic_add_agent(sub, 1u) ==
                        cnt - 1) {
-                __hip_atomic_store(sub, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                store_agent(sub, 0u);
                 const unsigned ngroups = bpc < 8 ? (unsigned)bpc : 8u;
-                if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                if (atomic_add_agent(top, 1u) ==
                     ngroups - 1) {
-                    __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    store_agent(top, 0u);
                     last = 1;
                 }
             }
@@ -626,7 +811,7 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(TrkParams p, Tr
     if (srow && tid == 0) stamp_max(srow, 4, wall_clock64());  // sums final
     // every wave computes the loop update (same values in every lane); then wave 0
     // prepares the next step while waves 1 and 2 write the record and the state
-    const LoopUpd u = loop_update(p, s_c, s_fin[2 * p.iE], s_fin[2 * p.iE + 1], s_fin[2 * p.iP],
+    const LoopUpd u = loop_update_i(p, s_c, s_fin[2 * p.iE], s_fin[2 * p.iE + 1], s_fin[2 * p.iP],
                                   s_fin[2 * p.iP + 1], s_fin[2 * p.iL], s_fin[2 * p.iL + 1], o.pdi,
                                   o.phaseC);
     if (wv == 0 || wv == 3) {
@@ -640,20 +825,20 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(TrkParams p, Tr
         nx.pos = s_c.pos + 2 * o.n;
         nx.Index = s_c.Index + (o.phaseC ? 10 : 1);
         if (srow && wv == 0 && lane == 0) stamp_max(srow, 5, wall_clock64());  // loop updated
-        prepare_desc(p, nx, o.pdi, o.phaseC, wv == 0 ? 0 : 1, lane, b.desc + ch);
+        prepare_desc_i(p, nx, o.pdi, o.phaseC, wv == 0 ? 0 : 1, lane, b.desc + ch);
         if (srow && wv == 0 && lane == 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             stamp_max(srow, 6, wall_clock64());  // next descriptor stored
         }
         if (srow && wv == 0 && (p.probe & 32)) {  // the same again with a warm instruction cache
             if (lane == 0) stamp_max(srow, 0, wall_clock64());
-            const LoopUpd u2 = loop_update(p, s_c, s_fin[2 * p.iE], s_fin[2 * p.iE + 1],
+            const LoopUpd u2 = loop_update_i(p, s_c, s_fin[2 * p.iE], s_fin[2 * p.iE + 1],
                                            s_fin[2 * p.iP], s_fin[2 * p.iP + 1], s_fin[2 * p.iL],
                                            s_fin[2 * p.iL + 1], o.pdi, o.phaseC);
             nx.codeFreq = u2.codeFreq;
             nx.carrierFreq = u2.carrierFreq;
             if (lane == 0) stamp_max(srow, 1, wall_clock64());
-            prepare_desc(p, nx, o.pdi, o.phaseC, 0, lane, b.desc + ch);
+            prepare_desc_i(p, nx, o.pdi, o.phaseC, 0, lane, b.desc + ch);
             if (lane == 0) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 stamp_max(srow, 2, wall_clock64());
@@ -662,11 +847,11 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(TrkParams p, Tr
     } else if (p.probe & 4) {
         return;
     } else if (wv == 1) {
-        if (lane == 0) write_record(p, b, ch, s_c, o, u, s_fin);
+        if (lane == 0) write_record_i(p, b, ch, s_c, o, u, s_fin);
         if (b.taps_rec && lane < NV && s_c.slot < p.rec_cap)
             b.taps_rec[((int64_t)ch * p.rec_cap + s_c.slot) * NV + lane] = s_fin[lane];
     } else if (lane == 0) {
-        write_state(p, b, ch, s_c, o, u, s_fin);
+        write_state_i(p, b, ch, b.chan + ch, s_c, o, u, s_fin);
         if (srow) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             stamp_max(srow, 7, wall_clock64());  // state stored
@@ -676,23 +861,335 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(TrkParams p, Tr
     }
 }
 
-// Prepare the StepDesc of every channel from its current state (start of a phase).
-__global__ void track_prepare_kernel(TrkParams p, TrkBuffers b, int pdi, int phaseC)
+// ---------------------------------------------------------------------------
+// The persistent step loop: one launch runs `nsteps` tracking steps of every channel.
+// The blocks of a channel stay resident and loop over the steps; block 0 of the channel
+// also reduces the block partials, runs the loop update in the step kernel's wave roles
+// and publishes the next descriptor, with the channel state kept in its LDS for the
+// whole launch. Hand-offs inside the launch are R2 granules (guide G16): 8-byte
+// {tag, 32-bit word} relaxed agent-scope stores, polled until every tag matches
+// (block partials -> block 0; descriptor -> every block). The next step's IF bytes
+// are prefetched while the descriptor is in flight (its start, A + n, is known).
+// Every wait is bounded (~2 s): on timeout run_err is set and the blocks leave.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void publish_words(unsigned long long* g, const unsigned* src, int n,
+                                              unsigned tag, int tid)
 {
+    for (int e = tid; e < n; e += kTrkThreads)
+        store_agent(g + e, ((unsigned long long)tag << 32) | src[e]);
+}
+
+// Poll n granules until every tag equals `tag`; their words land in dst (LDS). Called by
+// every thread of the block; a granule seen once is not read again (its producer may
+// already have moved on). false (and run_err set) on timeout.
+__device__ bool sweep_words(const unsigned long long* g, int n, unsigned tag, unsigned* dst,
+                            int tid, unsigned* err)
+{
+    const unsigned long long t0 = wall_clock64();
+    unsigned todo = 0;  // bit k: granule tid + k*T still missing
+    for (int k = 0, e = tid; e < n; k++, e += kTrkThreads) todo |= 1u << k;
+    for (;;) {
+        for (int k = 0; (todo >> k) != 0; k++) {
+            if (!((todo >> k) & 1u)) continue;
+            const int e = tid + k * kTrkThreads;
+            const unsigned long long v = load_agent(g + e);
+            if ((unsigned)(v >> 32) == tag) {
+                dst[e] = (unsigned)v;
+                todo &= ~(1u << k);
+            }
+        }
+        if (__syncthreads_and(todo == 0)) return true;
+        // 100 MHz wall clock: give up after 2 s (a block of the grid is not resident)
+        if (__syncthreads_or(tid == 0 && wall_clock64() - t0 > 200000000ull)) {
+            if (tid == 0) atomicExch(err, 1u);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// Grid census (guide G16: residency is a precondition, not a given): every block
+// arrives on one counter; the last arrival starts the launch, a block that waits ~20 ms
+// aborts it instead (one CAS decides). On abort every block leaves before touching any
+// state, run_err[0] = 2, and the host re-runs the steps with the step kernel.
+__device__ bool census(unsigned* w, int tid)
+{
+    __shared__ int s_go;
+    if (tid == 0) {
+        unsigned* arrive = w + 1;
+        unsigned* state = w + 2;  // 0 pending, 1 go, 2 abort
+        if (atomic_add_agent(arrive, 1u) == gridDim.x - 1)
+            atomicCAS(state, 0u, 1u);
+        const unsigned long long t0 = wall_clock64();
+        unsigned st;
+        while ((st = __hip_atomic_load((g_u32*)state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
+            if (wall_clock64() - t0 > 2000000ull) atomicCAS(state, 0u, 2u);
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (st == 2) atomicCAS(w, 0u, 2u);
+        s_go = st == 1;
+    }
+    __syncthreads();
+    return s_go != 0;
+}
+
+// LDS barrier that leaves global loads (the next step's IF prefetch) in flight:
+// __syncthreads() would wait vmcnt(0) first.
+__device__ __forceinline__ void lds_barrier()
+{
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+}
+
+// The next step's 16-B IF groups of this lane straight into LDS (global_load_lds, no
+// VGPRs): group j of lane tid at s_raw[j*256 + tid]; each wave-instruction writes its
+// 64 lanes' 1 KiB contiguously from the wave's base.
+template <int SUB>
+__device__ __forceinline__ void prefetch_raw(const int8_t* iq, int64_t g0, int64_t gmax, int4* s_raw,
+                                             int tid)
+{
+    const int wbase = tid & ~63;
+#pragma unroll
+    for (int j = 0; j < SUB; j++) {
+        int64_t gj = g0 + j;
+        gj = gj < gmax ? gj : gmax;
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(iq + 16 * gj),
+                                         (__attribute__((address_space(3))) void*)(s_raw + j * kTrkThreads + wbase),
+                                         16, 0, 0);
+    }
+}
+
+// Persistent step loop, grid nch x bpc. Every block of a channel keeps its own copy of
+// the channel's scalar state and descriptor and runs the scalar end of every step itself
+// (the same fp64 code on the same sums: bit-identical copies), so a step needs one
+// exchange only: each block publishes its partial sums and reads everyone's. Block 0
+// of the channel writes the records, C/N0 and, at the end, the state.
+template <int NT, int SUB, bool DIVIDE>
+__global__ __launch_bounds__(kTrkThreads) void track_run_kernel(const TrkParams* __restrict__ pp,
+                                                               const TrkBuffers* __restrict__ bp, int bpc,
+                                                               int nsteps, unsigned tag0)
+{
+    const TrkParams& p = *pp;
+    const TrkBuffers& b = *bp;
+    constexpr int M = 8 * SUB;
+    constexpr int NV = 2 * NT;
+    constexpr int T = kTrkThreads;
+    static_assert(M <= kLaneMax, "lane span exceeds the rotation table");
+    const int ch = blockIdx.x / bpc;
+    const int blk = blockIdx.x - ch * bpc;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const bool io = blk == 0;
+
+    constexpr int kSlot = 8 * T * 2;                  // running sums [8][T] double2
+    constexpr int kRed = NV * (T + 32);               // block reduction
+    constexpr int kPart = kMaxBpcRun * NV;            // everyone's partials (as words)
+    constexpr int kMem0 = kSlot > kRed ? kSlot : kRed;
+    constexpr int kMem = kMem0 > kPart + 16 * NV ? kMem0 : kPart + 16 * NV;
+    __shared__ __attribute__((aligned(16))) double s_mem[kMem];
+    __shared__ __attribute__((aligned(16))) int4 s_raw[SUB * T];   // this step's IF
+    __shared__ __attribute__((aligned(16))) StepDesc s_d[2];       // this step / the next
+    __shared__ __attribute__((aligned(16))) TrkChan s_c[2];        // state before / after
+    __shared__ double s_fin[NV];
+    __shared__ double2 s_zero;
+
+    if (!census(b.run_err, tid)) return;
+    g_chan* cp = (g_chan*)(b.chan + ch);
+    if (cp->status != GNSS_OK) return;  // set before this launch: channel-uniform
+    const int64_t n1_target = cp->n1_target;
+    const int8_t* iq = b.iq - p.buf_base;  // absolute-byte addressing
+    const int64_t gmax = (p.buf_base + p.buf_len) / 16 - 1;  // last resident 16-B group
+    const unsigned cabits = lane < 32 ? ((g_cu32*)b.ca_bits)[ch * 32 + lane] : 0u;
+    unsigned long long* pg = b.pgran + (int64_t)ch * 2 * kMaxBpcRun * 2 * NV;
+    constexpr int kChanWords = (int)(sizeof(TrkChan) / 8);
+
+    // step 0's descriptor and the state, as the previous launch left them
+    for (int e = tid; e < kDescWords; e += T)
+        reinterpret_cast<unsigned*>(&s_d[0])[e] = ((const g_u32*)(b.desc + ch))[e];
+    if (tid < kChanWords) reinterpret_cast<uint64_t*>(&s_c[0])[tid] = ((const g_u64*)cp)[tid];
+    if (tid == 0) s_zero = make_double2(0.0, 0.0);
+    __syncthreads();
+    if (!s_d[0].bad)
+        prefetch_raw<SUB>(iq, s_d[0].g_first + ((int64_t)blk * T + tid) * SUB, gmax, s_raw, tid);
+
+    int cur = 0;
+    for (int s = 0; s < nsteps; s++) {
+        const StepDesc& D = s_d[cur];
+        const int bad = D.bad;
+        const bool stop = !D.phaseC && D.Index + 1 > n1_target;  // 1-ms run of this channel done
+        if (bad || stop || D.d * M >= 1.0) {  // (a code rate beyond Fs/M breaks the one-boundary lane)
+            if (io) {  // leave the state and this (unused) descriptor for the host / next launch
+                if (tid == 0 && !stop) s_c[cur].status = bad ? bad : GNSS_EINDEX;
+                __syncthreads();
+                if (tid < kChanWords)
+                    reinterpret_cast<uint64_t*>(b.chan + ch)[tid] = reinterpret_cast<const uint64_t*>(&s_c[cur])[tid];
+                for (int e = tid; e < kDescWords; e += T)
+                    reinterpret_cast<unsigned*>(b.desc + ch)[e] = reinterpret_cast<const unsigned*>(&D)[e];
+            }
+            return;
+        }
+        const int64_t A = uni(D.A), n = uni(D.n);
+        // timing probe (GNSS_STAMPS), channel 0, row s: [0] step start, [1] computed,
+        // [2] partial out, [3] all partials in, [4] next descriptor ready (block 0);
+        // [5..9] the same for the channel's last block
+        unsigned long long* srow = b.stamps && ch == 0 && s < kStampSlots && (io || blk == bpc - 1)
+                                       ? b.stamps + (size_t)s * kStampRow + (io ? 0 : 5) : nullptr;
+        if (srow && tid == 0) srow[0] = wall_clock64();
+
+        // ---- correlate this block's lanes (IF prefetched into s_raw)
+        {
+            const int64_t g0 = uni(D.g_first) + ((int64_t)blk * T + tid) * SUB;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's global_load_lds landed
+            double oI[NT], oQ[NT];
+            lane_correlate<NT, SUB, DIVIDE, true>(p, &D, LdsRaw{s_raw + tid}, 8 * g0 - A, cabits,
+                                                  reinterpret_cast<double2*>(s_mem) + tid, &s_zero, oI, oQ);
+            __syncthreads();  // slots and s_raw free
+            if (srow && tid == 0) srow[1] = wall_clock64();
+            // the next step starts at A + n (ftell after this read); its end is not known yet
+            if (s + 1 < nsteps)
+                prefetch_raw<SUB>(iq, ((A + n) >> 3) + ((int64_t)blk * T + tid) * SUB, gmax, s_raw, tid);
+            // block sum in a fixed order, LDS barriers only (the prefetch stays in flight)
+            double* red = s_mem;            // [NV][T]
+            double* red2 = s_mem + NV * T;  // [NV][32]
+#pragma unroll
+            for (int q = 0; q < NT; q++) {
+                red[(2 * q) * T + tid] = oI[q];
+                red[(2 * q + 1) * T + tid] = oQ[q];
+            }
+            lds_barrier();
+            for (int e = tid; e < NV * 32; e += T) {
+                const double* r = red + (e >> 5) * T + (e & 31) * 8;
+                double a = r[0];
+#pragma unroll
+                for (int k = 1; k < 8; k++) a += r[k];
+                red2[e] = a;
+            }
+            lds_barrier();
+            if (tid < NV * 4) {  // 4 lanes per value, then a fixed-order combine
+                const int v = tid >> 2, q = tid & 3;
+                const double* r = red2 + v * 32 + q * 8;
+                double a = r[0];
+#pragma unroll
+                for (int k = 1; k < 8; k++) a += r[k];
+                const double a1 = __shfl_xor(a, 1, 64);
+                const double a2 = (q & 1) ? a1 + a : a + a1;
+                const double a3 = __shfl_xor(a2, 2, 64);
+                const double sum = (q & 2) ? a3 + a2 : a2 + a3;
+                if (q == 0) {
+                    const unsigned long long w = (unsigned long long)__double_as_longlong(sum);
+                    const unsigned tg = tag0 + s + 1;
+                    unsigned long long* g = pg + (((int64_t)(s & 1) * kMaxBpcRun + blk) * NV + v) * 2;
+                    store_agent(g, ((unsigned long long)tg << 32) | (w & 0xffffffffull));
+                    store_agent(g + 1, ((unsigned long long)tg << 32) | (w >> 32));
+                }
+            }
+            if (srow && tid == 0) srow[2] = wall_clock64();
+            lds_barrier();  // red2 read before the partial words overwrite it
+        }
+
+        // ---- every block's partial, summed in a fixed order (bit-identical in all blocks)
+        unsigned* pw = reinterpret_cast<unsigned*>(s_mem);
+        if (!sweep_words(pg + (int64_t)(s & 1) * kMaxBpcRun * NV * 2, bpc * NV * 2, tag0 + s + 1, pw,
+                         tid, b.run_err))
+            return;
+        if (srow && tid == 0) srow[3] = wall_clock64();
+        constexpr int J = T / NV < 16 ? T / NV : 16;  // J*NV <= T threads
+        double* s_tmp = s_mem + kPart;
+        if (tid < J * NV) {
+            const int v = tid % NV, j = tid / NV;
+            double a = 0.0;
+            for (int k = j; k < bpc; k += J) {
+                const unsigned lo = pw[(k * NV + v) * 2], hi = pw[(k * NV + v) * 2 + 1];
+                a += __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+            }
+            s_tmp[j * NV + v] = a;
+        }
+        lds_barrier();
+        const int phaseC = D.phaseC;
+        if (tid < NV) {
+            double a = 0.0;
+#pragma unroll
+            for (int j = 0; j < J; j++) a += s_tmp[j * NV + tid];
+            s_fin[tid] = phaseC ? -a : a;  // :447-449
+        }
+        lds_barrier();
+
+        // ---- the loop update (every wave) and the step's scalar end: wave 0 the code half
+        // of the next descriptor, wave 3 the carrier half, wave 2 the new state, wave 1
+        // (block 0) the record
+        const TrkChan& c = s_c[cur];
+        StepOut o;
+        o.n = n;
+        o.delayValue = D.delayValue;
+        o.remSample = D.remSample;
+        o.remChip = D.remChip_next;
+        o.remPhase = D.remPhase_next;
+        o.pdi = D.pdi;
+        o.phaseC = phaseC;
+        const LoopUpd u = loop_update_i(p, c, s_fin[2 * p.iE], s_fin[2 * p.iE + 1], s_fin[2 * p.iP],
+                                      s_fin[2 * p.iP + 1], s_fin[2 * p.iL], s_fin[2 * p.iL + 1], o.pdi,
+                                      o.phaseC);
+        if (wv == 0 || wv == 3) {
+            NcoState nx;
+            nx.remChip = o.remChip;
+            nx.remPhase = o.remPhase;
+            nx.codeFreq = u.codeFreq;
+            nx.carrierFreq = u.carrierFreq;
+            nx.numSample = o.n;
+            nx.pos = c.pos + 2 * o.n;
+            nx.Index = c.Index + (o.phaseC ? 10 : 1);
+            prepare_desc_i(p, nx, o.pdi, o.phaseC, wv == 0 ? 0 : 1, lane, &s_d[cur ^ 1]);
+        } else if (wv == 1) {
+            if (io) {
+                if (lane == 0) write_record_i(p, b, ch, c, o, u, s_fin);
+                if (b.taps_rec && lane < NV && c.slot < p.rec_cap)
+                    b.taps_rec[((int64_t)ch * p.rec_cap + c.slot) * NV + lane] = s_fin[lane];
+            }
+        } else if (lane == 0) {
+            TrkChan& g = s_c[cur ^ 1];
+            write_state_i(p, b, ch, &g, c, o, u, s_fin, io);
+            // the fields a step does not change carry over
+            g.carrierFreqBasis = c.carrierFreqBasis;
+            g.n1_target = c.n1_target;
+            g.codedelay0 = c.codedelay0;
+            g.sv1 = c.sv1;
+            g.prn = c.prn;
+            g.status = c.status;
+            g.countinx = c.countinx;
+        }
+        lds_barrier();
+        if (srow && tid == 0) srow[4] = wall_clock64();
+        cur ^= 1;
+    }
+    if (io) {  // the state and the next step's descriptor for the next launch
+        if (tid < kChanWords)
+            reinterpret_cast<uint64_t*>(b.chan + ch)[tid] = reinterpret_cast<const uint64_t*>(&s_c[cur])[tid];
+        for (int e = tid; e < kDescWords; e += T)
+            reinterpret_cast<unsigned*>(b.desc + ch)[e] = reinterpret_cast<const unsigned*>(&s_d[cur])[e];
+    }
+}
+
+// Prepare the StepDesc of every channel from its current state (start of a phase).
+__global__ void track_prepare_kernel(const TrkParams* __restrict__ pp, const TrkBuffers* __restrict__ bp,
+                                     int pdi, int phaseC)
+{
+    const TrkParams& p = *pp;
+    const TrkBuffers& b = *bp;
     const int ch = blockIdx.x;
     const TrkChan c = b.chan[ch];
     prepare_desc(p, nco_of(c), pdi, phaseC, threadIdx.x >> 6, threadIdx.x & 63, b.desc + ch);
 }
 
-__global__ void track_snapshot_kernel(TrkBuffers b, int nch)
+__global__ void track_snapshot_kernel(const TrkBuffers* __restrict__ bp, int nch)
 {
+    const TrkBuffers& b = *bp;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < nch) b.snap[i] = b.chan[i];
 }
 
 // trackingCT.m:178-213 on the phase-A P_i (length msToProcessCT_1ms).
-__global__ void track_bitedge_kernel(TrkBuffers b, int nch)
+__global__ void track_bitedge_kernel(const TrkBuffers* __restrict__ bp, int nch)
 {
+    const TrkBuffers& b = *bp;
     const int ch = blockIdx.x * blockDim.x + threadIdx.x;
     if (ch >= nch) return;
     TrkChan& c = b.chan[ch];
@@ -722,8 +1219,11 @@ __global__ void track_bitedge_kernel(TrkBuffers b, int nch)
 // Entry to phase C (trackingCT.m:379-406): countinx = -1 resumes from the state
 // after step msToProcessCT_1ms - 1 (quirk A.9); fresh C/N0 counters; seek to the
 // nominal (skip + 1000 + countinx) ms position (quirk A.12); first 10-ms StepDesc.
-__global__ void track_phase_c_init_kernel(TrkParams p, TrkBuffers b, int64_t skip)
+__global__ void track_phase_c_init_kernel(const TrkParams* __restrict__ pp, const TrkBuffers* __restrict__ bp,
+                                          int64_t skip)
 {
+    const TrkParams& p = *pp;
+    const TrkBuffers& b = *bp;
     const int ch = blockIdx.x;
     __shared__ TrkChan s_c;
     if (threadIdx.x == 0) {
@@ -753,13 +1253,13 @@ __global__ void track_phase_c_init_kernel(TrkParams p, TrkBuffers b, int64_t ski
     if (c.status == GNSS_OK) prepare_desc(p, nco_of(c), 10, 1, threadIdx.x >> 6, threadIdx.x & 63, b.desc + ch);
 }
 
-hipError_t launch_track_step(const TrkParams& p, const TrkBuffers& b, int bpc, int sub,
+hipError_t launch_track_step(const TrkParams& p, const TrkBuffers& b, const TrkDev& d, int bpc, int sub,
                              hipStream_t s)
 {
     dim3 grid(p.nch * bpc), block(kTrkThreads);
 #define GNSS_STEP(NT_, SUB_, DIV_)                                                             \
     if (p.ntaps == NT_ && sub == SUB_ && (p.exact_div != 0) == DIV_) {                         \
-        hipLaunchKernelGGL((track_step_kernel<NT_, SUB_, DIV_>), grid, block, 0, s, p, b, bpc); \
+        hipLaunchKernelGGL((track_step_kernel<NT_, SUB_, DIV_>), grid, block, 0, s, d.p, d.b, bpc); \
         return hipGetLastError();                                                              \
     }
     GNSS_STEP(3, 1, false) GNSS_STEP(3, 2, false) GNSS_STEP(3, 4, false)
@@ -769,29 +1269,64 @@ hipError_t launch_track_step(const TrkParams& p, const TrkBuffers& b, int bpc, i
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_track_prepare(const TrkParams& p, const TrkBuffers& b, int pdi, int phaseC,
-                                hipStream_t s)
+hipError_t launch_track_run(const TrkParams& p, const TrkBuffers& b, const TrkDev& d, int bpc, int sub,
+                            int nsteps, unsigned tag0, hipStream_t s)
 {
-    hipLaunchKernelGGL(track_prepare_kernel, dim3(p.nch), dim3(128), 0, s, p, b, pdi, phaseC);
+    dim3 grid(p.nch * bpc), block(kTrkThreads);
+#define GNSS_RUN(NT_, SUB_, DIV_)                                                              \
+    if (p.ntaps == NT_ && sub == SUB_ && (p.exact_div != 0) == DIV_) {                         \
+        hipLaunchKernelGGL((track_run_kernel<NT_, SUB_, DIV_>), grid, block, 0, s, d.p, d.b, bpc, \
+                           nsteps, tag0);                                                      \
+        return hipGetLastError();                                                              \
+    }
+    GNSS_RUN(3, 1, false) GNSS_RUN(3, 2, false) GNSS_RUN(3, 4, false)
+    GNSS_RUN(11, 1, false) GNSS_RUN(11, 2, false) GNSS_RUN(11, 4, false)
+    GNSS_RUN(3, 1, true) GNSS_RUN(11, 1, true)
+#undef GNSS_RUN
+    return hipErrorInvalidValue;
+}
+
+int track_run_blocks_per_cu(const TrkParams& p, int sub)
+{
+    int nb = 0;
+#define GNSS_OCC(NT_, SUB_, DIV_)                                                              \
+    if (p.ntaps == NT_ && sub == SUB_ && (p.exact_div != 0) == DIV_) {                         \
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(                                      \
+                &nb, reinterpret_cast<const void*>(track_run_kernel<NT_, SUB_, DIV_>),          \
+                kTrkThreads, 0) != hipSuccess)                                                 \
+            nb = 0;                                                                            \
+        return nb;                                                                             \
+    }
+    GNSS_OCC(3, 1, false) GNSS_OCC(3, 2, false) GNSS_OCC(3, 4, false)
+    GNSS_OCC(11, 1, false) GNSS_OCC(11, 2, false) GNSS_OCC(11, 4, false)
+    GNSS_OCC(3, 1, true) GNSS_OCC(11, 1, true)
+#undef GNSS_OCC
+    return 0;
+}
+
+hipError_t launch_track_prepare(const TrkParams& p, const TrkBuffers& b, const TrkDev& d, int pdi,
+                                int phaseC, hipStream_t s)
+{
+    hipLaunchKernelGGL(track_prepare_kernel, dim3(p.nch), dim3(128), 0, s, d.p, d.b, pdi, phaseC);
     return hipGetLastError();
 }
 
-hipError_t launch_track_snapshot(const TrkParams& p, const TrkBuffers& b, hipStream_t s)
+hipError_t launch_track_snapshot(const TrkParams& p, const TrkBuffers& b, const TrkDev& d, hipStream_t s)
 {
-    hipLaunchKernelGGL(track_snapshot_kernel, dim3((p.nch + 63) / 64), dim3(64), 0, s, b, p.nch);
+    hipLaunchKernelGGL(track_snapshot_kernel, dim3((p.nch + 63) / 64), dim3(64), 0, s, d.b, p.nch);
     return hipGetLastError();
 }
 
-hipError_t launch_track_bitedge(const TrkParams& p, const TrkBuffers& b, hipStream_t s)
+hipError_t launch_track_bitedge(const TrkParams& p, const TrkBuffers& b, const TrkDev& d, hipStream_t s)
 {
-    hipLaunchKernelGGL(track_bitedge_kernel, dim3((p.nch + 63) / 64), dim3(64), 0, s, b, p.nch);
+    hipLaunchKernelGGL(track_bitedge_kernel, dim3((p.nch + 63) / 64), dim3(64), 0, s, d.b, p.nch);
     return hipGetLastError();
 }
 
-hipError_t launch_track_phase_c_init(const TrkParams& p, const TrkBuffers& b, int64_t skip,
-                                     hipStream_t s)
+hipError_t launch_track_phase_c_init(const TrkParams& p, const TrkBuffers& b, const TrkDev& d,
+                                     int64_t skip, hipStream_t s)
 {
-    hipLaunchKernelGGL(track_phase_c_init_kernel, dim3(p.nch), dim3(128), 0, s, p, b, skip);
+    hipLaunchKernelGGL(track_phase_c_init_kernel, dim3(p.nch), dim3(128), 0, s, d.p, d.b, skip);
     return hipGetLastError();
 }
 
