@@ -669,23 +669,39 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     // < 1 with margin for the DLL's excursions (the kernel flags a violating step)
     const double cps_max = 1.1 * sg->codeFreqBasis / sg->Fs;
     auto sub_ok = [&](int sub) { return 8.0 * sub * cps_max < 1.0 && (sub == 1 || !P.exact_div); };
-    // (measured on MI355X, 8 channels: 1-ms steps are latency-bound -> the shortest lanes;
-    // 10-ms steps -> the longest, fewest blocks)
+    // The lane span depends on the step length only (not on the channel set or the path),
+    // so a channel's sums are bit-identical however the channels are sharded. 1-ms steps
+    // are latency-bound -> the shortest lanes; 10-ms steps: 24-sample lanes, 96 blocks per
+    // channel at Opensky rates, which loads the CUs evenly at 8 channels per GPU (3 blocks
+    // per CU; a step lasts as long as its slowest block).
     auto sub_for = [&](int pdi) {
-        int sub = pdi >= 10 ? 4 : 1;
-        while (sub > 1 && !sub_ok(sub)) sub /= 2;
+        int sub = pdi >= 10 ? 3 : 1;
+        while (sub > 1 && !sub_ok(sub)) sub--;
         return sub;
     };
     int sub1 = sub_for(1), sub10 = sub_for(10);
     if (const char* fs = getenv("GNSS_FORCE_SUB")) {  // test hook: exercise every kernel variant
         const int v = atoi(fs);
-        if ((v == 1 || v == 2 || v == 4) && sub_ok(v)) sub1 = sub10 = v;
+        if (v >= 1 && v <= 4 && sub_ok(v)) sub1 = sub10 = v;
     }
-    if (const char* pr = getenv("GNSS_PROBE")) P.probe = atoi(pr);
     auto bpc_for = [&](int pdi, int sub) {
         const double groups = (S * pdi * 1.01 + 64) / 8.0 + 2;
         return (int)std::ceil(groups / ((double)kTrkThreads * sub));
     };
+    // Persistent step loop (track_run_kernel) when every block of its grid can be
+    // resident: one launch per phase run. Residency from the occupancy query; the kernel's
+    // own census confirms it (the query can over-report, guide section 1) and a launch
+    // that finds a block missing changes nothing and is re-run one launch per step, as is
+    // everything with GNSS_NO_PERSIST. Both paths give the same bits.
+    int cus = 0;
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    auto persistent_ok = [&](int pdi, int sub) {
+        if (getenv("GNSS_NO_PERSIST") || bpc_for(pdi, sub) > kMaxBpcRun) return false;
+        const int occ = std::min(track_run_blocks_per_cu(P, sub), 4);
+        return occ >= 1 && (int64_t)nch * bpc_for(pdi, sub) <= (int64_t)occ * cus;
+    };
+    bool persist1 = persistent_ok(1, sub1), persist10 = persistent_ok(10, sub10);
+    if (const char* pr = getenv("GNSS_PROBE")) P.probe = atoi(pr);
     const int bpc1 = bpc_for(1, sub1), bpc10 = bpc_for(10, sub10);
     if (bpc10 > kMaxBpc) return fail(ctx, GNSS_EARG, "Sample too large for the step geometry");
 
@@ -754,19 +770,6 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         B.stamps = d_stamps.as<unsigned long long>();
     }
 
-    // Persistent step loop (track_run_kernel) when every block of its grid can be
-    // resident: one launch per phase run. Residency from the occupancy query; the kernel's
-    // own census confirms it (the query can over-report, guide section 1) and a launch
-    // that finds a block missing changes nothing and is re-run one launch per step, as
-    // is everything with GNSS_NO_PERSIST.
-    int cus = 0;
-    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
-    auto persistent_ok = [&](int bpc, int sub) {
-        if (getenv("GNSS_NO_PERSIST") || bpc > kMaxBpcRun) return false;
-        const int occ = std::min(track_run_blocks_per_cu(P, sub), 4);
-        return occ >= 1 && (int64_t)nch * bpc <= (int64_t)occ * cus;
-    };
-    bool persist1 = persistent_ok(bpc1, sub1), persist10 = persistent_ok(bpc10, sub10);
     DevBuf d_pgran, d_err;
     if (persist1 || persist10) {
         HIP_TRY(d_pgran.alloc(sizeof(unsigned long long) * (size_t)nch * 2 * kMaxBpcRun * 4 * ntaps));
@@ -1034,7 +1037,7 @@ int gnss_correlate_step(gnss_ctx* ctx, const gnss_file* file, const gnss_signal*
     int sub = 1;
     if (const char* fs = getenv("GNSS_FORCE_SUB")) {
         const int v = atoi(fs);
-        if ((v == 2 || v == 4) && !P.exact_div && 8.0 * v * codeFreq / sg->Fs < 1.0) sub = v;
+        if (v >= 2 && v <= 4 && !P.exact_div && 8.0 * v * codeFreq / sg->Fs < 1.0) sub = v;
     }
     const int bpc = (int)std::ceil(((S * pdi * 1.01 + 64) / 8.0 + 2) / ((double)kTrkThreads * sub));
     DevBuf d_chan, d_desc, d_ca, d_part, d_arrive, d_sums;

@@ -85,6 +85,18 @@ GNSS_HD unsigned ca_index32(int chip)
     return (unsigned)(chip + 1022) % 1023u;
 }
 
+// fmod of non-negative x by positive y with a quotient below 2^53, exact like C fmod:
+// trunc(RN(x/y)) is the true quotient or one more, and x - q*y is representable in both
+// cases, so the FMA is exact and one correction finishes it (the library fmod loops
+// over the exponent difference).
+GNSS_HD double fmod_pos(double x, double y)
+{
+    const double q = trunc(x / y);
+    double r = __builtin_fma(-q, y, x);
+    if (r < 0) r += y;
+    return r;
+}
+
 constexpr double kTwoPi = 2.0 * 3.14159265358979323846;  // MATLAB 2*pi
 constexpr double kTwoPiLo = 2.4492935982947064e-16;      // 2*pi - kTwoPi
 

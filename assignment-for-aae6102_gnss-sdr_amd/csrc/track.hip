@@ -167,15 +167,16 @@ __device__ __forceinline__ StepSize step_size(const TrkParams& p, const NcoState
 }
 
 // Prepare the descriptor of the step that follows state `c` (trackingCT.m:79-107 /
-// :411-441). Two waves work on it side by side:
+// :411-441). Three waves work on it side by side (divergent lanes of one wave would run
+// one after the other):
 //   role 0 (code): lanes < ntaps build the colon of their tap, lane 0 the scalars;
-//   role 1 (carrier): lanes < 32 the rotation table e^{i phi_m}, lane 63 remPhase.
+//   role 1 (carrier): lanes < 32 the rotation table e^{i phi_m} (depends on f only);
+//   role 2: lane 63 the next remPhase (needs numSample).
+// `taps` = the tap spacings (a copy in LDS where the caller has one).
 __device__ __forceinline__ void prepare_desc_i(const TrkParams& p, const NcoState& c, int pdi, int phaseC, int role,
-                             int lane, StepDesc* d)
+                             int lane, StepDesc* d, const double* taps = nullptr,
+                             unsigned long long* dbg = nullptr)
 {
-    const StepSize z = step_size(p, c, pdi, phaseC);
-    const int64_t n = z.n;
-    const double cps = z.cps;
     if (role == 1) {
         // carrier increment delta = 2*pi*f/Fs as a double-double; dhi has 48 bits so
         // m*dhi (m < 32) is exact
@@ -204,12 +205,20 @@ __device__ __forceinline__ void prepare_desc_i(const TrkParams& p, const NcoStat
                 d->dhi = dhi;
                 d->dlo = dlo;
             }
-        } else if (lane == 63) {
-            // remPhase = rem(Wave(numSample+1), 2*pi) (:104-106)
-            d->remPhase_next = rem_2pi(kTwoPi * (f * ((double)n / p.Fs)) + c.remPhase);
         }
         return;
     }
+    const StepSize z = step_size(p, c, pdi, phaseC);
+    const int64_t n = z.n;
+    const double cps = z.cps;
+    if (role == 2) {
+        if (lane == 63) {
+            // remPhase = rem(Wave(numSample+1), 2*pi) (:104-106)
+            d->remPhase_next = rem_2pi(kTwoPi * (c.carrierFreq * ((double)n / p.Fs)) + c.remPhase);
+        }
+        return;
+    }
+    if (dbg && lane == 0) dbg[0] = wall_clock64();
     const int64_t A = c.pos / 2;
     int bad = GNSS_OK;
     if (n <= 0 || n > (int64_t)(p.S * pdi * 1.01) + 64) bad = GNSS_EINDEX;
@@ -217,8 +226,9 @@ __device__ __forceinline__ void prepare_desc_i(const TrkParams& p, const NcoStat
     else if (2 * A < p.buf_base || 2 * (A + n) > p.buf_base + p.buf_len) bad = GNSS_EIO;
     if (lane < p.ntaps) {
         // t = (0 + Spacing + remChip) : cps : ((numSample-1)*cps + Spacing + remChip) (:96-98)
-        const double a = (0 + p.taps[lane]) + c.remChip;
-        const double bb = ((double)(n - 1) * cps + p.taps[lane]) + c.remChip;
+        const double tap = taps ? taps[lane] : p.taps[lane];
+        const double a = (0 + tap) + c.remChip;
+        const double bb = ((double)(n - 1) * cps + tap) + c.remChip;
         const Colon col = colon_make_hint(a, cps, bb, n - 1);
         d->tap_a[lane] = col.a;
         d->tap_c[lane] = col.c;
@@ -232,10 +242,10 @@ __device__ __forceinline__ void prepare_desc_i(const TrkParams& p, const NcoStat
         }
         if (tb != GNSS_OK && bad == GNSS_OK) bad = tb;
     }
-    // any lane's failure wins (bitwise-or of the positive codes is enough to flag)
-    int badw = bad;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) badw = max(badw, __shfl_xor(badw, o, 64));
+    if (dbg && lane == 0) dbg[1] = wall_clock64();
+    // the first failing lane's code wins
+    const unsigned long long fails = __ballot(bad != GNSS_OK);
+    const int badw = fails ? __builtin_amdgcn_readlane(bad, __ffsll((long long)fails) - 1) : GNSS_OK;
     if (lane == 0) {
         d->n = n;
         d->delayValue = z.dv;
@@ -255,6 +265,13 @@ __device__ __forceinline__ void prepare_desc_i(const TrkParams& p, const NcoStat
 __device__ __noinline__ void prepare_desc(const TrkParams& p, const NcoState& c, int pdi, int phaseC, int role, int lane, StepDesc* d)
 {
     prepare_desc_i(p, c, pdi, phaseC, role, lane, d);
+}
+
+// All three roles of prepare_desc by a 192-thread block (wave = role).
+__device__ __forceinline__ void prepare_desc_block(const TrkParams& p, const NcoState& c, int pdi, int phaseC,
+                                                   StepDesc* d)
+{
+    prepare_desc(p, c, pdi, phaseC, threadIdx.x >> 6, threadIdx.x & 63, d);
 }
 
 
@@ -311,21 +328,26 @@ struct LoopUpd {
 
 __device__ __forceinline__ LoopUpd loop_update_i(const TrkParams& p, const TrkChan& c, double E_i,
                                                double E_q, double P_i, double P_q, double L_i,
-                                               double L_q, int pdi, int phaseC)
+                                               double L_q, int pdi, int phaseC, int which = 3)
 {
-    LoopUpd u;
-    const double E = sqrt(E_i * E_i + E_q * E_q);
-    const double L = sqrt(L_i * L_i + L_q * L_q);
-    u.DLLdiscri = 0.5 * (E - L) / (E + L);
+    // which: 1 = the DLL half only, 2 = the PLL half only, 3 = both (wave-uniform)
+    LoopUpd u{0, 0, 0, 0, 0, 0};
     const double T = phaseC ? 0.001 : (0.001 * pdi);
-    u.code_output = c.code_outputLast + (p.tau2code / p.tau1code) * (u.DLLdiscri - c.DLLdiscriLast) +
-                    u.DLLdiscri * (T / p.tau1code);
-    u.codeFreq = p.codeFreqBasis - u.code_output;
-    u.PLLdiscri = atan_tab(P_q / P_i) / kTwoPi;
-    u.carrier_output = c.carrier_outputLast +
-                       (p.tau2carr / p.tau1carr) * (u.PLLdiscri - c.PLLdiscriLast) +
-                       u.PLLdiscri * (T / p.tau1carr);
-    u.carrierFreq = c.carrierFreqBasis + u.carrier_output;
+    if (which & 1) {
+        const double E = sqrt(E_i * E_i + E_q * E_q);
+        const double L = sqrt(L_i * L_i + L_q * L_q);
+        u.DLLdiscri = 0.5 * (E - L) / (E + L);
+        u.code_output = c.code_outputLast + (p.tau2code / p.tau1code) * (u.DLLdiscri - c.DLLdiscriLast) +
+                        u.DLLdiscri * (T / p.tau1code);
+        u.codeFreq = p.codeFreqBasis - u.code_output;
+    }
+    if (which & 2) {
+        u.PLLdiscri = atan_tab(P_q / P_i) / kTwoPi;
+        u.carrier_output = c.carrier_outputLast +
+                           (p.tau2carr / p.tau1carr) * (u.PLLdiscri - c.PLLdiscriLast) +
+                           u.PLLdiscri * (T / p.tau1carr);
+        u.carrierFreq = c.carrierFreqBasis + u.carrier_output;
+    }
     return u;
 }
 // out-of-line copy for the persistent kernel (keeps its register budget)
@@ -345,24 +367,35 @@ struct StepOut {
 
 // TckResultCT fields of the step (trackingCT.m:153-170 / :507-524) and the phase-A
 // P_i kept for the bit-edge search. `s` = the step's (negated in phase C) sums.
+// The prefix of delayValue sums the step's codedelay reads (quirk A.11): cumulative
+// column `cols` of an nsv x N matrix read column-major, capped at the step count.
+__device__ __forceinline__ int64_t record_cols(const TrkParams& p, const TrkChan& c, int phaseC)
+{
+    const int64_t Index = c.Index + (phaseC ? 10 : 1);
+    const int64_t nstep = c.nstep + 1;
+    int64_t cols = 0;
+    if (Index >= c.sv1) cols = (Index - c.sv1) / p.nsv + 1;
+    return cols > nstep ? nstep : cols;
+}
+
+// `pre`, when given, holds dvpre[nstep] and dvpre[cols] loaded ahead by the caller.
 __device__ __forceinline__ void write_record_i(const TrkParams& p, const TrkBuffers& b, int ch, const TrkChan& c,
-                             const StepOut& o, const LoopUpd& u, const double* s)
+                             const StepOut& o, const LoopUpd& u, const double* s,
+                             const int64_t* pre = nullptr)
 {
     const double P_i = s[2 * p.iP], P_q = s[2 * p.iP + 1];
     const int64_t pos = c.pos + 2 * o.n;  // ftell after fread
-    const int64_t Index = c.Index + (o.phaseC ? 10 : 1);
     const int64_t col = c.nstep;          // 0-based IndexSmall - 1
     int64_t* dvpre = b.dvpre + (int64_t)ch * (p.rec_cap + 1);
-    const int64_t dvsum = dvpre[col] + o.delayValue;
+    const int64_t dvsum = (pre ? pre[0] : dvpre[col]) + o.delayValue;
     dvpre[col + 1] = dvsum;
     const int64_t nstep = col + 1;
     // sum(delayValue(1:Index)) over an nsv x N matrix (column-major, quirk A.11)
-    int64_t cols = 0;
-    if (Index >= c.sv1) cols = (Index - c.sv1) / p.nsv + 1;
-    if (cols > nstep) cols = nstep;
-    const double codedelay = (double)c.codedelay0 + (double)(cols == nstep ? dvsum : dvpre[cols]);
+    const int64_t cols = record_cols(p, c, o.phaseC);
+    const double codedelay =
+        (double)c.codedelay0 + (double)(cols == nstep ? dvsum : (pre ? pre[1] : dvpre[cols]));
     const double absS = (double)pos;
-    const double m = fmod(absS / p.dataBytesPerSample, p.Fs * p.ms);  // mod() of positives
+    const double m = fmod_pos(absS / p.dataBytesPerSample, p.Fs * p.ms);  // mod() of positives
     const int64_t slot = c.slot;
     if (slot < p.rec_cap) {
         double* r = b.rec + ((int64_t)ch * p.rec_cap + slot) * GNSS_NFIELDS;
@@ -593,8 +626,7 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
             run_r += wr;
             run_i += wi;
             myslot[mm * T] = make_double2(run_r, run_i);
-            // RELOAD: at most two samples' table values in flight (VGPR budget of 3 waves/SIMD)
-            if (RELOAD && (mm & 1)) __builtin_amdgcn_sched_barrier(0);
+
         }
 #pragma unroll
         for (int s = 0; s < NT; s++) {
@@ -604,10 +636,13 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
             pre_i[s] += v.y;
         }
     };
-    if constexpr (RELOAD) {
+    if constexpr (RELOAD && NT > 3) {
         // descriptor in LDS: one subgroup at a time (unrolled, the compiler would keep
         // every subgroup's table values live)
 #pragma unroll 1
+        for (int j = 0; j < SUB; j++) subgroup(j);
+    } else if constexpr (RELOAD) {
+#pragma unroll 2
         for (int j = 0; j < SUB; j++) subgroup(j);
     } else {
 #pragma unroll
@@ -628,35 +663,77 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
 // Block-level sum of the lanes' tap sums in a fixed order (bit-reproducible). On return
 // thread v < 2*NT holds block sum v (I of tap v/2 for even v, Q for odd); s_mem is
 // free again for the caller. s_mem: [2NT][T] + [2NT][32] doubles.
+// A double moved across lanes by a DPP control (both halves; every lane active).
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// LDS barrier that leaves global loads (the next step's IF prefetch) in flight:
+// __syncthreads() would wait vmcnt(0) first.
+__device__ __forceinline__ void lds_barrier()
+{
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+}
+
+// The two fixed-order reductions both step loops share (their results are bit-identical
+// for a given lane geometry, whichever kernel, grid or channel set runs the step).
+//
+// Block: the NV tap sums of the block's 256 lanes: 8-lane runs, then four runs per lane,
+// then a DPP quad butterfly. Slots are free on entry (caller's barrier); the value is in
+// lanes tid = 4v (v < NV); LDS barriers only (global loads in flight stay so).
 template <int NT>
 __device__ __forceinline__ double block_partial(double* s_mem, const double (&oI)[NT],
                                                 const double (&oQ)[NT], int tid)
 {
     constexpr int NV = 2 * NT, T = kTrkThreads;
-    __syncthreads();  // every wave is done with the slots
     double* red = s_mem;            // [NV][T]
     double* red2 = s_mem + NV * T;  // [NV][32]
 #pragma unroll
-    for (int s = 0; s < NT; s++) {
-        red[(2 * s) * T + tid] = oI[s];
-        red[(2 * s + 1) * T + tid] = oQ[s];
+    for (int q = 0; q < NT; q++) {
+        red[(2 * q) * T + tid] = oI[q];
+        red[(2 * q + 1) * T + tid] = oQ[q];
     }
-    __syncthreads();
+    lds_barrier();
     for (int e = tid; e < NV * 32; e += T) {
-        const int v = e >> 5, g = e & 31;
-        const double* r = red + v * T + g * 8;
+        const double* r = red + (e >> 5) * T + (e & 31) * 8;
         double a = r[0];
 #pragma unroll
         for (int k = 1; k < 8; k++) a += r[k];
         red2[e] = a;
     }
-    __syncthreads();
+    lds_barrier();
     double a = 0.0;
-    if (tid < NV) {
-        a = red2[tid * 32];
-        for (int k = 1; k < 32; k++) a += red2[tid * 32 + k];
+    if (tid < NV * 4) {  // 4 lanes per value (waves 0, and 1 for 11 taps)
+        const double* r = red2 + (tid >> 2) * 32 + (tid & 3) * 8;
+        a = r[0];
+#pragma unroll
+        for (int k = 1; k < 8; k++) a += r[k];
+        a += dpp_f64<0xB1>(a);  // quad_perm [1,0,3,2]
+        a += dpp_f64<0x4E>(a);  // quad_perm [2,3,0,1] (IEEE addition commutes: lanes agree)
     }
-    __syncthreads();
+    lds_barrier();  // red2 read before the caller reuses the slots
+    return a;
+}
+
+// Channel: the sum over the bpc block partials of value v = tid >> 3 (tid < 8*NV): lane
+// q = tid & 7 adds blocks q, q+8, ... in order, then a DPP butterfly over the 8 lanes.
+// Every lane of the 8 returns the sum. load(k, v) = block k's partial of value v.
+template <class Load>
+__device__ __forceinline__ double channel_sum(int bpc, int tid, Load load)
+{
+    const int v = tid >> 3, q = tid & 7;
+    double a = 0.0;
+#pragma unroll 4
+    for (int k = q; k < bpc; k += 8) a += load(k, v);
+    a += dpp_f64<0xB1>(a);   // quad_perm [1,0,3,2]
+    a += dpp_f64<0x4E>(a);   // quad_perm [2,3,0,1]
+    a += dpp_f64<0x141>(a);  // row_half_mirror: the other quad of the 8
     return a;
 }
 
@@ -730,11 +807,16 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(const TrkParams
     }
 
     // ---- block reduction (fixed order), then hand the partial to the last arriver
+    __syncthreads();  // every wave is done with the slots
     const double bsum = block_partial<NT>(s_mem, oI, oQ, tid);
     if (srow && tid == 0) stamp_max(srow, 8 + kMaxBpc + blk, wall_clock64());  // block computed
     double* allp = b.partial + (int64_t)ch * bpc * NV;
+    if (tid < NV * 4 && (tid & 3) == 0) st_sc1(allp + (int64_t)blk * NV + (tid >> 2), bsum);  // write-through
+    if constexpr (NV * 4 > 64) {  // (11 taps: waves 0 and 1 store) every storing wave drains
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+    }
     if (wv == 0) {
-        if (lane < NV) st_sc1(allp + (int64_t)blk * NV + lane, bsum);  // write-through
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the storing wave drains
         if (lane == 0) {
             // two-level ticket: the blocks of the channel in this XCD group, then the
@@ -770,22 +852,9 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(const TrkParams
 
     // ---- last arriver: deterministic reduction of all block partials (sc1 loads)
     if (srow && tid == 0) stamp_max(srow, 3, wall_clock64());
-    constexpr int J = T / NV;
-    double* s_tmp = s_mem;  // [J][NV]
-    if (tid < J * NV) {
-        const int v = tid % NV, j = tid / NV;
-        double a = 0;
-        int k = j;
-        for (; k + 3 * J < bpc; k += 4 * J) {
-            const double x0 = ld_sc1(allp + (int64_t)k * NV + v);
-            const double x1 = ld_sc1(allp + (int64_t)(k + J) * NV + v);
-            const double x2 = ld_sc1(allp + (int64_t)(k + 2 * J) * NV + v);
-            const double x3 = ld_sc1(allp + (int64_t)(k + 3 * J) * NV + v);
-            a += x0; a += x1; a += x2; a += x3;
-        }
-        for (; k < bpc; k += J) a += ld_sc1(allp + (int64_t)k * NV + v);
-        s_tmp[j * NV + v] = a;
-    }
+    double csum = 0.0;
+    if (tid < 8 * NV)
+        csum = channel_sum(bpc, tid, [&](int k, int v) { return ld_sc1(allp + (int64_t)k * NV + v); });
     // the step's values the writers need, read before the next descriptor replaces them
     StepOut o;
     o.n = dp->n;
@@ -796,34 +865,33 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(const TrkParams
     o.pdi = dp->pdi;
     o.phaseC = dp->phaseC;
     const bool dbg = b.dbg_sums || (p.probe & 1);
-    __syncthreads();
-    if (tid < NV) {
-        double a = 0;
-        for (int j = 0; j < J; j++) a += s_tmp[j * NV + tid];
+    if (tid < 8 * NV && (tid & 7) == 0) {
+        const int v = tid >> 3;
         if (dbg) {
-            if (b.dbg_sums) b.dbg_sums[ch * NV + tid] = a;
+            if (b.dbg_sums) b.dbg_sums[ch * NV + v] = csum;
         } else {
-            s_fin[tid] = o.phaseC ? -a : a;  // :447-449
+            s_fin[v] = o.phaseC ? -csum : csum;  // :447-449
         }
     }
     if (dbg) return;
     __syncthreads();
     if (srow && tid == 0) stamp_max(srow, 4, wall_clock64());  // sums final
-    // every wave computes the loop update (same values in every lane); then wave 0
-    // prepares the next step while waves 1 and 2 write the record and the state
+    // every wave computes the loop update (same values in every lane); then waves 0, 3
+    // and 2 prepare the next step (code half, carrier table, remPhase) while wave 1
+    // writes the record and wave 2 the state
     const LoopUpd u = loop_update_i(p, s_c, s_fin[2 * p.iE], s_fin[2 * p.iE + 1], s_fin[2 * p.iP],
                                   s_fin[2 * p.iP + 1], s_fin[2 * p.iL], s_fin[2 * p.iL + 1], o.pdi,
                                   o.phaseC);
+    NcoState nx;
+    nx.remChip = o.remChip;
+    nx.remPhase = o.remPhase;
+    nx.codeFreq = u.codeFreq;
+    nx.carrierFreq = u.carrierFreq;
+    nx.numSample = o.n;
+    nx.pos = s_c.pos + 2 * o.n;
+    nx.Index = s_c.Index + (o.phaseC ? 10 : 1);
     if (wv == 0 || wv == 3) {
         if (p.probe & 8) return;
-        NcoState nx;
-        nx.remChip = o.remChip;
-        nx.remPhase = o.remPhase;
-        nx.codeFreq = u.codeFreq;
-        nx.carrierFreq = u.carrierFreq;
-        nx.numSample = o.n;
-        nx.pos = s_c.pos + 2 * o.n;
-        nx.Index = s_c.Index + (o.phaseC ? 10 : 1);
         if (srow && wv == 0 && lane == 0) stamp_max(srow, 5, wall_clock64());  // loop updated
         prepare_desc_i(p, nx, o.pdi, o.phaseC, wv == 0 ? 0 : 1, lane, b.desc + ch);
         if (srow && wv == 0 && lane == 0) {
@@ -850,7 +918,9 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(const TrkParams
         if (lane == 0) write_record_i(p, b, ch, s_c, o, u, s_fin);
         if (b.taps_rec && lane < NV && s_c.slot < p.rec_cap)
             b.taps_rec[((int64_t)ch * p.rec_cap + s_c.slot) * NV + lane] = s_fin[lane];
-    } else if (lane == 0) {
+    } else {
+        prepare_desc_i(p, nx, o.pdi, o.phaseC, 2, lane, b.desc + ch);  // lane 63: remPhase
+        if (lane != 0) return;
         write_state_i(p, b, ch, b.chan + ch, s_c, o, u, s_fin);
         if (srow) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -880,15 +950,17 @@ __device__ __forceinline__ void publish_words(unsigned long long* g, const unsig
 }
 
 // Poll n granules until every tag equals `tag`; their words land in dst (LDS). Called by
-// every thread of the block; a granule seen once is not read again (its producer may
-// already have moved on). false (and run_err set) on timeout.
+// every thread of the block. Each lane polls its own granules (tid + k*T) with no block
+// barrier per round, a granule seen once is not read again (its producer may already have
+// moved on); one barrier at the end. false (and run_err set) on timeout (~2 s).
 __device__ bool sweep_words(const unsigned long long* g, int n, unsigned tag, unsigned* dst,
                             int tid, unsigned* err)
 {
-    const unsigned long long t0 = wall_clock64();
     unsigned todo = 0;  // bit k: granule tid + k*T still missing
     for (int k = 0, e = tid; e < n; k++, e += kTrkThreads) todo |= 1u << k;
-    for (;;) {
+    unsigned long long t0 = 0;
+    int late = 0;
+    while (todo) {
         for (int k = 0; (todo >> k) != 0; k++) {
             if (!((todo >> k) & 1u)) continue;
             const int e = tid + k * kTrkThreads;
@@ -898,14 +970,16 @@ __device__ bool sweep_words(const unsigned long long* g, int n, unsigned tag, un
                 todo &= ~(1u << k);
             }
         }
-        if (__syncthreads_and(todo == 0)) return true;
-        // 100 MHz wall clock: give up after 2 s (a block of the grid is not resident)
-        if (__syncthreads_or(tid == 0 && wall_clock64() - t0 > 200000000ull)) {
-            if (tid == 0) atomicExch(err, 1u);
-            return false;
+        if (!todo) break;
+        // 100 MHz wall clock, read only once the wait is long
+        if (++late >= 64) {
+            const unsigned long long t = wall_clock64();
+            if (!t0) t0 = t;
+            else if (t - t0 > 200000000ull) { atomicExch(err, 1u); break; }
+            late = 0;
         }
-        __builtin_amdgcn_s_sleep(1);
     }
+    return !__syncthreads_or(todo != 0);
 }
 
 // Grid census (guide G16: residency is a precondition, not a given): every block
@@ -933,14 +1007,6 @@ __device__ bool census(unsigned* w, int tid)
     return s_go != 0;
 }
 
-// LDS barrier that leaves global loads (the next step's IF prefetch) in flight:
-// __syncthreads() would wait vmcnt(0) first.
-__device__ __forceinline__ void lds_barrier()
-{
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-    __builtin_amdgcn_s_barrier();
-}
-
 // The next step's 16-B IF groups of this lane straight into LDS (global_load_lds, no
 // VGPRs): group j of lane tid at s_raw[j*256 + tid]; each wave-instruction writes its
 // 64 lanes' 1 KiB contiguously from the wave's base.
@@ -965,7 +1031,7 @@ __device__ __forceinline__ void prefetch_raw(const int8_t* iq, int64_t g0, int64
 // exchange only: each block publishes its partial sums and reads everyone's. Block 0
 // of the channel writes the records, C/N0 and, at the end, the state.
 template <int NT, int SUB, bool DIVIDE>
-__global__ __launch_bounds__(kTrkThreads) void track_run_kernel(const TrkParams* __restrict__ pp,
+__global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(3, 3))) void track_run_kernel(const TrkParams* __restrict__ pp,
                                                                const TrkBuffers* __restrict__ bp, int bpc,
                                                                int nsteps, unsigned tag0)
 {
@@ -990,6 +1056,7 @@ __global__ __launch_bounds__(kTrkThreads) void track_run_kernel(const TrkParams*
     __shared__ __attribute__((aligned(16))) StepDesc s_d[2];       // this step / the next
     __shared__ __attribute__((aligned(16))) TrkChan s_c[2];        // state before / after
     __shared__ double s_fin[NV];
+    __shared__ double s_taps[GNSS_MAX_TAPS];
     __shared__ double2 s_zero;
 
     if (!census(b.run_err, tid)) return;
@@ -1007,11 +1074,14 @@ __global__ __launch_bounds__(kTrkThreads) void track_run_kernel(const TrkParams*
         reinterpret_cast<unsigned*>(&s_d[0])[e] = ((const g_u32*)(b.desc + ch))[e];
     if (tid < kChanWords) reinterpret_cast<uint64_t*>(&s_c[0])[tid] = ((const g_u64*)cp)[tid];
     if (tid == 0) s_zero = make_double2(0.0, 0.0);
+    if (tid < NT) s_taps[tid] = p.taps[tid];
     __syncthreads();
     if (!s_d[0].bad)
         prefetch_raw<SUB>(iq, s_d[0].g_first + ((int64_t)blk * T + tid) * SUB, gmax, s_raw, tid);
 
     int cur = 0;
+    // timing probe: per-channel launch span in row 0, words 20 + 3 ch .. (block 0)
+    const unsigned long long t_start = wall_clock64();
     for (int s = 0; s < nsteps; s++) {
         const StepDesc& D = s_d[cur];
         const int bad = D.bad;
@@ -1028,11 +1098,20 @@ __global__ __launch_bounds__(kTrkThreads) void track_run_kernel(const TrkParams*
             return;
         }
         const int64_t A = uni(D.A), n = uni(D.n);
+        // the record's two delayValue prefix reads, issued now and used in the tail
+        int64_t pre[2] = {0, 0};
+        if (io && wv == 1 && lane == 0) {
+            const TrkChan& c0 = s_c[cur];
+            const int64_t* dvp = b.dvpre + (int64_t)ch * (p.rec_cap + 1);
+            const int64_t cols = record_cols(p, c0, D.phaseC);
+            pre[0] = dvp[c0.nstep];
+            pre[1] = cols < c0.nstep + 1 ? dvp[cols] : 0;
+        }
         // timing probe (GNSS_STAMPS), channel 0, row s: [0] step start, [1] computed,
         // [2] partial out, [3] all partials in, [4] next descriptor ready (block 0);
         // [5..9] the same for the channel's last block
-        unsigned long long* srow = b.stamps && ch == 0 && s < kStampSlots && (io || blk == bpc - 1)
-                                       ? b.stamps + (size_t)s * kStampRow + (io ? 0 : 5) : nullptr;
+        unsigned long long* srow = b.stamps && ch == 0 && (io || blk == bpc - 1)
+                                       ? b.stamps + (size_t)(s % kStampSlots) * kStampRow + (io ? 0 : 5) : nullptr;
         if (srow && tid == 0) srow[0] = wall_clock64();
 
         // ---- correlate this block's lanes (IF prefetched into s_raw)
@@ -1044,46 +1123,17 @@ __global__ __launch_bounds__(kTrkThreads) void track_run_kernel(const TrkParams*
                                                   reinterpret_cast<double2*>(s_mem) + tid, &s_zero, oI, oQ);
             __syncthreads();  // slots and s_raw free
             if (srow && tid == 0) srow[1] = wall_clock64();
-            // the next step starts at A + n (ftell after this read); its end is not known yet
-            if (s + 1 < nsteps)
-                prefetch_raw<SUB>(iq, ((A + n) >> 3) + ((int64_t)blk * T + tid) * SUB, gmax, s_raw, tid);
-            // block sum in a fixed order, LDS barriers only (the prefetch stays in flight)
-            double* red = s_mem;            // [NV][T]
-            double* red2 = s_mem + NV * T;  // [NV][32]
-#pragma unroll
-            for (int q = 0; q < NT; q++) {
-                red[(2 * q) * T + tid] = oI[q];
-                red[(2 * q + 1) * T + tid] = oQ[q];
-            }
-            lds_barrier();
-            for (int e = tid; e < NV * 32; e += T) {
-                const double* r = red + (e >> 5) * T + (e & 31) * 8;
-                double a = r[0];
-#pragma unroll
-                for (int k = 1; k < 8; k++) a += r[k];
-                red2[e] = a;
-            }
-            lds_barrier();
-            if (tid < NV * 4) {  // 4 lanes per value, then a fixed-order combine
-                const int v = tid >> 2, q = tid & 3;
-                const double* r = red2 + v * 32 + q * 8;
-                double a = r[0];
-#pragma unroll
-                for (int k = 1; k < 8; k++) a += r[k];
-                const double a1 = __shfl_xor(a, 1, 64);
-                const double a2 = (q & 1) ? a1 + a : a + a1;
-                const double a3 = __shfl_xor(a2, 2, 64);
-                const double sum = (q & 2) ? a3 + a2 : a2 + a3;
-                if (q == 0) {
-                    const unsigned long long w = (unsigned long long)__double_as_longlong(sum);
-                    const unsigned tg = tag0 + s + 1;
-                    unsigned long long* g = pg + (((int64_t)(s & 1) * kMaxBpcRun + blk) * NV + v) * 2;
-                    store_agent(g, ((unsigned long long)tg << 32) | (w & 0xffffffffull));
-                    store_agent(g + 1, ((unsigned long long)tg << 32) | (w >> 32));
-                }
+            // block sum in a fixed order, published as granules
+            const double bsum = block_partial<NT>(s_mem, oI, oQ, tid);
+            if (tid < NV * 4 && (tid & 3) == 0) {
+                const int v = tid >> 2;
+                const unsigned long long w = (unsigned long long)__double_as_longlong(bsum);
+                const unsigned tg = tag0 + s + 1;
+                unsigned long long* g = pg + (((int64_t)(s & 1) * kMaxBpcRun + blk) * NV + v) * 2;
+                store_agent(g, ((unsigned long long)tg << 32) | (w & 0xffffffffull));
+                store_agent(g + 1, ((unsigned long long)tg << 32) | (w >> 32));
             }
             if (srow && tid == 0) srow[2] = wall_clock64();
-            lds_barrier();  // red2 read before the partial words overwrite it
         }
 
         // ---- every block's partial, summed in a fixed order (bit-identical in all blocks)
@@ -1092,26 +1142,25 @@ __global__ __launch_bounds__(kTrkThreads) void track_run_kernel(const TrkParams*
                          tid, b.run_err))
             return;
         if (srow && tid == 0) srow[3] = wall_clock64();
-        constexpr int J = T / NV < 16 ? T / NV : 16;  // J*NV <= T threads
-        double* s_tmp = s_mem + kPart;
-        if (tid < J * NV) {
-            const int v = tid % NV, j = tid / NV;
-            double a = 0.0;
-            for (int k = j; k < bpc; k += J) {
-                const unsigned lo = pw[(k * NV + v) * 2], hi = pw[(k * NV + v) * 2 + 1];
-                a += __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-            }
-            s_tmp[j * NV + v] = a;
-        }
-        lds_barrier();
-        const int phaseC = D.phaseC;
-        if (tid < NV) {
-            double a = 0.0;
+        // wave 2 issues the whole block's next IF (it starts at A + n, ftell after this
+        // read; the polls above would have queued behind it) and waits for it at the end
+        // of the tail: the correlator waves never stall on it
+        if (wv == 2 && s + 1 < nsteps) {
 #pragma unroll
-            for (int j = 0; j < J; j++) a += s_tmp[j * NV + tid];
-            s_fin[tid] = phaseC ? -a : a;  // :447-449
+            for (int h = 0; h < 4; h++)
+                prefetch_raw<SUB>(iq, ((A + n) >> 3) + ((int64_t)blk * T + h * 64 + lane) * SUB, gmax, s_raw,
+                                  h * 64 + lane);
         }
+        if (tid < 8 * NV) {
+            const double a = channel_sum(bpc, tid, [&](int k, int v) {
+                const unsigned lo = pw[(k * NV + v) * 2], hi = pw[(k * NV + v) * 2 + 1];
+                return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+            });
+            if ((tid & 7) == 0) s_fin[tid >> 3] = D.phaseC ? -a : a;  // :447-449
+        }
+        const int phaseC = D.phaseC;
         lds_barrier();
+        if (srow && io && tid == 0) srow[10] = wall_clock64();
 
         // ---- the loop update (every wave) and the step's scalar end: wave 0 the code half
         // of the next descriptor, wave 3 the carrier half, wave 2 the new state, wave 1
@@ -1127,38 +1176,50 @@ __global__ __launch_bounds__(kTrkThreads) void track_run_kernel(const TrkParams*
         o.phaseC = phaseC;
         const LoopUpd u = loop_update_i(p, c, s_fin[2 * p.iE], s_fin[2 * p.iE + 1], s_fin[2 * p.iP],
                                       s_fin[2 * p.iP + 1], s_fin[2 * p.iL], s_fin[2 * p.iL + 1], o.pdi,
-                                      o.phaseC);
-        if (wv == 0 || wv == 3) {
-            NcoState nx;
-            nx.remChip = o.remChip;
-            nx.remPhase = o.remPhase;
-            nx.codeFreq = u.codeFreq;
-            nx.carrierFreq = u.carrierFreq;
-            nx.numSample = o.n;
-            nx.pos = c.pos + 2 * o.n;
-            nx.Index = c.Index + (o.phaseC ? 10 : 1);
-            prepare_desc_i(p, nx, o.pdi, o.phaseC, wv == 0 ? 0 : 1, lane, &s_d[cur ^ 1]);
-        } else if (wv == 1) {
+                                      o.phaseC, wv == 0 ? 1 : wv == 3 ? 2 : 3);  // (each role's half)
+        if (srow && io && tid == 0) srow[11] = wall_clock64();
+        NcoState nx;
+        nx.remChip = o.remChip;
+        nx.remPhase = o.remPhase;
+        nx.codeFreq = u.codeFreq;
+        nx.carrierFreq = u.carrierFreq;
+        nx.numSample = o.n;
+        nx.pos = c.pos + 2 * o.n;
+        nx.Index = c.Index + (o.phaseC ? 10 : 1);
+        if (wv == 0 || wv == 3) {  // the code half / the carrier table of the next descriptor
+            prepare_desc_i(p, nx, o.pdi, o.phaseC, wv == 0 ? 0 : 1, lane, &s_d[cur ^ 1], s_taps,
+                           srow && io ? srow + 14 : nullptr);
+            if (srow && io && lane == 0) srow[wv == 0 ? 12 : 13] = wall_clock64();
+        } else if (wv == 1) {  // the record (block 0), then the state
             if (io) {
-                if (lane == 0) write_record_i(p, b, ch, c, o, u, s_fin);
+                if (lane == 0) write_record_i(p, b, ch, c, o, u, s_fin, pre);
                 if (b.taps_rec && lane < NV && c.slot < p.rec_cap)
                     b.taps_rec[((int64_t)ch * p.rec_cap + c.slot) * NV + lane] = s_fin[lane];
             }
-        } else if (lane == 0) {
-            TrkChan& g = s_c[cur ^ 1];
-            write_state_i(p, b, ch, &g, c, o, u, s_fin, io);
-            // the fields a step does not change carry over
-            g.carrierFreqBasis = c.carrierFreqBasis;
-            g.n1_target = c.n1_target;
-            g.codedelay0 = c.codedelay0;
-            g.sv1 = c.sv1;
-            g.prn = c.prn;
-            g.status = c.status;
-            g.countinx = c.countinx;
+            if (lane == 0) {
+                TrkChan& g = s_c[cur ^ 1];
+                write_state_i(p, b, ch, &g, c, o, u, s_fin, io);
+                // the fields a step does not change carry over
+                g.carrierFreqBasis = c.carrierFreqBasis;
+                g.n1_target = c.n1_target;
+                g.codedelay0 = c.codedelay0;
+                g.sv1 = c.sv1;
+                g.prn = c.prn;
+                g.status = c.status;
+                g.countinx = c.countinx;
+            }
+        } else {  // wave 2: remPhase of the next step, then its IF has landed
+            prepare_desc_i(p, nx, o.pdi, o.phaseC, 2, lane, &s_d[cur ^ 1], s_taps);  // lane 63
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         lds_barrier();
         if (srow && tid == 0) srow[4] = wall_clock64();
         cur ^= 1;
+    }
+    if (b.stamps && io && tid == 0 && ch < 64) {
+        b.stamps[20 + 3 * ch] = t_start;
+        b.stamps[21 + 3 * ch] = wall_clock64();
+        b.stamps[22 + 3 * ch] = (unsigned long long)nsteps;
     }
     if (io) {  // the state and the next step's descriptor for the next launch
         if (tid < kChanWords)
@@ -1176,7 +1237,7 @@ __global__ void track_prepare_kernel(const TrkParams* __restrict__ pp, const Trk
     const TrkBuffers& b = *bp;
     const int ch = blockIdx.x;
     const TrkChan c = b.chan[ch];
-    prepare_desc(p, nco_of(c), pdi, phaseC, threadIdx.x >> 6, threadIdx.x & 63, b.desc + ch);
+    prepare_desc_block(p, nco_of(c), pdi, phaseC, b.desc + ch);
 }
 
 __global__ void track_snapshot_kernel(const TrkBuffers* __restrict__ bp, int nch)
@@ -1250,7 +1311,7 @@ __global__ void track_phase_c_init_kernel(const TrkParams* __restrict__ pp, cons
     }
     __syncthreads();
     const TrkChan c = s_c;
-    if (c.status == GNSS_OK) prepare_desc(p, nco_of(c), 10, 1, threadIdx.x >> 6, threadIdx.x & 63, b.desc + ch);
+    if (c.status == GNSS_OK) prepare_desc_block(p, nco_of(c), 10, 1, b.desc + ch);
 }
 
 hipError_t launch_track_step(const TrkParams& p, const TrkBuffers& b, const TrkDev& d, int bpc, int sub,
@@ -1262,8 +1323,8 @@ hipError_t launch_track_step(const TrkParams& p, const TrkBuffers& b, const TrkD
         hipLaunchKernelGGL((track_step_kernel<NT_, SUB_, DIV_>), grid, block, 0, s, d.p, d.b, bpc); \
         return hipGetLastError();                                                              \
     }
-    GNSS_STEP(3, 1, false) GNSS_STEP(3, 2, false) GNSS_STEP(3, 4, false)
-    GNSS_STEP(11, 1, false) GNSS_STEP(11, 2, false) GNSS_STEP(11, 4, false)
+    GNSS_STEP(3, 1, false) GNSS_STEP(3, 2, false) GNSS_STEP(3, 3, false) GNSS_STEP(3, 4, false)
+    GNSS_STEP(11, 1, false) GNSS_STEP(11, 2, false) GNSS_STEP(11, 3, false) GNSS_STEP(11, 4, false)
     GNSS_STEP(3, 1, true) GNSS_STEP(11, 1, true)
 #undef GNSS_STEP
     return hipErrorInvalidValue;
@@ -1279,8 +1340,8 @@ hipError_t launch_track_run(const TrkParams& p, const TrkBuffers& b, const TrkDe
                            nsteps, tag0);                                                      \
         return hipGetLastError();                                                              \
     }
-    GNSS_RUN(3, 1, false) GNSS_RUN(3, 2, false) GNSS_RUN(3, 4, false)
-    GNSS_RUN(11, 1, false) GNSS_RUN(11, 2, false) GNSS_RUN(11, 4, false)
+    GNSS_RUN(3, 1, false) GNSS_RUN(3, 2, false) GNSS_RUN(3, 3, false) GNSS_RUN(3, 4, false)
+    GNSS_RUN(11, 1, false) GNSS_RUN(11, 2, false) GNSS_RUN(11, 3, false) GNSS_RUN(11, 4, false)
     GNSS_RUN(3, 1, true) GNSS_RUN(11, 1, true)
 #undef GNSS_RUN
     return hipErrorInvalidValue;
@@ -1297,8 +1358,8 @@ int track_run_blocks_per_cu(const TrkParams& p, int sub)
             nb = 0;                                                                            \
         return nb;                                                                             \
     }
-    GNSS_OCC(3, 1, false) GNSS_OCC(3, 2, false) GNSS_OCC(3, 4, false)
-    GNSS_OCC(11, 1, false) GNSS_OCC(11, 2, false) GNSS_OCC(11, 4, false)
+    GNSS_OCC(3, 1, false) GNSS_OCC(3, 2, false) GNSS_OCC(3, 3, false) GNSS_OCC(3, 4, false)
+    GNSS_OCC(11, 1, false) GNSS_OCC(11, 2, false) GNSS_OCC(11, 3, false) GNSS_OCC(11, 4, false)
     GNSS_OCC(3, 1, true) GNSS_OCC(11, 1, true)
 #undef GNSS_OCC
     return 0;
@@ -1307,7 +1368,7 @@ int track_run_blocks_per_cu(const TrkParams& p, int sub)
 hipError_t launch_track_prepare(const TrkParams& p, const TrkBuffers& b, const TrkDev& d, int pdi,
                                 int phaseC, hipStream_t s)
 {
-    hipLaunchKernelGGL(track_prepare_kernel, dim3(p.nch), dim3(128), 0, s, d.p, d.b, pdi, phaseC);
+    hipLaunchKernelGGL(track_prepare_kernel, dim3(p.nch), dim3(192), 0, s, d.p, d.b, pdi, phaseC);
     return hipGetLastError();
 }
 
@@ -1326,7 +1387,7 @@ hipError_t launch_track_bitedge(const TrkParams& p, const TrkBuffers& b, const T
 hipError_t launch_track_phase_c_init(const TrkParams& p, const TrkBuffers& b, const TrkDev& d,
                                      int64_t skip, hipStream_t s)
 {
-    hipLaunchKernelGGL(track_phase_c_init_kernel, dim3(p.nch), dim3(128), 0, s, d.p, d.b, skip);
+    hipLaunchKernelGGL(track_phase_c_init_kernel, dim3(p.nch), dim3(192), 0, s, d.p, d.b, skip);
     return hipGetLastError();
 }
 

@@ -66,14 +66,31 @@ def test_tracking_parity_opensky_8ch(pkg, po, ctx, opensky_short):
     assert len(T(16).P_i) == 1000 + cx[2] + 1000
 
 
-@pytest.mark.parametrize("sub", ["1", "2", "4"])
-def test_tracking_parity_every_kernel_variant(pkg, po, ctx, opensky_short, monkeypatch, sub):
+@pytest.mark.parametrize("persist", [True, False], ids=["persistent", "step"])
+@pytest.mark.parametrize("sub", ["1", "2", "3", "4"])
+def test_tracking_parity_every_kernel_variant(pkg, po, ctx, opensky_short, monkeypatch, sub, persist):
+    """Every lane span, through the persistent step loop and through one launch per step."""
     monkeypatch.setenv("GNSS_FORCE_SUB", sub)
+    if not persist:
+        monkeypatch.setenv("GNSS_NO_PERSIST", "1")
     skip, cfg, data = opensky_short
     file, signal, acq, track = params(pkg, skip, data)
     track.msToProcessCT_1ms, track.msToProcessCT_10ms = 700, 300
     A = acquired_of([16, 26, 31], [26051, 57908, 39064], [4579675.0, 4581800.0, 4581025.0])
     g = pkg.trackingCT(file, signal, track, A, ctx=ctx, raw=True)
+    r = po.trackingCT(file, signal, track, A, raw=True)
+    compare(pkg, g, r)
+
+
+def test_persistent_loop_runs_the_bench_shape(pkg, po, ctx, opensky_short):
+    """8 channels (the bench's trackingCT shape): each phase run is one persistent launch
+    (the step kernel would take one launch per step), with the same outputs."""
+    skip, cfg, data = opensky_short
+    file, signal, acq, track = params(pkg, skip, data)
+    track.msToProcessCT_1ms, track.msToProcessCT_10ms = 700, 1000
+    A = acquired_of(OPENSKY_A["svs"], OPENSKY_A["cd"], OPENSKY_A["ff"])
+    g = pkg.trackingCT(file, signal, track, A, ctx=ctx, raw=True)
+    assert ctx.timing()["track_launches"] <= 4
     r = po.trackingCT(file, signal, track, A, raw=True)
     compare(pkg, g, r)
 
@@ -143,6 +160,23 @@ def test_channel_shards_equal_full_run(pkg, ctx, opensky_short):
     for c, part in ((0, a), (1, b), (2, a)):
         assert np.array_equal(full.rec[c], part.rec[c])
         assert full.len[c] == part.len[c] and full.countinx[c] == part.countinx[c]
+
+
+def test_persistent_and_step_paths_bit_identical(pkg, ctx, opensky_short, monkeypatch):
+    """The persistent loop and one launch per step share the lane geometry and both
+    fixed-order reductions: the same records to the last bit."""
+    skip, cfg, data = opensky_short
+    file, signal, acq, track = params(pkg, skip, data)
+    track.msToProcessCT_1ms, track.msToProcessCT_10ms = 700, 300
+    A = acquired_of([3, 16, 22], [3684, 26051, 2611], [4580975.0, 4579675.0, 4581525.0])
+    p = pkg.trackingCT(file, signal, track, A, ctx=ctx, raw=True)
+    assert ctx.timing()["track_launches"] <= 4
+    monkeypatch.setenv("GNSS_NO_PERSIST", "1")
+    q = pkg.trackingCT(file, signal, track, A, ctx=ctx, raw=True)
+    assert ctx.timing()["track_launches"] > 100
+    for c in range(3):
+        assert np.array_equal(p.rec[c], q.rec[c])
+        assert p.len[c] == q.len[c] and p.countinx[c] == q.countinx[c]
 
 
 def test_not_enough_raw_data_in_1ms_phase(pkg, ctx, opensky_short):

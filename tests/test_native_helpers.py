@@ -20,3 +20,14 @@ def test_colon_make_hint_equals_colonop(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches 0" in r.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_fmod_pos_equals_c_fmod(tmp_path):
+    src = os.path.join(ROOT, "tests", "native", "fmod_pos.cpp")
+    exe = tmp_path / "fmod_pos"
+    subprocess.run([HIPCC, "-O2", "-std=c++17", "-ffp-contract=off", "-o", str(exe), src],
+                   check=True, capture_output=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches 0" in r.stdout

@@ -17,4 +17,22 @@ for path in sys.argv[1:]:
         print(f"  {name:32s} blk0 {us(a[:, i + 1] - a[:, i]):7.2f}   last {us(a[:, i + 6] - a[:, i + 5]):7.2f}")
     lastout = np.maximum(a[:, 2], a[:, 7])
     print(f"  {'last partial out -> blk0 all in':32s} {us(a[:, 3] - lastout):7.2f}")
-    print(f"  {'step period (blk0)':32s} {us(np.diff(a[:, 0])):7.2f}")
+    a = a[np.argsort(a[:, 0])]  # rows wrap (row = step % slots)
+    dp = np.diff(a[:, 0]) * 0.01
+    dp = dp[dp < 1000]
+    print(f"  {'step period (blk0)':32s} {np.median(dp):7.2f}  mean {dp.mean():6.2f}  p90 {np.percentile(dp, 90):6.2f}  p99 {np.percentile(dp, 99):6.2f}  max {dp.max():7.2f}")
+    b = np.fromfile(path, dtype=np.uint64)[:-1].reshape(-1, ROW)[:, :14].astype(np.int64)
+    b = b[(b[:, 0] != 0) & (b[:, 5] != 0) & (b[:, 10] != 0)]
+    if len(b):
+        print(f"  blk0 tail: all in -> s_fin {us(b[:, 10] - b[:, 3]):6.2f}, -> loop upd {us(b[:, 11] - b[:, 10]):6.2f}, "
+              f"-> code desc {us(b[:, 12] - b[:, 11]):6.2f}, -> carrier desc {us(b[:, 13] - b[:, 11]):6.2f}, "
+              f"-> ready {us(b[:, 4] - np.maximum(b[:, 12], b[:, 13])):6.2f}")
+    c = np.fromfile(path, dtype=np.uint64)[:-1].reshape(-1, ROW)[:, :16].astype(np.int64)
+    c = c[(c[:, 14] != 0) & (c[:, 15] != 0) & (c[:, 11] != 0)]
+    if len(c):
+        print(f"  code role: loop upd -> n {us(c[:, 14] - c[:, 11]):6.2f}, -> colon {us(c[:, 15] - c[:, 14]):6.2f}, "
+              f"-> stored {us(c[:, 12] - c[:, 15]):6.2f}")
+    r0 = np.fromfile(path, dtype=np.uint64)[:3080].astype(np.int64)
+    spans = [(ch, (r0[21 + 3 * ch] - r0[20 + 3 * ch]) * 0.01, r0[22 + 3 * ch]) for ch in range(64) if r0[21 + 3 * ch]]
+    if spans:
+        print("  per-channel launch span (us) / steps:", ", ".join(f"ch{c} {t:.0f}/{n}" for c, t, n in spans))
