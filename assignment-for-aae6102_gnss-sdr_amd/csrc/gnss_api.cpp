@@ -17,6 +17,9 @@
 #include <cstring>
 #include <cstdlib>
 #include <functional>
+#include <thread>
+#include <chrono>
+#include <vector>
 #include <fcntl.h>
 #include <map>
 #include <string>
@@ -37,6 +40,10 @@ struct gnss_ctx {
     std::map<std::tuple<size_t, size_t, int, int>, rocfft_plan> plans;
     void* fft_work = nullptr;
     size_t fft_work_size = 0;
+    // device scratch kept across calls (hipMalloc/hipFree per call cost ~1 ms and hipFree
+    // synchronises): name -> (pointer, bytes)
+    std::map<std::string, std::pair<void*, size_t>> pool;
+    int64_t acq_tw_S = 0;  // the acquisition twiddle tables in the pool are for this S
 };
 
 namespace {
@@ -65,18 +72,66 @@ int fail(gnss_ctx* ctx, int code, const char* fmt, ...)
 struct DevBuf {
     void* p = nullptr;
     size_t n = 0;
+    bool pooled = false;  // borrowed from the context's pool: not freed here
     DevBuf() = default;
     DevBuf(const DevBuf&) = delete;
     DevBuf& operator=(const DevBuf&) = delete;
-    ~DevBuf() { if (p) (void)hipFree(p); }
+    ~DevBuf() { release(); }
+    void release()
+    {
+        if (p && !pooled) (void)hipFree(p);
+        p = nullptr;
+        pooled = false;
+    }
     hipError_t alloc(size_t bytes)
     {
-        if (p) { (void)hipFree(p); p = nullptr; }
+        release();
         n = bytes;
         return hipMalloc(&p, bytes ? bytes : 16);
     }
+    // The context's buffer `key` (grown when too small; contents undefined, as hipMalloc).
+    // One key per live buffer; calls on a context are serialised on its stream.
+    hipError_t alloc(gnss_ctx* ctx, const char* key, size_t bytes)
+    {
+        release();
+        auto& e = ctx->pool[key];
+        const size_t want = bytes ? bytes : 16;
+        if (e.second < want) {
+            if (e.first) (void)hipFree(e.first);
+            e = {nullptr, 0};
+            const hipError_t r = hipMalloc(&e.first, want);
+            if (r != hipSuccess) {
+                e.first = nullptr;
+                return r;
+            }
+            e.second = want;
+        }
+        p = e.first;
+        n = bytes;
+        pooled = true;
+        return hipSuccess;
+    }
     template <class T> T* as() const { return reinterpret_cast<T*>(p); }
 };
+
+// f(0..n-1) over up to 16 host threads (the output expansion writes tens of MB into
+// fresh pages; one thread is bound by page faults and a single core's bandwidth).
+template <class F>
+void parallel_for(int n, F f)
+{
+    const int nt = std::max(1, std::min({n, 16, (int)std::thread::hardware_concurrency()}));
+    if (nt <= 1) {
+        for (int i = 0; i < n; i++) f(i);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve((size_t)nt);
+    for (int t = 0; t < nt; t++)
+        th.emplace_back([&, t]() {
+            for (int i = t; i < n; i += nt) f(i);
+        });
+    for (auto& x : th) x.join();
+}
 
 struct Events {
     hipEvent_t a = nullptr, b = nullptr;
@@ -295,6 +350,8 @@ void gnss_ctx_destroy(gnss_ctx* ctx)
     (void)hipStreamSynchronize(ctx->stream);
     for (auto& kv : ctx->plans) rocfft_plan_destroy(kv.second);
     if (ctx->fft_work) (void)hipFree(ctx->fft_work);
+    for (auto& kv : ctx->pool)
+        if (kv.second.first) (void)hipFree(kv.second.first);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -386,12 +443,12 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     for (int i = 0; i < np; i++) generate_ca(prns[i], &cah[(size_t)i * 1023]);
     DevBuf ca, sig, code, y, corr, peaks, scratch;
     DevBuf d_twr, d_twc, B, X, A;  // own FFT correlator buffers (freed after the stream drains)
-    HIP_TRY(ca.alloc(cah.size() * sizeof(float)));
+    HIP_TRY(ca.alloc(ctx, "acq.ca", cah.size() * sizeof(float)));
     HIP_TRY(hipMemcpyAsync(ca.p, cah.data(), cah.size() * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
     const int nsig = dl * nb;
-    HIP_TRY(corr.alloc(sizeof(float) * (size_t)np * nb * S));
-    HIP_TRY(peaks.alloc(sizeof(AcqPeak) * (size_t)np));
-    HIP_TRY(scratch.alloc(acq_scratch_bytes(np, np)));
+    HIP_TRY(corr.alloc(ctx, "acq.corr", sizeof(float) * (size_t)np * nb * S));
+    HIP_TRY(peaks.alloc(ctx, "acq.peaks", sizeof(AcqPeak) * (size_t)np));
+    HIP_TRY(scratch.alloc(ctx, "acq.scratch", acq_scratch_bytes(np, np)));
     const bool own_fft = acq_fft_supported(S) && !getenv("GNSS_ACQ_ROCFFT");
     int perm = 0;
     Events e_all, e_corr;  // e_corr.b marks the end of the PRN search
@@ -399,29 +456,35 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         // two-pass FFT correlator (acq_fft.hip): S = P * 2000
         const int P = (int)(S / 2000);
         perm = P;
-        std::vector<float2> twr(2000), twc((size_t)P * 2000);
-        for (int m = 0; m < 2000; m++) {
-            const double a = -2.0 * M_PI * (double)m / 2000.0;
-            twr[m] = make_float2((float)std::cos(a), (float)std::sin(a));
-        }
-        for (int m = 0; m < P; m++)
-            for (int k = 0; k < 2000; k++) {
-                const double a = -2.0 * M_PI * (double)((int64_t)m * k % S) / (double)S;
-                twc[(size_t)m * 2000 + k] = make_float2((float)std::cos(a), (float)std::sin(a));
+        // twiddles (fp64 on the host, rounded to fp32), kept in the context per S
+        const bool have_tw = ctx->acq_tw_S == S;
+        HIP_TRY(d_twr.alloc(ctx, "acq.d_twr", 2000 * sizeof(float2)));
+        HIP_TRY(d_twc.alloc(ctx, "acq.d_twc", (size_t)P * 2000 * sizeof(float2)));
+        if (!have_tw) {
+            std::vector<float2> twr(2000), twc((size_t)P * 2000);
+            for (int m = 0; m < 2000; m++) {
+                const double a = -2.0 * M_PI * (double)m / 2000.0;
+                twr[m] = make_float2((float)std::cos(a), (float)std::sin(a));
             }
-        HIP_TRY(d_twr.alloc(twr.size() * sizeof(float2)));
-        HIP_TRY(d_twc.alloc(twc.size() * sizeof(float2)));
-        HIP_TRY(hipMemcpyAsync(d_twr.p, twr.data(), twr.size() * sizeof(float2), hipMemcpyHostToDevice, ctx->stream));
-        HIP_TRY(hipMemcpyAsync(d_twc.p, twc.data(), twc.size() * sizeof(float2), hipMemcpyHostToDevice, ctx->stream));
+            for (int m = 0; m < P; m++)
+                for (int k = 0; k < 2000; k++) {
+                    const double a = -2.0 * M_PI * (double)((int64_t)m * k % S) / (double)S;
+                    twc[(size_t)m * 2000 + k] = make_float2((float)std::cos(a), (float)std::sin(a));
+                }
+            HIP_TRY(hipMemcpyAsync(d_twr.p, twr.data(), twr.size() * sizeof(float2), hipMemcpyHostToDevice, ctx->stream));
+            HIP_TRY(hipMemcpyAsync(d_twc.p, twc.data(), twc.size() * sizeof(float2), hipMemcpyHostToDevice, ctx->stream));
+            HIP_TRY(hipStreamSynchronize(ctx->stream));  // (the host vectors go out of scope)
+            ctx->acq_tw_S = S;
+        }
         const size_t ntr = (size_t)nsig + np;
-        HIP_TRY(B.alloc(sizeof(float2) * ntr * S));
-        HIP_TRY(X.alloc(sizeof(float2) * ntr * S));
+        HIP_TRY(B.alloc(ctx, "acq.B", sizeof(float2) * ntr * S));
+        HIP_TRY(X.alloc(ctx, "acq.X", sizeof(float2) * ntr * S));
         const int npairs = nb * np;
         // (bin, PRN) pairs per batch: the inverse intermediate stays ~256 MB (Infinity Cache)
         int batch = (int)std::max<int64_t>(1, ((int64_t)256 << 20) / ((int64_t)dl * S * 8));
         if (const char* e = getenv("GNSS_ACQ_BATCH")) batch = std::max(1, atoi(e));
         batch = std::min(batch, npairs);
-        HIP_TRY(A.alloc(sizeof(float2) * (size_t)batch * dl * S));
+        HIP_TRY(A.alloc(ctx, "acq.A", sizeof(float2) * (size_t)batch * dl * S));
         HIP_TRY(hipStreamSynchronize(ctx->stream));
         HIP_TRY(hipEventRecord(e_all.a, ctx->stream));
         HIP_TRY(launch_acq_fft_forward(blk, S, dl, nb, sg->IF, acq->freqMin, acq->freqStep, sg->Fs,
@@ -434,12 +497,12 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
                                              d_twc.as<float2>(), A.as<float2>(), corr.as<float>(), ctx->stream));
         }
     } else {
-    HIP_TRY(sig.alloc(sizeof(float2) * (size_t)nsig * S));
-    HIP_TRY(code.alloc(sizeof(float2) * (size_t)np * S));
+    HIP_TRY(sig.alloc(ctx, "acq.sig", sizeof(float2) * (size_t)nsig * S));
+    HIP_TRY(code.alloc(ctx, "acq.code", sizeof(float2) * (size_t)np * S));
     // PRN chunk so the product/IFFT buffer stays <= ~4 GB
     const size_t per_prn = sizeof(float2) * (size_t)nsig * S;
     int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)np, ((size_t)4 << 30) / per_prn));
-    HIP_TRY(y.alloc(per_prn * (size_t)chunk));
+    HIP_TRY(y.alloc(ctx, "acq.y", per_prn * (size_t)chunk));
 
     // plans outside the timed region
     rocfft_plan pl;
@@ -510,16 +573,16 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         cdh[k] = out->codedelay[k];
     }
     DevBuf fca, fcd, fx, kb;
-    HIP_TRY(fca.alloc(caf.size() * sizeof(float)));
-    HIP_TRY(fcd.alloc(cdh.size() * sizeof(int32_t)));
-    HIP_TRY(kb.alloc(sizeof(int64_t) * (size_t)na));
+    HIP_TRY(fca.alloc(ctx, "acq.fca", caf.size() * sizeof(float)));
+    HIP_TRY(fcd.alloc(ctx, "acq.fcd", cdh.size() * sizeof(int32_t)));
+    HIP_TRY(kb.alloc(ctx, "acq.kb", sizeof(int64_t) * (size_t)na));
     HIP_TRY(hipMemcpyAsync(fca.p, caf.data(), caf.size() * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(fcd.p, cdh.data(), cdh.size() * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
     const bool own_fine = fine_fft_supported(S, L) && !getenv("GNSS_FINE_ROCFFT");
     Events e_fine;
     if (own_fine) {
         // per-SV zero-padded FFT as datalen three-level transforms (acq_fft.hip)
-        HIP_TRY(fx.alloc(fine_fft_scratch_bytes(S, L, dl)));
+        HIP_TRY(fx.alloc(ctx, "acq.fx", fine_fft_scratch_bytes(S, L, dl)));
         HIP_TRY(hipEventRecord(e_fine.a, ctx->stream));
         HIP_TRY(launch_fine_fft_tables(S, L, dl, fx.p, ctx->stream));
         for (int k = 0; k < na; k++) {
@@ -529,7 +592,7 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
                                            kb.as<int64_t>() + k, ctx->stream));
         }
     } else {
-        HIP_TRY(fx.alloc(sizeof(double2) * (size_t)na * N));
+        HIP_TRY(fx.alloc(ctx, "acq.fx", sizeof(double2) * (size_t)na * N));
         rocfft_plan pl;
         if ((st = get_plan(ctx, N, na, 1, 0, &pl))) return st;
         HIP_TRY(hipEventRecord(e_fine.a, ctx->stream));
@@ -537,7 +600,7 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
                                   sg->codelength, N, fx.as<double2>(), ctx->stream));
         if ((st = run_fft(ctx, fx.p, N, na, 1, 0))) return st;
         DevBuf fscr;
-        HIP_TRY(fscr.alloc(acq_scratch_bytes(1, na)));
+        HIP_TRY(fscr.alloc(ctx, "acq.fscr", acq_scratch_bytes(1, na)));
         HIP_TRY(launch_fine_argmax(fx.as<double2>(), na, N, file->dataType == 2, fscr.p, kb.as<int64_t>(), ctx->stream));
     }
     HIP_TRY(hipEventRecord(e_fine.b, ctx->stream));
@@ -580,6 +643,10 @@ struct StepGraph {
 int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg, const gnss_track* tr,
                      const gnss_acquired* acq, gnss_track_out* out)
 {
+    // GNSS_HOSTPROF: host-side phases of this call on stderr
+    const bool hp = getenv("GNSS_HOSTPROF") != nullptr;
+    const auto h0 = std::chrono::steady_clock::now();
+    auto hms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count(); };
     if (!ctx || !file || !sg || !tr || !acq || !out) return GNSS_EARG;
     HIP_TRY(hipSetDevice(ctx->device));
     ctx->timing = gnss_timing{};
@@ -725,19 +792,19 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         ca_bits(acq->sv[c], &cab[(size_t)i * 32]);
     }
     DevBuf d_chan, d_snap, d_desc, d_ca, d_part, d_arrive, d_rec, d_taps, d_cn1, d_cn10, d_dv, d_pi;
-    HIP_TRY(d_chan.alloc(sizeof(TrkChan) * nch));
-    HIP_TRY(d_snap.alloc(sizeof(TrkChan) * nch));
-    HIP_TRY(d_desc.alloc(sizeof(StepDesc) * nch));
-    HIP_TRY(d_ca.alloc(sizeof(unsigned) * cab.size()));
-    HIP_TRY(d_part.alloc(sizeof(double) * (size_t)nch * kMaxBpc * 2 * ntaps));
+    HIP_TRY(d_chan.alloc(ctx, "trk.d_chan", sizeof(TrkChan) * nch));
+    HIP_TRY(d_snap.alloc(ctx, "trk.d_snap", sizeof(TrkChan) * nch));
+    HIP_TRY(d_desc.alloc(ctx, "trk.d_desc", sizeof(StepDesc) * nch));
+    HIP_TRY(d_ca.alloc(ctx, "trk.d_ca", sizeof(unsigned) * cab.size()));
+    HIP_TRY(d_part.alloc(ctx, "trk.d_part", sizeof(double) * (size_t)nch * kMaxBpc * 2 * ntaps));
     const size_t arrive_bytes = sizeof(unsigned) * kArrivePerChan * kArriveStride * nch;
-    HIP_TRY(d_arrive.alloc(arrive_bytes));
-    HIP_TRY(d_rec.alloc(sizeof(double) * (size_t)nch * P.rec_cap * GNSS_NFIELDS));
-    if (out->taps) HIP_TRY(d_taps.alloc(sizeof(double) * (size_t)nch * P.rec_cap * 2 * ntaps));
-    HIP_TRY(d_cn1.alloc(sizeof(double) * (size_t)nch * P.cn0_cap));
-    HIP_TRY(d_cn10.alloc(sizeof(double) * (size_t)nch * P.cn0_cap));
-    HIP_TRY(d_dv.alloc(sizeof(int64_t) * (size_t)nch * (P.rec_cap + 1)));
-    HIP_TRY(d_pi.alloc(sizeof(double) * (size_t)nch * N1));
+    HIP_TRY(d_arrive.alloc(ctx, "trk.d_arrive", arrive_bytes));
+    HIP_TRY(d_rec.alloc(ctx, "trk.d_rec", sizeof(double) * (size_t)nch * P.rec_cap * GNSS_NFIELDS));
+    if (out->taps) HIP_TRY(d_taps.alloc(ctx, "trk.d_taps", sizeof(double) * (size_t)nch * P.rec_cap * 2 * ntaps));
+    HIP_TRY(d_cn1.alloc(ctx, "trk.d_cn1", sizeof(double) * (size_t)nch * P.cn0_cap));
+    HIP_TRY(d_cn10.alloc(ctx, "trk.d_cn10", sizeof(double) * (size_t)nch * P.cn0_cap));
+    HIP_TRY(d_dv.alloc(ctx, "trk.d_dv", sizeof(int64_t) * (size_t)nch * (P.rec_cap + 1)));
+    HIP_TRY(d_pi.alloc(ctx, "trk.d_pi", sizeof(double) * (size_t)nch * N1));
     HIP_TRY(hipMemcpyAsync(d_chan.p, ch0.data(), sizeof(TrkChan) * nch, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(d_ca.p, cab.data(), sizeof(unsigned) * cab.size(), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemsetAsync(d_arrive.p, 0, arrive_bytes, ctx->stream));
@@ -765,15 +832,15 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     DevBuf d_stamps;  // timing probe: per-launch wall-clock stamps of channel 0
     const char* stamp_path = getenv("GNSS_STAMPS");
     if (stamp_path) {
-        HIP_TRY(d_stamps.alloc(sizeof(unsigned long long) * ((size_t)kStampSlots * (8 + 3 * kMaxBpc) + 1)));
+        HIP_TRY(d_stamps.alloc(ctx, "trk.d_stamps", sizeof(unsigned long long) * ((size_t)kStampSlots * (8 + 3 * kMaxBpc) + 1)));
         HIP_TRY(hipMemsetAsync(d_stamps.p, 0, d_stamps.n, ctx->stream));
         B.stamps = d_stamps.as<unsigned long long>();
     }
 
     DevBuf d_pgran, d_err;
     if (persist1 || persist10) {
-        HIP_TRY(d_pgran.alloc(sizeof(unsigned long long) * (size_t)nch * 2 * kMaxBpcRun * 4 * ntaps));
-        HIP_TRY(d_err.alloc(16));
+        HIP_TRY(d_pgran.alloc(ctx, "trk.d_pgran", sizeof(unsigned long long) * (size_t)nch * 2 * kMaxBpcRun * 4 * ntaps));
+        HIP_TRY(d_err.alloc(ctx, "trk.d_err", 16));
         HIP_TRY(hipMemsetAsync(d_pgran.p, 0, d_pgran.n, ctx->stream));
         HIP_TRY(hipMemsetAsync(d_err.p, 0, 16, ctx->stream));
         B.pgran = d_pgran.as<unsigned long long>();
@@ -782,7 +849,7 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     unsigned tag = 0;  // hand-off tags grow across the launches of this call
 
     DevBuf d_args;  // the kernels' TrkParams / TrkBuffers
-    HIP_TRY(d_args.alloc(sizeof(TrkParams) + sizeof(TrkBuffers)));
+    HIP_TRY(d_args.alloc(ctx, "trk.d_args", sizeof(TrkParams) + sizeof(TrkBuffers)));
     HIP_TRY(hipMemcpyAsync(d_args.p, &P, sizeof(TrkParams), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(static_cast<char*>(d_args.p) + sizeof(TrkParams), &B, sizeof(TrkBuffers),
                            hipMemcpyHostToDevice, ctx->stream));
@@ -878,6 +945,7 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     run_steps_ref = run_steps;
 
     Events e_all;
+    if (hp) { HIP_TRY(hipStreamSynchronize(ctx->stream)); fprintf(stderr, "hostprof setup %.3f ms\n", hms()); }
     HIP_TRY(hipEventRecord(e_all.a, ctx->stream));
     // phase A: steps 1..N1-1, snapshot (for countinx = -1), step N1, bit-edge search
     HIP_TRY(launch_track_prepare(P, B, TD, 1, 0, ctx->stream));
@@ -890,6 +958,10 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     int cxmax = 0;
     for (auto& t : chh) cxmax = std::max(cxmax, t.countinx);
+    if (hp)
+        for (auto& t : chh)
+            fprintf(stderr, "hostprof bitedge prn %d status %d countinx %d n1_target %lld\n", t.prn, t.status,
+                    t.countinx, (long long)t.n1_target);
     // phase B continues phase A up to 1000 + countinx (inactive channels skip)
     if ((st = run_steps(1, cxmax))) return st;
     HIP_TRY(launch_track_phase_c_init(P, B, TD, file->skip, ctx->stream));
@@ -920,6 +992,7 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     }
 
     // results
+    if (hp) fprintf(stderr, "hostprof kernels done %.3f ms\n", hms());
     HIP_TRY(hipMemcpyAsync(chh.data(), d_chan.p, sizeof(TrkChan) * nch, hipMemcpyDeviceToHost, ctx->stream));
     std::vector<double> rec((size_t)nch * P.rec_cap * GNSS_NFIELDS);
     std::vector<double> tp(out->taps ? (size_t)nch * P.rec_cap * 2 * ntaps : 0);
@@ -930,6 +1003,7 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     HIP_TRY(hipMemcpyAsync(cn10.data(), d_cn10.p, cn10.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
 
+    if (hp) fprintf(stderr, "hostprof d2h done %.3f ms\n", hms());
     int status = GNSS_OK;
     for (auto& t : chh)
         if (t.status && (status == GNSS_OK || t.status == GNSS_ENODATA)) status = t.status;
@@ -946,34 +1020,37 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         const TrkChan& t = chh[i];
         const int cx = t.countinx;
         const int64_t n1 = N1 + cx;
-        const int64_t len = n1 + 10LL * n10;
-        if (out->len) out->len[c] = len;
+        if (out->len) out->len[c] = n1 + 10LL * n10;
         if (out->countinx) out->countinx[c] = cx;
         rows = std::max(rows, (int)(n1 / 20));
-        if (out->rec) {
-            for (int f = 0; f < GNSS_NFIELDS; f++) {
-                double* dst = out->rec + ((int64_t)c * GNSS_NFIELDS + f) * ML;
-                const double* src = rec.data() + (size_t)i * P.rec_cap * GNSS_NFIELDS + f;
-                for (int64_t k = 0; k < n1; k++) dst[k] = src[k * GNSS_NFIELDS];
-                for (int64_t s = 0; s < n10; s++) {
-                    const double v = src[(n1 + s) * GNSS_NFIELDS];
-                    for (int r = 0; r < 10; r++) dst[n1 + 10 * s + r] = v;
-                }
-            }
-        }
-        if (out->taps) {
-            for (int tq = 0; tq < 2 * ntaps; tq++) {
-                const int s = tq / 2, iq = tq % 2;
-                double* dst = out->taps + (((int64_t)c * 2 + iq) * ntaps + s) * ML;
-                const double* src = tp.data() + (size_t)i * P.rec_cap * 2 * ntaps + tq;
-                for (int64_t k = 0; k < n1; k++) dst[k] = src[k * 2 * ntaps];
-                for (int64_t q = 0; q < n10; q++) {
-                    const double v = src[(n1 + q) * 2 * ntaps];
-                    for (int r = 0; r < 10; r++) dst[n1 + 10 * q + r] = v;
-                }
-            }
-        }
     }
+    // the MATLAB layout: one row per millisecond, each 10-ms step's value on its ten rows
+    const int nrf = out->rec ? GNSS_NFIELDS : 0, ntf = out->taps ? 2 * ntaps : 0;
+    parallel_for(nch * (nrf + ntf), [&](int task) {
+        const int i = task / (nrf + ntf), f = task % (nrf + ntf);
+        const int c = chans[i];
+        const int64_t n1 = N1 + chh[i].countinx;
+        double* dst;
+        const double* src;
+        int64_t stride;
+        if (f < nrf) {
+            dst = out->rec + ((int64_t)c * GNSS_NFIELDS + f) * ML;
+            src = rec.data() + (size_t)i * P.rec_cap * GNSS_NFIELDS + f;
+            stride = GNSS_NFIELDS;
+        } else {
+            const int tq = f - nrf, sidx = tq / 2, iq = tq % 2;
+            dst = out->taps + (((int64_t)c * 2 + iq) * ntaps + sidx) * ML;
+            src = tp.data() + (size_t)i * P.rec_cap * 2 * ntaps + tq;
+            stride = 2 * ntaps;
+        }
+        for (int64_t k = 0; k < n1; k++) dst[k] = src[k * stride];
+        for (int64_t q = 0; q < n10; q++) {
+            const double v = src[(n1 + q) * stride];
+            for (int r = 0; r < 10; r++) dst[n1 + 10 * q + r] = v;
+        }
+        for (int64_t k = n1 + 10 * n10; k < ML; k++) dst[k] = 0;  // (a reused buffer's tail)
+    });
+    if (hp) fprintf(stderr, "hostprof expanded %.3f ms\n", hms());
     rows = std::max(rows, n10 / 20);
     out->cn0_rows = rows;
     if (out->CN0_Eph) {

@@ -495,6 +495,47 @@ __device__ __noinline__ void write_state(const TrkParams& p, const TrkBuffers& b
     write_state_i(p, b, ch, g, c, o, u, s, io);
 }
 
+// The same update in place (the persistent loop's single LDS copy of the state): one Zk
+// element changes per step, nothing is copied. C/N0 only where `io`.
+__device__ __forceinline__ void update_state_inplace(const TrkParams& p, const TrkBuffers& b, int ch,
+                                                     TrkChan& c, const StepOut& o, const LoopUpd& u,
+                                                     const double* s, bool io)
+{
+    const double P_i = s[2 * p.iP], P_q = s[2 * p.iP + 1];
+    int index_int = c.index_int + 1;  // 1..20
+    int snrIndex = c.snrIndex;
+    c.Zk[index_int - 1] = P_i * P_i + P_q * P_q;
+    if (index_int % 20 == 0) {
+        if (io) {
+            double Z[20];
+#pragma unroll
+            for (int k = 0; k < 20; k++) Z[k] = c.Zk[k];
+            const double cn = cn0_estimate(Z, 1 * p.ms * o.pdi);
+            double* cn0 = o.phaseC ? b.cn0_10 : b.cn0_1;
+            if (snrIndex <= p.cn0_cap) cn0[(int64_t)ch * p.cn0_cap + snrIndex - 1] = cn;
+        }
+        index_int = 0;
+        snrIndex += 1;
+    }
+    const int64_t pos = c.pos, Index = c.Index, nstep = c.nstep, slot = c.slot;
+    c.remChip = o.remChip;
+    c.remPhase = o.remPhase;
+    c.remSample = o.remSample;
+    c.carrier_outputLast = u.carrier_output;
+    c.PLLdiscriLast = u.PLLdiscri;
+    c.code_outputLast = u.code_output;
+    c.DLLdiscriLast = u.DLLdiscri;
+    c.codeFreq = u.codeFreq;
+    c.carrierFreq = u.carrierFreq;
+    c.numSample = o.n;
+    c.pos = pos + 2 * o.n;
+    c.Index = Index + (o.phaseC ? 10 : 1);
+    c.nstep = nstep + 1;
+    c.slot = slot + 1;
+    c.index_int = index_int;
+    c.snrIndex = snrIndex;
+}
+
 
 }  // namespace
 
@@ -950,24 +991,26 @@ __device__ __forceinline__ void publish_words(unsigned long long* g, const unsig
 }
 
 // Poll n granules until every tag equals `tag`; their words land in dst (LDS). Called by
-// every thread of the block. Each lane polls its own granules (tid + k*T) with no block
-// barrier per round, a granule seen once is not read again (its producer may already have
-// moved on); one barrier at the end. false (and run_err set) on timeout (~2 s).
+// every thread of the block; the np pollers (pid 0..np-1, pid < 0: not polling) each poll
+// granules pid + k*np with no block barrier per round, a granule seen once is not read
+// again (its producer may already have moved on); one barrier at the end. false (and
+// run_err set) on timeout (~2 s). n <= 64*np.
 __device__ bool sweep_words(const unsigned long long* g, int n, unsigned tag, unsigned* dst,
-                            int tid, unsigned* err)
+                            int pid, int np, unsigned* err)
 {
-    unsigned todo = 0;  // bit k: granule tid + k*T still missing
-    for (int k = 0, e = tid; e < n; k++, e += kTrkThreads) todo |= 1u << k;
+    unsigned long long todo = 0;  // bit k: granule pid + k*np still missing
+    if (pid >= 0)
+        for (int k = 0, e = pid; e < n; k++, e += np) todo |= 1ull << k;
     unsigned long long t0 = 0;
     int late = 0;
     while (todo) {
         for (int k = 0; (todo >> k) != 0; k++) {
-            if (!((todo >> k) & 1u)) continue;
-            const int e = tid + k * kTrkThreads;
+            if (!((todo >> k) & 1ull)) continue;
+            const int e = pid + k * np;
             const unsigned long long v = load_agent(g + e);
             if ((unsigned)(v >> 32) == tag) {
                 dst[e] = (unsigned)v;
-                todo &= ~(1u << k);
+                todo &= ~(1ull << k);
             }
         }
         if (!todo) break;
@@ -1054,7 +1097,9 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(3, 
     __shared__ __attribute__((aligned(16))) double s_mem[kMem];
     __shared__ __attribute__((aligned(16))) int4 s_raw[SUB * T];   // this step's IF
     __shared__ __attribute__((aligned(16))) StepDesc s_d[2];       // this step / the next
-    __shared__ __attribute__((aligned(16))) TrkChan s_c[2];        // state before / after
+    __shared__ __attribute__((aligned(16))) TrkChan s_c;           // the channel state
+    __shared__ StepOut s_o;                                        // the step whose state and
+    __shared__ LoopUpd s_u;                                        //   record are pending
     __shared__ double s_fin[NV];
     __shared__ double s_taps[GNSS_MAX_TAPS];
     __shared__ double2 s_zero;
@@ -1072,14 +1117,32 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(3, 
     // step 0's descriptor and the state, as the previous launch left them
     for (int e = tid; e < kDescWords; e += T)
         reinterpret_cast<unsigned*>(&s_d[0])[e] = ((const g_u32*)(b.desc + ch))[e];
-    if (tid < kChanWords) reinterpret_cast<uint64_t*>(&s_c[0])[tid] = ((const g_u64*)cp)[tid];
+    if (tid < kChanWords) reinterpret_cast<uint64_t*>(&s_c)[tid] = ((const g_u64*)cp)[tid];
     if (tid == 0) s_zero = make_double2(0.0, 0.0);
     if (tid < NT) s_taps[tid] = p.taps[tid];
     __syncthreads();
     if (!s_d[0].bad)
         prefetch_raw<SUB>(iq, s_d[0].g_first + ((int64_t)blk * T + tid) * SUB, gmax, s_raw, tid);
 
-    int cur = 0;
+    int cur = 0;   // s_d[cur]: this step
+    bool pend = false;  // a finished step's state / record still to write (s_o, s_u, s_fin)
+    int64_t pre[2] = {0, 0};  // block 0: its record's delayValue prefix reads, issued early
+    bool pre_ok = false;      //   (for the pending step)
+    // The pending step's side effects, by wave 1 while the next step's partials are in
+    // flight (off the critical path): the state replica (every block, in place) and, in
+    // block 0, the record, C/N0 and taps.
+    auto flush = [&]() {
+        if (wv == 1) {
+            if (io) {
+                if (lane == 0) write_record_i(p, b, ch, s_c, s_o, s_u, s_fin, pre_ok ? pre : nullptr);
+                if (b.taps_rec && lane < NV && s_c.slot < p.rec_cap)
+                    b.taps_rec[((int64_t)ch * p.rec_cap + s_c.slot) * NV + lane] = s_fin[lane];
+            }
+            if (lane == 0) update_state_inplace(p, b, ch, s_c, s_o, s_u, s_fin, io);
+        }
+        pend = false;
+        pre_ok = false;
+    };
     // timing probe: per-channel launch span in row 0, words 20 + 3 ch .. (block 0)
     const unsigned long long t_start = wall_clock64();
     for (int s = 0; s < nsteps; s++) {
@@ -1087,25 +1150,25 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(3, 
         const int bad = D.bad;
         const bool stop = !D.phaseC && D.Index + 1 > n1_target;  // 1-ms run of this channel done
         if (bad || stop || D.d * M >= 1.0) {  // (a code rate beyond Fs/M breaks the one-boundary lane)
+            if (pend) flush();
+            __syncthreads();
             if (io) {  // leave the state and this (unused) descriptor for the host / next launch
-                if (tid == 0 && !stop) s_c[cur].status = bad ? bad : GNSS_EINDEX;
+                if (tid == 0 && !stop) s_c.status = bad ? bad : GNSS_EINDEX;
                 __syncthreads();
                 if (tid < kChanWords)
-                    reinterpret_cast<uint64_t*>(b.chan + ch)[tid] = reinterpret_cast<const uint64_t*>(&s_c[cur])[tid];
+                    reinterpret_cast<uint64_t*>(b.chan + ch)[tid] = reinterpret_cast<const uint64_t*>(&s_c)[tid];
                 for (int e = tid; e < kDescWords; e += T)
                     reinterpret_cast<unsigned*>(b.desc + ch)[e] = reinterpret_cast<const unsigned*>(&D)[e];
             }
             return;
         }
         const int64_t A = uni(D.A), n = uni(D.n);
-        // the record's two delayValue prefix reads, issued now and used in the tail
-        int64_t pre[2] = {0, 0};
-        if (io && wv == 1 && lane == 0) {
-            const TrkChan& c0 = s_c[cur];
+        if (pend && io && wv == 1 && lane == 0) {  // (used by the flush below, after the compute)
             const int64_t* dvp = b.dvpre + (int64_t)ch * (p.rec_cap + 1);
-            const int64_t cols = record_cols(p, c0, D.phaseC);
-            pre[0] = dvp[c0.nstep];
-            pre[1] = cols < c0.nstep + 1 ? dvp[cols] : 0;
+            const int64_t cols = record_cols(p, s_c, s_o.phaseC);
+            pre[0] = dvp[s_c.nstep];
+            pre[1] = cols < s_c.nstep + 1 ? dvp[cols] : 0;
+            pre_ok = true;
         }
         // timing probe (GNSS_STAMPS), channel 0, row s: [0] step start, [1] computed,
         // [2] partial out, [3] all partials in, [4] next descriptor ready (block 0);
@@ -1114,7 +1177,17 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(3, 
                                        ? b.stamps + (size_t)(s % kStampSlots) * kStampRow + (io ? 0 : 5) : nullptr;
         if (srow && tid == 0) srow[0] = wall_clock64();
 
-        // ---- correlate this block's lanes (IF prefetched into s_raw)
+        // ---- correlate this block's lanes (IF prefetched into s_raw). The CU's other
+        // blocks (other channels) may be in their latency-bound scalar end meanwhile: the
+        // correlator runs at a low wave priority, everything after it at the highest. The
+        // low level rotates with the step (0..2) so the channels sharing a CU take turns
+        // (by age alone the first-dispatched channel would always win and the last one set
+        // the launch's length).
+        switch ((s + ch) % 3) {
+        case 0: __builtin_amdgcn_s_setprio(0); break;
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        default: __builtin_amdgcn_s_setprio(2); break;
+        }
         {
             const int64_t g0 = uni(D.g_first) + ((int64_t)blk * T + tid) * SUB;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's global_load_lds landed
@@ -1122,6 +1195,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(3, 
             lane_correlate<NT, SUB, DIVIDE, true>(p, &D, LdsRaw{s_raw + tid}, 8 * g0 - A, cabits,
                                                   reinterpret_cast<double2*>(s_mem) + tid, &s_zero, oI, oQ);
             __syncthreads();  // slots and s_raw free
+            __builtin_amdgcn_s_setprio(3);
             if (srow && tid == 0) srow[1] = wall_clock64();
             // block sum in a fixed order, published as granules
             const double bsum = block_partial<NT>(s_mem, oI, oQ, tid);
@@ -1134,12 +1208,24 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(3, 
                 store_agent(g + 1, ((unsigned long long)tg << 32) | (w >> 32));
             }
             if (srow && tid == 0) srow[2] = wall_clock64();
+            if (b.stamps && ch == 0 && tid == 0) {  // latest partial of the channel (all blocks)
+                unsigned long long* r = b.stamps + (size_t)(s % kStampSlots) * kStampRow;
+                atomicMax(r + 23, wall_clock64());
+                atomicMax(r + 24, ~wall_clock64());  // (earliest, complemented)
+            }
+        }
+
+        if (pend) {
+            if (srow && tid == 64) srow[16] = wall_clock64();
+            flush();  // (the sweep's closing barrier publishes it)
+            if (srow && tid == 64) srow[17] = wall_clock64();
         }
 
         // ---- every block's partial, summed in a fixed order (bit-identical in all blocks)
         unsigned* pw = reinterpret_cast<unsigned*>(s_mem);
+        // (waves 0, 2, 3 poll; wave 1 is flushing the previous step meanwhile)
         if (!sweep_words(pg + (int64_t)(s & 1) * kMaxBpcRun * NV * 2, bpc * NV * 2, tag0 + s + 1, pw,
-                         tid, b.run_err))
+                         wv == 1 ? -1 : tid - (wv > 1 ? 64 : 0), 3 * 64, b.run_err))
             return;
         if (srow && tid == 0) srow[3] = wall_clock64();
         // wave 2 issues the whole block's next IF (it starts at A + n, ftell after this
@@ -1162,10 +1248,10 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(3, 
         lds_barrier();
         if (srow && io && tid == 0) srow[10] = wall_clock64();
 
-        // ---- the loop update (every wave) and the step's scalar end: wave 0 the code half
-        // of the next descriptor, wave 3 the carrier half, wave 2 the new state, wave 1
-        // (block 0) the record
-        const TrkChan& c = s_c[cur];
+        // ---- the loop update and the next descriptor: wave 0 its code half (DLL half of
+        // the update), wave 3 its carrier table (PLL half), wave 2 the next remPhase; wave 1
+        // keeps the full update for this step's side effects (written next step)
+        const TrkChan& c = s_c;
         StepOut o;
         o.n = n;
         o.delayValue = D.delayValue;
@@ -1190,28 +1276,16 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(3, 
             prepare_desc_i(p, nx, o.pdi, o.phaseC, wv == 0 ? 0 : 1, lane, &s_d[cur ^ 1], s_taps,
                            srow && io ? srow + 14 : nullptr);
             if (srow && io && lane == 0) srow[wv == 0 ? 12 : 13] = wall_clock64();
-        } else if (wv == 1) {  // the record (block 0), then the state
-            if (io) {
-                if (lane == 0) write_record_i(p, b, ch, c, o, u, s_fin, pre);
-                if (b.taps_rec && lane < NV && c.slot < p.rec_cap)
-                    b.taps_rec[((int64_t)ch * p.rec_cap + c.slot) * NV + lane] = s_fin[lane];
-            }
+        } else if (wv == 1) {
             if (lane == 0) {
-                TrkChan& g = s_c[cur ^ 1];
-                write_state_i(p, b, ch, &g, c, o, u, s_fin, io);
-                // the fields a step does not change carry over
-                g.carrierFreqBasis = c.carrierFreqBasis;
-                g.n1_target = c.n1_target;
-                g.codedelay0 = c.codedelay0;
-                g.sv1 = c.sv1;
-                g.prn = c.prn;
-                g.status = c.status;
-                g.countinx = c.countinx;
+                s_o = o;
+                s_u = u;
             }
         } else {  // wave 2: remPhase of the next step, then its IF has landed
             prepare_desc_i(p, nx, o.pdi, o.phaseC, 2, lane, &s_d[cur ^ 1], s_taps);  // lane 63
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
+        pend = true;
         lds_barrier();
         if (srow && tid == 0) srow[4] = wall_clock64();
         cur ^= 1;
@@ -1221,9 +1295,11 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(3, 
         b.stamps[21 + 3 * ch] = wall_clock64();
         b.stamps[22 + 3 * ch] = (unsigned long long)nsteps;
     }
+    if (pend) flush();
+    __syncthreads();
     if (io) {  // the state and the next step's descriptor for the next launch
         if (tid < kChanWords)
-            reinterpret_cast<uint64_t*>(b.chan + ch)[tid] = reinterpret_cast<const uint64_t*>(&s_c[cur])[tid];
+            reinterpret_cast<uint64_t*>(b.chan + ch)[tid] = reinterpret_cast<const uint64_t*>(&s_c)[tid];
         for (int e = tid; e < kDescWords; e += T)
             reinterpret_cast<unsigned*>(b.desc + ch)[e] = reinterpret_cast<const unsigned*>(&s_d[cur])[e];
     }
@@ -1247,31 +1323,54 @@ __global__ void track_snapshot_kernel(const TrkBuffers* __restrict__ bp, int nch
     if (i < nch) b.snap[i] = b.chan[i];
 }
 
-// trackingCT.m:178-213 on the phase-A P_i (length msToProcessCT_1ms).
+// trackingCT.m:178-213 on the phase-A P_i (length msToProcessCT_1ms): the scan over i
+// stops at the first i whose 6-before / 17-after sign test passes with i >= 600, or at
+// the first i whose test runs past the end (MATLAB's index error). Every i's outcome
+// depends on P alone, so one block per channel tests all i at once and keeps the first
+// stopping one (the serial scan's answer).
 __global__ void track_bitedge_kernel(const TrkBuffers* __restrict__ bp, int nch)
 {
     const TrkBuffers& b = *bp;
-    const int ch = blockIdx.x * blockDim.x + threadIdx.x;
-    if (ch >= nch) return;
+    const int ch = blockIdx.x;
+    __shared__ int s_first;
+    if (threadIdx.x == 0) s_first = 0x7fffffff;
+    __syncthreads();
     TrkChan& c = b.chan[ch];
-    if (c.status != GNSS_OK) return;
+    if (c.status != GNSS_OK) return;  // (block-uniform)
     const double* P = b.p_i_1ms + (int64_t)ch * b.n1;
     const int64_t len = b.n1;
-    int cx = 0;
-    for (int64_t i = 7; i <= len - 1; i++) {
-        const double pi = P[i - 1];
-        const int si = (pi > 0) - (pi < 0);
-        bool ok = true;
-        for (int j = 6; j >= 1 && ok; j--) {
-            const double q = P[i - j - 1];
-            ok = ((q > 0) - (q < 0)) != si;
+    auto sgn = [](double x) { return (x > 0) - (x < 0); };
+    int mine = 0x7fffffff;
+    for (int64_t i = 7 + (int64_t)threadIdx.x; i <= len - 1; i += (int64_t)blockDim.x) {
+        const int si = sgn(P[i - 1]);
+        int before = 1;  // the 6 samples before differ in sign
+        for (int j = 6; j >= 1; j--) before &= sgn(P[i - j - 1]) != si ? 1 : 0;
+        int stop = 0;
+        if (before) {
+            int k = 1;  // the 17 after agree; reaching past the end first is MATLAB's error
+            for (; k <= 17; k++) {
+                if (i + k > len) { stop = 1; break; }
+                if (sgn(P[i + k - 1]) != si) break;
+            }
+            if (k > 17 && i >= 600) stop = 1;
         }
+        if (stop && (int)i < mine) mine = (int)i;
+    }
+    if (mine != 0x7fffffff) atomicMin(&s_first, mine);
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    const int64_t i = s_first;
+    int cx = 0;
+    if (i != 0x7fffffff) {
+        // re-run the stopping i's test serially to tell the error from the hit
+        const int si = sgn(P[i - 1]);
+        bool ok = true;
+        for (int j = 6; j >= 1 && ok; j--) ok = sgn(P[i - j - 1]) != si;
         for (int j = 1; j <= 17 && ok; j++) {
             if (i + j > len) { c.status = GNSS_EINDEX; return; }
-            const double q = P[i + j - 1];
-            ok = ((q > 0) - (q < 0)) == si;
+            ok = sgn(P[i + j - 1]) == si;
         }
-        if (ok && i >= 600) { cx = (int)(i % 20) - 1; break; }
+        cx = (int)(i % 20) - 1;
     }
     c.countinx = cx;
     c.n1_target = b.n1 + cx;
@@ -1380,7 +1479,7 @@ hipError_t launch_track_snapshot(const TrkParams& p, const TrkBuffers& b, const 
 
 hipError_t launch_track_bitedge(const TrkParams& p, const TrkBuffers& b, const TrkDev& d, hipStream_t s)
 {
-    hipLaunchKernelGGL(track_bitedge_kernel, dim3((p.nch + 63) / 64), dim3(64), 0, s, d.b, p.nch);
+    hipLaunchKernelGGL(track_bitedge_kernel, dim3(p.nch), dim3(256), 0, s, d.b, p.nch);
     return hipGetLastError();
 }
 

@@ -240,6 +240,12 @@ class TrackOutBuffers:
         o.CN0_Eph = self.CN0.ctypes.data_as(C.POINTER(C.c_double))
         o.cn0_cap = self.cn0_cap
         self.c = o
+        self.shape = (nsv, self.max_len, ntaps, self.cn0_cap)
+
+    def fits(self, nsv: int, track, ntaps: int) -> bool:
+        max_len = int(track.msToProcessCT_1ms) + 19 + int(track.msToProcessCT_10ms)
+        cn0_cap = max(int(track.msToProcessCT_1ms) + 19, int(track.msToProcessCT_10ms) // 10) // 20 + 1
+        return self.shape == (nsv, max_len, ntaps, cn0_cap)
 
 
 class StructArray:
@@ -309,14 +315,17 @@ def acquisition(file, signal, acq, *, ctx: Context | None = None, prn_list=None,
 
 
 def trackingCT(file, signal, track, Acquired, *, ctx: Context | None = None, taps=None,
-               channels=None, save_countinx: str | None = None, raw: bool = False):
+               channels=None, save_countinx: str | None = None, raw: bool = False,
+               out: "TrackOutBuffers | None" = None):
     """trackingCT.m:1-530 on the GPU -> (TckResultCT, CN0_Eph, countinx).
 
     TckResultCT is indexed by PRN (TckResultCT(prn).P_i), CN0_Eph is
     cn0_rows x nsv, countinx is 1 x nsv. `taps` enables the multi-correlator ACF
     taps (config 5); `channels` tracks a subset (multi-GPU shard). The side file
     countinx.mat of trackingCT.m:530 is written only when save_countinx names it.
-    With raw=True the TrackOutBuffers are returned instead of the structs.
+    With raw=True the TrackOutBuffers are returned instead of the structs; `out` reuses
+    a TrackOutBuffers of the same shape from an earlier call (no 10s of MB allocated and
+    freed per call; rows of channels outside `channels` keep their old contents).
     """
     ctx = ctx or default_context()
     nsv = len(Acquired.sv)
@@ -324,7 +333,13 @@ def trackingCT(file, signal, track, Acquired, *, ctx: Context | None = None, tap
     s = to_c_signal(signal)
     t, k2 = to_c_track(track, taps, channels)
     a = to_c_acquired(Acquired)
-    buf = TrackOutBuffers(nsv, track, 0 if taps is None else len(taps))
+    ntaps = 0 if taps is None else len(taps)
+    if out is not None and out.fits(nsv, track, ntaps):
+        buf = out
+        buf.len[:] = 0
+        buf.countinx[:] = 0
+    else:
+        buf = TrackOutBuffers(nsv, track, ntaps)
     st = ctx.lib.gnss_tracking_ct(ctx.h, C.byref(f), C.byref(s), C.byref(t), C.byref(a),
                                   C.byref(buf.c))
     if st == abi.ENODATA:

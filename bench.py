@@ -104,10 +104,13 @@ def main():
     pkg.synth.generate_device(ctx, cfg, dev)
     file.dev = dev
 
+    outs = [None]  # the trackingCT output buffers, reused from step to step
+
     def one_step():
         A = pkg.acquisition(file, signal, acq, ctx=ctx)
         ta = ctx.timing()
-        buf = pkg.trackingCT(file, signal, track, A, ctx=ctx, raw=True)
+        buf = pkg.trackingCT(file, signal, track, A, ctx=ctx, raw=True, out=outs[0])
+        outs[0] = buf
         tt = ctx.timing()
         return A, ta, tt, buf
 

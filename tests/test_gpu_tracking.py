@@ -179,6 +179,21 @@ def test_persistent_and_step_paths_bit_identical(pkg, ctx, opensky_short, monkey
         assert p.len[c] == q.len[c] and p.countinx[c] == q.countinx[c]
 
 
+def test_reused_output_buffers(pkg, ctx, opensky_short):
+    """trackingCT(out=...) writes the same records into a buffer from an earlier call."""
+    skip, cfg, data = opensky_short
+    file, signal, acq, track = params(pkg, skip, data)
+    track.msToProcessCT_1ms, track.msToProcessCT_10ms = 700, 200
+    A1 = acquired_of([3, 16], [3684, 26051], [4580975.0, 4579675.0])
+    A2 = acquired_of([22, 26], [2611, 57908], [4581525.0, 4581800.0])
+    fresh = pkg.trackingCT(file, signal, track, A2, ctx=ctx, raw=True)
+    buf = pkg.trackingCT(file, signal, track, A1, ctx=ctx, raw=True)
+    again = pkg.trackingCT(file, signal, track, A2, ctx=ctx, raw=True, out=buf)
+    assert again is buf
+    assert np.array_equal(fresh.rec, again.rec) and np.array_equal(fresh.CN0, again.CN0)
+    assert np.array_equal(fresh.len, again.len) and np.array_equal(fresh.countinx, again.countinx)
+
+
 def test_not_enough_raw_data_in_1ms_phase(pkg, ctx, opensky_short):
     """trackingCT.m:108-112: short record in the 1-ms phases -> TckResultCT = []."""
     skip, cfg, data = opensky_short

@@ -36,3 +36,13 @@ for path in sys.argv[1:]:
     spans = [(ch, (r0[21 + 3 * ch] - r0[20 + 3 * ch]) * 0.01, r0[22 + 3 * ch]) for ch in range(64) if r0[21 + 3 * ch]]
     if spans:
         print("  per-channel launch span (us) / steps:", ", ".join(f"ch{c} {t:.0f}/{n}" for c, t, n in spans))
+    d = np.fromfile(path, dtype=np.uint64)[:-1].reshape(-1, ROW)[:, :23].astype(np.int64)
+    d = d[(d[:, 16] != 0) & (d[:, 21] != 0) & (d[:, 2] != 0)]
+    if len(d):
+        print(f"  flush: blk0 start-after-publish {us(d[:, 16] - d[:, 2]):6.2f} dur {us(d[:, 17] - d[:, 16]):6.2f}; "
+              f"last dur {us(d[:, 22] - d[:, 21]):6.2f}")
+    e = np.fromfile(path, dtype=np.uint64)[:-1].reshape(-1, ROW)[:, :25]
+    e = e[(e[:, 23] != 0) & (e[:, 3] != 0)]
+    if len(e):
+        lat = e[:, 23].astype(np.int64); ear = (~e[:, 24]).astype(np.int64)
+        print(f"  all blocks: first->last partial out {us(lat - ear):6.2f}; latest partial -> blk0 all in {us(e[:, 3].astype(np.int64) - lat):6.2f}; blk0 partial -> latest {us(lat - e[:, 2].astype(np.int64)):6.2f}")
