@@ -133,9 +133,9 @@ def main():
     nch = len(A.sv)
 
     # roofline of the dominant kernel: the tracking correlator of the 10-ms phase (most
-    # of the time): the persistent track_run_kernel<3, 4, false> (one launch runs the
-    # whole phase) or, where its grid cannot be resident, track_step_kernel<3, 4, false>
-    # (one launch per step). A profiling pass brackets every launch with hipEvents on the
+    # of the time): the persistent track_run_kernel<3, 3, false> (one launch runs the
+    # whole phase; 24-sample lanes) or, where its grid cannot be resident,
+    # track_step_kernel<3, 3, false> (one launch per step). A profiling pass brackets every launch with hipEvents on the
     # ctx stream; algorithmic bytes = 2 B (int8 I + Q) per channel-sample of the launch.
     roof = None
     if not args.no_profile_pass:
@@ -149,9 +149,9 @@ def main():
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                "kernel": ("track_run_kernel<3, 4, false> (persistent: every step of the 10-ms phase, "
+                "kernel": ("track_run_kernel<3, 3, false> (persistent: every step of the 10-ms phase, "
                            "all channels)" if launches <= 2 else
-                           "track_step_kernel<3, 4, false> (10-ms phase step, all channels)"),
+                           "track_step_kernel<3, 3, false> (10-ms phase step, all channels)"),
                 "steps_per_launch": round(tp["track10_channel_samples"] / max(1, launches) /
                                           (nch * 10 * SAMPLES_PER_MS), 1),
                 "launches": int(launches), "avg_launch_us": round(avg_ms * 1e3, 3),

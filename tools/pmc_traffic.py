@@ -24,6 +24,6 @@ out = {"kernel": sys.argv[3], "dispatches": [int(fetch.size), int(write.size)],
 if fetch.size and write.size:
     out["bytes_per_launch"] = 2 * out["fetch_kb_per_dispatch_raw"] * 1024 + out["write_kb_per_dispatch"] * 1024
     out["note"] = ("median over dispatches; FETCH_SIZE doubled (gfx950 16-B/lane streaming reads), "
-                   "both KB -> bytes; workload tools/track_only.py 100 4000 (8 ch, 10-ms steps)")
+                   "both KB -> bytes; workload tools/track_only.py 1000 40000 (8 ch, the bench trackingCT: one persistent launch = 4000 10-ms steps)")
 json.dump(out, open(sys.argv[4], "w"), indent=1)
 print(json.dumps(out))
