@@ -1025,6 +1025,53 @@ __device__ bool sweep_words(const unsigned long long* g, int n, unsigned tag, un
     return !__syncthreads_or(todo != 0);
 }
 
+// 16-B granules {lo, tag, hi, tag}: one fp64 partial per granule, written by one
+// buffer_store_dwordx4 sc1 and read by one buffer_load_dwordx4 sc1 (MI355X_MICROARCH.md
+// hand-off table: 16-B sc1 stores and loads; each half carries the tag, so a torn read
+// is simply not accepted). Half the polls of two 8-B granules per value.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kBufRsrcWord3 = 0x00020000;  // raw buffer, gfx9 family
+constexpr int kPolSc1 = 16;                // cache policy: sc1 (device coherence)
+
+__device__ __forceinline__ void publish16(__amdgpu_buffer_rsrc_t r, int unit, double v, unsigned tag)
+{
+    const unsigned long long w = (unsigned long long)__double_as_longlong(v);
+    const u32x4 g = {(unsigned)w, tag, (unsigned)(w >> 32), tag};
+    __builtin_amdgcn_raw_buffer_store_b128(g, r, unit * 16, 0, kPolSc1);
+}
+
+// Poll n 16-B granules until both tags of each equal `tag`; granule e's words land in
+// dst[2e], dst[2e+1]. Same protocol as sweep_words (pollers pid 0..np-1, n <= 64*np).
+__device__ bool sweep16(__amdgpu_buffer_rsrc_t r, int n, unsigned tag, unsigned* dst, int pid, int np,
+                        unsigned* err, int base)
+{
+    unsigned long long todo = 0;
+    if (pid >= 0)
+        for (int k = 0, e = pid; e < n; k++, e += np) todo |= 1ull << k;
+    unsigned long long t0 = 0;
+    int late = 0;
+    while (todo) {
+        for (int k = 0; (todo >> k) != 0; k++) {
+            if (!((todo >> k) & 1ull)) continue;
+            const int e = pid + k * np;
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (base + e) * 16, 0, kPolSc1);
+            if (v.y == tag && v.w == tag) {
+                dst[2 * e] = v.x;
+                dst[2 * e + 1] = v.z;
+                todo &= ~(1ull << k);
+            }
+        }
+        if (!todo) break;
+        if (++late >= 64) {
+            const unsigned long long t = wall_clock64();
+            if (!t0) t0 = t;
+            else if (t - t0 > 200000000ull) { atomicExch(err, 1u); break; }
+            late = 0;
+        }
+    }
+    return !__syncthreads_or(todo != 0);
+}
+
 // Grid census (guide G16: residency is a precondition, not a given): every block
 // arrives on one counter; the last arrival starts the launch, a block that waits ~20 ms
 // aborts it instead (one CAS decides). On abort every block leaves before touching any
@@ -1111,7 +1158,9 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(3, 
     const int8_t* iq = b.iq - p.buf_base;  // absolute-byte addressing
     const int64_t gmax = (p.buf_base + p.buf_len) / 16 - 1;  // last resident 16-B group
     const unsigned cabits = lane < 32 ? ((g_cu32*)b.ca_bits)[ch * 32 + lane] : 0u;
-    unsigned long long* pg = b.pgran + (int64_t)ch * 2 * kMaxBpcRun * 2 * NV;
+    // this channel's granules: [parity][block][value] x 16 B
+    const __amdgpu_buffer_rsrc_t pg = __builtin_amdgcn_make_buffer_rsrc(
+        b.pgran + (int64_t)ch * 2 * kMaxBpcRun * 2 * NV, (short)0, 2 * kMaxBpcRun * NV * 16, kBufRsrcWord3);
     constexpr int kChanWords = (int)(sizeof(TrkChan) / 8);
 
     // step 0's descriptor and the state, as the previous launch left them
@@ -1199,14 +1248,8 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(3, 
             if (srow && tid == 0) srow[1] = wall_clock64();
             // block sum in a fixed order, published as granules
             const double bsum = block_partial<NT>(s_mem, oI, oQ, tid);
-            if (tid < NV * 4 && (tid & 3) == 0) {
-                const int v = tid >> 2;
-                const unsigned long long w = (unsigned long long)__double_as_longlong(bsum);
-                const unsigned tg = tag0 + s + 1;
-                unsigned long long* g = pg + (((int64_t)(s & 1) * kMaxBpcRun + blk) * NV + v) * 2;
-                store_agent(g, ((unsigned long long)tg << 32) | (w & 0xffffffffull));
-                store_agent(g + 1, ((unsigned long long)tg << 32) | (w >> 32));
-            }
+            if (tid < NV * 4 && (tid & 3) == 0)
+                publish16(pg, ((s & 1) * kMaxBpcRun + blk) * NV + (tid >> 2), bsum, tag0 + s + 1);
             if (srow && tid == 0) srow[2] = wall_clock64();
             if (b.stamps && ch == 0 && tid == 0) {  // latest partial of the channel (all blocks)
                 unsigned long long* r = b.stamps + (size_t)(s % kStampSlots) * kStampRow;
@@ -1224,8 +1267,10 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(3, 
         // ---- every block's partial, summed in a fixed order (bit-identical in all blocks)
         unsigned* pw = reinterpret_cast<unsigned*>(s_mem);
         // (waves 0, 2, 3 poll; wave 1 is flushing the previous step meanwhile)
-        if (!sweep_words(pg + (int64_t)(s & 1) * kMaxBpcRun * NV * 2, bpc * NV * 2, tag0 + s + 1, pw,
-                         wv == 1 ? -1 : tid - (wv > 1 ? 64 : 0), 3 * 64, b.run_err))
+        // (block 0: waves 0, 2, 3 poll while wave 1 writes the record; the other blocks'
+        // wave 1 flush is short and it joins the polling after it)
+        if (!sweep16(pg, bpc * NV, tag0 + s + 1, pw, io ? (wv == 1 ? -1 : tid - (wv > 1 ? 64 : 0)) : tid,
+                     io ? 3 * 64 : 4 * 64, b.run_err, (s & 1) * kMaxBpcRun * NV))
             return;
         if (srow && tid == 0) srow[3] = wall_clock64();
         // wave 2 issues the whole block's next IF (it starts at A + n, ftell after this
