@@ -1232,7 +1232,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(3, 
         // low level rotates with the step (0..2) so the channels sharing a CU take turns
         // (by age alone the first-dispatched channel would always win and the last one set
         // the launch's length).
-        switch ((s + ch) % 3) {
+        switch ((p.probe & 64) ? ch % 3 : (p.probe & 128) ? 0 : (s + ch) % 3) {
         case 0: __builtin_amdgcn_s_setprio(0); break;
         case 1: __builtin_amdgcn_s_setprio(1); break;
         default: __builtin_amdgcn_s_setprio(2); break;

@@ -144,7 +144,9 @@ def to_c_file(file):
         f.dev_data = dev.ptr
         f.nbytes = dev.nbytes
     elif data is not None:
-        arr = np.ascontiguousarray(data, dtype=np.int8)
+        # the record's byte image (an int16 array is passed through as its bytes)
+        arr = np.ascontiguousarray(data) if isinstance(data, np.ndarray) else np.asarray(data, np.int8)
+        arr = arr.reshape(-1).view(np.int8)
         keep.append(arr)
         f.data = arr.ctypes.data
         f.nbytes = arr.nbytes

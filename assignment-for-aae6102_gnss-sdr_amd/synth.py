@@ -91,3 +91,26 @@ def generate_device(ctx, cfg, dev_record, sample0=0, nsamples=None):
     ctx.check(ctx.lib.gnss_synth_if_device(ctx.h, C.byref(cfg), C.c_uint64(sample0),
                                            C.c_uint64(n), dev_record.ptr))
     return dev_record
+
+
+def convert_record(iq8: np.ndarray, dataPrecision: int = 1, dataType: int = 2, *, scale: int = 64,
+                   dc=(37, -23)) -> np.ndarray:
+    """Byte image of the same scene in another record format (initParameters.m:36-37):
+      (1, 2) int8 I/Q pairs (the input, unchanged);
+      (1, 1) int8 real: the I byte of each pair (Re of the -(IF+fd) carrier still holds
+             the SV at +-(IF+fd), the reference's carrier wipes the negative one);
+      (2, 2) int16 I/Q: I*scale + dc[0], Q*scale + dc[1] (a DC offset the reference's
+             per-read mean removal takes out, acquisition.m:28-32, trackingCT.m:84-88);
+      (2, 1) int16 real values (the reference de-interleaves them as I/Q anyway).
+    Returned as int8 bytes (little-endian int16 where dataPrecision is 2)."""
+    iq8 = np.asarray(iq8, dtype=np.int8)
+    i8, q8 = iq8[0::2], iq8[1::2]
+    if dataPrecision == 1:
+        return iq8.copy() if dataType == 2 else i8.copy()
+    i16 = i8.astype(np.int16) * np.int16(scale) + np.int16(dc[0])
+    if dataType == 1:
+        return i16.astype("<i2").view(np.int8)
+    q16 = q8.astype(np.int16) * np.int16(scale) + np.int16(dc[1])
+    out = np.empty(2 * len(i16), dtype="<i2")
+    out[0::2], out[1::2] = i16, q16
+    return out.view(np.int8)

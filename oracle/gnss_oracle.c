@@ -279,6 +279,53 @@ static int64_t file_size(const gnss_file *f)
     return s;
 }
 
+/* The IF samples of one fread, as the reference forms them (acquisition.m:28-37,
+ * :90-99; trackingCT.m:84-93, :416-426): `nsamp` samples requested at byte `off`.
+ *   int8 (dataPrecision 1): dataType 2 -> I/Q byte pairs, dataType 1 -> real bytes;
+ *   int16 (dataPrecision 2): fread(nsamp*dataType, 'int16') de-interleaved into
+ *     I = values(1:2:end), Q = values(2:2:end) WHATEVER dataType says, each half
+ *     minus its own mean (sum / length, exact for integer-valued doubles).
+ * Returns the length MATLAB's rawsignal gets (fewer than nsamp at EOF; nsamp/2 for
+ * int16 with dataType 1), -1 on an I/O failure, -2 where MATLAB raises an error
+ * (I and Q halves of unequal length: an odd number of values read). *bytes = the
+ * bytes fread consumed (the ftell advance). */
+static int64_t rd_cpx(const gnss_file *f, int64_t off, int64_t nsamp, cpx *out, int64_t *bytes)
+{
+    const int prec = f->dataPrecision, type = f->dataType;
+    const int64_t want = nsamp * type * prec;
+    int8_t *b = (int8_t *)malloc((size_t)(want > 0 ? want : 1));
+    if (!b) return -1;
+    int64_t got = rd_bytes(f, off, want, b);
+    if (got < 0) { free(b); return -1; }
+    int64_t m;
+    if (prec == 1) {
+        *bytes = got;
+        if (type == 2) {
+            if (got & 1) { free(b); return -2; }
+            m = got / 2;
+            for (int64_t k = 0; k < m; k++) { out[k].re = b[2 * k]; out[k].im = b[2 * k + 1]; }
+        } else {
+            m = got;
+            for (int64_t k = 0; k < m; k++) { out[k].re = b[k]; out[k].im = 0; }
+        }
+    } else {
+        const int64_t nv = got / 2; /* whole int16 values */
+        *bytes = 2 * nv;
+        if (nv & 1) { free(b); return -2; }
+        m = nv / 2;
+        const int16_t *v = (const int16_t *)b; /* little-endian host, as the file */
+        double si = 0, sq = 0;
+        for (int64_t k = 0; k < m; k++) { si += v[2 * k]; sq += v[2 * k + 1]; }
+        const double mi = si / (double)m, mq = sq / (double)m;
+        for (int64_t k = 0; k < m; k++) {
+            out[k].re = (double)v[2 * k] - mi;
+            out[k].im = (double)v[2 * k + 1] - mq;
+        }
+    }
+    free(b);
+    return m;
+}
+
 /* ------------------------------------------------------------------------ */
 /* acquisition.m                                                             */
 /* ------------------------------------------------------------------------ */
@@ -297,7 +344,8 @@ int or_acquisition(const gnss_file *file, const gnss_signal *sg, const gnss_acq 
 {
     memset(out, 0, sizeof(*out));
     if (diag) memset(diag, 0, sizeof(*diag));
-    if (file->dataPrecision != 1 || file->dataType != 2) return GNSS_EARG; /* int16/I-only: next */
+    if ((file->dataPrecision != 1 && file->dataPrecision != 2) || (file->dataType != 1 && file->dataType != 2))
+        return GNSS_EARG;
     const int64_t S = sg->Sample;
     const int nb = acq->freqNum, dl = acq->datalen;
     if (S <= 0 || nb <= 0 || dl <= 0 || acq->L <= 0) return GNSS_EARG;
@@ -311,10 +359,17 @@ int or_acquisition(const gnss_file *file, const gnss_signal *sg, const gnss_acq 
 
     /* read data (acquisition.m:27,34-37) */
     const int64_t off = file->skip * S * file->dataPrecision * file->dataType;
-    const int64_t nbytes = S * file->dataType * dl;
-    int8_t *raw8 = (int8_t *)malloc((size_t)nbytes);
-    if (!raw8) return GNSS_EIO;
-    if (rd_bytes(file, off, nbytes, raw8) != nbytes) { free(raw8); return GNSS_EIO; }
+    cpx *raw = (cpx *)malloc(sizeof(cpx) * (size_t)(S * dl));
+    if (!raw) return GNSS_EIO;
+    {
+        int64_t nb_read = 0;
+        const int64_t m = rd_cpx(file, off, S * dl, raw, &nb_read);
+        /* rawsignal(1+(idx-1)*Sample : idx*Sample) past the end is MATLAB's index
+         * error (int16 with dataType 1 always: half the samples); a short file: EIO */
+        if (m == -1) { free(raw); return GNSS_EIO; }
+        if (m == -2 || (m < S * dl && file->dataPrecision == 2 && file->dataType == 1)) { free(raw); return GNSS_EINDEX; }
+        if (m < S * dl) { free(raw); return GNSS_EIO; }
+    }
 
     /* carrier(freqband,:) = exp(1i*2*pi*(IF+dopplershift)*sampleindex./Fs) (:41-44) */
     cpx *carrier = (cpx *)malloc(sizeof(cpx) * (size_t)(nb * S));
@@ -339,7 +394,7 @@ int or_acquisition(const gnss_file *file, const gnss_signal *sg, const gnss_acq 
         int idx = j / nb, b = j % nb;
         cpx *x = Xc + (int64_t)j * S;
         for (int64_t n = 0; n < S; n++) {
-            double xr = raw8[2 * (idx * S + n)], xi = raw8[2 * (idx * S + n) + 1];
+            double xr = raw[idx * S + n].re, xi = raw[idx * S + n].im;
             cpx c = carrier[b * S + n];
             x[n].re = xr * c.re - xi * c.im;
             x[n].im = xr * c.im + xi * c.re;
@@ -417,16 +472,21 @@ int or_acquisition(const gnss_file *file, const gnss_signal *sg, const gnss_acq 
             out->codedelay[k] = res_cp[ip] - 1;
         }
     }
-    free(Xc); free(carrier); free(raw8);
+    free(Xc); free(carrier); free(raw);
     fft_plan_free(&pl);
 
     if (out->n == 0) return GNSS_ENODATA; /* :84-85 */
 
     /* fine frequency (:89-126) */
     const int64_t Ls = (int64_t)acq->L * S;
-    const int64_t lbytes = S * file->dataType * (acq->L + 1);
-    int8_t *lraw = (int8_t *)malloc((size_t)lbytes);
-    if (rd_bytes(file, off, lbytes, lraw) != lbytes) { free(lraw); return GNSS_EIO; }
+    cpx *lraw = (cpx *)malloc(sizeof(cpx) * (size_t)(S * (acq->L + 1)));
+    {
+        int64_t nb_read = 0;
+        const int64_t m = rd_cpx(file, off, S * (acq->L + 1), lraw, &nb_read);
+        if (m == -1) { free(lraw); return GNSS_EIO; }
+        if (m == -2) { free(lraw); return GNSS_EINDEX; }
+        if (m < S * (acq->L + 1)) { free(lraw); return GNSS_EIO; }
+    }
     const int64_t N = Ls * dl; /* fftlength = length(CarrSignal)*acq.datalen (:108) */
     fftplan fp;
     fft_plan_init(&fp, N);
@@ -442,16 +502,20 @@ int or_acquisition(const gnss_file *file, const gnss_signal *sg, const gnss_acq 
             double cvi = floor((invFs * (double)k) / invFc);      /* :104 */
             int8_t code = ca[(int64_t)fmod(cvi, sg->codelength)]; /* :105 rem(.,1023)+1 */
             int64_t j = start + k - 1;                            /* 1-based sample */
-            x[k - 1].re = (double)lraw[2 * (j - 1)] * code;
-            x[k - 1].im = (double)lraw[2 * (j - 1) + 1] * code;
+            x[k - 1].re = lraw[j - 1].re * code;
+            x[k - 1].im = lraw[j - 1].im * code;
         }
         fft_exec(&fp, x, -1);
         /* abs(fftshift(.)); max over 1:halffftlength*2 -> first index (:110-116) */
         int64_t half = (N + 1) / 2;
         double best = -1;
         int64_t kbest = 0;
+        const int shifted = file->dataType == 2; /* :109-112 */
         for (int64_t i = 0; i < 2 * half && i < N; i++) {
-            int64_t j = (i + N / 2) % N; /* fftshift: shifted[i] = F[(i + floor(N/2)) mod N] */
+            /* fftshift: shifted[i] = F[(i + floor(N/2)) mod N]. A real CarrSignal
+             * (dataType 1) has an exactly conjugate-symmetric fft in MATLAB: |F(N-i)|
+             * is |F(i)| bit for bit, so the first index of a tie is the lower bin. */
+            int64_t j = shifted ? (i + N / 2) % N : (i <= N - i ? i : N - i);
             double a = hypot(x[j].re, x[j].im);
             if (a > best) { best = a; kbest = i + 1; }
         }
@@ -459,7 +523,10 @@ int or_acquisition(const gnss_file *file, const gnss_signal *sg, const gnss_acq 
 #pragma omp atomic write
             status = GNSS_EINDEX; /* odd fftlength: MATLAB indexes past the end */
         }
-        out->fineFreq[s] = -(double)kbest * (sg->Fs / (double)N) + sg->Fs / 2; /* :119 */
+        if (shifted)
+            out->fineFreq[s] = -(double)kbest * (sg->Fs / (double)N) + sg->Fs / 2; /* :119 */
+        else
+            out->fineFreq[s] = (double)kbest * (sg->Fs / (double)N); /* :117 */
         free(x);
     }
     fft_plan_free(&fp);
@@ -475,9 +542,24 @@ int or_acquisition(const gnss_file *file, const gnss_signal *sg, const gnss_acq 
 static inline int chip_ok(int64_t c, int pdi) { return c >= 0 && c <= 1023 * (int64_t)pdi + 1; }
 static inline int ca_index(int64_t c) { return (int)((c + 1022) % 1023); }
 
+static void correlate_cpx(const cpx *x, int64_t n, double remChip, double codeFreq, double Fs,
+                          double carrierFreq, double remPhase, const int8_t *ca, int pdi, int ntaps,
+                          const double *taps, double *sums);
+
 void or_correlate_step(const int8_t *iq, int64_t n, double remChip, double codeFreq, double Fs,
                        double carrierFreq, double remPhase, const int8_t *ca, int pdi, int ntaps,
                        const double *taps, double *sums)
+{
+    cpx *x = (cpx *)malloc(sizeof(cpx) * (size_t)(n > 0 ? n : 1));
+    for (int64_t k = 0; k < n; k++) { x[k].re = iq[2 * k]; x[k].im = iq[2 * k + 1]; }
+    correlate_cpx(x, n, remChip, codeFreq, Fs, carrierFreq, remPhase, ca, pdi, ntaps, taps, sums);
+    free(x);
+}
+
+/* The correlator of trackingCT.m:96-118 on rawsignal0DC (complex doubles). */
+static void correlate_cpx(const cpx *x, int64_t n, double remChip, double codeFreq, double Fs,
+                          double carrierFreq, double remPhase, const int8_t *ca, int pdi, int ntaps,
+                          const double *taps, double *sums)
 {
     (void)pdi;
     const double d = codeFreq / Fs;
@@ -497,7 +579,7 @@ void or_correlate_step(const int8_t *iq, int64_t n, double remChip, double codeF
         /* CarrTime = (0:numSample)./Fs; Wave = (2*pi*(carrierFreq.*CarrTime)) + remPhase */
         double W = TWO_PI * (carrierFreq * ((double)k / Fs)) + remPhase;
         double cw = cos(W), sw = sin(W);
-        double xr = iq[2 * k], xi = iq[2 * k + 1];
+        double xr = x[k].re, xi = x[k].im;
         double I = xr * sw + xi * cw; /* imag(raw.*carrsig) */
         double Q = xr * cw - xi * sw; /* real(raw.*carrsig) */
         for (int s = 0; s < ntaps; s++) {
@@ -617,7 +699,7 @@ static double dv_linear_sum(const int64_t *dv, int64_t filled, int64_t Index, in
 
 /* One tracking step (body of trackingCT.m:79-170 / 407-524). Returns status. */
 static int trk_step(const trk_ctx *t, chan_state *c, int ch, int sv1, int pdi, int phaseC,
-                    int64_t Index, int64_t *dv, int64_t dv_col, double *cn0, int8_t *buf,
+                    int64_t Index, int64_t *dv, int64_t dv_col, double *cn0, cpx *buf,
                     const int8_t *ca, int64_t codedelay0, double *p_i_log)
 {
     const gnss_signal *sg = t->sg;
@@ -634,9 +716,11 @@ static int trk_step(const trk_ctx *t, chan_state *c, int ch, int sv1, int pdi, i
     }
     dv[dv_col] = delayValue;
     const int64_t n = c->numSample;
-    int64_t got = rd_bytes(t->file, c->pos, 2 * n, buf);
-    if (got < 0) return GNSS_EIO;
-    if (got != 2 * n) return phaseC ? GNSS_EIO : GNSS_ENODATA; /* :108-112 / :442 */
+    int64_t got = 0;
+    const int64_t m = rd_cpx(t->file, c->pos, n, buf, &got); /* :84-93 / :416-426 */
+    if (m == -1) return GNSS_EIO;
+    if (m == -2) return GNSS_EINDEX;
+    if (m != n) return phaseC ? GNSS_EIO : GNSS_ENODATA; /* :108-112 / :442 */
     c->pos += got; /* ftell */
 
     /* code range check: MATLAB would raise an index error */
@@ -655,8 +739,8 @@ static int trk_step(const trk_ctx *t, chan_state *c, int ch, int sv1, int pdi, i
     }
 
     double sums[2 * GNSS_MAX_TAPS];
-    or_correlate_step(buf, n, c->remChip, c->codeFreq, sg->Fs, c->carrierFreq, c->remPhase, ca, pdi,
-                      t->ntaps, t->taps, sums);
+    correlate_cpx(buf, n, c->remChip, c->codeFreq, sg->Fs, c->carrierFreq, c->remPhase, ca, pdi,
+                  t->ntaps, t->taps, sums);
     if (phaseC)
         for (int s = 0; s < 2 * t->ntaps; s++) sums[s] = -sums[s]; /* :447-449 */
 
@@ -755,7 +839,7 @@ static int track_channel(const trk_ctx *t, const gnss_acquired *acq, int ch, dou
     const int64_t cd0 = acq->codedelay[ch];
     int8_t ca[1023];
     if (or_generate_ca(acq->sv[ch], ca)) return GNSS_EARG;
-    int8_t *buf = (int8_t *)malloc((size_t)(2 * (S * 10 + 4096)));
+    cpx *buf = (cpx *)malloc(sizeof(cpx) * (size_t)(2 * (S * 10 + 4096)));
     int64_t *dv = (int64_t *)calloc((size_t)(N1 + 32 + N10), sizeof(int64_t));
     double *plog = (double *)calloc((size_t)(N1 + 1), sizeof(double));
     chan_state c;
@@ -804,7 +888,8 @@ done:
 int or_tracking_ct(const gnss_file *file, const gnss_signal *sg, const gnss_track *tr,
                    const gnss_acquired *acq, gnss_track_out *out, int nthreads)
 {
-    if (file->dataPrecision != 1 || file->dataType != 2) return GNSS_EARG;
+    if ((file->dataPrecision != 1 && file->dataPrecision != 2) || (file->dataType != 1 && file->dataType != 2))
+        return GNSS_EARG;
     trk_ctx t;
     memset(&t, 0, sizeof(t));
     t.file = file; t.sg = sg; t.tr = tr; t.out = out; t.nsv = acq->n;

@@ -78,9 +78,22 @@ def correlate_step(iq, n, remChip, codeFreq, Fs, carrierFreq, remPhase, ca, taps
     return np.array(out)
 
 
+def read_samples(buf, dataPrecision, dataType, nsamp):
+    """fread + the reference's sample forming (acquisition.m:28-37, trackingCT.m:84-93) on the
+    record bytes `buf` (int8 view): int8 I/Q or real; int16 values de-interleaved into I/Q
+    (whatever dataType says) minus each half's mean."""
+    buf = np.asarray(buf, dtype=np.int8)
+    if dataPrecision == 1:
+        v = buf[: nsamp * dataType].astype(float)
+        return v[0::2] + 1j * v[1::2] if dataType == 2 else v + 0j
+    v = buf[: 2 * nsamp * dataType].view("<i2").astype(float)
+    si, co = v[0::2], v[1::2]
+    return (si - np.mean(si)) + 1j * (co - np.mean(co))
+
+
 def acquisition(raw8, S, Fs, IF, fc, freqMin, freqStep, freqNum, datalen, prns):
-    """acquisition.m:40-78 (peak search only) on int8 I/Q bytes."""
-    raw = raw8[0::2].astype(float) + 1j * raw8[1::2].astype(float)
+    """acquisition.m:40-78 (peak search only) on int8 I/Q bytes or complex samples."""
+    raw = raw8 if np.iscomplexobj(raw8) else raw8[0::2].astype(float) + 1j * raw8[1::2].astype(float)
     n = np.arange(1, S + 1)
     res = []
     for prn in prns:
