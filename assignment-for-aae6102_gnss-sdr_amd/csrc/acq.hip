@@ -18,7 +18,8 @@ __device__ __forceinline__ float cos_rev(float x) { return __builtin_amdgcn_cosf
 
 // temp1 = rawsignal(ms idx) .* carrier(freqband,:)  (acquisition.m:41-44,56)
 // carrier(b, n) = exp(1i*2*pi*(IF + freqMin + freqStep*(b-1))*n/Fs), n = 1..S
-__global__ void acq_wipe_kernel(const int8_t* __restrict__ iq, int64_t S, int datalen, int nbins,
+template <class Src>
+__global__ void acq_wipe_kernel(const Src src, int64_t S, int datalen, int nbins,
                                 double IF, double freqMin, double freqStep, double Fs,
                                 float2* __restrict__ out)
 {
@@ -31,7 +32,7 @@ __global__ void acq_wipe_kernel(const int8_t* __restrict__ iq, int64_t S, int da
         cyc -= floor(cyc);
         const float ph = (float)cyc;
         const float c = cos_rev(ph), s = sin_rev(ph);
-        const char2 x = *reinterpret_cast<const char2*>(iq + 2 * ((int64_t)idx * S + n));
+        const double2 x = src.at((int64_t)idx * S + n);
         const float xr = (float)x.x, xi = (float)x.y;
         out[(int64_t)j * S + n] = make_float2(xr * c - xi * s, xr * s + xi * c);
     }
@@ -193,7 +194,8 @@ __global__ void acq_peak_final_kernel(const float* __restrict__ corr, int nbins,
 
 // CarrSignal = longrawsignal(S-cd : S-cd+L*S-1) .* longCaCode, zero-padded to N
 // (acquisition.m:103-108); fp64, code index floor((1/Fs*k)/(1/fc)) as the reference.
-__global__ void fine_build_kernel(const int8_t* __restrict__ iq, int64_t S, int L,
+template <class Src>
+__global__ void fine_build_kernel(const Src src, int64_t S, int L,
                                   const int32_t* __restrict__ codedelay,
                                   const float* __restrict__ ca, double invFs, double invFc,
                                   double codelength, int64_t N, double2* __restrict__ out)
@@ -208,8 +210,8 @@ __global__ void fine_build_kernel(const int8_t* __restrict__ iq, int64_t S, int 
         if (k0 < Ls) {
             const double cvi = floor((invFs * (double)(k0 + 1)) / invFc);
             const float code = ca[(int64_t)s * 1023 + (int64_t)fmod(cvi, codelength)];
-            const char2 x = *reinterpret_cast<const char2*>(iq + 2 * (base + k0));
-            v = make_double2((double)x.x * code, (double)x.y * code);
+            const double2 x = src.at(base + k0);
+            v = make_double2(x.x * code, x.y * code);
         }
         o[k0] = v;
     }
@@ -232,11 +234,14 @@ __global__ void fine_argmax_part_kernel(const double2* __restrict__ F, int64_t N
     const int64_t half = N / 2;
     for (int64_t i = (int64_t)blk * blockDim.x + threadIdx.x; i < N;
          i += (int64_t)nblk * blockDim.x) {
-        int64_t j = shifted ? i + half : i;
+        int64_t j = shifted == 1 ? i + half : i;
         if (j >= N) j -= N;
         const double2 v = f[j];
         const double a = hypot(v.x, v.y);
-        if (a > m || (a == m && i < bi)) { m = a; bi = i; }
+        // shifted 2: real CarrSignal, exactly conjugate-symmetric in MATLAB -> the lower
+        // index of a mirror pair
+        const int64_t ii = (shifted == 2 && N - i < i) ? N - i : i;
+        if (a > m || (a == m && ii < bi)) { m = a; bi = ii; }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -274,12 +279,16 @@ constexpr int kFineBlocks = 512;
 
 }  // namespace
 
-hipError_t launch_acq_wipe(const int8_t* iq, int64_t S, int datalen, int nbins, double IF,
+hipError_t launch_acq_wipe(const int8_t* iq, const double2* xs, int64_t S, int datalen, int nbins, double IF,
                            double freqMin, double freqStep, double Fs, float2* out, hipStream_t s)
 {
     dim3 grid((unsigned)((S + 255) / 256), (unsigned)(datalen * nbins));
-    hipLaunchKernelGGL(acq_wipe_kernel, grid, dim3(256), 0, s, iq, S, datalen, nbins, IF, freqMin,
-                       freqStep, Fs, out);
+    if (xs)
+        hipLaunchKernelGGL(acq_wipe_kernel<SrcC64>, grid, dim3(256), 0, s, SrcC64{xs}, S, datalen, nbins, IF,
+                           freqMin, freqStep, Fs, out);
+    else
+        hipLaunchKernelGGL(acq_wipe_kernel<SrcIQ8>, grid, dim3(256), 0, s, SrcIQ8{iq}, S, datalen, nbins, IF,
+                           freqMin, freqStep, Fs, out);
     return hipGetLastError();
 }
 
@@ -319,13 +328,17 @@ hipError_t launch_acq_peak(const float* corr, int nprn, int nbins, int64_t S, in
     return hipGetLastError();
 }
 
-hipError_t launch_fine_build(const int8_t* iq, int64_t S, int L, const int32_t* codedelay,
+hipError_t launch_fine_build(const int8_t* iq, const double2* xs, int64_t S, int L, const int32_t* codedelay,
                              const float* ca, int nsv, double Fs, double codeFreqBasis,
                              double codelength, int64_t N, double2* out, hipStream_t s)
 {
     dim3 grid(4096, (unsigned)nsv);
-    hipLaunchKernelGGL(fine_build_kernel, grid, dim3(256), 0, s, iq, S, L, codedelay, ca, 1 / Fs,
-                       1 / codeFreqBasis, codelength, N, out);
+    if (xs)
+        hipLaunchKernelGGL(fine_build_kernel<SrcC64>, grid, dim3(256), 0, s, SrcC64{xs}, S, L, codedelay, ca,
+                           1 / Fs, 1 / codeFreqBasis, codelength, N, out);
+    else
+        hipLaunchKernelGGL(fine_build_kernel<SrcIQ8>, grid, dim3(256), 0, s, SrcIQ8{iq}, S, L, codedelay, ca,
+                           1 / Fs, 1 / codeFreqBasis, codelength, N, out);
     return hipGetLastError();
 }
 

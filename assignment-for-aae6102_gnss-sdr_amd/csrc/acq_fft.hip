@@ -262,9 +262,9 @@ __device__ __forceinline__ void load_row_tw(V* s_tw, const V* tw_row, int tid)
 // ---- F1: forward rows. Transform s < nsig: rawsignal(ms) .* carrier(bin) (acquisition.m:41-44,56);
 // s >= nsig: the code replica of PRN s - nsig (acquisition.m:49-51). Row n2 holds
 // x[P*n1 + n2]; output B[s][n2][k1] * w_S^(-n2*k1).
-template <int P>
+template <int P, class Src>
 __global__ __launch_bounds__(kRowThreads) void fwd_rows_kernel(
-    const int8_t* __restrict__ iq, int nbins, int nsig, double IF, double freqMin, double freqStep,
+    const Src src, int nbins, int nsig, double IF, double freqMin, double freqStep,
     double Fs, const float* __restrict__ ca, double code_step, const float2* __restrict__ tw_row,
     const float2* __restrict__ tw_col, float2* __restrict__ B)
 {
@@ -275,14 +275,13 @@ __global__ __launch_bounds__(kRowThreads) void fwd_rows_kernel(
     if (s < nsig) {
         const int idx = s / nbins, bin = s - idx * nbins;
         const double f = (IF + (freqMin + freqStep * (double)bin)) / Fs;  // cycles per sample
-        const int8_t* x = iq + 2 * (int64_t)idx * S;
         for (int n1 = tid; n1 < kRow; n1 += kRowThreads) {
             const int64_t n = (int64_t)P * n1 + n2;
             double cyc = f * (double)(n + 1);  // n is 1-based in the reference
             cyc -= floor(cyc);
             const float ph = (float)cyc;
             const float c = __builtin_amdgcn_cosf(ph), sn = __builtin_amdgcn_sinf(ph);
-            const char2 r = *reinterpret_cast<const char2*>(x + 2 * n);
+            const double2 r = src.at((int64_t)idx * S + n);
             const float xr = (float)r.x, xi = (float)r.y;
             s_a[n1] = make_float2(xr * c - xi * sn, xr * sn + xi * c);
         }
@@ -418,9 +417,9 @@ __global__ void fine_twiddle_kernel(double2* __restrict__ t, int64_t len)
     t[m] = make_double2(c, s);
 }
 
-template <int P>
+template <int P, class Src>
 __global__ __launch_bounds__(kRowThreads) void fine_rows_kernel(
-    const int8_t* __restrict__ iq, int64_t base, const float* __restrict__ ca, double invFs,
+    const Src src, int64_t base, const float* __restrict__ ca, double invFs,
     double invFc, double codelength, int D, int64_t N, const double2* __restrict__ tw_row,
     const double2* __restrict__ tabA, const double2* __restrict__ tabB, double2* __restrict__ E)
 {
@@ -434,8 +433,8 @@ __global__ __launch_bounds__(kRowThreads) void fine_rows_kernel(
         const int64_t n = (int64_t)P * T * m1 + (int64_t)P * m2 + n2;
         const double cvi = floor((invFs * (double)(n + 1)) / invFc);
         const double code = (double)ca[(int64_t)fmod(cvi, codelength)];
-        const char2 raw = *reinterpret_cast<const char2*>(iq + 2 * (base + n));
-        const double2 x = make_double2((double)raw.x * code, (double)raw.y * code);
+        const double2 raw = src.at(base + n);
+        const double2 x = make_double2(raw.x * code, raw.y * code);
         s_a[m1] = cmul(x, tabA[((int64_t)m1 * r) % RD]);
     }
     __syncthreads();
@@ -501,7 +500,10 @@ __global__ __launch_bounds__(kColThreads) void fine_cols_kernel(
             const int64_t q = k1 + (int64_t)T * kRow * k2;
             const int64_t k = (int64_t)D * q + r;  // natural bin of the N-point FFT
             int64_t i = k;
-            if (shifted) { i = k + half; if (i >= N) i -= N; }
+            if (shifted == 1) { i = k + half; if (i >= N) i -= N; }
+            // 2: real CarrSignal (dataType 1): MATLAB's fft is exactly conjugate-symmetric,
+            // a mirror pair ties and its first (lower) index wins
+            else if (shifted == 2 && N - k < k) i = N - k;
             best_merge(bm, bi, hypot(y.x, y.y), i);
         });
     }
@@ -546,8 +548,8 @@ bool acq_fft_supported(int64_t S) { return S == 13 * kRow || S == 29 * kRow; }
 
 // The forward spectra: X[s] for s < nsig ((ms, bin) signals, s = ms*nbins + bin) and the
 // code spectra C[p] (stored after them: X + nsig*S).
-hipError_t launch_acq_fft_forward(const int8_t* iq, int64_t S, int datalen, int nbins, double IF,
-                                  double freqMin, double freqStep, double Fs, const float* ca,
+hipError_t launch_acq_fft_forward(const int8_t* iq, const double2* xs, int64_t S, int datalen, int nbins,
+                                  double IF, double freqMin, double freqStep, double Fs, const float* ca,
                                   int nprn, double codeFreqBasis, const float2* tw_row,
                                   const float2* tw_col, float2* B, float2* X, hipStream_t s)
 {
@@ -555,8 +557,12 @@ hipError_t launch_acq_fft_forward(const int8_t* iq, int64_t S, int datalen, int 
     const double step = codeFreqBasis / Fs;
 #define GNSS_FWD(P_)                                                                            \
     if (S == (int64_t)P_ * kRow) {                                                              \
-        hipLaunchKernelGGL(fwd_rows_kernel<P_>, dim3(P_, ntr), dim3(kRowThreads), 0, s, iq, nbins, \
-                           nsig, IF, freqMin, freqStep, Fs, ca, step, tw_row, tw_col, B);       \
+        if (xs)                                                                                 \
+            hipLaunchKernelGGL((fwd_rows_kernel<P_, SrcC64>), dim3(P_, ntr), dim3(kRowThreads), 0, s, \
+                               SrcC64{xs}, nbins, nsig, IF, freqMin, freqStep, Fs, ca, step, tw_row, tw_col, B); \
+        else                                                                                    \
+            hipLaunchKernelGGL((fwd_rows_kernel<P_, SrcIQ8>), dim3(P_, ntr), dim3(kRowThreads), 0, s, \
+                               SrcIQ8{iq}, nbins, nsig, IF, freqMin, freqStep, Fs, ca, step, tw_row, tw_col, B); \
         hipLaunchKernelGGL(fwd_cols_kernel<P_>, dim3((kRow + kColThreads - 1) / kColThreads, ntr), \
                            dim3(kColThreads), 0, s, B, X);                                      \
         return hipGetLastError();                                                               \
@@ -617,7 +623,7 @@ hipError_t launch_fine_fft_tables(int64_t S, int L, int datalen, void* scratch, 
 }
 
 // First fftshift-ed argmax (1-based) of |fft(CarrSignal, N)| for one SV (acquisition.m:103-116).
-hipError_t launch_fine_fft_argmax(const int8_t* iq, int64_t S, int L, int datalen, int64_t base,
+hipError_t launch_fine_fft_argmax(const int8_t* iq, const double2* xs, int64_t S, int L, int datalen, int64_t base,
                                   const float* ca, double Fs, double codeFreqBasis,
                                   double codelength, int shifted, void* scratch, int64_t* kbest,
                                   hipStream_t s)
@@ -632,9 +638,14 @@ hipError_t launch_fine_fft_argmax(const int8_t* iq, int64_t S, int L, int datale
     const int nblk = kRow / kFineJC;
 #define GNSS_FINE(P_)                                                                           \
     if (S == (int64_t)P_ * kRow) {                                                              \
-        hipLaunchKernelGGL(fine_rows_kernel<P_>, dim3(P_ * kFineT, datalen), dim3(kRowThreads), 0, s, \
-                           iq, base, ca, 1 / Fs, 1 / codeFreqBasis, codelength, datalen, N,     \
-                           tw_row, tabA, tabB, E);                                              \
+        if (xs)                                                                                 \
+            hipLaunchKernelGGL((fine_rows_kernel<P_, SrcC64>), dim3(P_ * kFineT, datalen), dim3(kRowThreads), \
+                               0, s, SrcC64{xs}, base, ca, 1 / Fs, 1 / codeFreqBasis, codelength, datalen, N, \
+                               tw_row, tabA, tabB, E);                                          \
+        else                                                                                    \
+            hipLaunchKernelGGL((fine_rows_kernel<P_, SrcIQ8>), dim3(P_ * kFineT, datalen), dim3(kRowThreads), \
+                               0, s, SrcIQ8{iq}, base, ca, 1 / Fs, 1 / codeFreqBasis, codelength, datalen, N, \
+                               tw_row, tabA, tabB, E);                                          \
         hipLaunchKernelGGL(fine_cols_kernel<P_>, dim3(nblk, datalen), dim3(kColThreads), 0, s, E, \
                            datalen, N, shifted, tabM, part);                                    \
         hipLaunchKernelGGL(fine_best_final_kernel, dim3(1), dim3(256), 0, s, part, nblk * datalen, \

@@ -417,8 +417,15 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     if (diag) memset(diag, 0, sizeof(*diag));
     ctx->timing = gnss_timing{};
     HIP_TRY(hipSetDevice(ctx->device));
-    if (file->dataPrecision != 1 || file->dataType != 2)
-        return fail(ctx, GNSS_EARG, "only int8 I/Q records (dataPrecision 1, dataType 2) are supported");
+    const int prec = file->dataPrecision, dtyp = file->dataType;
+    if ((prec != 1 && prec != 2) || (dtyp != 1 && dtyp != 2))
+        return fail(ctx, GNSS_EARG, "dataPrecision must be 1 (int8) or 2 (int16), dataType 1 (I) or 2 (I/Q)");
+    // int16 values are de-interleaved into I/Q whatever dataType says (acquisition.m:28-32):
+    // with dataType 1 the block holds half the samples and rawsignal(..idx*Sample) fails
+    if (prec == 2 && dtyp == 1)
+        return fail(ctx, GNSS_EINDEX, "int16 real record: rawsignal has Sample*datalen/2 samples (MATLAB index error)");
+    const int64_t bps = (int64_t)prec * dtyp;  // file bytes per sample
+    const bool iq8 = prec == 1 && dtyp == 2;   // the kernels' native input
     const int64_t S = sg->Sample;
     const int nb = acq->freqNum, dl = acq->datalen, L = acq->L;
     if (S <= 0 || nb <= 0 || dl <= 0 || L <= 0) return fail(ctx, GNSS_EARG, "bad acquisition sizes");
@@ -431,13 +438,32 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     const int np = (int)prns.size();
 
     const int64_t off = file->skip * S * file->dataPrecision * file->dataType;  // :27
-    const int64_t need = S * file->dataType * std::max<int64_t>(dl, L + 1);
+    const int64_t need = S * bps * std::max<int64_t>(dl, L + 1);
     const int64_t flen = file_length(file);
-    if (flen < off + S * file->dataType * dl) return fail(ctx, GNSS_EIO, "IF record too short for acquisition");
+    if (flen < off + S * bps * dl) return fail(ctx, GNSS_EIO, "IF record too short for acquisition");
     IfWindow w;
     int st = stage_window(ctx, file, off, off + need, w);
     if (st) return st;
     const int8_t* blk = w.ptr + (off - w.base);
+    // other formats: the samples of each fread as fp64 complex (ifmt.hip): the 20-ms block
+    // (:28-37) and, with its own means, the (L+1)-ms fine block (:90-99)
+    DevBuf xs_acq, xs_fine, xs_sums;
+    Events e_conv;
+    if (!iq8) {
+        const int64_t nfine = flen >= off + S * bps * (L + 1) ? S * (L + 1) : 0;
+        HIP_TRY(xs_acq.alloc(ctx, "acq.xs", sizeof(double2) * (size_t)(S * dl)));
+        if (nfine) HIP_TRY(xs_fine.alloc(ctx, "acq.xs_fine", sizeof(double2) * (size_t)nfine));
+        HIP_TRY(xs_sums.alloc(ctx, "acq.xs_sums", 32));
+        HIP_TRY(hipEventRecord(e_conv.a, ctx->stream));
+        HIP_TRY(launch_stage_cpx(blk, prec, dtyp, S * dl, xs_acq.as<double2>(), xs_sums.as<unsigned long long>(),
+                                 ctx->stream));
+        if (nfine)
+            HIP_TRY(launch_stage_cpx(blk, prec, dtyp, nfine, xs_fine.as<double2>(),
+                                     xs_sums.as<unsigned long long>() + 2, ctx->stream));
+        HIP_TRY(hipEventRecord(e_conv.b, ctx->stream));
+    }
+    const double2* xa = iq8 ? nullptr : xs_acq.as<double2>();
+    const double2* xf = iq8 ? nullptr : xs_fine.as<double2>();
 
     std::vector<float> cah((size_t)np * 1023);
     for (int i = 0; i < np; i++) generate_ca(prns[i], &cah[(size_t)i * 1023]);
@@ -487,7 +513,7 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         HIP_TRY(A.alloc(ctx, "acq.A", sizeof(float2) * (size_t)batch * dl * S));
         HIP_TRY(hipStreamSynchronize(ctx->stream));
         HIP_TRY(hipEventRecord(e_all.a, ctx->stream));
-        HIP_TRY(launch_acq_fft_forward(blk, S, dl, nb, sg->IF, acq->freqMin, acq->freqStep, sg->Fs,
+        HIP_TRY(launch_acq_fft_forward(blk, xa, S, dl, nb, sg->IF, acq->freqMin, acq->freqStep, sg->Fs,
                                        ca.as<float>(), np, sg->codeFreqBasis, d_twr.as<float2>(),
                                        d_twc.as<float2>(), B.as<float2>(), X.as<float2>(), ctx->stream));
         const float2* C = X.as<float2>() + (size_t)nsig * S;
@@ -514,7 +540,7 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     }
 
     HIP_TRY(hipEventRecord(e_all.a, ctx->stream));
-    HIP_TRY(launch_acq_wipe(blk, S, dl, nb, sg->IF, acq->freqMin, acq->freqStep, sg->Fs, sig.as<float2>(), ctx->stream));
+    HIP_TRY(launch_acq_wipe(blk, xa, S, dl, nb, sg->IF, acq->freqMin, acq->freqStep, sg->Fs, sig.as<float2>(), ctx->stream));
     if ((st = run_fft(ctx, sig.p, S, nsig, 0, 0))) return st;
     HIP_TRY(launch_acq_code(ca.as<float>(), nullptr, np, S, sg->codeFreqBasis, sg->Fs, code.as<float2>(), ctx->stream));
     if ((st = run_fft(ctx, code.p, S, np, 0, 0))) return st;
@@ -562,7 +588,8 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     }
 
     // fine frequency (:89-126)
-    if (flen < off + S * file->dataType * (L + 1)) return fail(ctx, GNSS_EIO, "IF record too short for fine search");
+    if (flen < off + S * bps * (L + 1)) return fail(ctx, GNSS_EIO, "IF record too short for fine search");
+    const int fshift = dtyp == 2 ? 1 : 2;  // fftshift (:109) / real: first of a mirror pair
     const int na = out->n;
     const int64_t N = (int64_t)L * S * dl;  // :108
     if (N % 2) return fail(ctx, GNSS_EINDEX, "odd fftlength: MATLAB indexes past the end (:116)");
@@ -587,8 +614,8 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         HIP_TRY(launch_fine_fft_tables(S, L, dl, fx.p, ctx->stream));
         for (int k = 0; k < na; k++) {
             const int64_t base = S - cdh[k] - 1;  // 0-based sample of CarrSignal(1) (:105)
-            HIP_TRY(launch_fine_fft_argmax(blk, S, L, dl, base, fca.as<float>() + (size_t)k * 1023, sg->Fs,
-                                           sg->codeFreqBasis, sg->codelength, file->dataType == 2, fx.p,
+            HIP_TRY(launch_fine_fft_argmax(blk, xf, S, L, dl, base, fca.as<float>() + (size_t)k * 1023, sg->Fs,
+                                           sg->codeFreqBasis, sg->codelength, fshift, fx.p,
                                            kb.as<int64_t>() + k, ctx->stream));
         }
     } else {
@@ -596,12 +623,12 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         rocfft_plan pl;
         if ((st = get_plan(ctx, N, na, 1, 0, &pl))) return st;
         HIP_TRY(hipEventRecord(e_fine.a, ctx->stream));
-        HIP_TRY(launch_fine_build(blk, S, L, fcd.as<int32_t>(), fca.as<float>(), na, sg->Fs, sg->codeFreqBasis,
+        HIP_TRY(launch_fine_build(blk, xf, S, L, fcd.as<int32_t>(), fca.as<float>(), na, sg->Fs, sg->codeFreqBasis,
                                   sg->codelength, N, fx.as<double2>(), ctx->stream));
         if ((st = run_fft(ctx, fx.p, N, na, 1, 0))) return st;
         DevBuf fscr;
         HIP_TRY(fscr.alloc(ctx, "acq.fscr", acq_scratch_bytes(1, na)));
-        HIP_TRY(launch_fine_argmax(fx.as<double2>(), na, N, file->dataType == 2, fscr.p, kb.as<int64_t>(), ctx->stream));
+        HIP_TRY(launch_fine_argmax(fx.as<double2>(), na, N, fshift, fscr.p, kb.as<int64_t>(), ctx->stream));
     }
     HIP_TRY(hipEventRecord(e_fine.b, ctx->stream));
     HIP_TRY(hipEventRecord(e_all.b, ctx->stream));
@@ -618,7 +645,7 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         ctx->timing.acq_corr_ms = f;
     }
     ctx->timing.acq_fine_ms = e_fine.ms();
-    ctx->timing.acq_ms = e_all.ms();
+    ctx->timing.acq_ms = e_all.ms() + (iq8 ? 0.0 : e_conv.ms());
     return GNSS_OK;
 }
 
@@ -650,8 +677,19 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     if (!ctx || !file || !sg || !tr || !acq || !out) return GNSS_EARG;
     HIP_TRY(hipSetDevice(ctx->device));
     ctx->timing = gnss_timing{};
-    if (file->dataPrecision != 1 || file->dataType != 2)
-        return fail(ctx, GNSS_EARG, "only int8 I/Q records (dataPrecision 1, dataType 2) are supported");
+    const int prec = file->dataPrecision, dtyp = file->dataType;
+    if ((prec != 1 && prec != 2) || (dtyp != 1 && dtyp != 2))
+        return fail(ctx, GNSS_EARG, "dataPrecision must be 1 (int8) or 2 (int16), dataType 1 (I) or 2 (I/Q)");
+    if (prec == 2 && dtyp == 1) {
+        // fread(numSample, 'int16') de-interleaved as I/Q (trackingCT.m:84-88): an odd
+        // numSample gives I and Q halves of unequal length (MATLAB raises), an even one
+        // numSample/2 samples against numSample carrier values -> "Not enough raw data"
+        // (:108-112). Every channel's first step has remChip 0 and codeFreq = codeFreqBasis.
+        const double n0 = std::round((sg->codelength * 1 - 0.0) / (sg->codeFreqBasis / sg->Fs));
+        if (out->len) for (int c = 0; c < acq->n; c++) out->len[c] = 0;
+        if (std::fmod(n0, 2.0) != 0) return fail(ctx, GNSS_EINDEX, "int16 real record: odd numSample (MATLAB error)");
+        return fail(ctx, GNSS_ENODATA, "Not enough raw data");
+    }
     const int nsv = acq->n;
     if (nsv <= 0 || nsv > GNSS_MAX_SV) return fail(ctx, GNSS_EARG, "no channels");
     const int64_t S = sg->Sample;
@@ -703,6 +741,8 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     P.codelength = sg->codelength;
     P.S = (double)S;
     P.dataBytesPerSample = (double)(file->dataPrecision * file->dataType);
+    P.bps = prec * dtyp;
+    P.fmt = prec == 2 ? 1 : 0;  // int16 I/Q: staged as is with mean removal; int8 real: as I/Q
     P.inv_Fs = 1.0 / sg->Fs;
     P.exact_div = fast_div_exact(sg->Fs, (int64_t)(S * 10 * 1.02) + 64) ? 0 : 1;
     P.nsv = nsv;
@@ -724,10 +764,42 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     P.file_len = file_length(file);
     if (P.file_len < 0) return fail(ctx, GNSS_EIO, "cannot open IF record");
     IfWindow w;
+    lo &= ~(int64_t)31;  // whole 8-sample groups of any format
     int st = stage_window(ctx, file, lo, hi, w);
     if (st) return st;
+    const int8_t* iq_dev = w.ptr;
     P.buf_base = w.base;
     P.buf_len = w.len;
+    // formats (ifmt.hip): the correlator reads int8 I/Q pairs (fmt 0) or int16 I/Q pairs
+    // (fmt 1); staged byte of sample k = 2k / 4k
+    DevBuf d_conv, d_pref, d_pscr;
+    {
+        const int64_t s0 = std::max<int64_t>(lo, w.base);             // file bytes
+        const int64_t s1 = std::min<int64_t>(hi, w.base + w.len);
+        const int8_t* src = w.ptr + (s0 - w.base);
+        if (prec == 1 && dtyp == 1) {  // samples = bytes; staged as (x, 0) pairs
+            const int64_t n = std::max<int64_t>(s1 - s0, 0);
+            HIP_TRY(d_conv.alloc(ctx, "trk.d_conv", (size_t)(2 * n + 64)));
+            HIP_TRY(launch_real8_to_iq8(src, n, d_conv.as<int8_t>(), ctx->stream));
+            iq_dev = d_conv.as<int8_t>();
+            P.buf_base = 2 * s0;
+            P.buf_len = 2 * n;
+        } else if (prec == 2) {  // int16 I/Q: the file bytes, plus group prefix sums
+            iq_dev = src;
+            P.buf_base = s0;
+            P.buf_len = std::max<int64_t>(s1 - s0, 0);
+            const int64_t ng = P.buf_len / 32;
+            HIP_TRY(d_pref.alloc(ctx, "trk.d_pref", 2 * sizeof(long long) * (size_t)(ng + 1)));
+            const size_t scr = prefix16_scratch_bytes(ng);
+            HIP_TRY(d_pscr.alloc(ctx, "trk.d_pscr", scr));
+            long long* pi = d_pref.as<long long>();
+            HIP_TRY(launch_prefix16(reinterpret_cast<const short*>(src), ng, pi, pi + ng + 1, d_pscr.p, scr,
+                                    ctx->stream));
+            P.pref_i = pi;
+            P.pref_q = pi + ng + 1;
+            P.stage16 = reinterpret_cast<const short*>(iq_dev - P.buf_base);
+        }
+    }
 
     // geometry: SUB x 8 contiguous samples per lane, 256 lanes per block, bpc blocks per
     // channel; SUB grows with the step's total work (more per-lane amortisation once the
@@ -744,12 +816,13 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     auto sub_for = [&](int pdi) {
         int sub = pdi >= 10 ? 3 : 1;
         while (sub > 1 && !sub_ok(sub)) sub--;
+        if (P.fmt == 1 && sub != 3) sub = 1;  // (int16 kernels: 8- and 24-sample lanes)
         return sub;
     };
     int sub1 = sub_for(1), sub10 = sub_for(10);
     if (const char* fs = getenv("GNSS_FORCE_SUB")) {  // test hook: exercise every kernel variant
         const int v = atoi(fs);
-        if (v >= 1 && v <= 4 && sub_ok(v)) sub1 = sub10 = v;
+        if (v >= 1 && v <= 4 && sub_ok(v) && (P.fmt == 0 || v == 1 || v == 3)) sub1 = sub10 = v;
     }
     auto bpc_for = [&](int pdi, int sub) {
         const double groups = (S * pdi * 1.01 + 64) / 8.0 + 2;
@@ -763,7 +836,7 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     int cus = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
     auto persistent_ok = [&](int pdi, int sub) {
-        if (getenv("GNSS_NO_PERSIST") || bpc_for(pdi, sub) > kMaxBpcRun) return false;
+        if (getenv("GNSS_NO_PERSIST") || P.fmt != 0 || bpc_for(pdi, sub) > kMaxBpcRun) return false;
         const int occ = std::min(track_run_blocks_per_cu(P, sub), 4);
         return occ >= 1 && (int64_t)nch * bpc_for(pdi, sub) <= (int64_t)occ * cus;
     };
@@ -814,7 +887,7 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     HIP_TRY(hipMemsetAsync(d_rec.p, 0, d_rec.n, ctx->stream));
 
     TrkBuffers B{};
-    B.iq = w.ptr;
+    B.iq = iq_dev;
     B.chan = d_chan.as<TrkChan>();
     B.snap = d_snap.as<TrkChan>();
     B.desc = d_desc.as<StepDesc>();
@@ -1086,6 +1159,8 @@ int gnss_correlate_step(gnss_ctx* ctx, const gnss_file* file, const gnss_signal*
     P.codelength = sg->codelength;
     P.S = (double)S;
     P.dataBytesPerSample = 2;
+    P.bps = 2;  // int8 I/Q records only
+    P.fmt = 0;
     P.inv_Fs = 1.0 / sg->Fs;
     P.exact_div = fast_div_exact(sg->Fs, (int64_t)(S * 10 * 1.02) + 64) ? 0 : 1;
     P.ntaps = n_taps;

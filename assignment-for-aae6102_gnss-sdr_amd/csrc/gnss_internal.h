@@ -131,8 +131,8 @@ struct TrkParams {
     double dataBytesPerSample;  // dataPrecision*dataType
     double inv_Fs;            // RN(1/Fs)
     int32_t exact_div;        // 1: FMA-corrected k/Fs not verified for this Fs -> divide
-    int64_t buf_base;         // file byte held at dev_if[0]
-    int64_t buf_len;          // bytes resident
+    int64_t buf_base;         // staged byte held at iq[0] (staged byte of sample k = sbps*k)
+    int64_t buf_len;          // staged bytes resident
     int64_t file_len;         // bytes in the record (EOF)
     int32_t ntaps, iE, iP, iL;
     int32_t nsv;              // GLOBAL number of channels (quirk A.11)
@@ -140,6 +140,14 @@ struct TrkParams {
     int32_t rec_cap;          // compact record slots per channel
     int32_t cn0_cap;          // rows per channel per phase array
     int32_t probe;            // timing probe (GNSS_PROBE): 1 = skip the scalar loop update
+    // IF record format (initParameters.m:36-37): bps = file bytes per sample
+    // (dataPrecision*dataType); fmt = the staged layout the correlator reads:
+    // 0 = int8 I/Q pairs (int8 real records are staged with Q = 0), 1 = int16 I/Q pairs
+    // with the per-read mean removed (trackingCT.m:84-88) from prefix sums
+    int32_t bps, fmt;
+    const long long* pref_i;  // fmt 1: sum of I over the staged samples before group g
+    const long long* pref_q;  //   (8-sample groups from buf_base), Q likewise
+    const short* stage16;     // fmt 1: the staged int16 I/Q (absolute: stage16[2k] = I of k)
     double taps[GNSS_MAX_TAPS];
 };
 
@@ -151,6 +159,7 @@ constexpr int kLaneMax = 32;
 struct StepDesc {
     int64_t n, delayValue, A, g_first, g_last, Index;
     double remSample, d, inv_d, f, phi0, dhi, dlo, remChip_next, remPhase_next;
+    double mu_r, mu_i;  // fmt 1: mean of I / Q over the step's samples (else 0)
     // carrier rotation of lane sample m against the lane's first sample:
     // phi[m] = RN(m*dhi + m*dlo) ~ m * 2*pi*f/Fs, rcs[m] = (cos, sin)(phi[m])
     double phi[kLaneMax];
@@ -226,7 +235,7 @@ struct AcqPeak {           // per-PRN detector result
     double peak2;
 };
 
-hipError_t launch_acq_wipe(const int8_t* iq, int64_t S, int datalen, int nbins, double IF,
+hipError_t launch_acq_wipe(const int8_t* iq, const double2* xs, int64_t S, int datalen, int nbins, double IF,
                            double freqMin, double freqStep, double Fs, float2* out, hipStream_t s);
 hipError_t launch_acq_code(const float* ca, const int32_t* prn_slot, int nprn, int64_t S,
                            double codeFreqBasis, double Fs, float2* out, hipStream_t s);
@@ -239,7 +248,7 @@ hipError_t launch_acq_peak(const float* corr, int nprn, int nbins, int64_t S, in
 
 // Two-pass FFT correlator for S = P * 2000 (acq_fft.hip)
 bool acq_fft_supported(int64_t S);
-hipError_t launch_acq_fft_forward(const int8_t* iq, int64_t S, int datalen, int nbins, double IF,
+hipError_t launch_acq_fft_forward(const int8_t* iq, const double2* xs, int64_t S, int datalen, int nbins, double IF,
                                   double freqMin, double freqStep, double Fs, const float* ca,
                                   int nprn, double codeFreqBasis, const float2* tw_row,
                                   const float2* tw_col, float2* B, float2* X, hipStream_t s);
@@ -250,17 +259,45 @@ hipError_t launch_acq_fft_correlate(const float2* C, const float2* X, int64_t S,
 bool fine_fft_supported(int64_t S, int L);
 size_t fine_fft_scratch_bytes(int64_t S, int L, int datalen);
 hipError_t launch_fine_fft_tables(int64_t S, int L, int datalen, void* scratch, hipStream_t s);
-hipError_t launch_fine_fft_argmax(const int8_t* iq, int64_t S, int L, int datalen, int64_t base,
+hipError_t launch_fine_fft_argmax(const int8_t* iq, const double2* xs, int64_t S, int L, int datalen, int64_t base,
                                   const float* ca, double Fs, double codeFreqBasis,
                                   double codelength, int shifted, void* scratch, int64_t* kbest,
                                   hipStream_t s);
-hipError_t launch_fine_build(const int8_t* iq, int64_t S, int L, const int32_t* codedelay,
+hipError_t launch_fine_build(const int8_t* iq, const double2* xs, int64_t S, int L, const int32_t* codedelay,
                              const float* ca, int nsv, double Fs, double codeFreqBasis,
                              double codelength, int64_t N, double2* out, hipStream_t s);
 hipError_t launch_fine_argmax(const double2* F, int nsv, int64_t N, int shifted, void* scratch,
                               int64_t* kbest, hipStream_t s);
 
 size_t acq_scratch_bytes(int nprn, int nsv);
+
+// IF record formats (ifmt.hip)
+// one fread's samples as fp64 complex (prec 1 / type 1: (x, 0); prec 2 / type 2: I, Q
+// minus their means); sums = 2 words of device scratch
+hipError_t launch_stage_cpx(const int8_t* src, int prec, int type, int64_t nsamp, double2* out,
+                            unsigned long long* sums, hipStream_t s);
+// int8 real samples -> int8 I/Q pairs with Q = 0
+hipError_t launch_real8_to_iq8(const int8_t* src, int64_t n, int8_t* dst, hipStream_t s);
+// int16 I/Q: exclusive prefix sums of I and Q over ngroups 8-sample groups (ngroups + 1
+// entries each)
+size_t prefix16_scratch_bytes(int64_t ngroups);
+hipError_t launch_prefix16(const short* src, int64_t ngroups, long long* pref_i, long long* pref_q,
+                           void* scratch, size_t scratch_bytes, hipStream_t s);
+
+// The acquisition kernels' sample source: the record's int8 I/Q bytes, or an fp64
+// complex staging of another format (launch_stage_cpx).
+struct SrcIQ8 {
+    const int8_t* p;
+    __device__ __forceinline__ double2 at(int64_t n) const
+    {
+        const char2 r = *reinterpret_cast<const char2*>(p + 2 * n);
+        return make_double2((double)r.x, (double)r.y);
+    }
+};
+struct SrcC64 {
+    const double2* p;
+    __device__ __forceinline__ double2 at(int64_t n) const { return p[n]; }
+};
 
 // Synthetic IF (synth.hip)
 hipError_t launch_synth_if(const gnss_synth& cfg, const float* ca, uint64_t sample0,

@@ -219,11 +219,12 @@ __device__ __forceinline__ void prepare_desc_i(const TrkParams& p, const NcoStat
         return;
     }
     if (dbg && lane == 0) dbg[0] = wall_clock64();
-    const int64_t A = c.pos / 2;
+    const int64_t A = c.pos / p.bps;  // first sample of the fread (ftell / bytes per sample)
+    const int64_t sb = p.fmt ? 4 : 2;  // staged bytes per sample
     int bad = GNSS_OK;
     if (n <= 0 || n > (int64_t)(p.S * pdi * 1.01) + 64) bad = GNSS_EINDEX;
-    else if (2 * (A + n) > p.file_len) bad = phaseC ? GNSS_EIO : GNSS_ENODATA;  // :108-112 / :442
-    else if (2 * A < p.buf_base || 2 * (A + n) > p.buf_base + p.buf_len) bad = GNSS_EIO;
+    else if (p.bps * (A + n) > p.file_len) bad = phaseC ? GNSS_EIO : GNSS_ENODATA;  // :108-112 / :442
+    else if (sb * A < p.buf_base || sb * (A + n) > p.buf_base + p.buf_len) bad = GNSS_EIO;
     if (lane < p.ntaps) {
         // t = (0 + Spacing + remChip) : cps : ((numSample-1)*cps + Spacing + remChip) (:96-98)
         const double tap = taps ? taps[lane] : p.taps[lane];
@@ -247,6 +248,29 @@ __device__ __forceinline__ void prepare_desc_i(const TrkParams& p, const NcoStat
     const unsigned long long fails = __ballot(bad != GNSS_OK);
     const int badw = fails ? __builtin_amdgcn_readlane(bad, __ffsll((long long)fails) - 1) : GNSS_OK;
     if (lane == 0) {
+        double mr = 0.0, mi = 0.0;
+        if (p.fmt == 1 && badw == GNSS_OK) {
+            // rawsignal0DC = I - mean(I) + 1i*(Q - mean(Q)) over the n samples read
+            // (trackingCT.m:84-88 / :417-421): integer sums, exact, from the group prefix
+            // sums plus the samples of the partial group; mean = sum / n rounded once
+            const int64_t gb = p.buf_base / 32;  // first staged 8-sample group
+            auto pre = [&](int64_t k, long long& si, long long& sq) {
+                const int64_t g = k >> 3;
+                si = p.pref_i[g - gb];
+                sq = p.pref_q[g - gb];
+                for (int64_t j = 8 * g; j < k; j++) {
+                    si += p.stage16[2 * j];
+                    sq += p.stage16[2 * j + 1];
+                }
+            };
+            long long i0, q0, i1, q1;
+            pre(A, i0, q0);
+            pre(A + n, i1, q1);
+            mr = (double)(i1 - i0) / (double)n;
+            mi = (double)(q1 - q0) / (double)n;
+        }
+        d->mu_r = mr;
+        d->mu_i = mi;
         d->n = n;
         d->delayValue = z.dv;
         d->A = A;
@@ -384,7 +408,7 @@ __device__ __forceinline__ void write_record_i(const TrkParams& p, const TrkBuff
                              const int64_t* pre = nullptr)
 {
     const double P_i = s[2 * p.iP], P_q = s[2 * p.iP + 1];
-    const int64_t pos = c.pos + 2 * o.n;  // ftell after fread
+    const int64_t pos = c.pos + p.bps * o.n;  // ftell after fread
     const int64_t col = c.nstep;          // 0-based IndexSmall - 1
     int64_t* dvpre = b.dvpre + (int64_t)ch * (p.rec_cap + 1);
     const int64_t dvsum = (pre ? pre[0] : dvpre[col]) + o.delayValue;
@@ -482,7 +506,7 @@ __device__ __forceinline__ void write_state_i(const TrkParams& p, const TrkBuffe
     g->codeFreq = u.codeFreq;
     g->carrierFreq = u.carrierFreq;
     g->numSample = o.n;
-    g->pos = c.pos + 2 * o.n;
+    g->pos = c.pos + p.bps * o.n;
     g->Index = c.Index + (o.phaseC ? 10 : 1);
     g->nstep = c.nstep + 1;
     g->slot = c.slot + 1;
@@ -528,7 +552,7 @@ __device__ __forceinline__ void update_state_inplace(const TrkParams& p, const T
     c.codeFreq = u.codeFreq;
     c.carrierFreq = u.carrierFreq;
     c.numSample = o.n;
-    c.pos = pos + 2 * o.n;
+    c.pos = pos + p.bps * o.n;
     c.Index = Index + (o.phaseC ? 10 : 1);
     c.nstep = nstep + 1;
     c.slot = slot + 1;
@@ -572,7 +596,7 @@ struct LdsRaw {
     __device__ __forceinline__ int4 get(int j) const { return p[j * kTrkThreads]; }
 };
 
-template <int NT, int SUB, bool DIVIDE, bool RELOAD, class Desc, class Raw>
+template <int NT, int SUB, bool DIVIDE, bool RELOAD, int FMT, class Desc, class Raw>
 __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* dp, const Raw& raw,
                                                int64_t ks, unsigned cabits, double2* myslot,
                                                const double2* zero, double (&oI)[NT], double (&oQ)[NT])
@@ -631,27 +655,52 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
 #pragma unroll
     for (int s = 0; s < NT; s++) { pre_r[s] = 0.0; pre_i[s] = 0.0; }
 
+    // fmt 1: I - mean(I), Q - mean(Q) per sample, as the reference forms rawsignal0DC
+    double mu_r = 0.0, mu_i = 0.0;
+    if constexpr (FMT == 1) {
+        mu_r = uni(dp->mu_r);
+        mu_i = uni(dp->mu_i);
+    }
+
     // one 8-sample subgroup: running sums into the LDS slots, tap prefixes captured
     auto subgroup = [&](const int j) {
-        const int4 rj = raw.get(j);
-        unsigned wd[4] = {(unsigned)rj.x, (unsigned)rj.y, (unsigned)rj.z, (unsigned)rj.w};
-        if (lo > 8 * j || hi < 8 * j + 8) {
+        // fmt 0: 8 int8 I/Q pairs in one 16-B group; fmt 1: 8 int16 I/Q pairs in two
+        constexpr int NW = FMT == 1 ? 8 : 4;
+        unsigned wd[NW];
+        bool part = lo > 8 * j || hi < 8 * j + 8;
+        if constexpr (FMT == 1) {
+            const int4 ra = raw.get(2 * j), rb = raw.get(2 * j + 1);
+            wd[0] = (unsigned)ra.x; wd[1] = (unsigned)ra.y; wd[2] = (unsigned)ra.z; wd[3] = (unsigned)ra.w;
+            wd[4] = (unsigned)rb.x; wd[5] = (unsigned)rb.y; wd[6] = (unsigned)rb.z; wd[7] = (unsigned)rb.w;
+        } else {
+            const int4 rj = raw.get(j);
+            wd[0] = (unsigned)rj.x; wd[1] = (unsigned)rj.y; wd[2] = (unsigned)rj.z; wd[3] = (unsigned)rj.w;
+            if (part) {
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int m0 = 8 * j + 2 * q;
-                const unsigned k0 = (m0 >= lo && m0 < hi) ? 0x0000FFFFu : 0u;
-                const unsigned k1 = (m0 + 1 >= lo && m0 + 1 < hi) ? 0xFFFF0000u : 0u;
-                wd[q] &= k0 | k1;
+                for (int q = 0; q < 4; q++) {
+                    const int m0 = 8 * j + 2 * q;
+                    const unsigned k0 = (m0 >= lo && m0 < hi) ? 0x0000FFFFu : 0u;
+                    const unsigned k1 = (m0 + 1 >= lo && m0 + 1 < hi) ? 0xFFFF0000u : 0u;
+                    wd[q] &= k0 | k1;
+                }
             }
         }
         const double kbj = kb + (double)(8 * j);
 #pragma unroll
         for (int mm = 0; mm < 8; mm++) {
             const int m = 8 * j + mm;
-            const unsigned word = wd[mm >> 1];
-            const int sh = (mm & 1) * 16;
-            const double xr = (double)(int8_t)((word >> sh) & 0xFF);
-            const double xi = (double)(int8_t)((word >> (sh + 8)) & 0xFF);
+            double xr, xi;
+            if constexpr (FMT == 1) {
+                const unsigned word = wd[mm];
+                xr = (double)(short)(word & 0xFFFFu) - mu_r;
+                xi = (double)(short)(word >> 16) - mu_i;
+                if (part && !(m >= lo && m < hi)) { xr = 0.0; xi = 0.0; }
+            } else {
+                const unsigned word = wd[mm >> 1];
+                const int sh = (mm & 1) * 16;
+                xr = (double)(int8_t)((word >> sh) & 0xFF);
+                xi = (double)(int8_t)((word >> (sh + 8)) & 0xFF);
+            }
             double wr = xr, wi = xi;
             // m = 0: W = Wb, phi = 0, rcs = (1, 0) -> w = x exactly; skipped when known
             if (RELOAD || m > 0) {
@@ -786,7 +835,7 @@ __device__ __forceinline__ double channel_sum(int bpc, int tid, Load load)
 // VGPRs. Grid: nch x bpc blocks; block b of a channel owns the 256*SUB consecutive
 // 8-sample groups starting at g_first + 256*SUB*b.
 // ---------------------------------------------------------------------------
-template <int NT, int SUB, bool DIVIDE>
+template <int NT, int SUB, bool DIVIDE, int FMT = 0>
 __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(const TrkParams* __restrict__ pp,
                                                                 const TrkBuffers* __restrict__ bp, int bpc)
 {
@@ -818,11 +867,14 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(const TrkParams
     // issue the IF loads first (clamped so every lane loads something valid)
     const int8_t* iq = b.iq - p.buf_base;  // absolute-byte addressing
     const int bad = dp->bad;
-    int4 raw[SUB];
+    constexpr int GB = FMT == 1 ? 2 : 1;  // 16-B loads per 8-sample group
+    int4 raw[SUB * GB];
 #pragma unroll
     for (int j = 0; j < SUB; j++) {
         const int64_t gj = g0 + j <= g_last ? g0 + j : g_last;
-        raw[j] = bad ? make_int4(0, 0, 0, 0) : ld_g16(iq + 16 * gj);
+#pragma unroll
+        for (int h = 0; h < GB; h++)
+            raw[GB * j + h] = bad ? make_int4(0, 0, 0, 0) : ld_g16(iq + 16 * GB * gj + 16 * h);
     }
     const unsigned cabits = lane < 32 ? ((g_cu32*)b.ca_bits)[ch * 32 + lane] : 0u;
     // the channel state, for whichever block arrives last
@@ -843,7 +895,7 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(const TrkParams
     } else {
         if (tid == 0) s_zero = make_double2(0.0, 0.0);
         __syncthreads();
-        lane_correlate<NT, SUB, DIVIDE, false>(p, dp, RegRaw<SUB>{raw}, 8 * g0 - dp->A, cabits,
+        lane_correlate<NT, SUB, DIVIDE, false, FMT>(p, dp, RegRaw<SUB * GB>{raw}, 8 * g0 - dp->A, cabits,
                                         reinterpret_cast<double2*>(s_mem) + tid, &s_zero, oI, oQ);
     }
 
@@ -929,7 +981,7 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(const TrkParams
     nx.codeFreq = u.codeFreq;
     nx.carrierFreq = u.carrierFreq;
     nx.numSample = o.n;
-    nx.pos = s_c.pos + 2 * o.n;
+    nx.pos = s_c.pos + p.bps * o.n;
     nx.Index = s_c.Index + (o.phaseC ? 10 : 1);
     if (wv == 0 || wv == 3) {
         if (p.probe & 8) return;
@@ -1241,7 +1293,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(3, 
             const int64_t g0 = uni(D.g_first) + ((int64_t)blk * T + tid) * SUB;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's global_load_lds landed
             double oI[NT], oQ[NT];
-            lane_correlate<NT, SUB, DIVIDE, true>(p, &D, LdsRaw{s_raw + tid}, 8 * g0 - A, cabits,
+            lane_correlate<NT, SUB, DIVIDE, true, 0>(p, &D, LdsRaw{s_raw + tid}, 8 * g0 - A, cabits,
                                                   reinterpret_cast<double2*>(s_mem) + tid, &s_zero, oI, oQ);
             __syncthreads();  // slots and s_raw free
             __builtin_amdgcn_s_setprio(3);
@@ -1315,7 +1367,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(3, 
         nx.codeFreq = u.codeFreq;
         nx.carrierFreq = u.carrierFreq;
         nx.numSample = o.n;
-        nx.pos = c.pos + 2 * o.n;
+        nx.pos = c.pos + p.bps * o.n;
         nx.Index = c.Index + (o.phaseC ? 10 : 1);
         if (wv == 0 || wv == 3) {  // the code half / the carrier table of the next descriptor
             prepare_desc_i(p, nx, o.pdi, o.phaseC, wv == 0 ? 0 : 1, lane, &s_d[cur ^ 1], s_taps,
@@ -1462,14 +1514,17 @@ hipError_t launch_track_step(const TrkParams& p, const TrkBuffers& b, const TrkD
                              hipStream_t s)
 {
     dim3 grid(p.nch * bpc), block(kTrkThreads);
-#define GNSS_STEP(NT_, SUB_, DIV_)                                                             \
-    if (p.ntaps == NT_ && sub == SUB_ && (p.exact_div != 0) == DIV_) {                         \
-        hipLaunchKernelGGL((track_step_kernel<NT_, SUB_, DIV_>), grid, block, 0, s, d.p, d.b, bpc); \
+#define GNSS_STEP(NT_, SUB_, DIV_, FMT_)                                                       \
+    if (p.ntaps == NT_ && sub == SUB_ && (p.exact_div != 0) == DIV_ && p.fmt == FMT_) {        \
+        hipLaunchKernelGGL((track_step_kernel<NT_, SUB_, DIV_, FMT_>), grid, block, 0, s, d.p, d.b, bpc); \
         return hipGetLastError();                                                              \
     }
-    GNSS_STEP(3, 1, false) GNSS_STEP(3, 2, false) GNSS_STEP(3, 3, false) GNSS_STEP(3, 4, false)
-    GNSS_STEP(11, 1, false) GNSS_STEP(11, 2, false) GNSS_STEP(11, 3, false) GNSS_STEP(11, 4, false)
-    GNSS_STEP(3, 1, true) GNSS_STEP(11, 1, true)
+    GNSS_STEP(3, 1, false, 0) GNSS_STEP(3, 2, false, 0) GNSS_STEP(3, 3, false, 0) GNSS_STEP(3, 4, false, 0)
+    GNSS_STEP(11, 1, false, 0) GNSS_STEP(11, 2, false, 0) GNSS_STEP(11, 3, false, 0) GNSS_STEP(11, 4, false, 0)
+    GNSS_STEP(3, 1, true, 0) GNSS_STEP(11, 1, true, 0)
+    // int16 I/Q records (per-read mean removal): the per-step path only
+    GNSS_STEP(3, 1, false, 1) GNSS_STEP(3, 3, false, 1) GNSS_STEP(11, 1, false, 1) GNSS_STEP(11, 3, false, 1)
+    GNSS_STEP(3, 1, true, 1) GNSS_STEP(11, 1, true, 1)
 #undef GNSS_STEP
     return hipErrorInvalidValue;
 }
