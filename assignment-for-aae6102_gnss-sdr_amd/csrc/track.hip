@@ -117,6 +117,17 @@ __device__ __forceinline__ double wave_at(double kd, double f, double phi0, doub
     return y + phi0;
 }
 
+// sin/cos of a carrier phase Wave (up to ~3e5 rad): reduced by 2*pi as a double-double
+// first (W - k*kTwoPi is exact: both are multiples of 2^-50 below 8 in magnitude), so the
+// library's small-argument path runs instead of its Payne-Hanek reduction.
+__device__ __forceinline__ void sincos_wave(double W, double* sn, double* cs)
+{
+    const double k = rint(W * (1.0 / kTwoPi));
+    double r = __builtin_fma(-k, kTwoPi, W);
+    r = __builtin_fma(-k, kTwoPiLo, r);
+    sincos(r, sn, cs);
+}
+
 // The NCO state a step is prepared from.
 struct NcoState {
     double remChip, remPhase, codeFreq, carrierFreq;
@@ -648,7 +659,7 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
     const double kb = (double)ks;
     const double Wb = wave_at<DIVIDE>(kb, f, phi0, Fs, rFs);
     double sb, cb;
-    sincos(Wb, &sb, &cb);
+    sincos_wave(Wb, &sb, &cb);
 
     double run_r = 0.0, run_i = 0.0;
     double pre_r[NT], pre_i[NT];
@@ -732,7 +743,7 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
 #pragma unroll 1
         for (int j = 0; j < SUB; j++) subgroup(j);
     } else if constexpr (RELOAD) {
-#pragma unroll 2
+#pragma unroll
         for (int j = 0; j < SUB; j++) subgroup(j);
     } else {
 #pragma unroll
