@@ -1,5 +1,5 @@
 """MI355X-native GPS L1 C/A acquisition + conventional tracking (drop-in for
-acquisition.m / trackingCT.m of KangWelly/Assignment-for-AAE6102_GNSS-SDR).
+acquisition.m / trackingCT.m (and the tracking loop of trackingCT_POS_updated.m) of KangWelly/Assignment-for-AAE6102_GNSS-SDR).
 
 The compute path is the HIP C-ABI library lib/libgnss_mi355x.so (hand-written
 gfx950 kernels + rocFFT); this package is the host-side mirror of the
@@ -9,7 +9,7 @@ directory name is not a Python identifier).
 """
 from . import abi, synth
 from .sdr import (Context, DeviceRecord, StructArray, TrackOutBuffers, acquisition, ca_code,
-                  default_context, initParameters, trackingCT)
+                  default_context, initParameters, trackingCT, trackingCT_POS)
 
 __all__ = ["abi", "synth", "Context", "DeviceRecord", "StructArray", "TrackOutBuffers",
-           "acquisition", "ca_code", "default_context", "initParameters", "trackingCT"]
+           "acquisition", "ca_code", "default_context", "initParameters", "trackingCT", "trackingCT_POS"]

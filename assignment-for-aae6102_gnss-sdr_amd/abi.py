@@ -20,6 +20,10 @@ FIELDS = ["P_i", "P_q", "E_i", "E_q", "L_i", "L_q", "PLLdiscri", "DLLdiscri", "c
           "remChip", "codeFreq", "carrierFreq", "remPhase", "remSample", "numSample",
           "delayValue", "absoluteSample", "codedelay2"]
 NFIELDS = len(FIELDS)
+# the same slots under trackingCT_POS_updated.m:273-292's names (gnss_tracking_ct_pos)
+FIELDS_POS = ["P_i", "P_q", "E_i", "E_q", "L_i", "L_q", "carrError", "codeError", "codedelay",
+              "remChip", "codeFreq", "carrFreq", "remCarrPhase", "absoluteSampleCodedelay",
+              "numSample", "delayValue", "absoluteSample", "codedelay2"]
 
 
 class GnssFile(C.Structure):
@@ -106,6 +110,9 @@ PROTOTYPES = {
     "gnss_tracking_ct": (C.c_int, [C.c_void_p, C.POINTER(GnssFile), C.POINTER(GnssSignal),
                                    C.POINTER(GnssTrack), C.POINTER(GnssAcquired),
                                    C.POINTER(GnssTrackOut)]),
+    "gnss_tracking_ct_pos": (C.c_int, [C.c_void_p, C.POINTER(GnssFile), C.POINTER(GnssSignal),
+                                       C.POINTER(GnssTrack), C.POINTER(GnssAcquired), C.c_int32,
+                                       C.POINTER(C.c_int32), C.POINTER(GnssTrackOut)]),
     "gnss_ca_code": (C.c_int, [C.c_int, C.c_void_p]),
     "gnss_correlate_step": (C.c_int, [C.c_void_p, C.POINTER(GnssFile), C.POINTER(GnssSignal),
                                       C.c_int, C.c_int, C.c_double, C.c_double, C.c_double,

@@ -667,8 +667,15 @@ struct StepGraph {
 
 }  // namespace
 
-int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg, const gnss_track* tr,
-                     const gnss_acquired* acq, gnss_track_out* out)
+// The sibling loop of trackingCT_POS_updated.m (its tracking half): steps and countinx.
+struct PosCfg {
+    int32_t ctPOS;            // track.ctPOS (datalength, trackingCT_POS_updated.m:50)
+    const int32_t* countinx;  // countinx(svIndex) of countinx.mat (:29), by channel position
+};
+
+// trackingCT.m (pos == nullptr) or the tracking loop of trackingCT_POS_updated.m
+static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg, const gnss_track* tr,
+                         const gnss_acquired* acq, gnss_track_out* out, const PosCfg* pos)
 {
     // GNSS_HOSTPROF: host-side phases of this call on stderr
     const bool hp = getenv("GNSS_HOSTPROF") != nullptr;
@@ -680,6 +687,12 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     const int prec = file->dataPrecision, dtyp = file->dataType;
     if ((prec != 1 && prec != 2) || (dtyp != 1 && dtyp != 2))
         return fail(ctx, GNSS_EARG, "dataPrecision must be 1 (int8) or 2 (int16), dataType 1 (I) or 2 (I/Q)");
+    if (pos && prec != 1)
+        // trackingCT_POS_updated.m:196,207 reads numSample*dataType int16 values but advances
+        // file_ptr by numSample*dataType BYTES: overlapping, misaligned reads (not reproduced)
+        return fail(ctx, GNSS_EARG, "trackingCT_POS_updated: int8 records only");
+    if (pos && (pos->ctPOS <= 0 || !pos->countinx || tr->n_taps != 0))
+        return fail(ctx, GNSS_EARG, "trackingCT_POS_updated: ctPOS > 0, countinx and E/P/L taps required");
     if (prec == 2 && dtyp == 1) {
         // fread(numSample, 'int16') de-interleaved as I/Q (trackingCT.m:84-88): an odd
         // numSample gives I and Q halves of unequal length (MATLAB raises), an even one
@@ -694,9 +707,16 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     if (nsv <= 0 || nsv > GNSS_MAX_SV) return fail(ctx, GNSS_EARG, "no channels");
     const int64_t S = sg->Sample;
     const int N1 = tr->msToProcessCT_1ms;
-    const int n10 = tr->msToProcessCT_10ms / 10;
-    if (N1 < 24) return fail(ctx, GNSS_EARG, "msToProcessCT_1ms must be >= 24 (bit-edge search window)");
-    if (out->max_len < (int64_t)N1 + 19 + (int64_t)tr->msToProcessCT_10ms) return fail(ctx, GNSS_EARG, "max_len too small");
+    const int n10 = pos ? 0 : tr->msToProcessCT_10ms / 10;
+    if (!pos && N1 < 24) return fail(ctx, GNSS_EARG, "msToProcessCT_1ms must be >= 24 (bit-edge search window)");
+    if (N1 < 0) return fail(ctx, GNSS_EARG, "msToProcessCT_1ms < 0");
+    if (out->max_len < (pos ? (int64_t)pos->ctPOS : (int64_t)N1 + 19 + (int64_t)tr->msToProcessCT_10ms))
+        return fail(ctx, GNSS_EARG, "max_len too small");
+    // trackingCT_POS_updated.m: per channel, steps 1..n1 at 1 ms (msIndex <= 1000 +
+    // countinx(svIndex), :183), then 10 ms up to ctPOS steps (:294)
+    auto pos_n1 = [&](int c) -> int64_t {
+        return std::max<int64_t>(0, std::min<int64_t>(pos->ctPOS, (int64_t)N1 + pos->countinx[c]));
+    };
     if (8.0 * (sg->codeFreqBasis * 1.01) / sg->Fs >= 1.0)
         return fail(ctx, GNSS_EARG, "Fs too low for the 8-sample lane groups (need Fs > 8.2 MHz)");
 
@@ -705,7 +725,15 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     double taps3[3] = {-tr->CorrelatorSpacing, 0, tr->CorrelatorSpacing};
     const double* taps = taps3;
     int ntaps = 3;
-    if (tr->n_taps > 0) {
+    // trackingCT_POS_updated.m:42,210-217: Spacing = 0.6:-0.05:-0.6 (colon values 0.5, 0,
+    // -0.5 exactly at 3, 13, 23); Early at Spacing(3) = +0.5, Late at Spacing(23) = -0.5,
+    // Prompt Code(ceil(t + 0.05) + 1)
+    const double taps_pos[3] = {0.5, 0.0, -0.5};
+    if (pos) {
+        taps = taps_pos;
+        P.conv = 1;
+        P.tap_post[1] = 0.05;
+    } else if (tr->n_taps > 0) {
         if (!tr->tap_offsets) return fail(ctx, GNSS_EARG, "tap_offsets missing");
         ntaps = tr->n_taps;
         taps = tr->tap_offsets;
@@ -714,10 +742,12 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     P.iE = P.iP = P.iL = -1;
     for (int s = 0; s < ntaps; s++) {
         P.taps[s] = taps[s];
+        if (pos) continue;
         if (taps[s] == -tr->CorrelatorSpacing && P.iE < 0) P.iE = s;
         if (taps[s] == 0 && P.iP < 0) P.iP = s;
         if (taps[s] == tr->CorrelatorSpacing && P.iL < 0) P.iL = s;
     }
+    if (pos) { P.iE = 0; P.iP = 1; P.iL = 2; }
     if (P.iE < 0 || P.iP < 0 || P.iL < 0) return fail(ctx, GNSS_EARG, "taps must contain -spacing, 0, +spacing");
     P.ntaps = ntaps;
 
@@ -745,10 +775,10 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     P.fmt = prec == 2 ? 1 : 0;  // int16 I/Q: staged as is with mean removal; int8 real: as I/Q
     P.inv_Fs = 1.0 / sg->Fs;
     P.exact_div = fast_div_exact(sg->Fs, (int64_t)(S * 10 * 1.02) + 64) ? 0 : 1;
-    P.nsv = nsv;
+    P.nsv = pos ? 1 : nsv;  // (POS: codedelay sums the channel's own row)
     P.nch = nch;
-    P.rec_cap = N1 + 19 + n10;
-    P.cn0_cap = std::max(N1 + 19, n10) / 20 + 1;
+    P.rec_cap = pos ? pos->ctPOS : N1 + 19 + n10;
+    P.cn0_cap = pos ? pos->ctPOS / 20 + 1 : std::max(N1 + 19, n10) / 20 + 1;
 
     // IF window resident in HBM: from the earliest channel start to the latest
     // possible phase-C end (countinx <= 18, numSample within 1%)
@@ -757,6 +787,12 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     for (int c : chans) {
         const int64_t cd = acq->codedelay[c];
         lo = std::min(lo, (S - cd + 1 + file->skip * S) * bps);
+        if (pos) {  // one continuous read: n1 1-ms steps, then 10-ms steps (no re-seek)
+            const int64_t n1 = pos_n1(c);
+            const double ns = (double)n1 * S + (double)(pos->ctPOS - n1) * 10.0 * S;
+            hi = std::max(hi, (S - cd + 1 + file->skip * S) * bps + (int64_t)(ns * 1.01 + 4096) * bps);
+            continue;
+        }
         const int64_t c0 = (S - cd + 1 + (file->skip + N1 + 18) * S) * bps;
         const int64_t a1 = (S - cd + 1 + file->skip * S) * bps + (int64_t)((N1 + 18) * S * 1.01 + 64) * bps;
         hi = std::max(hi, std::max(c0 + (int64_t)(n10 * 10 * S * 1.01 + 4096) * bps, a1));
@@ -861,6 +897,13 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         t.sv1 = c + 1;
         t.prn = acq->sv[c];
         t.n1_target = N1;
+        if (pos) {  // trackingCT_POS_updated.m:108-110,290 (file_ptr; codedelay base S - cd + 1)
+            t.pos = (int64_t)(((double)S - acq->codedelay[c] + 1 + (double)file->skip * sg->Fs * sg->ms) * bps);
+            t.codedelay0 = S - acq->codedelay[c] + 1;
+            t.sv1 = 1;
+            t.n1_target = pos_n1(c);
+            t.countinx = pos->countinx[c];
+        }
         if (acq->sv[c] < 1 || acq->sv[c] > 51) return fail(ctx, GNSS_EARG, "bad PRN");
         ca_bits(acq->sv[c], &cab[(size_t)i * 32]);
     }
@@ -1020,26 +1063,43 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     Events e_all;
     if (hp) { HIP_TRY(hipStreamSynchronize(ctx->stream)); fprintf(stderr, "hostprof setup %.3f ms\n", hms()); }
     HIP_TRY(hipEventRecord(e_all.a, ctx->stream));
-    // phase A: steps 1..N1-1, snapshot (for countinx = -1), step N1, bit-edge search
-    HIP_TRY(launch_track_prepare(P, B, TD, 1, 0, ctx->stream));
-    if ((st = run_steps(1, N1 - 1))) return st;
-    HIP_TRY(launch_track_snapshot(P, B, TD, ctx->stream));
-    if ((st = run_steps(1, 1))) return st;
-    HIP_TRY(launch_track_bitedge(P, B, TD, ctx->stream));
     std::vector<TrkChan> chh((size_t)nch);
-    HIP_TRY(hipMemcpyAsync(chh.data(), d_chan.p, sizeof(TrkChan) * nch, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-    int cxmax = 0;
-    for (auto& t : chh) cxmax = std::max(cxmax, t.countinx);
-    if (hp)
-        for (auto& t : chh)
-            fprintf(stderr, "hostprof bitedge prn %d status %d countinx %d n1_target %lld\n", t.prn, t.status,
-                    t.countinx, (long long)t.n1_target);
-    // phase B continues phase A up to 1000 + countinx (inactive channels skip)
-    if ((st = run_steps(1, cxmax))) return st;
-    HIP_TRY(launch_track_phase_c_init(P, B, TD, file->skip, ctx->stream));
-    // phase C
-    if ((st = run_steps(10, n10))) return st;
+    if (pos) {
+        // trackingCT_POS_updated.m:179-413: every channel continues from its own state and
+        // file pointer; 1-ms steps while msIndex <= 1000 + countinx(svIndex), then 10 ms
+        int64_t n1max = 0, n1min = INT64_MAX;
+        for (int c : chans) { n1max = std::max(n1max, pos_n1(c)); n1min = std::min(n1min, pos_n1(c)); }
+        HIP_TRY(launch_track_prepare(P, B, TD, 1, 0, ctx->stream));
+        if ((st = run_steps(1, (int)n1max))) return st;
+        if (n1min < pos->ctPOS) {
+            HIP_TRY(hipMemcpyAsync(chh.data(), d_chan.p, sizeof(TrkChan) * nch, hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(hipStreamSynchronize(ctx->stream));
+            for (auto& t : chh) t.n1_target = pos->ctPOS;  // (Index + 1 per step: the last step)
+            HIP_TRY(hipMemcpyAsync(d_chan.p, chh.data(), sizeof(TrkChan) * nch, hipMemcpyHostToDevice, ctx->stream));
+            HIP_TRY(launch_track_prepare(P, B, TD, 10, 0, ctx->stream));
+            if ((st = run_steps(10, (int)(pos->ctPOS - n1min)))) return st;
+        }
+    } else {
+        // phase A: steps 1..N1-1, snapshot (for countinx = -1), step N1, bit-edge search
+        HIP_TRY(launch_track_prepare(P, B, TD, 1, 0, ctx->stream));
+        if ((st = run_steps(1, N1 - 1))) return st;
+        HIP_TRY(launch_track_snapshot(P, B, TD, ctx->stream));
+        if ((st = run_steps(1, 1))) return st;
+        HIP_TRY(launch_track_bitedge(P, B, TD, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(chh.data(), d_chan.p, sizeof(TrkChan) * nch, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        int cxmax = 0;
+        for (auto& t : chh) cxmax = std::max(cxmax, t.countinx);
+        if (hp)
+            for (auto& t : chh)
+                fprintf(stderr, "hostprof bitedge prn %d status %d countinx %d n1_target %lld\n", t.prn, t.status,
+                        t.countinx, (long long)t.n1_target);
+        // phase B continues phase A up to 1000 + countinx (inactive channels skip)
+        if ((st = run_steps(1, cxmax))) return st;
+        HIP_TRY(launch_track_phase_c_init(P, B, TD, file->skip, ctx->stream));
+        // phase C
+        if ((st = run_steps(10, n10))) return st;
+    }
     HIP_TRY(hipEventRecord(e_all.b, ctx->stream));
     HIP_TRY(hipEventSynchronize(e_all.b));
     ctx->timing.track_ms = e_all.ms();
@@ -1087,12 +1147,14 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     }
 
     const int64_t ML = out->max_len;
-    int rows = N1 / 20;
+    int rows = pos ? pos->ctPOS / 20 : N1 / 20;
+    // series length before the 10-ms values (POS: every step has its own row)
+    auto n1_of = [&](int i) -> int64_t { return pos ? (int64_t)pos->ctPOS : (int64_t)N1 + chh[i].countinx; };
     for (int i = 0; i < nch; i++) {
         const int c = chans[i];
         const TrkChan& t = chh[i];
         const int cx = t.countinx;
-        const int64_t n1 = N1 + cx;
+        const int64_t n1 = n1_of(i);
         if (out->len) out->len[c] = n1 + 10LL * n10;
         if (out->countinx) out->countinx[c] = cx;
         rows = std::max(rows, (int)(n1 / 20));
@@ -1102,7 +1164,7 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     parallel_for(nch * (nrf + ntf), [&](int task) {
         const int i = task / (nrf + ntf), f = task % (nrf + ntf);
         const int c = chans[i];
-        const int64_t n1 = N1 + chh[i].countinx;
+        const int64_t n1 = n1_of(i);
         double* dst;
         const double* src;
         int64_t stride;
@@ -1125,12 +1187,12 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     });
     if (hp) fprintf(stderr, "hostprof expanded %.3f ms\n", hms());
     rows = std::max(rows, n10 / 20);
-    out->cn0_rows = rows;
+    out->cn0_rows = rows;  // (POS: CN0_CT, one row per 20 steps of either pdi)
     if (out->CN0_Eph) {
         for (int i = 0; i < nch; i++) {
             const int c = chans[i];
             const int cx = chh[i].countinx;
-            const int r1 = std::max(N1, N1 + cx) / 20, r10 = n10 / 20;
+            const int r1 = pos ? rows : std::max(N1, N1 + cx) / 20, r10 = n10 / 20;
             for (int r = 0; r < out->cn0_cap; r++) {
                 double v = 0;
                 if (r < r10) v = cn10[(size_t)i * P.cn0_cap + r];
@@ -1140,6 +1202,19 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         }
     }
     return GNSS_OK;
+}
+
+int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg, const gnss_track* tr,
+                     const gnss_acquired* acq, gnss_track_out* out)
+{
+    return tracking_impl(ctx, file, sg, tr, acq, out, nullptr);
+}
+
+int gnss_tracking_ct_pos(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg, const gnss_track* tr,
+                         const gnss_acquired* acq, int32_t ctPOS, const int32_t* countinx, gnss_track_out* out)
+{
+    const PosCfg pc{ctPOS, countinx};
+    return tracking_impl(ctx, file, sg, tr, acq, out, &pc);
 }
 
 int gnss_correlate_step(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg, int prn, int pdi,

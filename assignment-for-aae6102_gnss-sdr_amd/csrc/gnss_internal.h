@@ -149,6 +149,13 @@ struct TrkParams {
     const long long* pref_q;  //   (8-sample groups from buf_base), Q likewise
     const short* stage16;     // fmt 1: the staged int16 I/Q (absolute: stage16[2k] = I of k)
     double taps[GNSS_MAX_TAPS];
+    // Loop conventions: 0 = trackingCT.m; 1 = trackingCT_POS_updated.m:179-408 (numSample
+    // by ceil, prompt replica Code(ceil(t + 0.05) + 1), codeFreq = f0 + codeNco, loop T =
+    // signal.ms for every pdi, Index + 1 per step, no phase-C negation or re-seek,
+    // codedelay from the channel's own delayValue row)
+    int32_t conv;
+    // added to a tap's colon element before ceil (the +0.05 of trackingCT_POS_updated.m:216)
+    double tap_post[GNSS_MAX_TAPS];
 };
 
 // Samples per lane of the step kernel: 8 * SUB, SUB <= 4.

@@ -165,6 +165,12 @@ __device__ __forceinline__ StepSize step_size(const TrkParams& p, const NcoState
 {
     StepSize z;
     z.cps = c.codeFreq / p.Fs;
+    if (p.conv) {  // trackingCT_POS_updated.m:188-191 / :304-307 (ceil; no remSample)
+        z.remSample = 0.0;
+        z.n = (int64_t)ceil((p.codelength * pdi - c.remChip) / z.cps);
+        z.dv = z.n - (int64_t)(p.S * pdi);
+        return z;
+    }
     if (phaseC) {
         z.dv = c.numSample - (int64_t)(p.S * pdi);                      // :411
         z.remSample = (p.codelength * pdi - c.remChip) / z.cps;          // :414
@@ -234,7 +240,7 @@ __device__ __forceinline__ void prepare_desc_i(const TrkParams& p, const NcoStat
     const int64_t sb = p.fmt ? 4 : 2;  // staged bytes per sample
     int bad = GNSS_OK;
     if (n <= 0 || n > (int64_t)(p.S * pdi * 1.01) + 64) bad = GNSS_EINDEX;
-    else if (p.bps * (A + n) > p.file_len) bad = phaseC ? GNSS_EIO : GNSS_ENODATA;  // :108-112 / :442
+    else if (p.bps * (A + n) > p.file_len) bad = (phaseC || p.conv) ? GNSS_EIO : GNSS_ENODATA;  // :108-112 / :442
     else if (sb * A < p.buf_base || sb * (A + n) > p.buf_base + p.buf_len) bad = GNSS_EIO;
     if (lane < p.ntaps) {
         // t = (0 + Spacing + remChip) : cps : ((numSample-1)*cps + Spacing + remChip) (:96-98)
@@ -244,13 +250,15 @@ __device__ __forceinline__ void prepare_desc_i(const TrkParams& p, const NcoStat
         const Colon col = colon_make_hint(a, cps, bb, n - 1);
         d->tap_a[lane] = col.a;
         d->tap_c[lane] = col.c;
-        const int64_t c0 = (int64_t)ceil(colon_elem(col, 0));
-        const int64_t c1 = (int64_t)ceil(colon_elem(col, n - 1));
+        const double post = p.tap_post[lane];
+        const int64_t c0 = (int64_t)ceil(colon_elem(col, 0) + post);
+        const int64_t c1 = (int64_t)ceil(colon_elem(col, n - 1) + post);
         int tb = (col.n != n - 1 || c0 < 0 || c1 > 1023LL * pdi + 1) ? GNSS_EINDEX : GNSS_OK;
         if (lane == p.iP) {
-            // remChip = (t_CodePrompt(numSample) + codeFreq/Fs) - codeFreqBasis*ms*pdi (:102)
+            // remChip = (t_CodePrompt(numSample) + codeFreq/Fs) - codeFreqBasis*ms*pdi (:102);
+            // trackingCT_POS_updated.m:220: ... - signal.codelength*pdi
             d->remChip_next = (colon_elem(col, n - 1) + c.codeFreq / p.Fs) -
-                              p.codeFreqBasis * p.ms * pdi;
+                              (p.conv ? p.codelength * pdi : p.codeFreqBasis * p.ms * pdi);
         }
         if (tb != GNSS_OK && bad == GNSS_OK) bad = tb;
     }
@@ -367,14 +375,16 @@ __device__ __forceinline__ LoopUpd loop_update_i(const TrkParams& p, const TrkCh
 {
     // which: 1 = the DLL half only, 2 = the PLL half only, 3 = both (wave-uniform)
     LoopUpd u{0, 0, 0, 0, 0, 0};
-    const double T = phaseC ? 0.001 : (0.001 * pdi);
+    // trackingCT_POS_updated.m:257-258,266-267 use t = signal.ms at every pdi
+    const double T = p.conv ? p.ms : phaseC ? 0.001 : (0.001 * pdi);
     if (which & 1) {
         const double E = sqrt(E_i * E_i + E_q * E_q);
         const double L = sqrt(L_i * L_i + L_q * L_q);
         u.DLLdiscri = 0.5 * (E - L) / (E + L);
         u.code_output = c.code_outputLast + (p.tau2code / p.tau1code) * (u.DLLdiscri - c.DLLdiscriLast) +
                         u.DLLdiscri * (T / p.tau1code);
-        u.codeFreq = p.codeFreqBasis - u.code_output;
+        // trackingCT_POS_updated.m:262: codeFreq = codeFreqBasis + codeNco
+        u.codeFreq = p.conv ? p.codeFreqBasis + u.code_output : p.codeFreqBasis - u.code_output;
     }
     if (which & 2) {
         u.PLLdiscri = atan_tab(P_q / P_i) / kTwoPi;
@@ -408,6 +418,7 @@ __device__ __forceinline__ int64_t record_cols(const TrkParams& p, const TrkChan
 {
     const int64_t Index = c.Index + (phaseC ? 10 : 1);
     const int64_t nstep = c.nstep + 1;
+    if (p.conv) return nstep;  // sum(delayValue(svIndex,(1:Index))), trackingCT_POS_updated.m:290
     int64_t cols = 0;
     if (Index >= c.sv1) cols = (Index - c.sv1) / p.nsv + 1;
     return cols > nstep ? nstep : cols;
@@ -440,7 +451,8 @@ __device__ __forceinline__ void write_record_i(const TrkParams& p, const TrkBuff
         r[GNSS_F_PLLdiscri] = u.PLLdiscri;       r[GNSS_F_DLLdiscri] = u.DLLdiscri;
         r[GNSS_F_codedelay] = codedelay;         r[GNSS_F_remChip] = o.remChip;
         r[GNSS_F_codeFreq] = u.codeFreq;         r[GNSS_F_carrierFreq] = u.carrierFreq;
-        r[GNSS_F_remPhase] = o.remPhase;         r[GNSS_F_remSample] = o.remSample;
+        // (trackingCT_POS_updated.m:289 has no remSample: the slot holds absoluteSampleCodedelay)
+        r[GNSS_F_remPhase] = o.remPhase;         r[GNSS_F_remSample] = p.conv ? m : o.remSample;
         r[GNSS_F_numSample] = (double)o.n;       r[GNSS_F_delayValue] = (double)o.delayValue;
         r[GNSS_F_absoluteSample] = absS;         r[GNSS_F_codedelay2] = m;
     }
@@ -632,7 +644,10 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
 #pragma unroll
     for (int s = 0; s < NT; s++) {
         const Colon col{uni(dp->tap_a[s]), d, uni(dp->tap_c[s]), n - 1};
-        const double t0 = colon_elem(col, kf);
+        // the replica index is ceil(t + post): post = 0, or the prompt's +0.05 of
+        // trackingCT_POS_updated.m:216 (t + 0.0 is t exactly)
+        const double post = p.tap_post[s];
+        const double t0 = colon_elem(col, kf) + post;
         const double c0 = ceil(t0);
         const double R = (double)(kf - ks) + (c0 - t0) * inv_d;  // samples to the boundary
         const double rr = rint(R);
@@ -642,7 +657,7 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
             pb = ms;
             const int64_t kx = ks + ms;
             if (ms >= 0 && ms < M && kx >= 0 && kx <= n - 1)
-                pb = ceil(colon_elem(col, kx)) > c0 ? ms : ms + 1;
+                pb = ceil(colon_elem(col, kx) + post) > c0 ? ms : ms + 1;
         }
         cap[s] = (pb < M ? pb : M) - 1;  // Prefix(p) = running sum through sample p-1
         const unsigned i0 = ca_index32((int)c0);

@@ -4,6 +4,8 @@
     Acquired = acquisition(file, signal, acq)                      acquisition.m:1
     [TckResultCT, CN0_Eph, countinx] = trackingCT(file, signal, track, Acquired)
                                                                    trackingCT.m:1
+    [TckResultCT_pos, CN0_CT] = trackingCT_POS(file, signal, track, Acquired, countinx)
+                                   tracking loop of trackingCT_POS_updated.m:1-413
 
 Same names, same struct fields, same argument meaning; the work happens in the
 HIP C-ABI library (abi.py). Differences forced by the language are documented
@@ -225,13 +227,17 @@ def to_c_track(track, taps=None, channels=None):
 class TrackOutBuffers:
     """Caller-allocated trackingCT outputs (see gnss_track_out in the header)."""
 
-    def __init__(self, nsv: int, track, ntaps: int = 0):
+    def __init__(self, nsv: int, track, ntaps: int = 0, ctPOS: int | None = None):
         self.max_len = int(track.msToProcessCT_1ms) + 19 + int(track.msToProcessCT_10ms)
+        if ctPOS is not None:  # trackingCT_POS_updated: one row per step
+            self.max_len = int(ctPOS)
         self.rec = np.zeros((nsv, abi.NFIELDS, self.max_len))
         self.taps = np.zeros((nsv, 2, ntaps, self.max_len)) if ntaps else None
         self.len = np.zeros(nsv, dtype=np.int64)
         self.countinx = np.zeros(nsv, dtype=np.int32)
         self.cn0_cap = max(int(track.msToProcessCT_1ms) + 19, int(track.msToProcessCT_10ms) // 10) // 20 + 1
+        if ctPOS is not None:
+            self.cn0_cap = int(ctPOS) // 20 + 1
         self.CN0 = np.zeros((self.cn0_cap, nsv))
         o = abi.GnssTrackOut()
         o.max_len = self.max_len
@@ -269,12 +275,13 @@ class StructArray:
         return sorted(self._e)
 
 
-def build_tck_result(Acquired, buf: TrackOutBuffers, channels=None) -> StructArray:
+def build_tck_result(Acquired, buf: TrackOutBuffers, channels=None, fields=None) -> StructArray:
     entries = {}
     chans = range(len(Acquired.sv)) if channels is None else channels
+    fields = fields or abi.FIELDS
     for c in chans:
         n = int(buf.len[c])
-        e = SimpleNamespace(**{f: buf.rec[c, k, :n].copy() for k, f in enumerate(abi.FIELDS)})
+        e = SimpleNamespace(**{f: buf.rec[c, k, :n].copy() for k, f in enumerate(fields)})
         if buf.taps is not None:
             e.taps_i = buf.taps[c, 0, :, :n].copy()
             e.taps_q = buf.taps[c, 1, :, :n].copy()
@@ -356,6 +363,35 @@ def trackingCT(file, signal, track, Acquired, *, ctx: Context | None = None, tap
         sio.savemat(save_countinx, {"countinx": countinx.reshape(1, -1)})
     cn0 = buf.CN0[: buf.c.cn0_rows].copy()
     return build_tck_result(Acquired, buf, channels), cn0, countinx
+
+
+def trackingCT_POS(file, signal, track, Acquired, countinx, *, ctx: Context | None = None,
+                   channels=None, raw: bool = False):
+    """The tracking loop of trackingCT_POS_updated.m (:92-144, :179-413) on the GPU ->
+    (TckResultCT_pos, CN0_CT).
+
+    The reference reads `countinx` from countinx.mat (:29) and indexes it by the channel's
+    position in Acquired (quirk A.17); pass that vector here. track.ctPOS is the step count
+    (datalength, :50). The positioning half of the reference function (pseudoranges,
+    least squares, :420-565) is out of scope: TckResultCT_pos carries the fields of
+    :273-292 (E_i ... delayValue, absoluteSampleCodedelay) per PRN, one row per step.
+    """
+    ctx = ctx or default_context()
+    nsv = len(Acquired.sv)
+    f, k1 = to_c_file(file)
+    s = to_c_signal(signal)
+    t, k2 = to_c_track(track, None, channels)
+    a = to_c_acquired(Acquired)
+    cx = np.ascontiguousarray(np.asarray(countinx).reshape(-1)[:nsv], dtype=np.int32)
+    ctPOS = int(track.ctPOS)
+    buf = TrackOutBuffers(nsv, track, 0, ctPOS=ctPOS)
+    st = ctx.lib.gnss_tracking_ct_pos(ctx.h, C.byref(f), C.byref(s), C.byref(t), C.byref(a),
+                                      ctPOS, cx.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(buf.c))
+    ctx.check(st)
+    if raw:
+        return buf
+    cn0 = buf.CN0[: buf.c.cn0_rows].copy()
+    return build_tck_result(Acquired, buf, channels, abi.FIELDS_POS), cn0
 
 
 def ca_code(prn: int) -> np.ndarray:

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define GNSS_ABI_VERSION 2
+#define GNSS_ABI_VERSION 3
 
 /* ---- status codes (SURVEY §8b "Error conventions") --------------------- */
 #define GNSS_OK         0
@@ -137,6 +137,16 @@ enum gnss_track_field {
     GNSS_NFIELDS
 };
 
+/* gnss_tracking_ct_pos stores trackingCT_POS_updated.m:273-292's fields in the same
+ * slots: PLLdiscri = carrError, DLLdiscri = codeError, carrierFreq = carrFreq,
+ * remPhase = remCarrPhase, and the remSample slot (that loop has no remSample) holds
+ * absoluteSampleCodedelay. */
+#define GNSS_F_carrError               GNSS_F_PLLdiscri
+#define GNSS_F_codeError               GNSS_F_DLLdiscri
+#define GNSS_F_carrFreq                GNSS_F_carrierFreq
+#define GNSS_F_remCarrPhase            GNSS_F_remPhase
+#define GNSS_F_absoluteSampleCodedelay GNSS_F_remSample
+
 /* Outputs of trackingCT. Caller-allocated:
  *   rec      [nsv][GNSS_NFIELDS][max_len]  TckResultCT series per channel
  *            (series length 1000 + countinx + msToProcessCT_10ms, phase-C values
@@ -209,6 +219,28 @@ int gnss_acquisition(gnss_ctx *ctx, const gnss_file *file, const gnss_signal *si
 int gnss_tracking_ct(gnss_ctx *ctx, const gnss_file *file, const gnss_signal *signal,
                      const gnss_track *track, const gnss_acquired *acquired,
                      gnss_track_out *out);
+
+/* The tracking loop of trackingCT_POS_updated.m (its positioning half,
+ * :420-565, is out of scope). Replaces the per-channel correlator / NCO / DLL / PLL of
+ * trackingCT_POS_updated.m:92-144,179-413:
+ *   - file_ptr = (Sample - codedelay + 1 + skip*Sample)*bytes (:108-110), one continuous
+ *     read per channel (no re-seek at the 1 -> 10 ms switch);
+ *   - steps msIndex = 1..ctPOS (track.ctPOS, :50); pdi = 1 while msIndex <= 1000 +
+ *     countinx[svIndex] (:183; 1000 = track.msToProcessCT_1ms, countinx as loaded from
+ *     countinx.mat at :29, indexed by channel POSITION), else 10;
+ *   - numSample = ceil(...) (:189); E/P/L at Spacing(3) = +0.5, prompt Code(ceil(t+0.05)+1),
+ *     Spacing(23) = -0.5 (:42,210-217); no negation; codeFreq = f0 + codeNco (:262);
+ *     loop filters with T = signal.ms at every pdi (:257,266);
+ *   - C/N0 every 20 steps of either pdi into one CN0_CT (:237-250);
+ *   - one record row per step (Index = msIndex), codedelay = Sample - codedelay + 1 +
+ *     sum(delayValue(svIndex,1:Index)) (:290).
+ * out: rec[nsv][GNSS_NFIELDS][max_len] (max_len >= ctPOS, len = ctPOS), CN0_Eph = CN0_CT
+ * (cn0_rows = ctPOS/20), countinx echoed. int8 records only (GNSS_EARG for int16: the
+ * reference advances file_ptr by numSample*dataType bytes after reading twice that,
+ * :196,207). EOF inside the loop -> GNSS_EIO (MATLAB raises on the short vector).    */
+int gnss_tracking_ct_pos(gnss_ctx *ctx, const gnss_file *file, const gnss_signal *signal,
+                         const gnss_track *track, const gnss_acquired *acquired, int32_t ctPOS,
+                         const int32_t *countinx, gnss_track_out *out);
 
 /* Per-step parity hook: ONE trackingCT correlation step (trackingCT.m:79-118: numSample
  * from remChip/codeFreq, E/P/L or ACF replicas, carrier wipe, sums; no negation, no

@@ -544,7 +544,7 @@ static inline int ca_index(int64_t c) { return (int)((c + 1022) % 1023); }
 
 static void correlate_cpx(const cpx *x, int64_t n, double remChip, double codeFreq, double Fs,
                           double carrierFreq, double remPhase, const int8_t *ca, int pdi, int ntaps,
-                          const double *taps, double *sums);
+                          const double *taps, const double *post, double *sums);
 
 void or_correlate_step(const int8_t *iq, int64_t n, double remChip, double codeFreq, double Fs,
                        double carrierFreq, double remPhase, const int8_t *ca, int pdi, int ntaps,
@@ -552,14 +552,16 @@ void or_correlate_step(const int8_t *iq, int64_t n, double remChip, double codeF
 {
     cpx *x = (cpx *)malloc(sizeof(cpx) * (size_t)(n > 0 ? n : 1));
     for (int64_t k = 0; k < n; k++) { x[k].re = iq[2 * k]; x[k].im = iq[2 * k + 1]; }
-    correlate_cpx(x, n, remChip, codeFreq, Fs, carrierFreq, remPhase, ca, pdi, ntaps, taps, sums);
+    correlate_cpx(x, n, remChip, codeFreq, Fs, carrierFreq, remPhase, ca, pdi, ntaps, taps, NULL, sums);
     free(x);
 }
 
-/* The correlator of trackingCT.m:96-118 on rawsignal0DC (complex doubles). */
+/* The correlator of trackingCT.m:96-118 on rawsignal0DC (complex doubles). post[s]
+ * (NULL = none) is added to tap s's colon element before ceil: the prompt's
+ * Code(ceil(t_CodePrompt + 0.05) + indx) of trackingCT_POS_updated.m:216. */
 static void correlate_cpx(const cpx *x, int64_t n, double remChip, double codeFreq, double Fs,
                           double carrierFreq, double remPhase, const int8_t *ca, int pdi, int ntaps,
-                          const double *taps, double *sums)
+                          const double *taps, const double *post, double *sums)
 {
     (void)pdi;
     const double d = codeFreq / Fs;
@@ -584,6 +586,7 @@ static void correlate_cpx(const cpx *x, int64_t n, double remChip, double codeFr
         double Q = xr * cw - xi * sw; /* real(raw.*carrsig) */
         for (int s = 0; s < ntaps; s++) {
             double t = or_colon_elem(&col[s], k);
+            if (post) t = t + post[s];
             double code = ca[ca_index((int64_t)ceil(t))];
             acc[2 * s] += code * I;
             acc[2 * s + 1] += code * Q;
@@ -740,7 +743,7 @@ static int trk_step(const trk_ctx *t, chan_state *c, int ch, int sv1, int pdi, i
 
     double sums[2 * GNSS_MAX_TAPS];
     correlate_cpx(buf, n, c->remChip, c->codeFreq, sg->Fs, c->carrierFreq, c->remPhase, ca, pdi,
-                  t->ntaps, t->taps, sums);
+                  t->ntaps, t->taps, NULL, sums);
     if (phaseC)
         for (int s = 0; s < 2 * t->ntaps; s++) sums[s] = -sums[s]; /* :447-449 */
 
@@ -941,6 +944,169 @@ int or_tracking_ct(const gnss_file *file, const gnss_signal *sg, const gnss_trac
     if (r1 > rows) rows = r1;
     if (tr->msToProcessCT_10ms / 10 / 20 > rows) rows = tr->msToProcessCT_10ms / 10 / 20;
     out->cn0_rows = rows;
+    return status;
+}
+
+/* ------------------------------------------------------------------------ */
+/* trackingCT_POS_updated.m: its tracking loop (positioning half out of scope) */
+/* ------------------------------------------------------------------------ */
+
+/* The C/N0 moment estimator of trackingCT_POS_updated.m:241-246 (= trackingCT.m:124-131). */
+static double cn0_moment(const double *Zk, double T)
+{
+    double mean = 0;
+    for (int k = 0; k < 20; k++) mean += Zk[k];
+    mean = mean / 20;
+    double var = 0;
+    for (int k = 0; k < 20; k++) var += (Zk[k] - mean) * (Zk[k] - mean);
+    var = var / 19;
+    double m2v = mean * mean - var;
+    double scale = 1 / T; /* 1/(1*t*pdi) */
+    if (m2v >= 0) {
+        double NA2 = sqrt(m2v);
+        double varIQ = 0.5 * (mean - NA2);
+        return fabs(10 * log10(scale * NA2 / (2 * varIQ)));
+    }
+    double y = sqrt(-m2v); /* complex NA2 = i*y (quirk A.16) */
+    double nr = 0, ni = scale * y;
+    double dr = 2 * (0.5 * mean), di = 2 * (0.5 * -y);
+    double den = dr * dr + di * di;
+    double zr = (nr * dr + ni * di) / den, zi = (ni * dr - nr * di) / den;
+    double lr = 10 * (log(hypot(zr, zi)) / log(10.0));
+    double li = 10 * (atan2(zi, zr) / log(10.0));
+    return hypot(lr, li);
+}
+
+/* One channel of trackingCT_POS_updated.m:92-118 (init) and :179-408 (the msIndex loop,
+ * both pdi branches; the channel loop is independent per svIndex: each channel seeks its
+ * own file_ptr before every read). */
+static int trkpos_channel(const trk_ctx *t, const gnss_acquired *acq, int ch, int32_t ctPOS,
+                          int32_t cx, double *cn0)
+{
+    const gnss_signal *sg = t->sg;
+    const gnss_file *f = t->file;
+    const double S = (double)sg->Sample;
+    const double taps[3] = {0.5, 0.0, -0.5};  /* Spacing(3), Spacing(13), Spacing(23) (:42) */
+    const double post[3] = {0.0, 0.05, 0.0};  /* ceil(t_CodePrompt+0.05) (:216) */
+    int8_t ca[1023];
+    if (or_generate_ca(acq->sv[ch], ca)) return GNSS_EARG;
+    cpx *buf = (cpx *)malloc(sizeof(cpx) * (size_t)(2 * (sg->Sample * 10 + 4096)));
+    int st = GNSS_OK;
+    const int64_t AcqCodeDelay = acq->codedelay[ch];
+    int64_t file_ptr = (int64_t)((S - (double)AcqCodeDelay + 1 + (double)f->skip * sg->Fs * sg->ms) *
+                                 f->dataPrecision * f->dataType); /* :108-110 */
+    const double AcqFreq = acq->fineFreq[ch];                     /* :113-114 */
+    double carrFreq = AcqFreq, codeFreq = sg->codeFreqBasis, remChip = 0, remCarrPhase = 0;
+    double carrNco = 0, oldCarrNco = 0, oldCarrError = 0, codeNco = 0, code_outputLast = 0,
+           DLLdiscriLast = 0;
+    double Zk[20] = {0};
+    int index_int = 0, snrIndex = 1;
+    double dvsum = 0;
+    const double tT = sg->ms; /* t = signal.ms (:48) */
+    for (int64_t Index = 1; Index <= ctPOS && st == GNSS_OK; Index++) {
+        const int pdi = (Index <= t->tr->msToProcessCT_1ms + (int64_t)cx) ? 1 : 10; /* :183,:294 */
+        const double cps = codeFreq / sg->Fs;                                          /* :188 */
+        const int64_t n = (int64_t)ceil((sg->codelength * pdi - remChip) / cps);       /* :189 */
+        const int64_t delayValue = n - (int64_t)(S * pdi);                             /* :191 */
+        int64_t got = 0;
+        const int64_t m = rd_cpx(f, file_ptr, n, buf, &got); /* fseek + fread (:193-205) */
+        if (m == -1 || m != n) { st = GNSS_EIO; break; }     /* short read: MATLAB raises */
+        if (m == -2) { st = GNSS_EINDEX; break; }
+        const int64_t ftell_pos = file_ptr + got;
+        file_ptr = file_ptr + n * f->dataType;               /* :207 (int8: = ftell) */
+        /* code index range (MATLAB would raise on an out-of-range Code index) */
+        for (int s = 0; s < 3 && st == GNSS_OK; s++) {
+            double a = (0 + taps[s]) + remChip;
+            double b = ((double)(n - 1) * cps + taps[s]) + remChip;
+            or_colon col;
+            or_colon_init(&col, a, cps, b);
+            if (col.n != n - 1 || !chip_ok((int64_t)ceil(or_colon_elem(&col, 0) + post[s]), pdi) ||
+                !chip_ok((int64_t)ceil(or_colon_elem(&col, n - 1) + post[s]), pdi))
+                st = GNSS_EINDEX;
+        }
+        if (st) break;
+        double sums[6];
+        correlate_cpx(buf, n, remChip, codeFreq, sg->Fs, carrFreq, remCarrPhase, ca, pdi, 3, taps, post,
+                      sums); /* :210-235 */
+        {   /* remChip = t_CodePrompt(numSample) + codePhaseStep - codelength*pdi (:220) */
+            double a = (0 + taps[1]) + remChip;
+            double b = ((double)(n - 1) * cps + taps[1]) + remChip;
+            or_colon col;
+            or_colon_init(&col, a, cps, b);
+            remChip = or_colon_elem(&col, n - 1) + cps - sg->codelength * pdi;
+        }
+        /* Wave = 2*pi*(carrFreq.*CarrTime) + remCarrPhase; rem(Wave(n+1), 2*pi) (:222-224) */
+        remCarrPhase = fmod(TWO_PI * (carrFreq * ((double)n / sg->Fs)) + remCarrPhase, TWO_PI);
+        const double E_i = sums[0], E_q = sums[1], P_i = sums[2], P_q = sums[3], L_i = sums[4],
+                     L_q = sums[5];
+        /* C/N0 (:238-250) */
+        index_int += 1;
+        Zk[index_int - 1] = P_i * P_i + P_q * P_q;
+        if (index_int % 20 == 0) {
+            double cn = cn0_moment(Zk, 1 * tT * pdi);
+            if (cn0 && snrIndex <= t->out->cn0_cap) cn0[(int64_t)(snrIndex - 1) * t->nsv + ch] = cn;
+            index_int = 0;
+            snrIndex += 1;
+        }
+        /* DLL (:253-262) */
+        double E = sqrt(E_i * E_i + E_q * E_q);
+        double L = sqrt(L_i * L_i + L_q * L_q);
+        double codeError = 0.5 * (E - L) / (E + L);
+        codeNco = or_loop_filter(code_outputLast, codeError, DLLdiscriLast, t->tau1code, t->tau2code, tT);
+        DLLdiscriLast = codeError;
+        code_outputLast = codeNco;
+        codeFreq = sg->codeFreqBasis + codeNco;
+        /* PLL (:265-270) */
+        double carrError = atan(P_q / P_i) / TWO_PI;
+        carrNco = or_loop_filter(oldCarrNco, carrError, oldCarrError, t->tau1carr, t->tau2carr, tT);
+        oldCarrNco = carrNco;
+        oldCarrError = carrError;
+        carrFreq = AcqFreq + carrNco;
+        /* record (:273-292) */
+        dvsum += (double)delayValue;
+        const double absS = (double)ftell_pos;
+        const double cd2 = or_mod(absS / (f->dataPrecision * f->dataType), sg->Fs * sg->ms);
+        const double codedelay = (S - (double)AcqCodeDelay + 1) + dvsum;
+        double vals[GNSS_NFIELDS] = {P_i, P_q, E_i, E_q, L_i, L_q, carrError, codeError, codedelay,
+                                     remChip, codeFreq, carrFreq, remCarrPhase, cd2, (double)n,
+                                     (double)delayValue, absS, cd2};
+        for (int fi = 0; fi < GNSS_NFIELDS; fi++) rec_put(t, ch, fi, Index - 1, Index, vals[fi]);
+        taps_put(t, ch, Index - 1, Index, sums);
+    }
+    if (!st && t->out->len) t->out->len[ch] = ctPOS;
+    free(buf);
+    return st;
+}
+
+int or_tracking_ct_pos(const gnss_file *file, const gnss_signal *sg, const gnss_track *tr,
+                       const gnss_acquired *acq, int32_t ctPOS, const int32_t *countinx,
+                       gnss_track_out *out, int nthreads)
+{
+    if (file->dataPrecision != 1 || (file->dataType != 1 && file->dataType != 2) || ctPOS <= 0 ||
+        !countinx || tr->n_taps != 0 || out->max_len < ctPOS)
+        return GNSS_EARG;
+    trk_ctx t;
+    memset(&t, 0, sizeof(t));
+    t.file = file; t.sg = sg; t.tr = tr; t.out = out; t.nsv = acq->n;
+    t.fsize = file_size(file);
+    t.ntaps = 3;
+    or_calc_loop_coef(tr->DLLBW, tr->DLLDamp, tr->DLLGain, &t.tau1code, &t.tau2code); /* :87-88 */
+    or_calc_loop_coef(tr->PLLBW, tr->PLLDamp, tr->PLLGain, &t.tau1carr, &t.tau2carr);
+    int nch = tr->chan ? tr->n_chan : acq->n;
+    int nt = nthreads_of(nthreads);
+    int status = GNSS_OK;
+    if (out->CN0_Eph) memset(out->CN0_Eph, 0, sizeof(double) * (size_t)out->cn0_cap * (size_t)acq->n);
+#pragma omp parallel for num_threads(nt) schedule(dynamic)
+    for (int i = 0; i < nch; i++) {
+        int ch = tr->chan ? tr->chan[i] : i;
+        int st = trkpos_channel(&t, acq, ch, ctPOS, countinx[ch], out->CN0_Eph);
+        if (out->countinx) out->countinx[ch] = countinx[ch];
+#pragma omp critical
+        {
+            if (st && status == GNSS_OK) status = st;
+        }
+    }
+    out->cn0_rows = ctPOS / 20;
     return status;
 }
 

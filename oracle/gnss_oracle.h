@@ -50,6 +50,12 @@ int or_acquisition(const gnss_file *file, const gnss_signal *signal, const gnss_
 int or_tracking_ct(const gnss_file *file, const gnss_signal *signal, const gnss_track *track,
                    const gnss_acquired *acquired, gnss_track_out *out, int nthreads);
 
+/* The tracking loop of trackingCT_POS_updated.m:92-144,179-413 (see gnss_tracking_ct_pos
+ * in include/gnss_mi355x.h for the conventions; positioning is out of scope). */
+int or_tracking_ct_pos(const gnss_file *file, const gnss_signal *signal, const gnss_track *track,
+                       const gnss_acquired *acquired, int32_t ctPOS, const int32_t *countinx,
+                       gnss_track_out *out, int nthreads);
+
 /* One trackingCT-style correlation step on host bytes (the body of
  * trackingCT.m:96-118 / :429-449 without the negation): sums[2*ntaps] =
  * (I, Q) per tap. Exposed for per-step parity tests. */

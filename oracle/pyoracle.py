@@ -49,6 +49,9 @@ def load():
         lib.or_tracking_ct.argtypes = [C.POINTER(abi.GnssFile), C.POINTER(abi.GnssSignal),
                                        C.POINTER(abi.GnssTrack), C.POINTER(abi.GnssAcquired),
                                        C.POINTER(abi.GnssTrackOut), C.c_int]
+        lib.or_tracking_ct_pos.argtypes = [C.POINTER(abi.GnssFile), C.POINTER(abi.GnssSignal),
+                                           C.POINTER(abi.GnssTrack), C.POINTER(abi.GnssAcquired),
+                                           C.c_int32, C.c_void_p, C.POINTER(abi.GnssTrackOut), C.c_int]
         lib.or_correlate_step.argtypes = [C.c_void_p, C.c_int64, C.c_double, C.c_double, C.c_double,
                                           C.c_double, C.c_double, C.c_void_p, C.c_int, C.c_int,
                                           C.c_void_p, C.c_void_p]
@@ -136,6 +139,25 @@ def trackingCT(file, signal, track, Acquired, taps=None, channels=None, nthreads
         raise abi.GnssError(st, "or_tracking_ct")
     cn0 = buf.CN0[: buf.c.cn0_rows].copy()
     return sdr.build_tck_result(Acquired, buf, channels), cn0, buf.countinx.astype(np.int64)
+
+
+def trackingCT_POS(file, signal, track, Acquired, countinx, channels=None, nthreads=0, raw=False):
+    nsv = len(Acquired.sv)
+    f, k1 = sdr.to_c_file(file)
+    s = sdr.to_c_signal(signal)
+    t, k2 = sdr.to_c_track(track, None, channels)
+    a = sdr.to_c_acquired(Acquired)
+    cx = np.ascontiguousarray(np.asarray(countinx).reshape(-1)[:nsv], dtype=np.int32)
+    buf = sdr.TrackOutBuffers(nsv, track, 0, ctPOS=int(track.ctPOS))
+    st = load().or_tracking_ct_pos(C.byref(f), C.byref(s), C.byref(t), C.byref(a), int(track.ctPOS),
+                                   cx.ctypes.data, C.byref(buf.c), nthreads)
+    if raw:
+        buf.status = st
+        return buf
+    if st != abi.OK:
+        raise abi.GnssError(st, "or_tracking_ct_pos")
+    cn0 = buf.CN0[: buf.c.cn0_rows].copy()
+    return sdr.build_tck_result(Acquired, buf, channels, abi.FIELDS_POS), cn0
 
 
 def correlate_step(iq, numSample, remChip, codeFreq, Fs, carrierFreq, remPhase, ca, pdi, taps):

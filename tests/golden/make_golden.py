@@ -76,5 +76,29 @@ def main():
     print("golden vectors written:", Aq.sv, Aq.codedelay, Aq.fineFreq - 4.58e6, buf.countinx)
 
 
+# trackingCT_POS_updated.m tracking loop: 2 channels, 60 + countinx steps at 1 ms, then
+# 10 ms up to ctPOS = 70 steps (countinx -1 exercises the early switch)
+POS_N1, POS_CX, POS_CTPOS = 60, [5, -1], 70
+
+
+def main_pos():
+    data = record()
+    file, signal, acq, track, _, _ = pkg.initParameters()
+    file.skip, file.data = SKIP, data
+    A = SimpleNamespace(sv=np.array([3, 16]), SNR=np.array([20.0, 26.0]),
+                        Doppler=np.array([1000.0, 0.0]), codedelay=np.array([3683, 26051]),
+                        fineFreq=np.array([4580990.0, 4579695.0]))
+    track.msToProcessCT_1ms, track.ctPOS = POS_N1, POS_CTPOS
+    buf = po.trackingCT_POS(file, signal, track, A, POS_CX, raw=True)
+    assert buf.status == 0
+    np.savez_compressed(os.path.join(HERE, "golden_pos_small.npz"), rec=buf.rec[:, :, :POS_CTPOS],
+                        len=buf.len, CN0=buf.CN0[: buf.c.cn0_rows], sv=A.sv, codedelay=A.codedelay,
+                        fineFreq=A.fineFreq, countinx=np.array(POS_CX), skip=SKIP, N1=POS_N1,
+                        ctPOS=POS_CTPOS)
+    print("POS golden written:", buf.len, buf.c.cn0_rows)
+
+
 if __name__ == "__main__":
-    main()
+    if "--pos-only" not in sys.argv:
+        main()
+    main_pos()

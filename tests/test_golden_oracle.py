@@ -78,3 +78,43 @@ def test_oracle_reproduces_golden_acquisition(pkg, po):
     assert np.allclose(d.SNR, z["SNR"], rtol=0, atol=1e-9)
     assert np.array_equal(A.sv, z["sv"]) and np.array_equal(A.codedelay, z["codedelay"])
     assert np.array_equal(A.fineFreq, z["fineFreq"]) and np.array_equal(A.Doppler, z["Doppler"])
+
+
+def check_pos_against_golden(pkg, g, rec, length, cn0, tol=1e-12):
+    assert np.array_equal(length, g["len"])
+    F = pkg.abi.FIELDS_POS
+    for c in range(len(g["sv"])):
+        n = int(g["len"][c])
+        ref, got = g["rec"][c, :, :n], rec[c, :, :n]
+        for k, f in enumerate(F):
+            if f in INT_FIELDS or f == "absoluteSampleCodedelay":
+                assert np.array_equal(got[k], ref[k]), f
+        scale = np.sqrt(np.mean(ref[0] ** 2 + ref[1] ** 2))
+        for k in range(6):
+            assert np.max(np.abs(got[k] - ref[k])) / scale < tol, F[k]
+        for f in ("remChip", "codeFreq", "carrFreq", "remCarrPhase", "carrError", "codeError"):
+            k = F.index(f)
+            assert np.allclose(got[k], ref[k], rtol=1e-9, atol=1e-9), f
+    assert np.allclose(cn0, g["CN0"], rtol=1e-9, atol=1e-9)
+
+
+def pos_inputs(pkg, po):
+    g = np.load(os.path.join(GOLDEN, "golden_pos_small.npz"))
+    _, data = golden_record(pkg, po)
+    file, signal, acq, track, _, _ = pkg.initParameters()
+    file.skip, file.data = int(g["skip"]), data
+    track.msToProcessCT_1ms, track.ctPOS = int(g["N1"]), int(g["ctPOS"])
+    A = SimpleNamespace(sv=g["sv"], SNR=np.zeros(2), Doppler=np.zeros(2), codedelay=g["codedelay"],
+                        fineFreq=g["fineFreq"])
+    return g, file, signal, track, A
+
+
+def test_oracle_reproduces_golden_pos(pkg, po):
+    g, file, signal, track, A = pos_inputs(pkg, po)
+    buf = po.trackingCT_POS(file, signal, track, A, g["countinx"], raw=True)
+    assert buf.status == 0
+    check_pos_against_golden(pkg, g, buf.rec, buf.len, buf.CN0[: buf.c.cn0_rows])
+    # one row per step: the 1 -> 10 ms switch at N1 + countinx (numSample x10)
+    ns = g["rec"][1, pkg.abi.FIELDS_POS.index("numSample")]
+    k = int(g["N1"]) + int(g["countinx"][1])
+    assert np.all(ns[:k] < 60000) and np.all(ns[k:] > 570000)
