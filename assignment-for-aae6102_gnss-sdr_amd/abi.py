@@ -137,7 +137,8 @@ def load(path: str | None = None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    # GNSS_LIB: a timing-probe build (tools/build_probe.sh) in place of the product library
+    p = path or os.environ.get("GNSS_LIB") or LIB_PATH
     if not os.path.exists(p):
         raise ImportError(f"{p} missing: the HIP extension is not built "
                           "(run `python -c 'import __graft_entry__ as g; g.build()'`)")

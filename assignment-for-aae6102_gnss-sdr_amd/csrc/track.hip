@@ -619,6 +619,13 @@ struct LdsRaw {
     __device__ __forceinline__ int4 get(int j) const { return p[j * kTrkThreads]; }
 };
 
+// Timing-probe builds only (tools/build_probe.sh, never the product library): bit 1 drops
+// the lane's sincos, bit 2 the per-tap boundary search, bit 4 the per-sample Wave / eta
+// (the rotation table alone). Their sums are wrong; they time the correlator's parts.
+#ifndef GNSS_CORR_PROBE
+#define GNSS_CORR_PROBE 0
+#endif
+
 template <int NT, int SUB, bool DIVIDE, bool RELOAD, int FMT, class Desc, class Raw>
 __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* dp, const Raw& raw,
                                                int64_t ks, unsigned cabits, double2* myslot,
@@ -643,6 +650,12 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
     double v1[NT], dv[NT];
 #pragma unroll
     for (int s = 0; s < NT; s++) {
+        if constexpr ((GNSS_CORR_PROBE & 2) != 0) {
+            cap[s] = M - 1 - s;
+            v1[s] = 1.0;
+            dv[s] = (double)(cabits & 1u);
+            continue;
+        }
         const Colon col{uni(dp->tap_a[s]), d, uni(dp->tap_c[s]), n - 1};
         // the replica index is ceil(t + post): post = 0, or the prompt's +0.05 of
         // trackingCT_POS_updated.m:216 (t + 0.0 is t exactly)
@@ -674,7 +687,12 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
     const double kb = (double)ks;
     const double Wb = wave_at<DIVIDE>(kb, f, phi0, Fs, rFs);
     double sb, cb;
-    sincos_wave(Wb, &sb, &cb);
+    if constexpr ((GNSS_CORR_PROBE & 1) != 0) {
+        sb = Wb * 1e-9;
+        cb = 1.0;
+    } else {
+        sincos_wave(Wb, &sb, &cb);
+    }
 
     double run_r = 0.0, run_i = 0.0;
     double pre_r[NT], pre_i[NT];
@@ -727,20 +745,30 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
                 xr = (double)(int8_t)((word >> sh) & 0xFF);
                 xi = (double)(int8_t)((word >> (sh + 8)) & 0xFF);
             }
-            double wr = xr, wi = xi;
-            // m = 0: W = Wb, phi = 0, rcs = (1, 0) -> w = x exactly; skipped when known
-            if (RELOAD || m > 0) {
+            // m = 0: W = Wb, phi[0] = 0, rcs[0] = (1, 0) (prepare_desc: 0*dhi + 0*dlo, sincos(0))
+            // -> w = x exactly, no rotation
+            if constexpr ((GNSS_CORR_PROBE & 4) != 0) {
+                const double2 rcs = ld_rcs(dp, m);
+                run_r = __builtin_fma(xr, rcs.x, run_r);
+                run_r = __builtin_fma(-xi, rcs.y, run_r);
+                run_i = __builtin_fma(xr, rcs.y, run_i);
+                run_i = __builtin_fma(xi, rcs.x, run_i);
+            } else if (m > 0) {
+                // w = x * (rc + i rs) * (1 + i eta): the first-order residue folded into the
+                // rotation, the products accumulated by FMA into the running sums
                 const double W = wave_at<DIVIDE>(kbj + (double)mm, f, phi0, Fs, rFs);
                 const double eta = (W - Wb) - dp->phi[m];
                 const double2 rcs = ld_rcs(dp, m);
-                const double rc = rcs.x, rs = rcs.y;
-                const double yr = __builtin_fma(xr, rc, -(xi * rs));
-                const double yi = __builtin_fma(xr, rs, xi * rc);
-                wr = __builtin_fma(-eta, yi, yr);
-                wi = __builtin_fma(eta, yr, yi);
+                const double rc = __builtin_fma(-eta, rcs.y, rcs.x);
+                const double rs = __builtin_fma(eta, rcs.x, rcs.y);
+                run_r = __builtin_fma(xr, rc, run_r);
+                run_r = __builtin_fma(-xi, rs, run_r);
+                run_i = __builtin_fma(xr, rs, run_i);
+                run_i = __builtin_fma(xi, rc, run_i);
+            } else {
+                run_r += xr;
+                run_i += xi;
             }
-            run_r += wr;
-            run_i += wi;
             myslot[mm * T] = make_double2(run_r, run_i);
 
         }
@@ -1365,7 +1393,10 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(3, 
                 const unsigned lo = pw[(k * NV + v) * 2], hi = pw[(k * NV + v) * 2 + 1];
                 return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
             });
-            if ((tid & 7) == 0) s_fin[tid >> 3] = D.phaseC ? -a : a;  // :447-449
+            if constexpr (GNSS_CORR_PROBE != 0)  // (probe builds: E = P = L = 1, a steady loop)
+                if ((tid & 7) == 0) s_fin[tid >> 3] = ((tid >> 3) & 1) ? 0.0 * a : 1.0 + 0.0 * a;
+            if constexpr (GNSS_CORR_PROBE == 0)
+                if ((tid & 7) == 0) s_fin[tid >> 3] = D.phaseC ? -a : a;  // :447-449
         }
         const int phaseC = D.phaseC;
         lds_barrier();
