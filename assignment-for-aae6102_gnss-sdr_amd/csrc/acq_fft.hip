@@ -251,6 +251,91 @@ __device__ __forceinline__ void fft2000(V* a, const V* tw, int tid)
     __syncthreads();
 }
 
+// 20 = 5 x 4: x index n = 4*n1 + n2, output k = k1 + 5*k2 (natural order in v)
+constexpr double kTc20[13] = {1., 0.9510565162951535, 0.8090169943749475, 0.5877852522924731,
+                              0.30901699437494745, 0., -0.30901699437494745, -0.5877852522924731,
+                              -0.8090169943749475, -0.9510565162951535, -1., -0.9510565162951535,
+                              -0.8090169943749475};  // cos(2 pi m/20)
+constexpr double kTs20[13] = {0., 0.30901699437494745, 0.5877852522924731, 0.8090169943749475,
+                              0.9510565162951535, 1., 0.9510565162951535, 0.8090169943749475,
+                              0.5877852522924731, 0.30901699437494745, 0., -0.30901699437494745,
+                              -0.5877852522924731};  // sin(2 pi m/20)
+template <int DIR, class V> __device__ __forceinline__ void dft20(V (&v)[20])
+{
+    using R = Re<V>;
+    V y[4][5];  // y[n2][k1] = DFT_5 over n1 of x[4*n1 + n2]
+#pragma unroll
+    for (int n2 = 0; n2 < 4; n2++) {
+#pragma unroll
+        for (int n1 = 0; n1 < 5; n1++) y[n2][n1] = v[4 * n1 + n2];
+        dft5<DIR>(y[n2]);
+    }
+#pragma unroll
+    for (int n2 = 1; n2 < 4; n2++)
+#pragma unroll
+        for (int k1 = 1; k1 < 5; k1++) {
+            const int m = n2 * k1;  // <= 12
+            y[n2][k1] = cmul(y[n2][k1], mk<V>((R)kTc20[m], DIR < 0 ? (R)-kTs20[m] : (R)kTs20[m]));
+        }
+#pragma unroll
+    for (int k1 = 0; k1 < 5; k1++) {
+        V a = y[0][k1], b = y[1][k1], c = y[2][k1], d = y[3][k1];
+        dft4<DIR>(a, b, c, d);
+        v[k1] = a; v[k1 + 5] = b; v[k1 + 10] = c; v[k1 + 15] = d;
+    }
+}
+
+template <int R, int DIR, class V> __device__ __forceinline__ void dft_r(V (&v)[R])
+{
+    if constexpr (R == 5) dft5<DIR>(v);
+    else if constexpr (R == 10) dft10<DIR>(v);
+    else if constexpr (R == 16) dft16<DIR>(v);
+    else dft20<DIR>(v);
+}
+
+// ---- BATCH 2000-point transforms side by side in LDS (transform b at a + b*2000), one
+// radix-R Stockham stage; every butterfly of the batch is spread over the block's threads.
+template <int DIR, int R, int NS, int BATCH, class V>
+__device__ __forceinline__ void stage_batch(V* a, const V* tw, int tid)
+{
+    constexpr int NB = kRow / R, TOT = NB * BATCH, PER = (TOT + kRowThreads - 1) / kRowThreads;
+    V v[PER][R];
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int u0 = tid + q * kRowThreads, u = u0 < TOT ? u0 : TOT - 1;
+        const int b = u / NB, j = u - b * NB, k = j % NS;
+        const V* src = a + b * kRow;
+#pragma unroll
+        for (int i = 0; i < R; i++) v[q][i] = src[j + i * NB];
+        if (NS > 1) {
+#pragma unroll
+            for (int i = 1; i < R; i++) v[q][i] = twid<DIR>(v[q][i], tw[i * k * (kRow / (NS * R))]);
+        }
+        dft_r<R, DIR>(v[q]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int u = tid + q * kRowThreads;
+        if (u < TOT) {
+            const int b = u / NB, j = u - b * NB, k = j % NS, d = (j / NS) * NS * R + k;
+            V* dst = a + b * kRow;
+#pragma unroll
+            for (int i = 0; i < R; i++) dst[d + i * NS] = v[q][i];
+        }
+    }
+    __syncthreads();
+}
+
+// 2000 = 10 x 10 x 20: three LDS passes per batch of transforms (natural order at the end).
+template <int DIR, int BATCH, class V>
+__device__ __forceinline__ void fft2000_batch(V* a, const V* tw, int tid)
+{
+    stage_batch<DIR, 10, 1, BATCH>(a, tw, tid);
+    stage_batch<DIR, 10, 10, BATCH>(a, tw, tid);
+    stage_batch<DIR, 20, 100, BATCH>(a, tw, tid);
+}
+
 template <class V>
 __device__ __forceinline__ void load_row_tw(V* s_tw, const V* tw_row, int tid)
 {
@@ -338,7 +423,9 @@ __global__ __launch_bounds__(kColThreads) void inv_cols_kernel(
     });
 }
 
-// ---- I2: inverse rows, |.|^2/S^2 summed over the ms in order, stored tau2-major.
+// ---- I2: inverse rows, |.|^2/S^2 summed over the ms in order, stored tau2-major. Two
+// ms per pass (their 2000-point transforms side by side, fft2000_batch): half the
+// barriers per transform, every lane busy in the radix-20 pass.
 template <int P>
 __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel(
     const float2* __restrict__ A, int nprn, int datalen, int first_pair, float scale,
@@ -348,8 +435,7 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel(
     constexpr int V4 = kRow / 2;  // float4 = two complex
     constexpr int QV = (V4 + kRowThreads - 1) / kRowThreads;
     static_assert(QV == 4, "row copy is written for 4 float4 per lane");
-    // s_a is padded to QV*256 float4 so the row copy needs no bounds test
-    __shared__ float4 s_a4[QV * kRowThreads];
+    __shared__ float4 s_a4[2 * V4];
     __shared__ float2 s_tw[kRow];
     float2* s_a = reinterpret_cast<float2*>(s_a4);
     const int tau2 = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
@@ -358,29 +444,35 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel(
 #pragma unroll
     for (int i = 0; i < Q; i++) acc[i] = 0.f;
     const float4* src = reinterpret_cast<const float4*>(A + ((int64_t)g * datalen * P + tau2) * kRow);
-    // clamped: every lane loads, only e < V4 is used (named registers: an array here
-    // ends up in scratch)
-    auto ld = [&](const float4* p, int i) {
+    // row `idx` (clamped to the last ms: an odd datalen's spare transform is not summed);
+    // named registers (an array here ends up in scratch)
+    auto ld = [&](int idx, int i) {
         const int e = tid + i * kRowThreads;
-        return p[e < V4 ? e : V4 - 1];
+        const int r = idx < datalen ? idx : datalen - 1;
+        return src[(int64_t)r * P * V4 + (e < V4 ? e : V4 - 1)];
     };
-    float4 n0 = ld(src, 0), n1 = ld(src, 1), n2 = ld(src, 2), n3 = ld(src, 3);
-    for (int idx = 0; idx < datalen; idx++) {
-        s_a4[tid] = n0;
-        s_a4[tid + kRowThreads] = n1;
-        s_a4[tid + 2 * kRowThreads] = n2;
-        s_a4[tid + 3 * kRowThreads] = n3;
-        if (idx + 1 < datalen) {  // prefetch the next ms while this one transforms
-            const float4* s2 = src + (int64_t)(idx + 1) * P * V4;
-            n0 = ld(s2, 0); n1 = ld(s2, 1); n2 = ld(s2, 2); n3 = ld(s2, 3);
+    auto st = [&](int h, int i, float4 v) {
+        const int e = tid + i * kRowThreads;
+        if (e < V4) s_a4[h * V4 + e] = v;
+    };
+    float4 a0 = ld(0, 0), a1 = ld(0, 1), a2 = ld(0, 2), a3 = ld(0, 3);
+    float4 b0 = ld(1, 0), b1 = ld(1, 1), b2 = ld(1, 2), b3 = ld(1, 3);
+    for (int idx = 0; idx < datalen; idx += 2) {
+        st(0, 0, a0); st(0, 1, a1); st(0, 2, a2); st(0, 3, a3);
+        st(1, 0, b0); st(1, 1, b1); st(1, 2, b2); st(1, 3, b3);
+        if (idx + 2 < datalen) {  // prefetch the next two ms while these transform
+            a0 = ld(idx + 2, 0); a1 = ld(idx + 2, 1); a2 = ld(idx + 2, 2); a3 = ld(idx + 2, 3);
+            b0 = ld(idx + 3, 0); b1 = ld(idx + 3, 1); b2 = ld(idx + 3, 2); b3 = ld(idx + 3, 3);
         }
         __syncthreads();
-        fft2000<1>(s_a, s_tw, tid);
+        fft2000_batch<1, 2>(s_a, s_tw, tid);
+        const bool second = idx + 1 < datalen;
 #pragma unroll
-        for (int i = 0; i < Q; i++) {
-            const int t1 = tid + i * kRowThreads;
-            const float2 v = s_a[t1 < kRow ? t1 : kRow - 1];
+        for (int i = 0; i < Q; i++) {  // the ms in order (acquisition.m:53-61)
+            const int t1 = tid + i * kRowThreads, t = t1 < kRow ? t1 : kRow - 1;
+            const float2 v = s_a[t], w = s_a[kRow + t];
             acc[i] += (v.x * v.x + v.y * v.y) * scale;
+            if (second) acc[i] += (w.x * w.x + w.y * w.y) * scale;
         }
         __syncthreads();
     }
