@@ -56,8 +56,16 @@ def setup_dist(args):
         rank = int(os.environ["RANK"])
         world = int(os.environ["WORLD_SIZE"])
         local = int(os.environ.get("LOCAL_RANK", rank))
+        # rehearsal hooks for a one-GPU box (never set by the driver): every rank on one
+        # device, collectives over gloo
+        if os.environ.get("BENCH_FORCE_DEVICE"):
+            local = int(os.environ["BENCH_FORCE_DEVICE"])
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return rank, world, local, dist
 
 
