@@ -394,6 +394,34 @@ def trackingCT_POS(file, signal, track, Acquired, countinx, *, ctx: Context | No
     return build_tck_result(Acquired, buf, channels, abi.FIELDS_POS), cn0
 
 
+def colon(a: float, d: float, b: float) -> np.ndarray:
+    """MATLAB's a:d:b with MathWorks' published colon construction (both ends toward the
+    midpoint), the values the reference's tap vectors hold (e.g. -0.5:0.1:0.5 of the
+    11-tap ACF, trackingCT_multiCorr-GIVEN.m:25). Same arithmetic as colon_make in
+    csrc/gnss_internal.h."""
+    if d == 0 or (a < b and d < 0) or (b < a and d > 0):
+        return np.zeros(0)
+    tol = 2.0 * 2.220446049250313e-16 * max(abs(a), abs(b))
+    sig = 1.0 if d > 0 else -1.0
+    if a == math.floor(a) and d == 1:
+        n = math.floor(b) - a
+    elif a == math.floor(a) and d == math.floor(d):
+        q = math.floor(a / d)
+        n = math.floor((b - (a - q * d)) / d) - q
+    else:
+        n = round((b - a) / d)  # (b - a)/d is never a half-integer for these ranges
+        if sig * (a + n * d - b) > tol:
+            n -= 1
+    n = int(n)
+    c = a + n * d
+    if sig * (c - b) > -tol:
+        c = b
+    out = np.empty(n + 1)
+    for k in range(n + 1):
+        out[k] = (a + c) / 2 if 2 * k == n else (a + k * d if k <= n // 2 else c - (n - k) * d)
+    return out
+
+
 def ca_code(prn: int) -> np.ndarray:
     """generateCAcode(PRN) as used by the kernels (1023 chips of +-1)."""
     lib = abi.load()

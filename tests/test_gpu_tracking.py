@@ -227,3 +227,25 @@ def test_file_route_positioned_reads(pkg, ctx, opensky_short, tmp_path):
     file.data, file.fileRoute = None, str(p)
     b = pkg.trackingCT(file, signal, track, A, ctx=ctx, raw=True)
     assert np.array_equal(a.rec, b.rec)
+
+
+def test_config5_shape_32_channels_11_taps(pkg, po, ctx):
+    """BASELINE config 5's shape at reduced length: 32 channels (every PRN present), the 11
+    ACF taps -0.5:0.1:0.5, one GPU (the per-step path: the persistent grid is not resident
+    for 32 channels), against the oracle."""
+    from types import SimpleNamespace
+    skip, N1, N10 = 0, 650, 20  # (the bit-edge search needs i >= 600, trackingCT.m:179-204)
+    cfg = pkg.synth.all_prn(32, skip_ms=skip)
+    data = po.synth_if(cfg, 0, (skip + N1 + 19 + N10 + 4) * 58000)
+    file, signal, acq, track = params(pkg, skip, data)
+    track.msToProcessCT_1ms, track.msToProcessCT_10ms = N1, N10
+    cds = [int(round((-cfg.sv[i].code_phase0) % 1023 / (1.023e6 / 58e6))) % 58000 for i in range(32)]
+    A = SimpleNamespace(sv=np.array([cfg.sv[i].prn for i in range(32)]), SNR=np.zeros(32),
+                        Doppler=np.zeros(32), codedelay=np.array(cds),
+                        fineFreq=np.array([4.58e6 + cfg.sv[i].doppler_hz for i in range(32)]))
+    taps = pkg.colon(-0.5, 0.1, 0.5)
+    assert np.array_equal(taps, po.colon(-0.5, 0.1, 0.5))
+    g = pkg.trackingCT(file, signal, track, A, ctx=ctx, taps=taps, raw=True)
+    r = po.trackingCT(file, signal, track, A, taps=taps, raw=True)
+    assert r.status == 0
+    compare(pkg, g, r)
