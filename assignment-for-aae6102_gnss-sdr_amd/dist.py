@@ -59,6 +59,38 @@ def gather_acquired(local, prns_local, world_prns, group=None, device=None):
                            codedelay=rows[:, 3].astype(np.int64), fineFreq=rows[:, 4])
 
 
+def gather_tracking_rows(buf, shards, group=None, device=None):
+    """All-gather only the channel rows each rank tracked (rank r owns shards[r], e.g.
+    shard(nsv, world, r)): every rank sends its own rows of rec / len / countinx / CN0
+    columns (padded to the largest shard) and writes the others' rows into `buf`, which
+    then holds the full result on every rank. Traffic per rank = its own rows, not the
+    whole buffer."""
+    import torch.distributed as dist
+    me = dist.get_rank(group)
+    width = max(len(s) for s in shards)
+    mine = list(shards[me])
+    rec = np.zeros((width,) + buf.rec.shape[1:], dtype=buf.rec.dtype)
+    rec[: len(mine)] = buf.rec[mine]
+    meta = np.zeros((width, 2), dtype=np.int64)
+    meta[: len(mine), 0] = buf.len[mine]
+    meta[: len(mine), 1] = buf.countinx[mine]
+    cn0 = np.zeros((buf.CN0.shape[0], width))
+    cn0[:, : len(mine)] = buf.CN0[:, mine]
+    rows = np.array([buf.c.cn0_rows], dtype=np.int64)
+    parts = zip(_all_gather_array(rec, group, device), _all_gather_array(meta, group, device),
+                _all_gather_array(cn0, group, device))
+    for r, (pr, pm, pc) in enumerate(parts):
+        if r == me:
+            continue
+        ch = list(shards[r])
+        buf.rec[ch] = pr[: len(ch)]
+        buf.len[ch] = pm[: len(ch), 0]
+        buf.countinx[ch] = pm[: len(ch), 1]
+        buf.CN0[:, ch] = pc[:, : len(ch)]
+    buf.c.cn0_rows = int(max(_all_gather_array(rows, group, device))[0])
+    return buf
+
+
 def gather_tracking(buf, nsv: int, group=None, device=None):
     """All-gather the channel rows each rank filled in its TrackOutBuffers.
 

@@ -50,9 +50,11 @@ def _worker(rank, world, port, out_dir):
     chans = D.shard(3, world, rank)
     buf = po.trackingCT(file, signal, track, Aq, channels=chans, nthreads=1, raw=True)
     G = D.gather_tracking(buf, 3)
+    B = D.gather_tracking_rows(buf, [D.shard(3, world, r) for r in range(world)])  # (in place)
     if rank == 0:
         np.savez(os.path.join(out_dir, "dist.npz"), sv=A.sv, codedelay=A.codedelay,
-                 fineFreq=A.fineFreq, SNR=A.SNR, rec=G.rec, len=G.len, countinx=G.countinx, CN0=G.CN0)
+                 fineFreq=A.fineFreq, SNR=A.SNR, rec=G.rec, len=G.len, countinx=G.countinx, CN0=G.CN0,
+                 rec_rows=B.rec, len_rows=B.len, cx_rows=B.countinx, CN0_rows=B.CN0[: B.c.cn0_rows])
     dist.barrier()
     dist.destroy_process_group()
 
@@ -78,3 +80,7 @@ def test_sharded_equals_single_process(tmp_path, pkg, po):
     assert np.array_equal(z["len"], buf.len) and np.array_equal(z["countinx"], buf.countinx)
     assert np.array_equal(z["rec"], buf.rec)  # bit-identical: same oracle, global svindex kept
     assert np.array_equal(z["CN0"], buf.CN0[: buf.c.cn0_rows])
+    # the row-packed gather (each rank sends only its channels) gives the same buffers
+    assert np.array_equal(z["rec_rows"], buf.rec) and np.array_equal(z["len_rows"], buf.len)
+    assert np.array_equal(z["cx_rows"], buf.countinx)
+    assert np.array_equal(z["CN0_rows"], buf.CN0[: buf.c.cn0_rows])
