@@ -647,13 +647,14 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
     const int64_t kf0 = ks + lo;
     const int64_t kf = kf0 < 0 ? 0 : (kf0 > n - 1 ? n - 1 : kf0);
     int cap[NT];
-    double v1[NT], dv[NT];
+    // code values around each tap's boundary as sign bits (bit s set: -1): a0 before it,
+    // a1 after; v1 = a1 and dv = a0 - a1 are rebuilt in the epilogue (2 VGPRs, not 4*NT)
+    unsigned neg0 = 0u, neg1 = 0u;
 #pragma unroll
     for (int s = 0; s < NT; s++) {
         if constexpr ((GNSS_CORR_PROBE & 2) != 0) {
             cap[s] = M - 1 - s;
-            v1[s] = 1.0;
-            dv[s] = (double)(cabits & 1u);
+            neg0 |= (cabits & 1u) << s;
             continue;
         }
         const Colon col{uni(dp->tap_a[s]), d, uni(dp->tap_c[s]), n - 1};
@@ -677,10 +678,8 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
         const unsigned i1 = i0 == 1022u ? 0u : i0 + 1u;
         const unsigned w0 = __shfl(cabits, (int)(i0 >> 5), 64);
         const unsigned w1 = __shfl(cabits, (int)(i1 >> 5), 64);
-        const double a0 = ((w0 >> (i0 & 31)) & 1u) ? -1.0 : 1.0;
-        const double a1 = ((w1 >> (i1 & 31)) & 1u) ? -1.0 : 1.0;
-        v1[s] = a1;
-        dv[s] = a0 - a1;
+        neg0 |= ((w0 >> (i0 & 31)) & 1u) << s;
+        neg1 |= ((w1 >> (i1 & 31)) & 1u) << s;
     }
 
     // ---- carrier base of the lane
@@ -797,8 +796,11 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
     // I = imag(raw .* carrsig), Q = real(raw .* carrsig) (trackingCT.m:107-118)
 #pragma unroll
     for (int s = 0; s < NT; s++) {
-        const double ur = __builtin_fma(dv[s], pre_r[s], v1[s] * run_r);
-        const double ui = __builtin_fma(dv[s], pre_i[s], v1[s] * run_i);
+        const double a0 = ((neg0 >> s) & 1u) ? -1.0 : 1.0;
+        const double v1 = ((neg1 >> s) & 1u) ? -1.0 : 1.0;
+        const double dv = a0 - v1;
+        const double ur = __builtin_fma(dv, pre_r[s], v1 * run_r);
+        const double ui = __builtin_fma(dv, pre_i[s], v1 * run_i);
         oI[s] = __builtin_fma(cb, ui, sb * ur);
         oQ[s] = __builtin_fma(cb, ur, -(sb * ui));
     }
@@ -1227,7 +1229,7 @@ __device__ __forceinline__ void prefetch_raw(const int8_t* iq, int64_t g0, int64
 // exchange only: each block publishes its partial sums and reads everyone's. Block 0
 // of the channel writes the records, C/N0 and, at the end, the state.
 template <int NT, int SUB, bool DIVIDE>
-__global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(3, 3))) void track_run_kernel(const TrkParams* __restrict__ pp,
+__global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT > 3 ? 2 : 3, NT > 3 ? 2 : 3))) void track_run_kernel(const TrkParams* __restrict__ pp,
                                                                const TrkBuffers* __restrict__ bp, int bpc,
                                                                int nsteps, unsigned tag0)
 {
