@@ -9,7 +9,7 @@ directory name is not a Python identifier).
 """
 from . import abi, synth
 from .sdr import (Context, DeviceRecord, StructArray, TrackOutBuffers, acquisition, ca_code, colon,
-                  default_context, initParameters, trackingCT, trackingCT_POS)
+                  default_context, initParameters, naviDecode_updated, trackingCT, trackingCT_POS)
 
 __all__ = ["abi", "synth", "Context", "DeviceRecord", "StructArray", "TrackOutBuffers",
-           "acquisition", "ca_code", "colon", "default_context", "initParameters", "trackingCT", "trackingCT_POS"]
+           "acquisition", "ca_code", "colon", "default_context", "initParameters", "naviDecode_updated", "trackingCT", "trackingCT_POS"]

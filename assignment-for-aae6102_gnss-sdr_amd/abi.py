@@ -26,6 +26,20 @@ FIELDS_POS = ["P_i", "P_q", "E_i", "E_q", "L_i", "L_q", "carrError", "codeError"
               "numSample", "delayValue", "absoluteSample", "codedelay2"]
 
 
+# ephemeris(prn) fields of naviDecode_updated.m (ini_eph.m order; updateflag separate)
+EPH_FIELDS = ["TOW", "TOW1", "sfb", "sfb1", "weeknum", "N", "health", "IODC", "TGD", "toc", "af2",
+              "af1", "af0", "IODE2", "Crs", "deltan", "M0", "Cuc", "ecc", "Cus", "sqrta", "toe", "Cic",
+              "omegae", "Cis", "i0", "Crc", "w", "omegadot", "IODE3", "idot", "updatetime",
+              "updatetime_tow"]
+EPH_NFIELDS = len(EPH_FIELDS)
+
+
+class GnssNavOut(C.Structure):
+    _fields_ = [("eph_cap", C.c_int32), ("eph", C.POINTER(C.c_double)),
+                ("eph_len", C.POINTER(C.c_int32)), ("updateflag", C.POINTER(C.c_int32)),
+                ("nav1", C.POINTER(C.c_int64)), ("sfb1", C.POINTER(C.c_int64))]
+
+
 class GnssFile(C.Structure):
     _fields_ = [("path", C.c_char_p), ("data", C.c_void_p), ("dev_data", C.c_void_p),
                 ("nbytes", C.c_uint64), ("skip", C.c_int64), ("dataType", C.c_int32),
@@ -113,6 +127,8 @@ PROTOTYPES = {
     "gnss_tracking_ct_pos": (C.c_int, [C.c_void_p, C.POINTER(GnssFile), C.POINTER(GnssSignal),
                                        C.POINTER(GnssTrack), C.POINTER(GnssAcquired), C.c_int32,
                                        C.POINTER(C.c_int32), C.POINTER(GnssTrackOut)]),
+    "gnss_navi_decode": (C.c_int, [C.POINTER(GnssAcquired), C.POINTER(C.c_double),
+                                   C.POINTER(C.c_int64), C.c_int64, C.POINTER(GnssNavOut)]),
     "gnss_ca_code": (C.c_int, [C.c_int, C.c_void_p]),
     "gnss_correlate_step": (C.c_int, [C.c_void_p, C.POINTER(GnssFile), C.POINTER(GnssSignal),
                                       C.c_int, C.c_int, C.c_double, C.c_double, C.c_double,

@@ -6,6 +6,8 @@
                                                                    trackingCT.m:1
     [TckResultCT_pos, CN0_CT] = trackingCT_POS(file, signal, track, Acquired, countinx)
                                    tracking loop of trackingCT_POS_updated.m:1-413
+    [ephemeris, ALLTckResult, for_prest] = naviDecode_updated(Acquired, ALLTckResult)
+                                                                   naviDecode_updated.m:1
 
 Same names, same struct fields, same argument meaning; the work happens in the
 HIP C-ABI library (abi.py). Differences forced by the language are documented
@@ -392,6 +394,63 @@ def trackingCT_POS(file, signal, track, Acquired, countinx, *, ctx: Context | No
         return buf
     cn0 = buf.CN0[: buf.c.cn0_rows].copy()
     return build_tck_result(Acquired, buf, channels, abi.FIELDS_POS), cn0
+
+
+def naviDecode_updated(Acquired, ALLTckResult, *, eph_cap: int = 512):
+    """naviDecode_updated.m:1-253 -> (ephemeris, ALLTckResult, for_prest).
+
+    ALLTckResult(prn).P_i is read for every PRN of Acquired.sv, in that order (the
+    reference's channel order matters: its bit arrays carry over between channels).
+    ephemeris(prn) has the ini_eph.m fields as row vectors plus updateflag; for_prest.nav1
+    / for_prest.sfb1 are indexed by PRN like the MATLAB vectors (nav1 has max(sv) entries,
+    sfb1 ends at the last PRN that decoded a subframe 1). ALLTckResult is returned as given
+    with .sfb1 added per PRN (the reference's second output). Host code (csrc/navdecode.cpp).
+    """
+    lib = abi.load()
+    sv = [int(x) for x in Acquired.sv]
+    n = len(sv)
+    series = [np.ascontiguousarray(ALLTckResult(p).P_i, dtype=np.float64).ravel() for p in sv]
+    stride = max(len(x) for x in series)
+    P = np.zeros((n, stride))
+    for i, x in enumerate(series):
+        P[i, : len(x)] = x
+    lens = np.array([len(x) for x in series], dtype=np.int64)
+    eph = np.zeros((n, abi.EPH_NFIELDS, eph_cap))
+    elen = np.zeros((n, abi.EPH_NFIELDS), dtype=np.int32)
+    upd = np.zeros(n, dtype=np.int32)
+    nav1 = np.zeros(n, dtype=np.int64)
+    sfb1 = np.zeros(n, dtype=np.int64)
+    o = abi.GnssNavOut()
+    o.eph_cap = eph_cap
+    o.eph = eph.ctypes.data_as(C.POINTER(C.c_double))
+    o.eph_len = elen.ctypes.data_as(C.POINTER(C.c_int32))
+    o.updateflag = upd.ctypes.data_as(C.POINTER(C.c_int32))
+    o.nav1 = nav1.ctypes.data_as(C.POINTER(C.c_int64))
+    o.sfb1 = sfb1.ctypes.data_as(C.POINTER(C.c_int64))
+    a = to_c_acquired(Acquired)
+    st = lib.gnss_navi_decode(C.byref(a), P.ctypes.data_as(C.POINTER(C.c_double)),
+                              lens.ctypes.data_as(C.POINTER(C.c_int64)), stride, C.byref(o))
+    if st != abi.OK:
+        raise abi.GnssError(st, "gnss_navi_decode")
+    entries = {}
+    for i, p in enumerate(sv):
+        e = SimpleNamespace(**{f: eph[i, k, : elen[i, k]].copy() for k, f in enumerate(abi.EPH_FIELDS)})
+        e.updateflag = int(upd[i])
+        entries[p] = e
+    n1 = np.zeros(max(sv), dtype=np.int64)
+    for i, p in enumerate(sv):
+        n1[p - 1] = nav1[i]
+    have = [p for i, p in enumerate(sv) if sfb1[i]]
+    s1 = np.zeros(max(have) if have else 0, dtype=np.int64)
+    for i, p in enumerate(sv):
+        if sfb1[i]:
+            s1[p - 1] = sfb1[i]
+    for i, p in enumerate(sv):
+        try:
+            ALLTckResult(p).sfb1 = entries[p].sfb1.copy()
+        except (AttributeError, TypeError):
+            pass
+    return StructArray(entries), ALLTckResult, SimpleNamespace(nav1=n1, sfb1=s1)
 
 
 def colon(a: float, d: float, b: float) -> np.ndarray:

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define GNSS_ABI_VERSION 3
+#define GNSS_ABI_VERSION 4
 
 /* ---- status codes (SURVEY §8b "Error conventions") --------------------- */
 #define GNSS_OK         0
@@ -241,6 +241,36 @@ int gnss_tracking_ct(gnss_ctx *ctx, const gnss_file *file, const gnss_signal *si
 int gnss_tracking_ct_pos(gnss_ctx *ctx, const gnss_file *file, const gnss_signal *signal,
                          const gnss_track *track, const gnss_acquired *acquired, int32_t ctPOS,
                          const int32_t *countinx, gnss_track_out *out);
+
+/* ---- naviDecode_updated.m ---------------------------------
+ * Navigation-bit decode on the tracking output: bit synchronisation of P_i, preamble
+ * search, parity (paritychk_James.m) and subframe 1-3 fields (bin2dec_GPSSDR.m,
+ * comp2dec.m), with the reference's behaviour kept (repeat decodes are appended; bit
+ * arrays carry over between channels — see csrc/navdecode.cpp).
+ * Replaces [ephemeris, ~, for_prest] = naviDecode_updated(Acquired, ALLTckResult)
+ * (naviDecode_updated.m:1, called at SDR_main.m:54). Channel c's ephemeris(prn) is
+ * eph[c][field][0 .. eph_len[c][field]), prn = acquired->sv[c]. Host code (no GPU). */
+enum gnss_eph_field {
+    GNSS_E_TOW = 0, GNSS_E_TOW1, GNSS_E_sfb, GNSS_E_sfb1, GNSS_E_weeknum, GNSS_E_N, GNSS_E_health,
+    GNSS_E_IODC, GNSS_E_TGD, GNSS_E_toc, GNSS_E_af2, GNSS_E_af1, GNSS_E_af0, GNSS_E_IODE2, GNSS_E_Crs,
+    GNSS_E_deltan, GNSS_E_M0, GNSS_E_Cuc, GNSS_E_ecc, GNSS_E_Cus, GNSS_E_sqrta, GNSS_E_toe, GNSS_E_Cic,
+    GNSS_E_omegae, GNSS_E_Cis, GNSS_E_i0, GNSS_E_Crc, GNSS_E_w, GNSS_E_omegadot, GNSS_E_IODE3,
+    GNSS_E_idot, GNSS_E_updatetime, GNSS_E_updatetime_tow,
+    GNSS_EPH_NFIELDS
+};
+
+typedef struct gnss_nav_out {
+    int32_t  eph_cap;     /* values per field per channel (GNSS_EARG if one overflows) */
+    double  *eph;         /* [nsv][GNSS_EPH_NFIELDS][eph_cap]                            */
+    int32_t *eph_len;     /* [nsv][GNSS_EPH_NFIELDS]                                     */
+    int32_t *updateflag;  /* [nsv] ephemeris(prn).updateflag                             */
+    int64_t *nav1;        /* [nsv] for_prest.nav1(prn): first P_i index of the bit stream */
+    int64_t *sfb1;        /* [nsv] for_prest.sfb1(prn): first subframe 1 (0 if none)      */
+} gnss_nav_out;
+
+/* P_i of channel c at P_i[c*stride + k], k < len[c] (TckResultCT(sv[c]).P_i). */
+int gnss_navi_decode(const gnss_acquired *acquired, const double *P_i, const int64_t *len,
+                     int64_t stride, gnss_nav_out *out);
 
 /* Per-step parity hook: ONE trackingCT correlation step (trackingCT.m:79-118: numSample
  * from remChip/codeFreq, E/P/L or ACF replicas, carrier wipe, sums; no negation, no

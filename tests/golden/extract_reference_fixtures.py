@@ -8,6 +8,12 @@ are data (inputs + expected outputs), committed under tests/golden/:
                                (output of trackingCT_POS_updated.m on the real Opensky IF):
                                NCO state for steps 1..60 and 989..1100, discriminator
                                inputs, and carrError/codeError for steps 1..1100.
+  ref_navdecode_Opensky_90.npz the naviDecode_updated.m case: INPUT = the signs of the
+                               eight TckResult_Eph(prn).P_i series of the 90-s trackingCT
+                               run embedded in SDR/task3.fig (the decode uses P_i only
+                               through sign and >= 0, naviDecode_updated.m:43-74), and its
+                               OUTPUT from the same run, eph_Opensky_90.mat (ephemeris
+                               arrays) and sbf_Opensky_90.mat (nav1, sfb1).
 
 Only scipy.io.loadmat (a MAT-v5 parser that executes nothing) is used.
 """
@@ -56,5 +62,71 @@ def main():
     print("prns", prns, "wrote fixtures")
 
 
+def fig_series(path):
+    """YData/XData float arrays of a MATLAB .fig (SURVEY App. B recipe: the figure's
+    __function_workspace__ re-framed as a MAT-file and read with scipy's MAT-v5 reader)."""
+    import io
+    from scipy.io.matlab._mio5 import MatFile5Reader
+    m = sio.loadmat(path, squeeze_me=False)
+    ws = m["__function_workspace__"].tobytes()
+    buf = b"MATLAB 5.0 MAT-file".ljust(116) + b"\0" * 8 + ws[:4] + ws[8:]
+    r = MatFile5Reader(io.BytesIO(buf), squeeze_me=False)
+    r.mat_stream.seek(128)
+    r.initialize_read()
+    found = []
+
+    def walk(x):
+        if isinstance(x, np.ndarray):
+            if x.dtype == object:
+                for e in x.ravel():
+                    walk(e)
+            elif x.dtype.names:
+                for nm in x.dtype.names:
+                    for e in x[nm].ravel():
+                        walk(e)
+            elif 90000 < x.size < 92000 and x.dtype.kind == "f":
+                found.append(x.ravel())
+    while True:
+        try:
+            hdr, nxt = r.read_var_header()
+        except Exception:
+            break
+        try:
+            walk(r.read_var_array(hdr, process=True))
+        except Exception:
+            pass
+        r.mat_stream.seek(nxt)
+    return found
+
+
+def navdecode_fixture():
+    prns = [3, 4, 16, 22, 26, 27, 31, 32]
+    found = fig_series(os.path.join(REF, "task3.fig"))
+    # children in reverse plot order (PRN 32 first), each as an (XData, YData) pair
+    series = {}
+    for i, p in enumerate(reversed(prns)):
+        a, b = found[2 * i], found[2 * i + 1]
+        series[p] = b if np.array_equal(a, np.arange(1, len(a) + 1)) else a
+    lens = np.array([len(series[p]) for p in prns])
+    signs = np.zeros((len(prns), lens.max()), dtype=np.int8)
+    for i, p in enumerate(prns):
+        signs[i, : lens[i]] = np.sign(series[p]).astype(np.int8)
+    eph = sio.loadmat(os.path.join(REF, "eph_Opensky_90.mat"), squeeze_me=True, struct_as_record=False)["eph"]
+    sbf = sio.loadmat(os.path.join(REF, "sbf_Opensky_90.mat"), squeeze_me=True, struct_as_record=False)["sbf"]
+    out = {"prns": np.array(prns), "P_i_sign": signs, "len": lens,
+           "nav1": np.array([np.atleast_1d(sbf.nav1)[p - 1] for p in prns]),
+           "sfb1": np.array([np.atleast_1d(sbf.sfb1)[p - 1] if p <= np.atleast_1d(sbf.sfb1).size else 0
+                             for p in prns])}
+    fields = eph[prns[0] - 1]._fieldnames
+    for p in prns:
+        e = eph[p - 1]
+        for fn in fields:
+            out[f"eph_{p}_{fn}"] = np.atleast_1d(np.asarray(getattr(e, fn), dtype=np.float64)).ravel()
+    np.savez_compressed(os.path.join(HERE, "ref_navdecode_Opensky_90.npz"), **out)
+
+
 if __name__ == "__main__":
+    if "--navdecode" in sys.argv:
+        navdecode_fixture()
+        sys.exit(0)
     sys.exit(main())

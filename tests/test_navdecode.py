@@ -1,0 +1,62 @@
+"""naviDecode_updated.m against the reference's own output.
+
+Input: the eight TckResult_Eph(prn).P_i series of the reference's 90-s trackingCT run
+(embedded in SDR/task3.fig; their signs, which is all the decode reads). Expected: the
+files that same run saved, eph_Opensky_90.mat and sbf_Opensky_90.mat (SDR_main.m:54-56),
+extracted by tests/golden/extract_reference_fixtures.py --navdecode. Every ephemeris
+array (repeats included), updateflag, nav1 and sfb1 must match exactly. Host code: no GPU.
+"""
+import os
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+
+@pytest.fixture(scope="module")
+def ref():
+    return np.load(os.path.join(GOLDEN, "ref_navdecode_Opensky_90.npz"))
+
+
+def _inputs(pkg, z):
+    prns = [int(p) for p in z["prns"]]
+    A = SimpleNamespace(sv=np.array(prns), SNR=np.zeros(8), Doppler=np.zeros(8),
+                        codedelay=np.zeros(8, dtype=np.int64), fineFreq=np.zeros(8))
+    T = pkg.StructArray({p: SimpleNamespace(P_i=z["P_i_sign"][i, : z["len"][i]].astype(np.float64))
+                         for i, p in enumerate(prns)})
+    return prns, A, T
+
+
+def test_navdecode_matches_reference_eph_and_sbf(pkg, ref):
+    prns, A, T = _inputs(pkg, ref)
+    eph, T2, for_prest = pkg.naviDecode_updated(A, T)
+    for i, p in enumerate(prns):
+        assert for_prest.nav1[p - 1] == ref["nav1"][i], p
+        assert (for_prest.sfb1[p - 1] if p <= len(for_prest.sfb1) else 0) == ref["sfb1"][i], p
+        e = eph(p)
+        for f in pkg.abi.EPH_FIELDS:
+            want = ref[f"eph_{p}_{f}"]
+            got = getattr(e, f)
+            assert got.shape == want.shape, (p, f, got.shape, want.shape)
+            assert np.array_equal(got, want), (p, f)
+        want_flag = ref[f"eph_{p}_updateflag"]
+        assert e.updateflag == (int(want_flag[0]) if want_flag.size else 0), p
+    # MATLAB vector lengths of for_prest: nav1 up to max(sv), sfb1 up to the last PRN with a
+    # subframe 1 (31 here: PRN 32 decoded none)
+    assert len(for_prest.nav1) == 32 and len(for_prest.sfb1) == 31
+
+
+def test_navdecode_channel_order_matters(pkg, ref):
+    """The bit arrays carry over between channels (naviDecode_updated.m never clears
+    NaviData / NaviDataXOR): PRN 4 decoded on its own yields no subframe, while after PRN 3
+    (the reference run's order) it yields the 66 subframes eph_Opensky_90.mat holds."""
+    prns, A, T = _inputs(pkg, ref)
+    alone = SimpleNamespace(sv=np.array([4]), SNR=np.zeros(1), Doppler=np.zeros(1),
+                            codedelay=np.zeros(1, dtype=np.int64), fineFreq=np.zeros(1))
+    e1, _, f1 = pkg.naviDecode_updated(alone, T)
+    eall, _, fall = pkg.naviDecode_updated(A, T)
+    assert f1.nav1[3] == fall.nav1[3] == ref["nav1"][1]
+    assert len(e1(4).TOW) == 0
+    assert len(eall(4).TOW) == len(ref["eph_4_TOW"]) == 66
