@@ -13,7 +13,9 @@ are data (inputs + expected outputs), committed under tests/golden/:
                                run embedded in SDR/task3.fig (the decode uses P_i only
                                through sign and >= 0, naviDecode_updated.m:43-74), and its
                                OUTPUT from the same run, eph_Opensky_90.mat (ephemeris
-                               arrays) and sbf_Opensky_90.mat (nav1, sfb1).
+                               arrays) and sbf_Opensky_90.mat (nav1, sfb1); and the 40-s
+                               run's eph/sbf_Opensky_40.mat (its P_i = the first 1000 +
+                               countinx + 40000 values of the same series).
 
 Only scipy.io.loadmat (a MAT-v5 parser that executes nothing) is used.
 """
@@ -122,6 +124,19 @@ def navdecode_fixture():
         e = eph[p - 1]
         for fn in fields:
             out[f"eph_{p}_{fn}"] = np.atleast_1d(np.asarray(getattr(e, fn), dtype=np.float64)).ravel()
+    # the 40-s run (msToProcessCT_10ms = 40000) tracked the same IF with the same code: its
+    # P_i are the first 1000 + countinx + 40000 values of the 90-s series; expected outputs
+    # eph_Opensky_40.mat / sbf_Opensky_40.mat
+    eph40 = sio.loadmat(os.path.join(REF, "eph_Opensky_40.mat"), squeeze_me=True, struct_as_record=False)["eph"]
+    sbf40 = sio.loadmat(os.path.join(REF, "sbf_Opensky_40.mat"), squeeze_me=True, struct_as_record=False)["sbf"]
+    cx = np.atleast_1d(sio.loadmat(os.path.join(REF, "countinx.mat"), squeeze_me=True)["countinx"]).astype(int)
+    out["len40"] = np.array([1000 + cx[i] + 40000 for i in range(len(prns))])
+    out["nav1_40"] = np.array([np.atleast_1d(sbf40.nav1)[p - 1] for p in prns])
+    s40 = np.atleast_1d(sbf40.sfb1)
+    out["sfb1_40"] = np.array([s40[p - 1] if p <= s40.size else 0 for p in prns])
+    for p in prns:
+        for fn in fields:
+            out[f"eph40_{p}_{fn}"] = np.atleast_1d(np.asarray(getattr(eph40[p - 1], fn), dtype=np.float64)).ravel()
     np.savez_compressed(os.path.join(HERE, "ref_navdecode_Opensky_90.npz"), **out)
 
 
