@@ -43,8 +43,28 @@ struct gnss_ctx {
     // device scratch kept across calls (hipMalloc/hipFree per call cost ~1 ms and hipFree
     // synchronises): name -> (pointer, bytes)
     std::map<std::string, std::pair<void*, size_t>> pool;
+    // pinned host staging kept across calls (the per-step records' download): name ->
+    // (pointer, bytes); a pageable std::vector re-faults and bounces every call
+    std::map<std::string, std::pair<void*, size_t>> pinned;
     int64_t acq_tw_S = 0;  // the acquisition twiddle tables in the pool are for this S
 };
+
+namespace {
+// The context's pinned host buffer `key`, at least `bytes` (contents undefined).
+template <class T>
+T* pinned_buffer(gnss_ctx* ctx, const char* key, size_t count)
+{
+    auto& e = ctx->pinned[key];
+    const size_t want = std::max<size_t>(count * sizeof(T), 16);
+    if (e.second < want) {
+        if (e.first) (void)hipHostFree(e.first);
+        e = {nullptr, 0};
+        if (hipHostMalloc(&e.first, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+        e.second = want;
+    }
+    return static_cast<T*>(e.first);
+}
+}  // namespace
 
 namespace {
 
@@ -352,6 +372,8 @@ void gnss_ctx_destroy(gnss_ctx* ctx)
     if (ctx->fft_work) (void)hipFree(ctx->fft_work);
     for (auto& kv : ctx->pool)
         if (kv.second.first) (void)hipFree(kv.second.first);
+    for (auto& kv : ctx->pinned)
+        if (kv.second.first) (void)hipHostFree(kv.second.first);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -1127,11 +1149,14 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
     // results
     if (hp) fprintf(stderr, "hostprof kernels done %.3f ms\n", hms());
     HIP_TRY(hipMemcpyAsync(chh.data(), d_chan.p, sizeof(TrkChan) * nch, hipMemcpyDeviceToHost, ctx->stream));
-    std::vector<double> rec((size_t)nch * P.rec_cap * GNSS_NFIELDS);
-    std::vector<double> tp(out->taps ? (size_t)nch * P.rec_cap * 2 * ntaps : 0);
+    const size_t nrec = (size_t)nch * P.rec_cap * GNSS_NFIELDS;
+    const size_t ntp = out->taps ? (size_t)nch * P.rec_cap * 2 * ntaps : 0;
+    double* rec = pinned_buffer<double>(ctx, "trk.h_rec", nrec);
+    double* tp = ntp ? pinned_buffer<double>(ctx, "trk.h_taps", ntp) : nullptr;
+    if (!rec || (ntp && !tp)) return fail(ctx, GNSS_EDEVICE, "hipHostMalloc of the record staging failed");
     std::vector<double> cn1((size_t)nch * P.cn0_cap), cn10((size_t)nch * P.cn0_cap);
-    HIP_TRY(hipMemcpyAsync(rec.data(), d_rec.p, rec.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
-    if (out->taps) HIP_TRY(hipMemcpyAsync(tp.data(), d_taps.p, tp.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(rec, d_rec.p, nrec * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    if (out->taps) HIP_TRY(hipMemcpyAsync(tp, d_taps.p, ntp * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipMemcpyAsync(cn1.data(), d_cn1.p, cn1.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipMemcpyAsync(cn10.data(), d_cn10.p, cn10.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
@@ -1170,12 +1195,12 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
         int64_t stride;
         if (f < nrf) {
             dst = out->rec + ((int64_t)c * GNSS_NFIELDS + f) * ML;
-            src = rec.data() + (size_t)i * P.rec_cap * GNSS_NFIELDS + f;
+            src = rec + (size_t)i * P.rec_cap * GNSS_NFIELDS + f;
             stride = GNSS_NFIELDS;
         } else {
             const int tq = f - nrf, sidx = tq / 2, iq = tq % 2;
             dst = out->taps + (((int64_t)c * 2 + iq) * ntaps + sidx) * ML;
-            src = tp.data() + (size_t)i * P.rec_cap * 2 * ntaps + tq;
+            src = tp + (size_t)i * P.rec_cap * 2 * ntaps + tq;
             stride = 2 * ntaps;
         }
         for (int64_t k = 0; k < n1; k++) dst[k] = src[k * stride];
