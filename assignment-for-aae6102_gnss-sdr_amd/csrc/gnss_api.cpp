@@ -787,6 +787,15 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
     };
     coef(tr->DLLBW, tr->DLLDamp, tr->DLLGain, P.tau1code, P.tau2code);
     coef(tr->PLLBW, tr->PLLDamp, tr->PLLGain, P.tau1carr, P.tau2carr);
+    {   // the loop filters' constant quotients (device: loop_update_i); T as the kernel forms it
+        const double T1 = pos ? sg->ms : 0.001 * 1, T10 = pos ? sg->ms : 0.001;
+        P.dll_r = P.tau2code / P.tau1code;
+        P.pll_r = P.tau2carr / P.tau1carr;
+        P.dll_t1 = T1 / P.tau1code;
+        P.dll_t10 = T10 / P.tau1code;
+        P.pll_t1 = T1 / P.tau1carr;
+        P.pll_t10 = T10 / P.tau1carr;
+    }
     P.Fs = sg->Fs;
     P.codeFreqBasis = sg->codeFreqBasis;
     P.ms = sg->ms;

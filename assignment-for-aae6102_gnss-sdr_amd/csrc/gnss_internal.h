@@ -153,6 +153,9 @@ struct TrkParams {
     // by ceil, prompt replica Code(ceil(t + 0.05) + 1), codeFreq = f0 + codeNco, loop T =
     // signal.ms for every pdi, Index + 1 per step, no phase-C negation or re-seek,
     // codedelay from the channel's own delayValue row)
+    // loop-filter quotients of trackingCT.m:140,147 (T_POS_updated.m:257,266), IEEE on the
+    // host: tau2/tau1, and T/tau1 for pdi 1 and for the 10-ms steps (T = 1 ms in both)
+    double dll_r, dll_t1, dll_t10, pll_r, pll_t1, pll_t10;
     int32_t conv;
     // added to a tap's colon element before ceil (the +0.05 of trackingCT_POS_updated.m:216)
     double tap_post[GNSS_MAX_TAPS];

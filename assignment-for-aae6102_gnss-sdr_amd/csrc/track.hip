@@ -154,33 +154,54 @@ __device__ __forceinline__ double rem_2pi(double x)
     return r;
 }
 
-// numSample / remSample / delayValue of the step that follows state `c`
-// (trackingCT.m:79-82 / :411-415).
+// numSample / delayValue of the step that follows state `c` (trackingCT.m:79-82 /
+// :411-415; trackingCT_POS_updated.m:188-191 with ceil). The quotient q =
+// fl(num / cps) is only rounded, so it is taken from num * (1/cps) (a refined reciprocal,
+// within a few ulp of q) unless that lands within 1e-7 of a rounding boundary (.5 for
+// round, an integer for ceil), where the IEEE division decides: the same n, without a
+// division on the critical path. remSample (a record field only) is step_rem_sample().
 struct StepSize {
-    double cps, remSample;
+    double cps, inv_cps;
     int64_t n, dv;
 };
+
+// 1/x to about 1 ulp: hardware reciprocal and two Newton steps (the lanes' boundary search
+// only needs 1e-9 relative; exactness never depends on it)
+__device__ __forceinline__ double fast_rcp(double x)
+{
+    double r = __builtin_amdgcn_rcp(x);
+    double e = __builtin_fma(-x, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-x, r, 1.0);
+    return __builtin_fma(r, e, r);
+}
 
 __device__ __forceinline__ StepSize step_size(const TrkParams& p, const NcoState& c, int pdi, int phaseC)
 {
     StepSize z;
     z.cps = c.codeFreq / p.Fs;
-    if (p.conv) {  // trackingCT_POS_updated.m:188-191 / :304-307 (ceil; no remSample)
-        z.remSample = 0.0;
-        z.n = (int64_t)ceil((p.codelength * pdi - c.remChip) / z.cps);
+    z.inv_cps = fast_rcp(z.cps);
+    const double num = p.codelength * pdi - c.remChip;
+    const double qa = num * z.inv_cps;
+    if (p.conv) {  // ceil
+        z.n = fabs(qa - rint(qa)) > 1e-7 ? (int64_t)ceil(qa) : (int64_t)ceil(num / z.cps);
         z.dv = z.n - (int64_t)(p.S * pdi);
         return z;
     }
-    if (phaseC) {
-        z.dv = c.numSample - (int64_t)(p.S * pdi);                      // :411
-        z.remSample = (p.codelength * pdi - c.remChip) / z.cps;          // :414
-        z.n = (int64_t)round((p.codelength * pdi - c.remChip) / z.cps);  // :415
-    } else {
-        z.remSample = (p.codelength - c.remChip) / z.cps;                // :79
-        z.n = (int64_t)round((p.codelength * pdi - c.remChip) / z.cps);  // :80
-        z.dv = z.n - (int64_t)(p.S * pdi);                               // :82
-    }
+    // round (half away from zero; q > 0)
+    const double fr = qa - floor(qa);
+    z.n = fabs(fr - 0.5) > 1e-7 ? (int64_t)floor(qa + 0.5) : (int64_t)round(num / z.cps);
+    z.dv = phaseC ? c.numSample - (int64_t)(p.S * pdi)  // :411 (the previous step's numSample)
+                  : z.n - (int64_t)(p.S * pdi);         // :82
     return z;
+}
+
+// remSample of the step (trackingCT.m:79 / :414), for the record
+__device__ __forceinline__ double step_rem_sample(const TrkParams& p, const NcoState& c, int pdi, int phaseC)
+{
+    if (p.conv) return 0.0;  // (trackingCT_POS_updated.m has none)
+    const double cps = c.codeFreq / p.Fs;
+    return phaseC ? (p.codelength * pdi - c.remChip) / cps : (p.codelength - c.remChip) / cps;
 }
 
 // Prepare the descriptor of the step that follows state `c` (trackingCT.m:79-107 /
@@ -232,6 +253,8 @@ __device__ __forceinline__ void prepare_desc_i(const TrkParams& p, const NcoStat
         if (lane == 63) {
             // remPhase = rem(Wave(numSample+1), 2*pi) (:104-106)
             d->remPhase_next = rem_2pi(kTwoPi * (c.carrierFreq * ((double)n / p.Fs)) + c.remPhase);
+        } else if (lane == 62) {
+            d->remSample = step_rem_sample(p, c, pdi, phaseC);  // (off the code role's path)
         }
         return;
     }
@@ -296,9 +319,8 @@ __device__ __forceinline__ void prepare_desc_i(const TrkParams& p, const NcoStat
         d->g_first = A >> 3;
         d->g_last = (A + n - 1) >> 3;
         d->Index = c.Index;
-        d->remSample = z.remSample;
         d->d = cps;
-        d->inv_d = 1.0 / cps;
+        d->inv_d = z.inv_cps;
         d->pdi = pdi;
         d->phaseC = phaseC;
         d->bad = badw;
@@ -381,16 +403,17 @@ __device__ __forceinline__ LoopUpd loop_update_i(const TrkParams& p, const TrkCh
         const double E = sqrt(E_i * E_i + E_q * E_q);
         const double L = sqrt(L_i * L_i + L_q * L_q);
         u.DLLdiscri = 0.5 * (E - L) / (E + L);
-        u.code_output = c.code_outputLast + (p.tau2code / p.tau1code) * (u.DLLdiscri - c.DLLdiscriLast) +
-                        u.DLLdiscri * (T / p.tau1code);
+        // (tau2/tau1 and T/tau1 are the host's IEEE quotients, TrkParams.dll_*)
+        const double tq = pdi == 1 ? p.dll_t1 : (phaseC || p.conv) ? p.dll_t10 : T / p.tau1code;
+        u.code_output = c.code_outputLast + p.dll_r * (u.DLLdiscri - c.DLLdiscriLast) + u.DLLdiscri * tq;
         // trackingCT_POS_updated.m:262: codeFreq = codeFreqBasis + codeNco
         u.codeFreq = p.conv ? p.codeFreqBasis + u.code_output : p.codeFreqBasis - u.code_output;
     }
     if (which & 2) {
         u.PLLdiscri = atan_tab(P_q / P_i) / kTwoPi;
         u.carrier_output = c.carrier_outputLast +
-                           (p.tau2carr / p.tau1carr) * (u.PLLdiscri - c.PLLdiscriLast) +
-                           u.PLLdiscri * (T / p.tau1carr);
+                           p.pll_r * (u.PLLdiscri - c.PLLdiscriLast) +
+                           u.PLLdiscri * (pdi == 1 ? p.pll_t1 : (phaseC || p.conv) ? p.pll_t10 : T / p.tau1carr);
         u.carrierFreq = c.carrierFreqBasis + u.carrier_output;
     }
     return u;
