@@ -890,19 +890,24 @@ __device__ __forceinline__ double block_partial(double* s_mem, const double (&oI
     return a;
 }
 
-// Channel: the sum over the bpc block partials of value v = tid >> 3 (tid < 8*NV): lane
-// q = tid & 7 adds blocks q, q+8, ... in order, then a DPP butterfly over the 8 lanes.
-// Every lane of the 8 returns the sum. load(k, v) = block k's partial of value v.
-template <class Load>
+// Channel: the sum over the bpc block partials of value v = tid / L (tid < L*NV, L = 16
+// lanes per value where 16*NV fits the block, else 8): lane q = tid % L adds blocks q,
+// q+L, ... in order, then a DPP butterfly over the L lanes. Every lane of the L returns the
+// sum. load(k, v) = block k's partial of value v.
+template <int NV> constexpr int chan_lanes() { return 16 * NV <= kTrkThreads ? 16 : 8; }
+
+template <int NV, class Load>
 __device__ __forceinline__ double channel_sum(int bpc, int tid, Load load)
 {
-    const int v = tid >> 3, q = tid & 7;
+    constexpr int L = chan_lanes<NV>();
+    const int v = tid / L, q = tid % L;
     double a = 0.0;
 #pragma unroll 4
-    for (int k = q; k < bpc; k += 8) a += load(k, v);
+    for (int k = q; k < bpc; k += L) a += load(k, v);
     a += dpp_f64<0xB1>(a);   // quad_perm [1,0,3,2]
     a += dpp_f64<0x4E>(a);   // quad_perm [2,3,0,1]
     a += dpp_f64<0x141>(a);  // row_half_mirror: the other quad of the 8
+    if constexpr (L == 16) a += dpp_f64<0x140>(a);  // row_mirror: the other 8 of the 16
     return a;
 }
 
@@ -1025,8 +1030,9 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(const TrkParams
     // ---- last arriver: deterministic reduction of all block partials (sc1 loads)
     if (srow && tid == 0) stamp_max(srow, 3, wall_clock64());
     double csum = 0.0;
-    if (tid < 8 * NV)
-        csum = channel_sum(bpc, tid, [&](int k, int v) { return ld_sc1(allp + (int64_t)k * NV + v); });
+    constexpr int CL = chan_lanes<NV>();
+    if (tid < CL * NV)
+        csum = channel_sum<NV>(bpc, tid, [&](int k, int v) { return ld_sc1(allp + (int64_t)k * NV + v); });
     // the step's values the writers need, read before the next descriptor replaces them
     StepOut o;
     o.n = dp->n;
@@ -1037,8 +1043,8 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(const TrkParams
     o.pdi = dp->pdi;
     o.phaseC = dp->phaseC;
     const bool dbg = b.dbg_sums || (p.probe & 1);
-    if (tid < 8 * NV && (tid & 7) == 0) {
-        const int v = tid >> 3;
+    if (tid < CL * NV && tid % CL == 0) {
+        const int v = tid / CL;
         if (dbg) {
             if (b.dbg_sums) b.dbg_sums[ch * NV + v] = csum;
         } else {
@@ -1413,15 +1419,16 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
                 prefetch_raw<SUB>(iq, ((A + n) >> 3) + ((int64_t)blk * T + h * 64 + lane) * SUB, gmax, s_raw,
                                   h * 64 + lane);
         }
-        if (tid < 8 * NV) {
-            const double a = channel_sum(bpc, tid, [&](int k, int v) {
+        constexpr int CL = chan_lanes<NV>();
+        if (tid < CL * NV) {
+            const double a = channel_sum<NV>(bpc, tid, [&](int k, int v) {
                 const unsigned lo = pw[(k * NV + v) * 2], hi = pw[(k * NV + v) * 2 + 1];
                 return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
             });
             if constexpr (GNSS_CORR_PROBE != 0)  // (probe builds: E = P = L = 1, a steady loop)
-                if ((tid & 7) == 0) s_fin[tid >> 3] = ((tid >> 3) & 1) ? 0.0 * a : 1.0 + 0.0 * a;
+                if (tid % CL == 0) s_fin[tid / CL] = ((tid / CL) & 1) ? 0.0 * a : 1.0 + 0.0 * a;
             if constexpr (GNSS_CORR_PROBE == 0)
-                if ((tid & 7) == 0) s_fin[tid >> 3] = D.phaseC ? -a : a;  // :447-449
+                if (tid % CL == 0) s_fin[tid / CL] = D.phaseC ? -a : a;  // :447-449
         }
         const int phaseC = D.phaseC;
         lds_barrier();
