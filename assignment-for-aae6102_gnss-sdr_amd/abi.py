@@ -97,7 +97,7 @@ class GnssTiming(C.Structure):
 class GnssSynthSv(C.Structure):
     _fields_ = [("prn", C.c_int32), ("doppler_hz", C.c_double), ("code_phase0", C.c_double),
                 ("carr_phase0", C.c_double), ("cn0_dbhz", C.c_double), ("bit_seed", C.c_uint64),
-                ("bit_phase_chips", C.c_double)]
+                ("bit_phase_chips", C.c_double), ("lnav", C.c_int32), ("reserved", C.c_int32)]
 
 
 class GnssSynth(C.Structure):
@@ -129,6 +129,7 @@ PROTOTYPES = {
                                        C.POINTER(C.c_int32), C.POINTER(GnssTrackOut)]),
     "gnss_navi_decode": (C.c_int, [C.POINTER(GnssAcquired), C.POINTER(C.c_double),
                                    C.POINTER(C.c_int64), C.c_int64, C.POINTER(GnssNavOut)]),
+    "gnss_lnav_bits": (C.c_int, [C.c_int32, C.c_int32, C.c_void_p]),
     "gnss_ca_code": (C.c_int, [C.c_int, C.c_void_p]),
     "gnss_correlate_step": (C.c_int, [C.c_void_p, C.POINTER(GnssFile), C.POINTER(GnssSignal),
                                       C.c_int, C.c_int, C.c_double, C.c_double, C.c_double,

@@ -10,6 +10,8 @@ namespace gnss {
 
 namespace {
 
+constexpr int kLnavBits = 3000;  // two LNAV frames (60 s), repeated
+
 __device__ __forceinline__ uint64_t mix64(uint64_t z)
 {
     z += 0x9E3779B97F4A7C15ULL;
@@ -21,11 +23,12 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z)
 struct SynthSv {
     double amp, crate, frate, code_phase0, carr_phase0, bit_phase;
     uint64_t bit_seed;
+    int32_t lnav, pad;
 };
 
 __global__ void synth_kernel(const SynthSv* __restrict__ sv, int nsv, const float* __restrict__ ca,
                              double sigma, uint64_t seed, uint64_t sample0, uint64_t nsamples,
-                             int8_t* __restrict__ dst)
+                             int8_t* __restrict__ dst, const int8_t* __restrict__ lnav_bits)
 {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nsamples;
          i += (uint64_t)gridDim.x * blockDim.x) {
@@ -37,8 +40,15 @@ __global__ void synth_kernel(const SynthSv* __restrict__ sv, int nsv, const floa
             int64_t chip = (int64_t)floor(th) % 1023;
             if (chip < 0) chip += 1023;
             const double bitf = floor((th + v.bit_phase) / 20460.0);
-            const uint64_t bh = mix64(v.bit_seed ^ (uint64_t)(int64_t)bitf);
-            const double D = (bh & 1) ? 1.0 : -1.0;
+            double D;
+            if (v.lnav) {  // LNAV bit b -> (-1)^b (gnss_lnav_bits, kLnavBits-bit cycle)
+                int64_t k = (int64_t)bitf % kLnavBits;
+                if (k < 0) k += kLnavBits;
+                D = lnav_bits[k] ? -1.0 : 1.0;
+            } else {
+                const uint64_t bh = mix64(v.bit_seed ^ (uint64_t)(int64_t)bitf);
+                D = (bh & 1) ? 1.0 : -1.0;
+            }
             double ph = v.carr_phase0 - (double)n * v.frate;
             ph -= floor(ph);
             const double a = v.amp * D * (double)ca[s * 1023 + chip];
@@ -81,16 +91,27 @@ hipError_t launch_synth_if(const gnss_synth& cfg, const float* ca, uint64_t samp
         h[i].carr_phase0 = v.carr_phase0;
         h[i].bit_phase = v.bit_phase_chips;
         h[i].bit_seed = v.bit_seed;
+        h[i].lnav = v.lnav;
+        h[i].pad = 0;
     }
     SynthSv* d = nullptr;
-    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&d), sizeof(SynthSv) * GNSS_MAX_SV, s);
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&d), sizeof(SynthSv) * GNSS_MAX_SV + kLnavBits, s);
     if (e != hipSuccess) return e;
     e = hipMemcpyAsync(d, h, sizeof(SynthSv) * (size_t)(cfg.n_sv > 0 ? cfg.n_sv : 1),
                        hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return e;
+    static int8_t lnav[kLnavBits];  // (the same message on every SV)
+    static bool lnav_ready = false;
+    if (!lnav_ready) {
+        (void)gnss_lnav_bits(1, kLnavBits, lnav);
+        lnav_ready = true;
+    }
+    int8_t* d_lnav = reinterpret_cast<int8_t*>(d + GNSS_MAX_SV);
+    e = hipMemcpyAsync(d_lnav, lnav, kLnavBits, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return e;
     const uint64_t blocks = (nsamples + 255) / 256;
     hipLaunchKernelGGL(synth_kernel, dim3((unsigned)(blocks < 65536 ? blocks : 65536)), dim3(256), 0,
-                       s, d, cfg.n_sv, ca, cfg.noise_sigma, cfg.seed, sample0, nsamples, dst);
+                       s, d, cfg.n_sv, ca, cfg.noise_sigma, cfg.seed, sample0, nsamples, dst, d_lnav);
     e = hipGetLastError();
     (void)hipFreeAsync(d, s);
     return e;

@@ -81,6 +81,47 @@ def all_prn(n=32, skip_ms=0, seed=6105, Fs=58e6, IF=4.58e6):
     return scenario(svs, cds, dops, cn0s, Fs=Fs, IF=IF, skip_ms=skip_ms, seed=seed)
 
 
+# The synthetic LNAV ephemeris of csrc/lnav.cpp (gnss_lnav_bits, gnss_synth_sv.lnav = 1):
+# field -> (raw value, bits, signed, scale) as naviDecode_updated.m decodes it
+LNAV_TOW0 = 390114  # TOW of the first subframe 1, s
+LNAV_FIELDS = {
+    "weeknum": (131 + 2048, 10, False, 1.0), "N": (0, 4, False, 1.0), "health": (0, 5, False, 1.0),
+    "IODC": (56, 8, False, 1.0), "TGD": (4, 8, True, 2.0 ** -31), "toc": (24750, 16, False, 16.0),
+    "af2": (0, 8, True, 2.0 ** -55), "af1": (65415, 16, True, 2.0 ** -43),
+    "af0": (3497117, 22, True, 2.0 ** -31), "IODE2": (56, 8, False, 1.0),
+    "Crs": (62011, 16, True, 2.0 ** -5), "deltan": (12325, 16, True, 2.0 ** -43, "pi"),
+    "M0": (942312117, 32, True, 2.0 ** -31, "pi"), "Cuc": (65439, 16, True, 2.0 ** -29),
+    "ecc": (33351524, 32, False, 2.0 ** -33), "Cus": (101, 16, True, 2.0 ** -29),
+    "sqrta": (2702053453, 32, False, 2.0 ** -19), "toe": (24750, 16, False, 16.0),
+    "Cic": (65522, 16, True, 2.0 ** -29), "omegae": (944858321, 32, True, 2.0 ** -31, "pi"),
+    "Cis": (65502, 16, True, 2.0 ** -29), "i0": (663888912, 32, True, 2.0 ** -31, "pi"),
+    "Crc": (8513, 16, True, 2.0 ** -5), "w": (683398911, 32, True, 2.0 ** -31, "pi"),
+    "omegadot": (16776433, 24, True, 2.0 ** -43, "pi"), "IODE3": (56, 8, False, 1.0),
+    "idot": (16336, 14, True, 2.0 ** -43, "pi"),
+}
+
+
+def lnav_expected(field: str) -> float:
+    """The value naviDecode_updated.m decodes for a LNAV_FIELDS entry (bin2dec_GPSSDR /
+    comp2dec semantics: two's complement on the field width, times 2^LSB, times pi)."""
+    e = LNAV_FIELDS[field]
+    raw, bits, signed, scale = e[:4]
+    if field == "weeknum":
+        return float(raw)
+    v = raw - (1 << bits) if signed and raw >> (bits - 1) else raw
+    out = float(v) * scale
+    return out * math.pi if len(e) > 4 else out
+
+
+def lnav_bits(nbits: int) -> np.ndarray:
+    """gnss_lnav_bits: the transmitted bits (0/1) of the synthetic LNAV message."""
+    out = np.zeros(nbits, dtype=np.int8)
+    st = abi.load().gnss_lnav_bits(1, int(nbits), out.ctypes.data_as(C.c_void_p))
+    if st != abi.OK:
+        raise abi.GnssError(st, "gnss_lnav_bits")
+    return out
+
+
 def record_bytes(ms: float, Fs=58e6) -> int:
     return int(round(ms * math.ceil(Fs * 1e-3))) * 2
 

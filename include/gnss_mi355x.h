@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define GNSS_ABI_VERSION 4
+#define GNSS_ABI_VERSION 5
 
 /* ---- status codes (SURVEY §8b "Error conventions") --------------------- */
 #define GNSS_OK         0
@@ -293,6 +293,10 @@ typedef struct gnss_synth_sv {
     double  cn0_dbhz;
     uint64_t bit_seed;      /* 50 bps nav-bit stream seed                        */
     double  bit_phase_chips;/* nav-bit edge offset, chips                        */
+    int32_t lnav;           /* 1: the bits are the LNAV message of gnss_lnav_bits
+                               (bit k of the record = bit k mod 3000) instead of
+                               seeded random bits; device generator only          */
+    int32_t reserved;
 } gnss_synth_sv;
 
 typedef struct gnss_synth {
@@ -302,6 +306,11 @@ typedef struct gnss_synth {
     int32_t  n_sv;
     gnss_synth_sv sv[GNSS_MAX_SV];
 } gnss_synth;
+
+/* The synthetic LNAV message (subframes 1-5, TLM/HOW/parity per IS-GPS-200, the
+ * ephemeris fields naviDecode_updated.m reads; csrc/lnav.cpp): nbits transmitted bits
+ * (0/1) from the start of a subframe 1 with HOW TOW count 65020. */
+int gnss_lnav_bits(int32_t prn, int32_t nbits, int8_t *bits_out);
 
 /* Fill dev_dst (this ctx's HBM) with samples [sample0, sample0 + nsamples) of
  * the record, 2 bytes per sample (I then Q). */

@@ -78,3 +78,32 @@ def test_navdecode_matches_reference_40s_run(pkg, ref):
         assert (for_prest.sfb1[p - 1] if p <= len(for_prest.sfb1) else 0) == ref["sfb1_40"][i], p
         for f in pkg.abi.EPH_FIELDS:
             assert np.array_equal(getattr(eph(p), f), ref[f"eph40_{p}_{f}"]), (p, f)
+
+
+def _decode_bits(pkg, bits, offset_ms=7, invert=False):
+    """P_i of a locked channel carrying `bits` (20 ms each, sign (-1)^b, optional 180-degree
+    inversion), starting `offset_ms` into a bit, decoded by naviDecode_updated."""
+    d = np.repeat(np.where(bits == 1, -1.0, 1.0), 20)[offset_ms:]
+    if invert:
+        d = -d
+    P = d * 1000.0  # (the decoder skips the first 3 s, then starts at a sign change)
+    A = SimpleNamespace(sv=np.array([7]), SNR=np.zeros(1), Doppler=np.zeros(1),
+                        codedelay=np.zeros(1, dtype=np.int64), fineFreq=np.zeros(1))
+    T = pkg.StructArray({7: SimpleNamespace(P_i=P)})
+    return pkg.naviDecode_updated(A, T)
+
+
+@pytest.mark.parametrize("invert", [False, True], ids=["upright", "inverted"])
+def test_synthetic_lnav_roundtrip(pkg, invert):
+    """The synthetic LNAV message (gnss_lnav_bits: the generator of the synthetic IF's nav
+    bits) decodes to the ephemeris it encodes, either polarity (the D30* word inversion
+    undoes a 180-degree carrier ambiguity)."""
+    bits = pkg.synth.lnav_bits(3000)
+    eph, _, fp = _decode_bits(pkg, bits, invert=invert)
+    e = eph(7)
+    assert e.updateflag == 1
+    for f in pkg.synth.LNAV_FIELDS:
+        vals = getattr(e, f)
+        assert len(vals) > 0 and np.all(vals == pkg.synth.lnav_expected(f)), (f, vals[:3])
+    # TOW of every subframe decoded: 390114 + 6 k
+    assert np.all((e.TOW - pkg.synth.LNAV_TOW0) % 6 == 0)
