@@ -25,6 +25,14 @@ FIELDS_POS = ["P_i", "P_q", "E_i", "E_q", "L_i", "L_q", "carrError", "codeError"
               "remChip", "codeFreq", "carrFreq", "remCarrPhase", "absoluteSampleCodedelay",
               "numSample", "delayValue", "absoluteSample", "codedelay2"]
 
+# the 25 taps of trackingCT_POS_updated_multicorrelator.m in Spacing order (0.6:-0.05:-0.6,
+# :41), under the names of its TckResultCT fields (:374-423)
+MC_TAPS = 25
+MC_TAP_NAMES = ([f"E_{{}}{s}" for s in ["_060", "_055", "", "_045", "_040", "_035", "_030", "_025",
+                                         "_020", "_015", "_010", "_005"]] + ["P_{}"] +
+                [f"L_{{}}{s}" for s in ["005", "010", "015", "020", "025", "030", "035", "040", "045",
+                                         "", "055", "060"]])
+
 
 # ephemeris(prn) fields of naviDecode_updated.m (ini_eph.m order; updateflag separate)
 EPH_FIELDS = ["TOW", "TOW1", "sfb", "sfb1", "weeknum", "N", "health", "IODC", "TGD", "toc", "af2",
@@ -127,6 +135,9 @@ PROTOTYPES = {
     "gnss_tracking_ct_pos": (C.c_int, [C.c_void_p, C.POINTER(GnssFile), C.POINTER(GnssSignal),
                                        C.POINTER(GnssTrack), C.POINTER(GnssAcquired), C.c_int32,
                                        C.POINTER(C.c_int32), C.POINTER(GnssTrackOut)]),
+    "gnss_tracking_ct_mc": (C.c_int, [C.c_void_p, C.POINTER(GnssFile), C.POINTER(GnssSignal),
+                                      C.POINTER(GnssTrack), C.POINTER(GnssAcquired), C.c_int32,
+                                      C.c_int32, C.POINTER(GnssTrackOut)]),
     "gnss_navi_decode": (C.c_int, [C.POINTER(GnssAcquired), C.POINTER(C.c_double),
                                    C.POINTER(C.c_int64), C.c_int64, C.POINTER(GnssNavOut)]),
     "gnss_lnav_bits": (C.c_int, [C.c_int32, C.c_int32, C.c_void_p]),

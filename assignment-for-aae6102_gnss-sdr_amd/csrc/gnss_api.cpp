@@ -693,6 +693,9 @@ struct StepGraph {
 struct PosCfg {
     int32_t ctPOS;            // track.ctPOS (datalength, trackingCT_POS_updated.m:50)
     const int32_t* countinx;  // countinx(svIndex) of countinx.mat (:29), by channel position
+    // 0: trackingCT_POS_updated.m. 1 or 10: trackingCT_POS_updated_multicorrelator.m, every
+    // step at this pdi (track.pdi, :46), 25 taps, ctPOS = datalength/pdi steps (:170)
+    int32_t mc_pdi;
 };
 
 // trackingCT.m (pos == nullptr) or the tracking loop of trackingCT_POS_updated.m
@@ -713,7 +716,7 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
         // trackingCT_POS_updated.m:196,207 reads numSample*dataType int16 values but advances
         // file_ptr by numSample*dataType BYTES: overlapping, misaligned reads (not reproduced)
         return fail(ctx, GNSS_EARG, "trackingCT_POS_updated: int8 records only");
-    if (pos && (pos->ctPOS <= 0 || !pos->countinx || tr->n_taps != 0))
+    if (pos && (pos->ctPOS <= 0 || (!pos->countinx && !pos->mc_pdi) || tr->n_taps != 0))
         return fail(ctx, GNSS_EARG, "trackingCT_POS_updated: ctPOS > 0, countinx and E/P/L taps required");
     if (prec == 2 && dtyp == 1) {
         // fread(numSample, 'int16') de-interleaved as I/Q (trackingCT.m:84-88): an odd
@@ -737,6 +740,7 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
     // trackingCT_POS_updated.m: per channel, steps 1..n1 at 1 ms (msIndex <= 1000 +
     // countinx(svIndex), :183), then 10 ms up to ctPOS steps (:294)
     auto pos_n1 = [&](int c) -> int64_t {
+        if (pos->mc_pdi) return pos->mc_pdi == 1 ? pos->ctPOS : 0;
         return std::max<int64_t>(0, std::min<int64_t>(pos->ctPOS, (int64_t)N1 + pos->countinx[c]));
     };
     if (8.0 * (sg->codeFreqBasis * 1.01) / sg->Fs >= 1.0)
@@ -751,7 +755,19 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
     // -0.5 exactly at 3, 13, 23); Early at Spacing(3) = +0.5, Late at Spacing(23) = -0.5,
     // Prompt Code(ceil(t + 0.05) + 1)
     const double taps_pos[3] = {0.5, 0.0, -0.5};
-    if (pos) {
+    // trackingCT_POS_updated_multicorrelator.m:41,207-258: all 25 Spacing values as taps,
+    // Code(ceil(t) + 2) with Code = [CA(end) CA.. CA(1) CA(2)] (:94,233), no +0.05 on the
+    // prompt; E/P/L = Spacing(3)/(13)/(23) feed the loops (:348-359)
+    double taps_mc[25];
+    if (pos && pos->mc_pdi) {
+        const Colon sp = colon_make(0.6, -0.05, -0.6);
+        if (sp.n != 24) return fail(ctx, GNSS_EDEVICE, "Spacing colon");
+        for (int k = 0; k < 25; k++) taps_mc[k] = colon_elem(sp, k);
+        taps = taps_mc;
+        ntaps = 25;
+        P.conv = 1;
+        P.chip_off = 1;
+    } else if (pos) {
         taps = taps_pos;
         P.conv = 1;
         P.tap_post[1] = 0.05;
@@ -760,7 +776,8 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
         ntaps = tr->n_taps;
         taps = tr->tap_offsets;
     }
-    if (ntaps != 3 && ntaps != 11) return fail(ctx, GNSS_EARG, "n_taps must be 3 or 11");
+    if (ntaps != 3 && ntaps != 11 && !(pos && pos->mc_pdi))
+        return fail(ctx, GNSS_EARG, "n_taps must be 3 or 11");
     P.iE = P.iP = P.iL = -1;
     for (int s = 0; s < ntaps; s++) {
         P.taps[s] = taps[s];
@@ -770,6 +787,7 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
         if (taps[s] == tr->CorrelatorSpacing && P.iL < 0) P.iL = s;
     }
     if (pos) { P.iE = 0; P.iP = 1; P.iL = 2; }
+    if (pos && pos->mc_pdi) { P.iE = 2; P.iP = 12; P.iL = 22; }
     if (P.iE < 0 || P.iP < 0 || P.iL < 0) return fail(ctx, GNSS_EARG, "taps must contain -spacing, 0, +spacing");
     P.ntaps = ntaps;
 
@@ -788,7 +806,9 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
     coef(tr->DLLBW, tr->DLLDamp, tr->DLLGain, P.tau1code, P.tau2code);
     coef(tr->PLLBW, tr->PLLDamp, tr->PLLGain, P.tau1carr, P.tau2carr);
     {   // the loop filters' constant quotients (device: loop_update_i); T as the kernel forms it
-        const double T1 = pos ? sg->ms : 0.001 * 1, T10 = pos ? sg->ms : 0.001;
+        // (multicorrelator: (pdi*t)/tau1, :352,361)
+        const double T1 = pos ? (pos->mc_pdi ? 1 * sg->ms : sg->ms) : 0.001 * 1;
+        const double T10 = pos ? (pos->mc_pdi ? 10 * sg->ms : sg->ms) : 0.001;
         P.dll_r = P.tau2code / P.tau1code;
         P.pll_r = P.tau2carr / P.tau1carr;
         P.dll_t1 = T1 / P.tau1code;
@@ -883,13 +903,13 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
     auto sub_for = [&](int pdi) {
         int sub = pdi >= 10 ? 3 : 1;
         while (sub > 1 && !sub_ok(sub)) sub--;
-        if (P.fmt == 1 && sub != 3) sub = 1;  // (int16 kernels: 8- and 24-sample lanes)
+        if ((P.fmt == 1 || ntaps == 25) && sub != 3) sub = 1;  // (int16, 25 taps: 8- and 24-sample lanes)
         return sub;
     };
     int sub1 = sub_for(1), sub10 = sub_for(10);
     if (const char* fs = getenv("GNSS_FORCE_SUB")) {  // test hook: exercise every kernel variant
         const int v = atoi(fs);
-        if (v >= 1 && v <= 4 && sub_ok(v) && (P.fmt == 0 || v == 1 || v == 3)) sub1 = sub10 = v;
+        if (v >= 1 && v <= 4 && sub_ok(v) && ((P.fmt == 0 && ntaps != 25) || v == 1 || v == 3)) sub1 = sub10 = v;
     }
     auto bpc_for = [&](int pdi, int sub) {
         const double groups = (S * pdi * 1.01 + 64) / 8.0 + 2;
@@ -933,7 +953,7 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
             t.codedelay0 = S - acq->codedelay[c] + 1;
             t.sv1 = 1;
             t.n1_target = pos_n1(c);
-            t.countinx = pos->countinx[c];
+            t.countinx = pos->countinx ? pos->countinx[c] : 0;
         }
         if (acq->sv[c] < 1 || acq->sv[c] > 51) return fail(ctx, GNSS_EARG, "bad PRN");
         ca_bits(acq->sv[c], &cab[(size_t)i * 32]);
@@ -1247,7 +1267,17 @@ int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
 int gnss_tracking_ct_pos(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg, const gnss_track* tr,
                          const gnss_acquired* acq, int32_t ctPOS, const int32_t* countinx, gnss_track_out* out)
 {
-    const PosCfg pc{ctPOS, countinx};
+    const PosCfg pc{ctPOS, countinx, 0};
+    return tracking_impl(ctx, file, sg, tr, acq, out, &pc);
+}
+
+int gnss_tracking_ct_mc(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg, const gnss_track* tr,
+                        const gnss_acquired* acq, int32_t msPosCT, int32_t pdi, gnss_track_out* out)
+{
+    if (!ctx) return GNSS_EARG;
+    if (pdi != 1 && pdi != 10) return fail(ctx, GNSS_EARG, "multicorrelator: pdi must be 1 or 10");
+    if (msPosCT < pdi) return fail(ctx, GNSS_EARG, "multicorrelator: msPosCT/pdi must be >= 1");
+    const PosCfg pc{msPosCT / pdi, nullptr, pdi};  // msIndex = 1:datalength/pdi (:170)
     return tracking_impl(ctx, file, sg, tr, acq, out, &pc);
 }
 

@@ -157,6 +157,10 @@ struct TrkParams {
     // host: tau2/tau1, and T/tau1 for pdi 1 and for the 10-ms steps (T = 1 ms in both)
     double dll_r, dll_t1, dll_t10, pll_r, pll_t1, pll_t10;
     int32_t conv;
+    // replica index offset: 0 = Code(ceil(t) + 1) with Code = [CA(end) CA.. CA(1)]; 1 =
+    // Code(ceil(t) + 2) with Code = [CA(end) CA.. CA(1) CA(2)]
+    // (trackingCT_POS_updated_multicorrelator.m:94,233-258)
+    int32_t chip_off;
     // added to a tap's colon element before ceil (the +0.05 of trackingCT_POS_updated.m:216)
     double tap_post[GNSS_MAX_TAPS];
 };

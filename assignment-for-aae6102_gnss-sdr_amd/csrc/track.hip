@@ -276,7 +276,8 @@ __device__ __forceinline__ void prepare_desc_i(const TrkParams& p, const NcoStat
         const double post = p.tap_post[lane];
         const int64_t c0 = (int64_t)ceil(colon_elem(col, 0) + post);
         const int64_t c1 = (int64_t)ceil(colon_elem(col, n - 1) + post);
-        int tb = (col.n != n - 1 || c0 < 0 || c1 > 1023LL * pdi + 1) ? GNSS_EINDEX : GNSS_OK;
+        // Code index ceil(t) + 1 + chip_off within [1, 1023*pdi + 2 + chip_off]
+        int tb = (col.n != n - 1 || c0 + p.chip_off < 0 || c1 > 1023LL * pdi + 1) ? GNSS_EINDEX : GNSS_OK;
         if (lane == p.iP) {
             // remChip = (t_CodePrompt(numSample) + codeFreq/Fs) - codeFreqBasis*ms*pdi (:102);
             // trackingCT_POS_updated.m:220: ... - signal.codelength*pdi
@@ -697,7 +698,7 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
                 pb = ceil(colon_elem(col, kx) + post) > c0 ? ms : ms + 1;
         }
         cap[s] = (pb < M ? pb : M) - 1;  // Prefix(p) = running sum through sample p-1
-        const unsigned i0 = ca_index32((int)c0);
+        const unsigned i0 = ca_index32((int)c0 + p.chip_off);
         const unsigned i1 = i0 == 1022u ? 0u : i0 + 1u;
         const unsigned w0 = __shfl(cabits, (int)(i0 >> 5), 64);
         const unsigned w1 = __shfl(cabits, (int)(i1 >> 5), 64);
@@ -894,7 +895,10 @@ __device__ __forceinline__ double block_partial(double* s_mem, const double (&oI
 // lanes per value where 16*NV fits the block, else 8): lane q = tid % L adds blocks q,
 // q+L, ... in order, then a DPP butterfly over the L lanes. Every lane of the L returns the
 // sum. load(k, v) = block k's partial of value v.
-template <int NV> constexpr int chan_lanes() { return 16 * NV <= kTrkThreads ? 16 : 8; }
+template <int NV> constexpr int chan_lanes()
+{
+    return 16 * NV <= kTrkThreads ? 16 : 8 * NV <= kTrkThreads ? 8 : 4;  // (25 taps: 4)
+}
 
 template <int NV, class Load>
 __device__ __forceinline__ double channel_sum(int bpc, int tid, Load load)
@@ -906,7 +910,7 @@ __device__ __forceinline__ double channel_sum(int bpc, int tid, Load load)
     for (int k = q; k < bpc; k += L) a += load(k, v);
     a += dpp_f64<0xB1>(a);   // quad_perm [1,0,3,2]
     a += dpp_f64<0x4E>(a);   // quad_perm [2,3,0,1]
-    a += dpp_f64<0x141>(a);  // row_half_mirror: the other quad of the 8
+    if constexpr (L >= 8) a += dpp_f64<0x141>(a);   // row_half_mirror: the other quad of the 8
     if constexpr (L == 16) a += dpp_f64<0x140>(a);  // row_mirror: the other 8 of the 16
     return a;
 }
@@ -1611,6 +1615,8 @@ hipError_t launch_track_step(const TrkParams& p, const TrkBuffers& b, const TrkD
     GNSS_STEP(3, 1, false, 0) GNSS_STEP(3, 2, false, 0) GNSS_STEP(3, 3, false, 0) GNSS_STEP(3, 4, false, 0)
     GNSS_STEP(11, 1, false, 0) GNSS_STEP(11, 2, false, 0) GNSS_STEP(11, 3, false, 0) GNSS_STEP(11, 4, false, 0)
     GNSS_STEP(3, 1, true, 0) GNSS_STEP(11, 1, true, 0)
+    // the 25 taps of trackingCT_POS_updated_multicorrelator.m (int8; 8- and 24-sample lanes)
+    GNSS_STEP(25, 1, false, 0) GNSS_STEP(25, 3, false, 0) GNSS_STEP(25, 1, true, 0)
     // int16 I/Q records (per-read mean removal): the per-step path only
     GNSS_STEP(3, 1, false, 1) GNSS_STEP(3, 3, false, 1) GNSS_STEP(11, 1, false, 1) GNSS_STEP(11, 3, false, 1)
     GNSS_STEP(3, 1, true, 1) GNSS_STEP(11, 1, true, 1)

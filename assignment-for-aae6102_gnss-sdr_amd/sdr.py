@@ -396,6 +396,47 @@ def trackingCT_POS(file, signal, track, Acquired, countinx, *, ctx: Context | No
     return build_tck_result(Acquired, buf, channels, abi.FIELDS_POS), cn0
 
 
+def mc_result(Acquired, buf: TrackOutBuffers, channels=None) -> StructArray:
+    """TckResultCT_mltCorr: the loop fields plus every tap under the reference's names
+    (E_i_060 ... P_i ... L_q060, trackingCT_POS_updated_multicorrelator.m:374-439)."""
+    res = build_tck_result(Acquired, buf, channels, abi.FIELDS_POS)
+    for prn in res.prns():
+        e = res(prn)
+        for k, name in enumerate(abi.MC_TAP_NAMES):
+            setattr(e, name.format("i"), e.taps_i[k])
+            setattr(e, name.format("q"), e.taps_q[k])
+    return res
+
+
+def trackingCT_POS_updated_multicorrelator(file, signal, track, Acquired, *,
+                                           ctx: Context | None = None, channels=None,
+                                           raw: bool = False):
+    """The tracking loop of trackingCT_POS_updated_multicorrelator.m (:41-136, :170-440) on
+    the GPU -> (TckResultCT_mltCorr, CN0_CT).
+
+    track.msPosCT (datalength, :49; initParameters.m does not define it, the caller sets
+    it) and track.pdi (:46, 1 or 10) give msPosCT/pdi steps, every one at that pdi. The 25
+    taps at Spacing = 0.6:-0.05:-0.6 are all recorded; E/P/L = Spacing(3)/(13)/(23) drive
+    the loops. The positioning half (:446-590) is out of scope.
+    """
+    ctx = ctx or default_context()
+    nsv = len(Acquired.sv)
+    f, k1 = to_c_file(file)
+    s = to_c_signal(signal)
+    t, k2 = to_c_track(track, None, channels)
+    a = to_c_acquired(Acquired)
+    msPosCT, pdi = int(track.msPosCT), int(track.pdi)
+    nsteps = msPosCT // pdi if pdi > 0 else 0
+    buf = TrackOutBuffers(nsv, track, abi.MC_TAPS, ctPOS=max(nsteps, 1))
+    st = ctx.lib.gnss_tracking_ct_mc(ctx.h, C.byref(f), C.byref(s), C.byref(t), C.byref(a),
+                                     msPosCT, pdi, C.byref(buf.c))
+    ctx.check(st)
+    if raw:
+        return buf
+    cn0 = buf.CN0[: buf.c.cn0_rows].copy()
+    return mc_result(Acquired, buf, channels), cn0
+
+
 def naviDecode_updated(Acquired, ALLTckResult, *, eph_cap: int = 512):
     """naviDecode_updated.m:1-253 -> (ephemeris, ALLTckResult, for_prest).
 

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define GNSS_ABI_VERSION 5
+#define GNSS_ABI_VERSION 6
 
 /* ---- status codes (SURVEY §8b "Error conventions") --------------------- */
 #define GNSS_OK         0
@@ -241,6 +241,26 @@ int gnss_tracking_ct(gnss_ctx *ctx, const gnss_file *file, const gnss_signal *si
 int gnss_tracking_ct_pos(gnss_ctx *ctx, const gnss_file *file, const gnss_signal *signal,
                          const gnss_track *track, const gnss_acquired *acquired, int32_t ctPOS,
                          const int32_t *countinx, gnss_track_out *out);
+
+/* The tracking loop of trackingCT_POS_updated_multicorrelator.m (the
+ * 25-tap sibling; its positioning half, :446-590, is out of scope). Replaces the channel
+ * loop of trackingCT_POS_updated_multicorrelator.m:41-136,170-440:
+ *   - steps msIndex = 1..msPosCT/pdi (datalength = track.msPosCT, pdi = track.pdi, :46-49,
+ *     :170; pdi 1 or 10), every step at that pdi, one continuous read per channel from
+ *     file_ptr = (Sample - codedelay + 1 + skip*Sample)*bytes (:101-103);
+ *   - GNSS_MC_TAPS taps at Spacing = 0.6:-0.05:-0.6 (:41), replica Code(ceil(t) + 2) with
+ *     Code = [CA(end) repmat(CA,1,pdi) CA(1) CA(2)] (:94,233-258), no +0.05 on the prompt;
+ *     E/P/L = Spacing(3)/(13)/(23) feed the DLL/PLL; numSample = ceil(...) (:177);
+ *     codeFreq = f0 + codeNco; loop filters with T = pdi*t (:351-364);
+ *   - C/N0 every 20 steps with 1/(t*pdi) (:333-345);
+ *   - one record row per step (the fields of :428-439 in gnss_track_out.rec as for
+ *     gnss_tracking_ct_pos), every tap in gnss_track_out.taps[nsv][2][25][max_len] in
+ *     Spacing order (E_i_060 ... L_i060 of :374-423).
+ * max_len >= msPosCT/pdi; track->n_taps must be 0. int8 records only, EOF -> GNSS_EIO. */
+#define GNSS_MC_TAPS 25
+int gnss_tracking_ct_mc(gnss_ctx *ctx, const gnss_file *file, const gnss_signal *signal,
+                        const gnss_track *track, const gnss_acquired *acquired, int32_t msPosCT,
+                        int32_t pdi, gnss_track_out *out);
 
 /* ---- naviDecode_updated.m ---------------------------------
  * Navigation-bit decode on the tracking output: bit synchronisation of P_i, preamble

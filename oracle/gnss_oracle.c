@@ -544,7 +544,7 @@ static inline int ca_index(int64_t c) { return (int)((c + 1022) % 1023); }
 
 static void correlate_cpx(const cpx *x, int64_t n, double remChip, double codeFreq, double Fs,
                           double carrierFreq, double remPhase, const int8_t *ca, int pdi, int ntaps,
-                          const double *taps, const double *post, double *sums);
+                          const double *taps, const double *post, int chip_off, double *sums);
 
 void or_correlate_step(const int8_t *iq, int64_t n, double remChip, double codeFreq, double Fs,
                        double carrierFreq, double remPhase, const int8_t *ca, int pdi, int ntaps,
@@ -552,16 +552,18 @@ void or_correlate_step(const int8_t *iq, int64_t n, double remChip, double codeF
 {
     cpx *x = (cpx *)malloc(sizeof(cpx) * (size_t)(n > 0 ? n : 1));
     for (int64_t k = 0; k < n; k++) { x[k].re = iq[2 * k]; x[k].im = iq[2 * k + 1]; }
-    correlate_cpx(x, n, remChip, codeFreq, Fs, carrierFreq, remPhase, ca, pdi, ntaps, taps, NULL, sums);
+    correlate_cpx(x, n, remChip, codeFreq, Fs, carrierFreq, remPhase, ca, pdi, ntaps, taps, NULL, 0, sums);
     free(x);
 }
 
 /* The correlator of trackingCT.m:96-118 on rawsignal0DC (complex doubles). post[s]
  * (NULL = none) is added to tap s's colon element before ceil: the prompt's
- * Code(ceil(t_CodePrompt + 0.05) + indx) of trackingCT_POS_updated.m:216. */
+ * Code(ceil(t_CodePrompt + 0.05) + indx) of trackingCT_POS_updated.m:216. chip_off = 1:
+ * Code(ceil(t) + 2) with Code = [CA(1023) repmat(CA,1,pdi) CA(1) CA(2)]
+ * (trackingCT_POS_updated_multicorrelator.m:94,233-258), i.e. CA((ceil(t)) mod 1023 + 1). */
 static void correlate_cpx(const cpx *x, int64_t n, double remChip, double codeFreq, double Fs,
                           double carrierFreq, double remPhase, const int8_t *ca, int pdi, int ntaps,
-                          const double *taps, const double *post, double *sums)
+                          const double *taps, const double *post, int chip_off, double *sums)
 {
     (void)pdi;
     const double d = codeFreq / Fs;
@@ -587,7 +589,7 @@ static void correlate_cpx(const cpx *x, int64_t n, double remChip, double codeFr
         for (int s = 0; s < ntaps; s++) {
             double t = or_colon_elem(&col[s], k);
             if (post) t = t + post[s];
-            double code = ca[ca_index((int64_t)ceil(t))];
+            double code = ca[ca_index((int64_t)ceil(t) + chip_off)];
             acc[2 * s] += code * I;
             acc[2 * s + 1] += code * Q;
         }
@@ -743,7 +745,7 @@ static int trk_step(const trk_ctx *t, chan_state *c, int ch, int sv1, int pdi, i
 
     double sums[2 * GNSS_MAX_TAPS];
     correlate_cpx(buf, n, c->remChip, c->codeFreq, sg->Fs, c->carrierFreq, c->remPhase, ca, pdi,
-                  t->ntaps, t->taps, NULL, sums);
+                  t->ntaps, t->taps, NULL, 0, sums);
     if (phaseC)
         for (int s = 0; s < 2 * t->ntaps; s++) sums[s] = -sums[s]; /* :447-449 */
 
@@ -977,22 +979,31 @@ static double cn0_moment(const double *Zk, double T)
     return hypot(lr, li);
 }
 
+/* The two sibling loops: trackingCT_POS_updated.m (mc_pdi = 0: E/P/L, the prompt at
+ * ceil(t + 0.05), 1-ms steps up to 1000 + countinx then 10-ms steps, T = t) and
+ * trackingCT_POS_updated_multicorrelator.m (mc_pdi = 1 or 10: the 25 Spacing taps,
+ * Code(ceil(t) + 2), every step at mc_pdi, T = pdi*t). */
+typedef struct {
+    int ntaps, iE, iP, iL, chip_off, mc_pdi;
+    double taps[GNSS_MAX_TAPS], post[GNSS_MAX_TAPS];
+} trkpos_mode;
+
 /* One channel of trackingCT_POS_updated.m:92-118 (init) and :179-408 (the msIndex loop,
  * both pdi branches; the channel loop is independent per svIndex: each channel seeks its
- * own file_ptr before every read). */
+ * own file_ptr before every read); with mc_pdi, of
+ * trackingCT_POS_updated_multicorrelator.m:91-136 and :170-440. */
 static int trkpos_channel(const trk_ctx *t, const gnss_acquired *acq, int ch, int32_t ctPOS,
-                          int32_t cx, double *cn0)
+                          int32_t cx, double *cn0, const trkpos_mode *md)
 {
     const gnss_signal *sg = t->sg;
     const gnss_file *f = t->file;
     const double S = (double)sg->Sample;
-    const double taps[3] = {0.5, 0.0, -0.5};  /* Spacing(3), Spacing(13), Spacing(23) (:42) */
-    const double post[3] = {0.0, 0.05, 0.0};  /* ceil(t_CodePrompt+0.05) (:216) */
+    const double *taps = md->taps, *post = md->post;
     int8_t ca[1023];
     if (or_generate_ca(acq->sv[ch], ca)) return GNSS_EARG;
     cpx *buf = (cpx *)malloc(sizeof(cpx) * (size_t)(2 * (sg->Sample * 10 + 4096)));
     int st = GNSS_OK;
-    const int64_t AcqCodeDelay = acq->codedelay[ch];
+    const int64_t AcqCodeDelay = acq->codedelay[ch]; /* (multicorrelator: :95,101-103) */
     int64_t file_ptr = (int64_t)((S - (double)AcqCodeDelay + 1 + (double)f->skip * sg->Fs * sg->ms) *
                                  f->dataPrecision * f->dataType); /* :108-110 */
     const double AcqFreq = acq->fineFreq[ch];                     /* :113-114 */
@@ -1004,7 +1015,8 @@ static int trkpos_channel(const trk_ctx *t, const gnss_acquired *acq, int ch, in
     double dvsum = 0;
     const double tT = sg->ms; /* t = signal.ms (:48) */
     for (int64_t Index = 1; Index <= ctPOS && st == GNSS_OK; Index++) {
-        const int pdi = (Index <= t->tr->msToProcessCT_1ms + (int64_t)cx) ? 1 : 10; /* :183,:294 */
+        const int pdi = md->mc_pdi ? md->mc_pdi
+                                   : (Index <= t->tr->msToProcessCT_1ms + (int64_t)cx) ? 1 : 10; /* :183,:294 */
         const double cps = codeFreq / sg->Fs;                                          /* :188 */
         const int64_t n = (int64_t)ceil((sg->codelength * pdi - remChip) / cps);       /* :189 */
         const int64_t delayValue = n - (int64_t)(S * pdi);                             /* :191 */
@@ -1014,31 +1026,35 @@ static int trkpos_channel(const trk_ctx *t, const gnss_acquired *acq, int ch, in
         if (m == -2) { st = GNSS_EINDEX; break; }
         const int64_t ftell_pos = file_ptr + got;
         file_ptr = file_ptr + n * f->dataType;               /* :207 (int8: = ftell) */
-        /* code index range (MATLAB would raise on an out-of-range Code index) */
-        for (int s = 0; s < 3 && st == GNSS_OK; s++) {
+        /* code index range (MATLAB would raise on an out-of-range Code index): ceil(t) + 1 +
+         * chip_off within [1, 1023*pdi + 2 + chip_off] */
+        for (int s = 0; s < md->ntaps && st == GNSS_OK; s++) {
             double a = (0 + taps[s]) + remChip;
             double b = ((double)(n - 1) * cps + taps[s]) + remChip;
             or_colon col;
             or_colon_init(&col, a, cps, b);
-            if (col.n != n - 1 || !chip_ok((int64_t)ceil(or_colon_elem(&col, 0) + post[s]), pdi) ||
+            if (col.n != n - 1 ||
+                !chip_ok((int64_t)ceil(or_colon_elem(&col, 0) + post[s]) + md->chip_off, pdi) ||
                 !chip_ok((int64_t)ceil(or_colon_elem(&col, n - 1) + post[s]), pdi))
                 st = GNSS_EINDEX;
         }
         if (st) break;
-        double sums[6];
-        correlate_cpx(buf, n, remChip, codeFreq, sg->Fs, carrFreq, remCarrPhase, ca, pdi, 3, taps, post,
-                      sums); /* :210-235 */
-        {   /* remChip = t_CodePrompt(numSample) + codePhaseStep - codelength*pdi (:220) */
-            double a = (0 + taps[1]) + remChip;
-            double b = ((double)(n - 1) * cps + taps[1]) + remChip;
+        double tsums[2 * GNSS_MAX_TAPS];
+        correlate_cpx(buf, n, remChip, codeFreq, sg->Fs, carrFreq, remCarrPhase, ca, pdi, md->ntaps, taps,
+                      post, md->chip_off, tsums); /* :210-235 (multicorrelator :207-329) */
+        {   /* remChip = t_CodePrompt(numSample) + codePhaseStep - codelength*pdi (:220; mc :262) */
+            double a = (0 + taps[md->iP]) + remChip;
+            double b = ((double)(n - 1) * cps + taps[md->iP]) + remChip;
             or_colon col;
             or_colon_init(&col, a, cps, b);
             remChip = or_colon_elem(&col, n - 1) + cps - sg->codelength * pdi;
         }
         /* Wave = 2*pi*(carrFreq.*CarrTime) + remCarrPhase; rem(Wave(n+1), 2*pi) (:222-224) */
         remCarrPhase = fmod(TWO_PI * (carrFreq * ((double)n / sg->Fs)) + remCarrPhase, TWO_PI);
-        const double E_i = sums[0], E_q = sums[1], P_i = sums[2], P_q = sums[3], L_i = sums[4],
-                     L_q = sums[5];
+        const double E_i = tsums[2 * md->iE], E_q = tsums[2 * md->iE + 1], P_i = tsums[2 * md->iP],
+                     P_q = tsums[2 * md->iP + 1], L_i = tsums[2 * md->iL], L_q = tsums[2 * md->iL + 1];
+        /* loop T: t (:257,266); multicorrelator (pdi*t) (:352,361) */
+        const double Tl = md->mc_pdi ? pdi * tT : tT;
         /* C/N0 (:238-250) */
         index_int += 1;
         Zk[index_int - 1] = P_i * P_i + P_q * P_q;
@@ -1052,13 +1068,13 @@ static int trkpos_channel(const trk_ctx *t, const gnss_acquired *acq, int ch, in
         double E = sqrt(E_i * E_i + E_q * E_q);
         double L = sqrt(L_i * L_i + L_q * L_q);
         double codeError = 0.5 * (E - L) / (E + L);
-        codeNco = or_loop_filter(code_outputLast, codeError, DLLdiscriLast, t->tau1code, t->tau2code, tT);
+        codeNco = or_loop_filter(code_outputLast, codeError, DLLdiscriLast, t->tau1code, t->tau2code, Tl);
         DLLdiscriLast = codeError;
         code_outputLast = codeNco;
         codeFreq = sg->codeFreqBasis + codeNco;
         /* PLL (:265-270) */
         double carrError = atan(P_q / P_i) / TWO_PI;
-        carrNco = or_loop_filter(oldCarrNco, carrError, oldCarrError, t->tau1carr, t->tau2carr, tT);
+        carrNco = or_loop_filter(oldCarrNco, carrError, oldCarrError, t->tau1carr, t->tau2carr, Tl);
         oldCarrNco = carrNco;
         oldCarrError = carrError;
         carrFreq = AcqFreq + carrNco;
@@ -1071,25 +1087,25 @@ static int trkpos_channel(const trk_ctx *t, const gnss_acquired *acq, int ch, in
                                      remChip, codeFreq, carrFreq, remCarrPhase, cd2, (double)n,
                                      (double)delayValue, absS, cd2};
         for (int fi = 0; fi < GNSS_NFIELDS; fi++) rec_put(t, ch, fi, Index - 1, Index, vals[fi]);
-        taps_put(t, ch, Index - 1, Index, sums);
+        taps_put(t, ch, Index - 1, Index, tsums);
     }
     if (!st && t->out->len) t->out->len[ch] = ctPOS;
     free(buf);
     return st;
 }
 
-int or_tracking_ct_pos(const gnss_file *file, const gnss_signal *sg, const gnss_track *tr,
-                       const gnss_acquired *acq, int32_t ctPOS, const int32_t *countinx,
-                       gnss_track_out *out, int nthreads)
+static int trkpos_run(const gnss_file *file, const gnss_signal *sg, const gnss_track *tr,
+                      const gnss_acquired *acq, int32_t ctPOS, const int32_t *countinx,
+                      gnss_track_out *out, int nthreads, const trkpos_mode *md)
 {
     if (file->dataPrecision != 1 || (file->dataType != 1 && file->dataType != 2) || ctPOS <= 0 ||
-        !countinx || tr->n_taps != 0 || out->max_len < ctPOS)
+        (!countinx && !md->mc_pdi) || tr->n_taps != 0 || out->max_len < ctPOS)
         return GNSS_EARG;
     trk_ctx t;
     memset(&t, 0, sizeof(t));
     t.file = file; t.sg = sg; t.tr = tr; t.out = out; t.nsv = acq->n;
     t.fsize = file_size(file);
-    t.ntaps = 3;
+    t.ntaps = md->ntaps;
     or_calc_loop_coef(tr->DLLBW, tr->DLLDamp, tr->DLLGain, &t.tau1code, &t.tau2code); /* :87-88 */
     or_calc_loop_coef(tr->PLLBW, tr->PLLDamp, tr->PLLGain, &t.tau1carr, &t.tau2carr);
     int nch = tr->chan ? tr->n_chan : acq->n;
@@ -1099,8 +1115,9 @@ int or_tracking_ct_pos(const gnss_file *file, const gnss_signal *sg, const gnss_
 #pragma omp parallel for num_threads(nt) schedule(dynamic)
     for (int i = 0; i < nch; i++) {
         int ch = tr->chan ? tr->chan[i] : i;
-        int st = trkpos_channel(&t, acq, ch, ctPOS, countinx[ch], out->CN0_Eph);
-        if (out->countinx) out->countinx[ch] = countinx[ch];
+        const int32_t cx = countinx ? countinx[ch] : 0;
+        int st = trkpos_channel(&t, acq, ch, ctPOS, cx, out->CN0_Eph, md);
+        if (out->countinx) out->countinx[ch] = cx;
 #pragma omp critical
         {
             if (st && status == GNSS_OK) status = st;
@@ -1108,6 +1125,33 @@ int or_tracking_ct_pos(const gnss_file *file, const gnss_signal *sg, const gnss_
     }
     out->cn0_rows = ctPOS / 20;
     return status;
+}
+
+int or_tracking_ct_pos(const gnss_file *file, const gnss_signal *sg, const gnss_track *tr,
+                       const gnss_acquired *acq, int32_t ctPOS, const int32_t *countinx,
+                       gnss_track_out *out, int nthreads)
+{
+    trkpos_mode md;
+    memset(&md, 0, sizeof(md));
+    md.ntaps = 3; md.iE = 0; md.iP = 1; md.iL = 2;
+    md.taps[0] = 0.5; md.taps[1] = 0.0; md.taps[2] = -0.5; /* Spacing(3), (13), (23) (:42) */
+    md.post[1] = 0.05;                                     /* ceil(t_CodePrompt+0.05) (:216) */
+    return trkpos_run(file, sg, tr, acq, ctPOS, countinx, out, nthreads, &md);
+}
+
+int or_tracking_ct_mc(const gnss_file *file, const gnss_signal *sg, const gnss_track *tr,
+                      const gnss_acquired *acq, int32_t msPosCT, int32_t pdi, gnss_track_out *out,
+                      int nthreads)
+{
+    if ((pdi != 1 && pdi != 10) || msPosCT < pdi) return GNSS_EARG;
+    trkpos_mode md;
+    memset(&md, 0, sizeof(md));
+    md.ntaps = 25; md.iE = 2; md.iP = 12; md.iL = 22; md.chip_off = 1; md.mc_pdi = pdi;
+    or_colon sp; /* Spacing = 0.6:-0.05:-0.6 (:41) */
+    or_colon_init(&sp, 0.6, -0.05, -0.6);
+    if (sp.n != 24) return GNSS_EARG;
+    for (int k = 0; k < 25; k++) md.taps[k] = or_colon_elem(&sp, k);
+    return trkpos_run(file, sg, tr, acq, msPosCT / pdi, NULL, out, nthreads, &md); /* 1:datalength/pdi */
 }
 
 /* ------------------------------------------------------------------------ */

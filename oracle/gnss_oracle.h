@@ -55,6 +55,11 @@ int or_tracking_ct(const gnss_file *file, const gnss_signal *signal, const gnss_
 int or_tracking_ct_pos(const gnss_file *file, const gnss_signal *signal, const gnss_track *track,
                        const gnss_acquired *acquired, int32_t ctPOS, const int32_t *countinx,
                        gnss_track_out *out, int nthreads);
+/* The tracking loop of trackingCT_POS_updated_multicorrelator.m (25 taps, every step at
+ * pdi, msPosCT/pdi steps); outputs as gnss_tracking_ct_mc. */
+int or_tracking_ct_mc(const gnss_file *file, const gnss_signal *signal, const gnss_track *track,
+                      const gnss_acquired *acquired, int32_t msPosCT, int32_t pdi, gnss_track_out *out,
+                      int nthreads);
 
 /* One trackingCT-style correlation step on host bytes (the body of
  * trackingCT.m:96-118 / :429-449 without the negation): sums[2*ntaps] =

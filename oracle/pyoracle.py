@@ -52,6 +52,9 @@ def load():
         lib.or_tracking_ct_pos.argtypes = [C.POINTER(abi.GnssFile), C.POINTER(abi.GnssSignal),
                                            C.POINTER(abi.GnssTrack), C.POINTER(abi.GnssAcquired),
                                            C.c_int32, C.c_void_p, C.POINTER(abi.GnssTrackOut), C.c_int]
+        lib.or_tracking_ct_mc.argtypes = [C.POINTER(abi.GnssFile), C.POINTER(abi.GnssSignal),
+                                          C.POINTER(abi.GnssTrack), C.POINTER(abi.GnssAcquired),
+                                          C.c_int32, C.c_int32, C.POINTER(abi.GnssTrackOut), C.c_int]
         lib.or_correlate_step.argtypes = [C.c_void_p, C.c_int64, C.c_double, C.c_double, C.c_double,
                                           C.c_double, C.c_double, C.c_void_p, C.c_int, C.c_int,
                                           C.c_void_p, C.c_void_p]
@@ -158,6 +161,26 @@ def trackingCT_POS(file, signal, track, Acquired, countinx, channels=None, nthre
         raise abi.GnssError(st, "or_tracking_ct_pos")
     cn0 = buf.CN0[: buf.c.cn0_rows].copy()
     return sdr.build_tck_result(Acquired, buf, channels, abi.FIELDS_POS), cn0
+
+
+def trackingCT_mc(file, signal, track, Acquired, channels=None, nthreads=0, raw=False):
+    """trackingCT_POS_updated_multicorrelator.m's tracking loop (track.msPosCT, track.pdi)."""
+    nsv = len(Acquired.sv)
+    f, k1 = sdr.to_c_file(file)
+    s = sdr.to_c_signal(signal)
+    t, k2 = sdr.to_c_track(track, None, channels)
+    a = sdr.to_c_acquired(Acquired)
+    msPosCT, pdi = int(track.msPosCT), int(track.pdi)
+    buf = sdr.TrackOutBuffers(nsv, track, abi.MC_TAPS, ctPOS=max(msPosCT // max(pdi, 1), 1))
+    st = load().or_tracking_ct_mc(C.byref(f), C.byref(s), C.byref(t), C.byref(a), msPosCT, pdi,
+                                  C.byref(buf.c), nthreads)
+    if raw:
+        buf.status = st
+        return buf
+    if st != abi.OK:
+        raise abi.GnssError(st, "or_tracking_ct_mc")
+    cn0 = buf.CN0[: buf.c.cn0_rows].copy()
+    return sdr.mc_result(Acquired, buf, channels), cn0
 
 
 def correlate_step(iq, numSample, remChip, codeFreq, Fs, carrierFreq, remPhase, ca, pdi, taps):

@@ -98,7 +98,32 @@ def main_pos():
     print("POS golden written:", buf.len, buf.c.cn0_rows)
 
 
+def main_mc():
+    """trackingCT_POS_updated_multicorrelator.m tracking loop: 3 channels, 25 taps, at pdi 1
+    (60 steps) and pdi 10 (30 steps) on the record of tests/test_oracle_mc.py."""
+    import test_oracle_mc as tm
+    data = tm.mc_record(pkg, po)
+    out = {}
+    for pdi, ms in tm.MS.items():
+        file, signal, acq, track, _, _ = pkg.initParameters()
+        file.skip, file.data = tm.SKIP, data
+        track.msPosCT, track.pdi = ms, pdi
+        A = SimpleNamespace(sv=np.array(tm.SVS), SNR=np.full(3, 20.0), Doppler=np.zeros(3),
+                            codedelay=np.array(tm.CD), fineFreq=np.array(tm.FF))
+        buf = po.trackingCT_mc(file, signal, track, A, raw=True)
+        assert buf.status == 0
+        L = int(buf.len.max())
+        out.update({f"rec{pdi}": buf.rec[:, :, :L], f"taps{pdi}": buf.taps[:, :, :, :L],
+                    f"len{pdi}": buf.len, f"cn0{pdi}": buf.CN0[: buf.c.cn0_rows]})
+    np.savez_compressed(os.path.join(HERE, "golden_mc_small.npz"), **out)
+    print("multicorrelator golden written:", {k: v.shape for k, v in out.items()})
+
+
 if __name__ == "__main__":
+    if "--mc-only" in sys.argv:
+        main_mc()
+        sys.exit(0)
     if "--pos-only" not in sys.argv:
         main()
     main_pos()
+    main_mc()
