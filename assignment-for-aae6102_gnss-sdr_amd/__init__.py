@@ -11,9 +11,9 @@ directory name is not a Python identifier).
 """
 from . import abi, synth
 from .sdr import (Context, DeviceRecord, StructArray, TrackOutBuffers, acquisition, ca_code, colon,
-                  default_context, initParameters, naviDecode_updated, trackingCT, trackingCT_POS,
-                  trackingCT_POS_updated_multicorrelator)
+                  default_context, initParameters, naviDecode_updated, trackingCT, trackingCT_multiCorr,
+                  trackingCT_POS, trackingCT_POS_updated_multicorrelator)
 
 __all__ = ["abi", "synth", "Context", "DeviceRecord", "StructArray", "TrackOutBuffers",
            "acquisition", "ca_code", "colon", "default_context", "initParameters", "naviDecode_updated",
-           "trackingCT", "trackingCT_POS", "trackingCT_POS_updated_multicorrelator"]
+           "trackingCT", "trackingCT_multiCorr", "trackingCT_POS", "trackingCT_POS_updated_multicorrelator"]

@@ -138,6 +138,9 @@ PROTOTYPES = {
     "gnss_tracking_ct_mc": (C.c_int, [C.c_void_p, C.POINTER(GnssFile), C.POINTER(GnssSignal),
                                       C.POINTER(GnssTrack), C.POINTER(GnssAcquired), C.c_int32,
                                       C.c_int32, C.POINTER(GnssTrackOut)]),
+    "gnss_tracking_ct_multicorr": (C.c_int, [C.c_void_p, C.POINTER(GnssFile), C.POINTER(GnssSignal),
+                                             C.POINTER(GnssTrack), C.POINTER(GnssAcquired), C.c_int32,
+                                             C.POINTER(GnssTrackOut)]),
     "gnss_navi_decode": (C.c_int, [C.POINTER(GnssAcquired), C.POINTER(C.c_double),
                                    C.POINTER(C.c_int64), C.c_int64, C.POINTER(GnssNavOut)]),
     "gnss_lnav_bits": (C.c_int, [C.c_int32, C.c_int32, C.c_void_p]),

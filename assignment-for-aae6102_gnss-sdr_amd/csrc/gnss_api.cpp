@@ -698,9 +698,17 @@ struct PosCfg {
     int32_t mc_pdi;
 };
 
-// trackingCT.m (pos == nullptr) or the tracking loop of trackingCT_POS_updated.m
+// trackingCT_multiCorr-GIVEN.m (function trackingCT_multiCorr): `datalength` 1-ms steps
+// per channel (:27, hard-coded 50000 there), trackingCT conventions otherwise
+struct GivenCfg {
+    int32_t datalength;
+};
+
+// trackingCT.m (pos == gv == nullptr), the tracking loop of trackingCT_POS_updated.m (pos)
+// or of trackingCT_multiCorr-GIVEN.m (gv)
 static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg, const gnss_track* tr,
-                         const gnss_acquired* acq, gnss_track_out* out, const PosCfg* pos)
+                         const gnss_acquired* acq, gnss_track_out* out, const PosCfg* pos,
+                         const GivenCfg* gv = nullptr)
 {
     // GNSS_HOSTPROF: host-side phases of this call on stderr
     const bool hp = getenv("GNSS_HOSTPROF") != nullptr;
@@ -716,6 +724,10 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
         // trackingCT_POS_updated.m:196,207 reads numSample*dataType int16 values but advances
         // file_ptr by numSample*dataType BYTES: overlapping, misaligned reads (not reproduced)
         return fail(ctx, GNSS_EARG, "trackingCT_POS_updated: int8 records only");
+    if (gv && (prec != 1 || dtyp != 2 || gv->datalength <= 0 || tr->n_taps != 0 || (tr->chan && tr->n_chan > 0)))
+        // :47-48 forms every int8 record as I/Q pairs; codedelay sums the other channels' rows
+        // (the whole channel set, below)
+        return fail(ctx, GNSS_EARG, "trackingCT_multiCorr: int8 I/Q, datalength > 0, all channels");
     if (pos && (pos->ctPOS <= 0 || (!pos->countinx && !pos->mc_pdi) || tr->n_taps != 0))
         return fail(ctx, GNSS_EARG, "trackingCT_POS_updated: ctPOS > 0, countinx and E/P/L taps required");
     if (prec == 2 && dtyp == 1) {
@@ -731,11 +743,11 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
     const int nsv = acq->n;
     if (nsv <= 0 || nsv > GNSS_MAX_SV) return fail(ctx, GNSS_EARG, "no channels");
     const int64_t S = sg->Sample;
-    const int N1 = tr->msToProcessCT_1ms;
-    const int n10 = pos ? 0 : tr->msToProcessCT_10ms / 10;
-    if (!pos && N1 < 24) return fail(ctx, GNSS_EARG, "msToProcessCT_1ms must be >= 24 (bit-edge search window)");
+    const int N1 = gv ? gv->datalength : tr->msToProcessCT_1ms;
+    const int n10 = (pos || gv) ? 0 : tr->msToProcessCT_10ms / 10;
+    if (!pos && !gv && N1 < 24) return fail(ctx, GNSS_EARG, "msToProcessCT_1ms must be >= 24 (bit-edge search window)");
     if (N1 < 0) return fail(ctx, GNSS_EARG, "msToProcessCT_1ms < 0");
-    if (out->max_len < (pos ? (int64_t)pos->ctPOS : (int64_t)N1 + 19 + (int64_t)tr->msToProcessCT_10ms))
+    if (out->max_len < (pos ? (int64_t)pos->ctPOS : gv ? (int64_t)N1 : (int64_t)N1 + 19 + (int64_t)tr->msToProcessCT_10ms))
         return fail(ctx, GNSS_EARG, "max_len too small");
     // trackingCT_POS_updated.m: per channel, steps 1..n1 at 1 ms (msIndex <= 1000 +
     // countinx(svIndex), :183), then 10 ms up to ctPOS steps (:294)
@@ -767,6 +779,13 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
         ntaps = 25;
         P.conv = 1;
         P.chip_off = 1;
+    } else if (gv) {  // Spacing = -0.6:0.05:0.6 (:25), E/P/L = Spacing(3)/(13)/(23) (:94,106,118)
+        const Colon sp = colon_make(-0.6, 0.05, 0.6);
+        if (sp.n != 24) return fail(ctx, GNSS_EDEVICE, "Spacing colon");
+        for (int k = 0; k < 25; k++) taps_mc[k] = colon_elem(sp, k);
+        taps = taps_mc;
+        ntaps = 25;
+        P.given = 1;
     } else if (pos) {
         taps = taps_pos;
         P.conv = 1;
@@ -776,8 +795,10 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
         ntaps = tr->n_taps;
         taps = tr->tap_offsets;
     }
-    if (ntaps != 3 && ntaps != 11 && !(pos && pos->mc_pdi))
-        return fail(ctx, GNSS_EARG, "n_taps must be 3 or 11");
+    // 25: the taps of trackingCT_multiCorr-GIVEN.m:25 (-0.6:0.05:0.6) and of
+    // trackingCT_POS_updated_multicorrelator.m (int8 records: the step kernel's 25-tap build)
+    if (ntaps != 3 && ntaps != 11 && ntaps != 25) return fail(ctx, GNSS_EARG, "n_taps must be 3, 11 or 25");
+    if (ntaps == 25 && prec != 1) return fail(ctx, GNSS_EARG, "25 taps: int8 records only");
     P.iE = P.iP = P.iL = -1;
     for (int s = 0; s < ntaps; s++) {
         P.taps[s] = taps[s];
@@ -787,7 +808,7 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
         if (taps[s] == tr->CorrelatorSpacing && P.iL < 0) P.iL = s;
     }
     if (pos) { P.iE = 0; P.iP = 1; P.iL = 2; }
-    if (pos && pos->mc_pdi) { P.iE = 2; P.iP = 12; P.iL = 22; }
+    if ((pos && pos->mc_pdi) || gv) { P.iE = 2; P.iP = 12; P.iL = 22; }
     if (P.iE < 0 || P.iP < 0 || P.iL < 0) return fail(ctx, GNSS_EARG, "taps must contain -spacing, 0, +spacing");
     P.ntaps = ntaps;
 
@@ -838,6 +859,12 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
     for (int c : chans) {
         const int64_t cd = acq->codedelay[c];
         lo = std::min(lo, (S - cd + 1 + file->skip * S) * bps);
+        if (gv) {  // fseek(S - codedelay - 1 + skip*S) (:57), then one continuous read
+            const int64_t a0 = (S - cd - 1 + file->skip * S) * bps;
+            lo = std::min(lo, a0);
+            hi = std::max(hi, a0 + (int64_t)((double)N1 * S * 1.01 + 4096) * bps);
+            continue;
+        }
         if (pos) {  // one continuous read: n1 1-ms steps, then 10-ms steps (no re-seek)
             const int64_t n1 = pos_n1(c);
             const double ns = (double)n1 * S + (double)(pos->ctPOS - n1) * 10.0 * S;
@@ -955,6 +982,7 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
             t.n1_target = pos_n1(c);
             t.countinx = pos->countinx ? pos->countinx[c] : 0;
         }
+        if (gv) t.pos = (S - acq->codedelay[c] - 1 + file->skip * S) * bps;  // :57 (Codedelay = cd, :55)
         if (acq->sv[c] < 1 || acq->sv[c] > 51) return fail(ctx, GNSS_EARG, "bad PRN");
         ca_bits(acq->sv[c], &cab[(size_t)i * 32]);
     }
@@ -1115,7 +1143,12 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
     if (hp) { HIP_TRY(hipStreamSynchronize(ctx->stream)); fprintf(stderr, "hostprof setup %.3f ms\n", hms()); }
     HIP_TRY(hipEventRecord(e_all.a, ctx->stream));
     std::vector<TrkChan> chh((size_t)nch);
-    if (pos) {
+    if (gv) {
+        // trackingCT_multiCorr-GIVEN.m:52-314: datalength 1-ms steps, no bit-edge search, no
+        // 10-ms phase
+        HIP_TRY(launch_track_prepare(P, B, TD, 1, 0, ctx->stream));
+        if ((st = run_steps(1, N1))) return st;
+    } else if (pos) {
         // trackingCT_POS_updated.m:179-413: every channel continues from its own state and
         // file pointer; 1-ms steps while msIndex <= 1000 + countinx(svIndex), then 10 ms
         int64_t n1max = 0, n1min = INT64_MAX;
@@ -1240,6 +1273,21 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
         for (int64_t k = n1 + 10 * n10; k < ML; k++) dst[k] = 0;  // (a reused buffer's tail)
     });
     if (hp) fprintf(stderr, "hostprof expanded %.3f ms\n", hms());
+    if (gv && out->rec) {
+        // codedelay = Codedelay + sum(delayValue(1:msIndex)) (trackingCT_multiCorr-GIVEN.m:297):
+        // delayValue is ONE nsv x datalength matrix (:29) filled channel after channel, so the
+        // linear (column-major) sum takes the earlier channels' rows whole and this channel's
+        // own row up to msIndex (rows of later channels are still zero)
+        for (int c = 0; c < nsv; c++) {
+            double* cdr = out->rec + ((int64_t)c * GNSS_NFIELDS + GNSS_F_codedelay) * ML;
+            double sum = 0;
+            for (int64_t k = 0; k < N1; k++) {  // linear position k + 1
+                const int r = (int)(k % nsv);
+                if (r <= c) sum += out->rec[((int64_t)r * GNSS_NFIELDS + GNSS_F_delayValue) * ML + k / nsv];
+                cdr[k] = (double)acq->codedelay[c] + sum;
+            }
+        }
+    }
     rows = std::max(rows, n10 / 20);
     out->cn0_rows = rows;  // (POS: CN0_CT, one row per 20 steps of either pdi)
     if (out->CN0_Eph) {
@@ -1269,6 +1317,14 @@ int gnss_tracking_ct_pos(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
 {
     const PosCfg pc{ctPOS, countinx, 0};
     return tracking_impl(ctx, file, sg, tr, acq, out, &pc);
+}
+
+int gnss_tracking_ct_multicorr(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg,
+                               const gnss_track* tr, const gnss_acquired* acq, int32_t datalength,
+                               gnss_track_out* out)
+{
+    const GivenCfg g{datalength};
+    return tracking_impl(ctx, file, sg, tr, acq, out, nullptr, &g);
 }
 
 int gnss_tracking_ct_mc(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg, const gnss_track* tr,

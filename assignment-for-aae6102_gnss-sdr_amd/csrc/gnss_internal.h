@@ -161,6 +161,9 @@ struct TrkParams {
     // Code(ceil(t) + 2) with Code = [CA(end) CA.. CA(1) CA(2)]
     // (trackingCT_POS_updated_multicorrelator.m:94,233-258)
     int32_t chip_off;
+    // trackingCT_multiCorr-GIVEN.m's loop (trackingCT conventions otherwise): numSample by
+    // ceil (:60) and a short read raises (no "Not enough raw data" branch) -> GNSS_EIO
+    int32_t given;
     // added to a tap's colon element before ceil (the +0.05 of trackingCT_POS_updated.m:216)
     double tap_post[GNSS_MAX_TAPS];
 };

@@ -183,7 +183,7 @@ __device__ __forceinline__ StepSize step_size(const TrkParams& p, const NcoState
     z.inv_cps = fast_rcp(z.cps);
     const double num = p.codelength * pdi - c.remChip;
     const double qa = num * z.inv_cps;
-    if (p.conv) {  // ceil
+    if (p.conv || p.given) {  // ceil
         z.n = fabs(qa - rint(qa)) > 1e-7 ? (int64_t)ceil(qa) : (int64_t)ceil(num / z.cps);
         z.dv = z.n - (int64_t)(p.S * pdi);
         return z;
@@ -263,7 +263,7 @@ __device__ __forceinline__ void prepare_desc_i(const TrkParams& p, const NcoStat
     const int64_t sb = p.fmt ? 4 : 2;  // staged bytes per sample
     int bad = GNSS_OK;
     if (n <= 0 || n > (int64_t)(p.S * pdi * 1.01) + 64) bad = GNSS_EINDEX;
-    else if (p.bps * (A + n) > p.file_len) bad = (phaseC || p.conv) ? GNSS_EIO : GNSS_ENODATA;  // :108-112 / :442
+    else if (p.bps * (A + n) > p.file_len) bad = (phaseC || p.conv || p.given) ? GNSS_EIO : GNSS_ENODATA;  // :108-112 / :442
     else if (sb * A < p.buf_base || sb * (A + n) > p.buf_base + p.buf_len) bad = GNSS_EIO;
     if (lane < p.ntaps) {
         // t = (0 + Spacing + remChip) : cps : ((numSample-1)*cps + Spacing + remChip) (:96-98)

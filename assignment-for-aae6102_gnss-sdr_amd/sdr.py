@@ -396,10 +396,11 @@ def trackingCT_POS(file, signal, track, Acquired, countinx, *, ctx: Context | No
     return build_tck_result(Acquired, buf, channels, abi.FIELDS_POS), cn0
 
 
-def mc_result(Acquired, buf: TrackOutBuffers, channels=None) -> StructArray:
+def mc_result(Acquired, buf: TrackOutBuffers, channels=None, fields=None) -> StructArray:
     """TckResultCT_mltCorr: the loop fields plus every tap under the reference's names
-    (E_i_060 ... P_i ... L_q060, trackingCT_POS_updated_multicorrelator.m:374-439)."""
-    res = build_tck_result(Acquired, buf, channels, abi.FIELDS_POS)
+    (E_i_060 ... P_i ... L_q060, trackingCT_POS_updated_multicorrelator.m:374-439,
+    trackingCT_multiCorr-GIVEN.m:248-286)."""
+    res = build_tck_result(Acquired, buf, channels, fields or abi.FIELDS_POS)
     for prn in res.prns():
         e = res(prn)
         for k, name in enumerate(abi.MC_TAP_NAMES):
@@ -435,6 +436,32 @@ def trackingCT_POS_updated_multicorrelator(file, signal, track, Acquired, *,
         return buf
     cn0 = buf.CN0[: buf.c.cn0_rows].copy()
     return mc_result(Acquired, buf, channels), cn0
+
+
+def trackingCT_multiCorr(file, signal, track, Acquired, *, datalength: int = 50000,
+                         ctx: Context | None = None, raw: bool = False):
+    """trackingCT_multiCorr-GIVEN.m (function trackingCT_multiCorr) on the GPU ->
+    (TckResultCT, CN0_CT).
+
+    `datalength` 1-ms steps per channel (:27 hard-codes 50000) from fseek(Sample - codedelay
+    - 1 + skip*Sample) (:57), trackingCT.m's loop with ceil numSample on the 25 taps
+    Spacing = -0.6:0.05:0.6. TckResultCT(prn) carries the trackingCT field names of :287-297
+    plus E_i_060 ... L_q060; codedelay keeps the reference's linear sum over one shared
+    nsv x datalength delayValue matrix (earlier channels' rows included).
+    """
+    ctx = ctx or default_context()
+    nsv = len(Acquired.sv)
+    f, k1 = to_c_file(file)
+    s = to_c_signal(signal)
+    t, k2 = to_c_track(track, None, None)
+    a = to_c_acquired(Acquired)
+    buf = TrackOutBuffers(nsv, track, abi.MC_TAPS, ctPOS=max(int(datalength), 1))
+    st = ctx.lib.gnss_tracking_ct_multicorr(ctx.h, C.byref(f), C.byref(s), C.byref(t), C.byref(a),
+                                            int(datalength), C.byref(buf.c))
+    ctx.check(st)
+    if raw:
+        return buf
+    return mc_result(Acquired, buf, None, abi.FIELDS), buf.CN0[: buf.c.cn0_rows].copy()
 
 
 def naviDecode_updated(Acquired, ALLTckResult, *, eph_cap: int = 512):

@@ -117,7 +117,9 @@ typedef struct gnss_track {
      * trackingCT_multiCorr-GIVEN.m:25,92-143). n_taps = 0 -> the three E/P/L taps
      * [-CorrelatorSpacing 0 +CorrelatorSpacing] (trackingCT.m:24). Otherwise
      * tap_offsets[n_taps] (chips) must contain -CorrelatorSpacing, 0 and
-     * +CorrelatorSpacing, which feed the DLL/PLL exactly as E/P/L do.           */
+     * +CorrelatorSpacing, which feed the DLL/PLL exactly as E/P/L do. n_taps is
+     * 3, 11 (config 5: -0.5:0.1:0.5) or 25 (-0.6:0.05:0.6 of the GIVEN file; int8
+     * records only).                                                           */
     int32_t        n_taps;
     const double  *tap_offsets;
     /* Channel shard (multi-GPU): process Acquired channels chan[0..n_chan-1]
@@ -258,6 +260,23 @@ int gnss_tracking_ct_pos(gnss_ctx *ctx, const gnss_file *file, const gnss_signal
  *     Spacing order (E_i_060 ... L_i060 of :374-423).
  * max_len >= msPosCT/pdi; track->n_taps must be 0. int8 records only, EOF -> GNSS_EIO. */
 #define GNSS_MC_TAPS 25
+
+/* trackingCT_multiCorr-GIVEN.m (function trackingCT_multiCorr, the multi-correlator loop the
+ * assignment hands out). Replaces TckResultCT = trackingCT_multiCorr(file,
+ * signal, track, Acquired) (:1): per channel, fseek to (Sample - codedelay - 1 + skip*Sample)
+ * bytes*2 (:57) and `datalength` 1-ms steps (:27 hard-codes 50000) read continuously, with
+ * trackingCT.m's loop (round -> ceil for numSample, :60; remChip from codeFreqBasis*ms;
+ * codeFreq = f0 - code_output; T = 1 ms) on the GNSS_MC_TAPS taps Spacing = -0.6:0.05:0.6
+ * (:25), Code(ceil(t) + 1), E/P/L = Spacing(3)/(13)/(23) = -0.5/0/+0.5. Records as
+ * gnss_tracking_ct (rec fields of :287-297 in the trackingCT slots, remSample included; every
+ * tap in taps[nsv][2][25][max_len], the E_i_060 ... L_q060 of :163-286), one row per step;
+ * codedelay = codedelay + sum(delayValue(1:msIndex)) over ONE nsv x datalength matrix filled
+ * channel after channel (:29,297: earlier channels' rows count whole). CN0_CT every 20 steps.
+ * max_len >= datalength; int8 I/Q records only (:47-48 pairs every record), no channel shard;
+ * a short read -> GNSS_EIO (MATLAB raises; the function has no "Not enough raw data" branch). */
+int gnss_tracking_ct_multicorr(gnss_ctx *ctx, const gnss_file *file, const gnss_signal *signal,
+                               const gnss_track *track, const gnss_acquired *acquired,
+                               int32_t datalength, gnss_track_out *out);
 int gnss_tracking_ct_mc(gnss_ctx *ctx, const gnss_file *file, const gnss_signal *signal,
                         const gnss_track *track, const gnss_acquired *acquired, int32_t msPosCT,
                         int32_t pdi, gnss_track_out *out);

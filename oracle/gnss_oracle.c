@@ -660,6 +660,7 @@ typedef struct trk_ctx {
     const double *taps;
     double tau1code, tau2code, tau1carr, tau2carr;
     int nsv;
+    int given; /* trackingCT_multiCorr-GIVEN.m: ceil numSample (:60), a short read raises */
     gnss_track_out *out;
 } trk_ctx;
 
@@ -716,7 +717,8 @@ static int trk_step(const trk_ctx *t, chan_state *c, int ch, int sv1, int pdi, i
         c->numSample = (int64_t)or_round((sg->codelength * pdi - c->remChip) / (c->codeFreq / sg->Fs));
     } else {
         c->remSample = (sg->codelength - c->remChip) / (c->codeFreq / sg->Fs); /* :79 */
-        c->numSample = (int64_t)or_round((sg->codelength * pdi - c->remChip) / (c->codeFreq / sg->Fs));
+        const double q = (sg->codelength * pdi - c->remChip) / (c->codeFreq / sg->Fs);
+        c->numSample = (int64_t)(t->given ? ceil(q) : or_round(q)); /* (GIVEN :60 ceil) */
         delayValue = c->numSample - (int64_t)(S * pdi); /* :82 */
     }
     dv[dv_col] = delayValue;
@@ -725,7 +727,7 @@ static int trk_step(const trk_ctx *t, chan_state *c, int ch, int sv1, int pdi, i
     const int64_t m = rd_cpx(t->file, c->pos, n, buf, &got); /* :84-93 / :416-426 */
     if (m == -1) return GNSS_EIO;
     if (m == -2) return GNSS_EINDEX;
-    if (m != n) return phaseC ? GNSS_EIO : GNSS_ENODATA; /* :108-112 / :442 */
+    if (m != n) return (phaseC || t->given) ? GNSS_EIO : GNSS_ENODATA; /* :108-112 / :442 */
     c->pos += got; /* ftell */
 
     /* code range check: MATLAB would raise an index error */
@@ -946,6 +948,74 @@ int or_tracking_ct(const gnss_file *file, const gnss_signal *sg, const gnss_trac
     if (r1 > rows) rows = r1;
     if (tr->msToProcessCT_10ms / 10 / 20 > rows) rows = tr->msToProcessCT_10ms / 10 / 20;
     out->cn0_rows = rows;
+    return status;
+}
+
+/* ------------------------------------------------------------------------ */
+/* trackingCT_multiCorr-GIVEN.m (function trackingCT_multiCorr)              */
+/* ------------------------------------------------------------------------ */
+/* Per channel (:31-313): fseek to (Sample - codedelay - 1 + skip*Sample)*bytes (:57), then
+ * `datalength` 1-ms steps of trackingCT.m's step with ceil numSample (:58-60), 25 taps at
+ * Spacing = -0.6:0.05:0.6 (:25), Code(ceil(t)+1) (:140-164), E/P/L = Spacing(3)/(13)/(23).
+ * codedelay (:297) = Codedelay + sum(delayValue(1:msIndex)) over the one nsv x datalength
+ * matrix of :29, filled channel after channel: a pass after all channels. */
+int or_tracking_ct_given(const gnss_file *file, const gnss_signal *sg, const gnss_track *tr,
+                         const gnss_acquired *acq, int32_t datalength, gnss_track_out *out,
+                         int nthreads)
+{
+    if (file->dataPrecision != 1 || file->dataType != 2 || datalength <= 0 || tr->n_taps != 0 ||
+        (tr->chan && tr->n_chan > 0) || out->max_len < datalength)
+        return GNSS_EARG;
+    double sp[25];
+    or_colon spc;
+    or_colon_init(&spc, -0.6, 0.05, 0.6);
+    if (spc.n != 24) return GNSS_EARG;
+    for (int k = 0; k < 25; k++) sp[k] = or_colon_elem(&spc, k);
+    trk_ctx t;
+    memset(&t, 0, sizeof(t));
+    t.file = file; t.sg = sg; t.tr = tr; t.out = out; t.nsv = acq->n;
+    t.fsize = file_size(file);
+    t.ntaps = 25; t.taps = sp; t.iE = 2; t.iP = 12; t.iL = 22; t.given = 1;
+    or_calc_loop_coef(tr->DLLBW, tr->DLLDamp, tr->DLLGain, &t.tau1code, &t.tau2code); /* :21-22 */
+    or_calc_loop_coef(tr->PLLBW, tr->PLLDamp, tr->PLLGain, &t.tau1carr, &t.tau2carr);
+    const int nsv = acq->n;
+    const int64_t S = sg->Sample;
+    int status = GNSS_OK;
+    if (out->CN0_Eph) memset(out->CN0_Eph, 0, sizeof(double) * (size_t)out->cn0_cap * (size_t)nsv);
+#pragma omp parallel for num_threads(nthreads_of(nthreads)) schedule(dynamic)
+    for (int ch = 0; ch < nsv; ch++) {
+        int8_t ca[1023];
+        int st = or_generate_ca(acq->sv[ch], ca) ? GNSS_EARG : GNSS_OK;
+        cpx *buf = (cpx *)malloc(sizeof(cpx) * (size_t)(2 * (S + 4096)));
+        int64_t *dv = (int64_t *)calloc((size_t)datalength, sizeof(int64_t));
+        const int64_t cd0 = acq->codedelay[ch]; /* Codedelay = AcqCodeDelay (:53,55) */
+        chan_state c;
+        chan_init(&c, &t, acq, ch);
+        c.pos = (S - cd0 - 1 + file->skip * S) * file->dataPrecision * file->dataType; /* :57 */
+        for (int64_t i = 1; i <= datalength && st == GNSS_OK; i++)
+            st = trk_step(&t, &c, ch, ch + 1, 1, 0, i, dv, i - 1, out->CN0_Eph, buf, ca, cd0, NULL);
+        if (!st && out->len) out->len[ch] = datalength;
+        if (out->countinx) out->countinx[ch] = 0;
+        free(buf);
+        free(dv);
+#pragma omp critical
+        {
+            if (st && status == GNSS_OK) status = st;
+        }
+    }
+    if (status == GNSS_OK && out->rec) {
+        const int64_t ML = out->max_len;
+        for (int ch = 0; ch < nsv; ch++) {
+            double *cdr = out->rec + ((int64_t)ch * GNSS_NFIELDS + GNSS_F_codedelay) * ML;
+            double sum = 0;
+            for (int64_t k = 0; k < datalength; k++) { /* linear position k + 1 */
+                int r = (int)(k % nsv);
+                if (r <= ch) sum += out->rec[((int64_t)r * GNSS_NFIELDS + GNSS_F_delayValue) * ML + k / nsv];
+                cdr[k] = (double)acq->codedelay[ch] + sum;
+            }
+        }
+    }
+    out->cn0_rows = datalength / 20;
     return status;
 }
 

@@ -55,6 +55,11 @@ int or_tracking_ct(const gnss_file *file, const gnss_signal *signal, const gnss_
 int or_tracking_ct_pos(const gnss_file *file, const gnss_signal *signal, const gnss_track *track,
                        const gnss_acquired *acquired, int32_t ctPOS, const int32_t *countinx,
                        gnss_track_out *out, int nthreads);
+/* trackingCT_multiCorr-GIVEN.m's loop (datalength 1-ms steps, 25 taps); outputs as
+ * gnss_tracking_ct_multicorr. */
+int or_tracking_ct_given(const gnss_file *file, const gnss_signal *signal, const gnss_track *track,
+                         const gnss_acquired *acquired, int32_t datalength, gnss_track_out *out,
+                         int nthreads);
 /* The tracking loop of trackingCT_POS_updated_multicorrelator.m (25 taps, every step at
  * pdi, msPosCT/pdi steps); outputs as gnss_tracking_ct_mc. */
 int or_tracking_ct_mc(const gnss_file *file, const gnss_signal *signal, const gnss_track *track,

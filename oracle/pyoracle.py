@@ -55,6 +55,9 @@ def load():
         lib.or_tracking_ct_mc.argtypes = [C.POINTER(abi.GnssFile), C.POINTER(abi.GnssSignal),
                                           C.POINTER(abi.GnssTrack), C.POINTER(abi.GnssAcquired),
                                           C.c_int32, C.c_int32, C.POINTER(abi.GnssTrackOut), C.c_int]
+        lib.or_tracking_ct_given.argtypes = [C.POINTER(abi.GnssFile), C.POINTER(abi.GnssSignal),
+                                             C.POINTER(abi.GnssTrack), C.POINTER(abi.GnssAcquired),
+                                             C.c_int32, C.POINTER(abi.GnssTrackOut), C.c_int]
         lib.or_correlate_step.argtypes = [C.c_void_p, C.c_int64, C.c_double, C.c_double, C.c_double,
                                           C.c_double, C.c_double, C.c_void_p, C.c_int, C.c_int,
                                           C.c_void_p, C.c_void_p]
@@ -181,6 +184,24 @@ def trackingCT_mc(file, signal, track, Acquired, channels=None, nthreads=0, raw=
         raise abi.GnssError(st, "or_tracking_ct_mc")
     cn0 = buf.CN0[: buf.c.cn0_rows].copy()
     return sdr.mc_result(Acquired, buf, channels), cn0
+
+
+def trackingCT_multiCorr(file, signal, track, Acquired, datalength=50000, nthreads=0, raw=False):
+    """trackingCT_multiCorr-GIVEN.m's loop (datalength 1-ms steps, 25 taps)."""
+    nsv = len(Acquired.sv)
+    f, k1 = sdr.to_c_file(file)
+    s = sdr.to_c_signal(signal)
+    t, k2 = sdr.to_c_track(track, None, None)
+    a = sdr.to_c_acquired(Acquired)
+    buf = sdr.TrackOutBuffers(nsv, track, abi.MC_TAPS, ctPOS=max(int(datalength), 1))
+    st = load().or_tracking_ct_given(C.byref(f), C.byref(s), C.byref(t), C.byref(a), int(datalength),
+                                     C.byref(buf.c), nthreads)
+    if raw:
+        buf.status = st
+        return buf
+    if st != abi.OK:
+        raise abi.GnssError(st, "or_tracking_ct_given")
+    return sdr.mc_result(Acquired, buf, None, abi.FIELDS), buf.CN0[: buf.c.cn0_rows].copy()
 
 
 def correlate_step(iq, numSample, remChip, codeFreq, Fs, carrierFreq, remPhase, ca, pdi, taps):

@@ -119,7 +119,27 @@ def main_mc():
     print("multicorrelator golden written:", {k: v.shape for k, v in out.items()})
 
 
+def main_given():
+    """trackingCT_multiCorr-GIVEN.m loop: 3 channels, 25 taps, 80 x 1 ms on the record of
+    tests/test_oracle_given.py."""
+    import test_oracle_given as tg
+    data = tg.given_record(pkg, po)
+    file, signal, acq, track, _, _ = pkg.initParameters()
+    file.skip, file.data = tg.SKIP, data
+    A = SimpleNamespace(sv=np.array(tg.SVS), SNR=np.full(3, 20.0), Doppler=np.zeros(3),
+                        codedelay=np.array(tg.CD), fineFreq=np.array(tg.FF))
+    buf = po.trackingCT_multiCorr(file, signal, track, A, tg.DATALEN, raw=True)
+    assert buf.status == 0
+    L = tg.DATALEN
+    np.savez_compressed(os.path.join(HERE, "golden_given_small.npz"), rec=buf.rec[:, :, :L],
+                        taps=buf.taps[:, :, :, :L], len=buf.len, cn0=buf.CN0[: buf.c.cn0_rows])
+    print("GIVEN multiCorr golden written")
+
+
 if __name__ == "__main__":
+    if "--given-only" in sys.argv:
+        main_given()
+        sys.exit(0)
     if "--mc-only" in sys.argv:
         main_mc()
         sys.exit(0)

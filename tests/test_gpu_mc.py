@@ -66,3 +66,50 @@ def test_mc_errors(pkg, ctx, opensky_short):
     with pytest.raises(pkg.abi.GnssError) as e:
         pkg.trackingCT_POS_updated_multicorrelator(file, signal, track, A, ctx=ctx)
     assert e.value.status == pkg.abi.EARG
+
+
+# ---- trackingCT_multiCorr-GIVEN.m (gnss_tracking_ct_multicorr) --------
+def compare_given(pkg, g, r, tol=1e-8):
+    from test_gpu_tracking import compare
+    compare(pkg, g, r)
+    for c in range(len(g.len)):
+        n = int(r.len[c])
+        scale = np.sqrt(np.mean(r.rec[c, 0, :n] ** 2 + r.rec[c, 1, :n] ** 2))
+        err = np.max(np.abs(g.taps[c, :, :, :n] - r.taps[c, :, :, :n])) / scale
+        assert err < 1e-5 and err < tol, (c, err)
+
+
+def test_given_parity_opensky_8ch(pkg, po, ctx, opensky_short):
+    skip, cfg, data = opensky_short
+    file, signal, acq, track = params(pkg, skip, data)
+    A = acquired_of(OPENSKY["svs"], OPENSKY["cd"], OPENSKY["ff"])
+    g = pkg.trackingCT_multiCorr(file, signal, track, A, datalength=600, ctx=ctx, raw=True)
+    r = po.trackingCT_multiCorr(file, signal, track, A, 600, raw=True)
+    assert r.status == 0
+    compare_given(pkg, g, r)
+    T, cn0 = pkg.trackingCT_multiCorr(file, signal, track, A, datalength=600, ctx=ctx)
+    assert len(T(3).E_i_060) == 600 and np.array_equal(T(3).E_i, T(3).taps_i[2])
+    assert cn0.shape == (30, 8)
+
+
+def test_given_matches_golden_vectors(pkg, po, ctx):
+    import test_oracle_given as tg
+    g = np.load(tg.GOLDEN)
+    data = tg.given_record(pkg, po)
+    file, signal, acq, track = params(pkg, tg.SKIP, data)
+    A = acquired_of(tg.SVS, tg.CD, tg.FF)
+    b = pkg.trackingCT_multiCorr(file, signal, track, A, datalength=tg.DATALEN, ctx=ctx, raw=True)
+    tg.check_given_against_golden(g, b.rec, b.taps, b.len, b.CN0[: b.c.cn0_rows], 1e-8)
+
+
+def test_given_errors(pkg, ctx, opensky_short):
+    skip, cfg, data = opensky_short
+    file, signal, acq, track = params(pkg, skip, data[: 2 * 58000 * 300])
+    A = acquired_of([16], [26051], [4579675.0])
+    with pytest.raises(pkg.abi.GnssError) as e:  # short read: MATLAB raises
+        pkg.trackingCT_multiCorr(file, signal, track, A, datalength=400, ctx=ctx)
+    assert e.value.status == pkg.abi.EIO
+    file.dataPrecision = 2
+    with pytest.raises(pkg.abi.GnssError) as e:
+        pkg.trackingCT_multiCorr(file, signal, track, A, datalength=100, ctx=ctx)
+    assert e.value.status == pkg.abi.EARG

@@ -115,6 +115,28 @@ def test_tracking_parity_11_taps(pkg, po, ctx, opensky_short):
         assert np.array_equal(g.rec[c, 5, :n], g.taps[c, 1, 10, :n])
 
 
+def test_tracking_parity_25_taps(pkg, po, ctx, opensky_short):
+    """The 25 taps of trackingCT_multiCorr-GIVEN.m:25 (Spacing = -0.6:0.05:0.6; E = Spacing(3)
+    = -0.5, P = (13), L = (23) = +0.5) on trackingCT's loop, both phases (step kernel)."""
+    skip, cfg, data = opensky_short
+    file, signal, acq, track = params(pkg, skip, data)
+    track.msToProcessCT_1ms, track.msToProcessCT_10ms = 700, 300
+    taps = po.colon(-0.6, 0.05, 0.6)
+    assert len(taps) == 25 and (taps[2], taps[12], taps[22]) == (-0.5, 0.0, 0.5)
+    A = acquired_of([3, 26], [3684, 57908], [4580975.0, 4581800.0])  # (bit edges within 700 ms)
+    g = pkg.trackingCT(file, signal, track, A, ctx=ctx, taps=taps, raw=True)
+    r = po.trackingCT(file, signal, track, A, taps=taps, raw=True)
+    assert r.status == 0
+    compare(pkg, g, r)
+    for c in range(2):
+        n = int(r.len[c])
+        scale = np.sqrt(np.mean(r.taps[c, :, :, :n] ** 2))
+        assert np.max(np.abs(g.taps[c, :, :, :n] - r.taps[c, :, :, :n])) / scale < 1e-10
+        assert np.array_equal(g.rec[c, 0, :n], g.taps[c, 0, 12, :n])
+        assert np.array_equal(g.rec[c, 2, :n], g.taps[c, 0, 2, :n])
+        assert np.array_equal(g.rec[c, 5, :n], g.taps[c, 1, 22, :n])
+
+
 def test_correlate_step_random_states(pkg, po, ctx, opensky_short):
     import importlib
     sdr = importlib.import_module("assignment-for-aae6102_gnss-sdr_amd.sdr")

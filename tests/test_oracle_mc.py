@@ -11,6 +11,7 @@ must satisfy the same relations to the last bit, with T = pdi*t in the loop filt
 Code = [CA(end) repmat(CA,1,pdi) CA(1) CA(2)] indexed by ceil(t) + 2 (:94,233-258).
 """
 import ctypes as C
+import math
 import os
 
 import numpy as np
@@ -80,8 +81,8 @@ def test_mc_step_relations_bit_exact(mc_runs, pdi):
             for name, k in (("E", 2), ("P", 12), ("L", 22)):
                 assert r[f[name + "_i"], j] == buf.taps[c, 0, k, j]
                 assert r[f[name + "_q"], j] == buf.taps[c, 1, k, j]
-            E = np.sqrt(r[f["E_i"], j] ** 2 + r[f["E_q"], j] ** 2)
-            L = np.sqrt(r[f["L_i"], j] ** 2 + r[f["L_q"], j] ** 2)
+            E = math.sqrt(r[f["E_i"], j] * r[f["E_i"], j] + r[f["E_q"], j] * r[f["E_q"], j])
+            L = math.sqrt(r[f["L_i"], j] * r[f["L_i"], j] + r[f["L_q"], j] * r[f["L_q"], j])
             e = 0.5 * (E - L) / (E + L)
             assert r[f["codeError"], j] == e
             cn = lib.or_loop_filter(cn, e, cl, t1c, t2c, T)

@@ -10,6 +10,7 @@ bit, so the full loop is pinned by the same reference artefact (its correlator v
 the absent IF file: parity unpinned there, as for trackingCT).
 """
 import ctypes as C
+import math
 
 import numpy as np
 import pytest
@@ -66,8 +67,8 @@ def test_pos_step_relations_bit_exact(pos_run):
             assert r[f["codedelay"], j] == 58000 - CD[c] + 1 + dvsum  # :290
             assert r[f["codedelay2"], j] == (pos / 2) % 58000
             assert r[f["absoluteSampleCodedelay"], j] == r[f["codedelay2"], j]
-            E = np.sqrt(r[f["E_i"], j] ** 2 + r[f["E_q"], j] ** 2)
-            L = np.sqrt(r[f["L_i"], j] ** 2 + r[f["L_q"], j] ** 2)
+            E = math.sqrt(r[f["E_i"], j] * r[f["E_i"], j] + r[f["E_q"], j] * r[f["E_q"], j])
+            L = math.sqrt(r[f["L_i"], j] * r[f["L_i"], j] + r[f["L_q"], j] * r[f["L_q"], j])
             e = 0.5 * (E - L) / (E + L)
             assert r[f["codeError"], j] == e
             cn = lib.or_loop_filter(cn, e, cl, t1c, t2c, 0.001)
