@@ -113,3 +113,18 @@ def test_given_errors(pkg, ctx, opensky_short):
     with pytest.raises(pkg.abi.GnssError) as e:
         pkg.trackingCT_multiCorr(file, signal, track, A, datalength=100, ctx=ctx)
     assert e.value.status == pkg.abi.EARG
+
+
+def test_mc_channel_shards_equal_full_run(pkg, ctx, opensky_short):
+    """Channel shards (the multi-GPU split) of the 25-tap loop reproduce the full run's rows
+    bit for bit (lane geometry and reductions do not depend on the channel set)."""
+    skip, cfg, data = opensky_short
+    file, signal, acq, track = params(pkg, skip, data)
+    track.msPosCT, track.pdi = 300, 10
+    A = acquired_of(OPENSKY["svs"], OPENSKY["cd"], OPENSKY["ff"])
+    full = pkg.trackingCT_POS_updated_multicorrelator(file, signal, track, A, ctx=ctx, raw=True)
+    for shard in ([0, 2, 4, 6], [1, 3, 5, 7]):
+        part = pkg.trackingCT_POS_updated_multicorrelator(file, signal, track, A, ctx=ctx,
+                                                          channels=shard, raw=True)
+        for c in shard:
+            assert np.array_equal(part.rec[c], full.rec[c]) and np.array_equal(part.taps[c], full.taps[c])
