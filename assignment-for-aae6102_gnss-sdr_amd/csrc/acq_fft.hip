@@ -516,10 +516,11 @@ __global__ __launch_bounds__(kRowThreads) void fine_rows_kernel(
     const double2* __restrict__ tabA, const double2* __restrict__ tabB, double2* __restrict__ E)
 {
     constexpr int T = kFineT;
-    __shared__ double2 s_a[kRow], s_tw[kRow];
+    // twiddles read from the (L2-resident) global table: 32 KB of LDS per block instead of
+    // 64, five blocks per CU instead of two
+    __shared__ double2 s_a[kRow];
     const int rho = blockIdx.x, r = blockIdx.y, tid = threadIdx.x;
     const int m2 = rho / P, n2 = rho - m2 * P;
-    load_row_tw(s_tw, tw_row, tid);
     const int64_t RD = (int64_t)kRow * D;
     for (int m1 = tid; m1 < kRow; m1 += kRowThreads) {
         const int64_t n = (int64_t)P * T * m1 + (int64_t)P * m2 + n2;
@@ -530,7 +531,7 @@ __global__ __launch_bounds__(kRowThreads) void fine_rows_kernel(
         s_a[m1] = cmul(x, tabA[((int64_t)m1 * r) % RD]);
     }
     __syncthreads();
-    fft2000<-1>(s_a, s_tw, tid);
+    fft2000<-1>(s_a, tw_row, tid);
     double sn, cs;
     const int64_t e = ((int64_t)(P * m2 + n2) * r) % N;
     sincospi(-2.0 * (double)e / (double)N, &sn, &cs);
