@@ -269,12 +269,14 @@ def main():
     barrier(dist, local)
     t0 = time.perf_counter()
     acq_units = trk_units = 0
-    acq_ms = trk_ms = 0.0
+    acq_ms = trk_ms = acq_corr_ms = acq_fine_ms = 0.0
     for _ in range(args.steps):
         A, ta, tt, buf = one_step()
         acq_units += ta["acq_hypothesis_samples"]
         trk_units += tt["track_channel_samples"]
         acq_ms += ta["acq_ms"]
+        acq_corr_ms += ta["acq_corr_ms"]
+        acq_fine_ms += ta["acq_fine_ms"]
         trk_ms += tt["track_ms"]
     barrier(dist, local)
     elapsed = time.perf_counter() - t0
@@ -348,6 +350,13 @@ def main():
         "acq_ms": round(acq_ms / args.steps, 3),
         "track_ms": round(trk_ms / args.steps, 3),
         "roofline": roof,
+        # the acquisition's own line (16 B per hypothesis-sample over the
+        # correlation time, the fine-frequency FFTs timed separately)
+        "acq_roofline": ({"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                          "achieved": round(16.0 * acq_units / (acq_corr_ms * 1e-3) / 1e9, 2),
+                          "frac": round(16.0 * acq_units / (acq_corr_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                          "corr_ms": round(acq_corr_ms / args.steps, 3),
+                          "fine_ms": round(acq_fine_ms / args.steps, 3)} if acq_corr_ms else None),
         "cpu_baseline": cpu,
     }
     if rank == 0:
