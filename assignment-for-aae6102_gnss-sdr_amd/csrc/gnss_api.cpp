@@ -528,8 +528,14 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         HIP_TRY(B.alloc(ctx, "acq.B", sizeof(float2) * ntr * S));
         HIP_TRY(X.alloc(ctx, "acq.X", sizeof(float2) * ntr * S));
         const int npairs = nb * np;
-        // (bin, PRN) pairs per batch: the inverse intermediate stays ~256 MB (Infinity Cache)
-        int batch = (int)std::max<int64_t>(1, ((int64_t)256 << 20) / ((int64_t)dl * S * 8));
+        // (bin, PRN) pairs per batch: the inverse intermediate round-trips through HBM
+        // anyway (PMC, profiles/acq_traffic_r01.json), so batches of ~1 GiB, balanced (no
+        // small tail batch that leaves the chip idle): config 2 measured 7.94 ms of
+        // correlation at 28 pairs per batch (256 MB), 7.09-7.29 at 112, 7.15-7.30 at 232
+        // (tools/gpu_acq_batch.sh). Pairs are independent: the bits do not depend on it.
+        const int target = (int)std::max<int64_t>(1, ((int64_t)1 << 30) / ((int64_t)dl * S * 8));
+        const int nbat = (npairs + target - 1) / target;
+        int batch = (npairs + nbat - 1) / nbat;
         if (const char* e = getenv("GNSS_ACQ_BATCH")) batch = std::max(1, atoi(e));
         batch = std::min(batch, npairs);
         HIP_TRY(A.alloc(ctx, "acq.A", sizeof(float2) * (size_t)batch * dl * S));
