@@ -498,7 +498,7 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel(
 //            -> |X| and the first maximum in fftshift order (:110-116)
 
 constexpr int kFineT = 10;
-constexpr int kFineJC = 8;  // j1 columns per FC block
+constexpr int kFineJC = 16;  // j1 columns per FC block
 
 __global__ void fine_twiddle_kernel(double2* __restrict__ t, int64_t len)
 {
