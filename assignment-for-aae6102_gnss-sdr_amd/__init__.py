@@ -10,10 +10,10 @@ reference's MATLAB interface. Import with
 directory name is not a Python identifier).
 """
 from . import abi, synth
-from .sdr import (Context, DeviceRecord, StructArray, TrackOutBuffers, acquisition, ca_code, colon,
+from .sdr import (Context, DeviceRecord, DeviceTrackOutBuffers, StructArray, TrackOutBuffers, acquisition, ca_code, colon,
                   default_context, initParameters, naviDecode_updated, trackingCT, trackingCT_multiCorr,
                   trackingCT_POS, trackingCT_POS_updated_multicorrelator)
 
-__all__ = ["abi", "synth", "Context", "DeviceRecord", "StructArray", "TrackOutBuffers",
+__all__ = ["abi", "synth", "Context", "DeviceRecord", "DeviceTrackOutBuffers", "StructArray", "TrackOutBuffers",
            "acquisition", "ca_code", "colon", "default_context", "initParameters", "naviDecode_updated",
            "trackingCT", "trackingCT_multiCorr", "trackingCT_POS", "trackingCT_POS_updated_multicorrelator"]

@@ -20,6 +20,7 @@ FIELDS = ["P_i", "P_q", "E_i", "E_q", "L_i", "L_q", "PLLdiscri", "DLLdiscri", "c
           "remChip", "codeFreq", "carrierFreq", "remPhase", "remSample", "numSample",
           "delayValue", "absoluteSample", "codedelay2"]
 NFIELDS = len(FIELDS)
+OUT_DEVICE = 1  # gnss_track_out.flags: rec / taps are device pointers (ABI v7)
 # the same slots under trackingCT_POS_updated.m:273-292's names (gnss_tracking_ct_pos)
 FIELDS_POS = ["P_i", "P_q", "E_i", "E_q", "L_i", "L_q", "carrError", "codeError", "codedelay",
               "remChip", "codeFreq", "carrFreq", "remCarrPhase", "absoluteSampleCodedelay",
@@ -90,7 +91,8 @@ class GnssTrackOut(C.Structure):
     _fields_ = [("max_len", C.c_int64), ("rec", C.POINTER(C.c_double)),
                 ("taps", C.POINTER(C.c_double)), ("len", C.POINTER(C.c_int64)),
                 ("countinx", C.POINTER(C.c_int32)), ("CN0_Eph", C.POINTER(C.c_double)),
-                ("cn0_cap", C.c_int32), ("cn0_rows", C.c_int32)]
+                ("cn0_cap", C.c_int32), ("cn0_rows", C.c_int32), ("flags", C.c_int32),
+                ("reserved", C.c_int32)]
 
 
 class GnssTiming(C.Structure):
@@ -173,6 +175,13 @@ def load(path: str | None = None):
     if not os.path.exists(p):
         raise ImportError(f"{p} missing: the HIP extension is not built "
                           "(run `python -c 'import __graft_entry__ as g; g.build()'`)")
+    # PyTorch-ROCm ships its own HIP / HSA runtime: load it BEFORE this library's, or torch
+    # finds no GPU later in the same process (device-resident outputs and the RCCL gathers
+    # hand torch tensors to the library). The library then shares the process with both.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(p)
     for name, (res, args) in PROTOTYPES.items():
         fn = getattr(lib, name)

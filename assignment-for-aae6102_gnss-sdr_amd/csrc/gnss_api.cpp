@@ -755,6 +755,8 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
     if (N1 < 0) return fail(ctx, GNSS_EARG, "msToProcessCT_1ms < 0");
     if (out->max_len < (pos ? (int64_t)pos->ctPOS : gv ? (int64_t)N1 : (int64_t)N1 + 19 + (int64_t)tr->msToProcessCT_10ms))
         return fail(ctx, GNSS_EARG, "max_len too small");
+    const bool odev = (out->flags & GNSS_OUT_DEVICE) != 0;  // rec / taps in device memory
+    if (odev && gv) return fail(ctx, GNSS_EARG, "GNSS_OUT_DEVICE: not for trackingCT_multiCorr (host codedelay pass)");
     // trackingCT_POS_updated.m: per channel, steps 1..n1 at 1 ms (msIndex <= 1000 +
     // countinx(svIndex), :183), then 10 ms up to ctPOS steps (:294)
     auto pos_n1 = [&](int c) -> int64_t {
@@ -1219,12 +1221,14 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
     HIP_TRY(hipMemcpyAsync(chh.data(), d_chan.p, sizeof(TrkChan) * nch, hipMemcpyDeviceToHost, ctx->stream));
     const size_t nrec = (size_t)nch * P.rec_cap * GNSS_NFIELDS;
     const size_t ntp = out->taps ? (size_t)nch * P.rec_cap * 2 * ntaps : 0;
-    double* rec = pinned_buffer<double>(ctx, "trk.h_rec", nrec);
-    double* tp = ntp ? pinned_buffer<double>(ctx, "trk.h_taps", ntp) : nullptr;
-    if (!rec || (ntp && !tp)) return fail(ctx, GNSS_EDEVICE, "hipHostMalloc of the record staging failed");
+    double* rec = odev ? nullptr : pinned_buffer<double>(ctx, "trk.h_rec", nrec);
+    double* tp = ntp && !odev ? pinned_buffer<double>(ctx, "trk.h_taps", ntp) : nullptr;
+    if (!odev && (!rec || (ntp && !tp))) return fail(ctx, GNSS_EDEVICE, "hipHostMalloc of the record staging failed");
     std::vector<double> cn1((size_t)nch * P.cn0_cap), cn10((size_t)nch * P.cn0_cap);
-    HIP_TRY(hipMemcpyAsync(rec, d_rec.p, nrec * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
-    if (out->taps) HIP_TRY(hipMemcpyAsync(tp, d_taps.p, ntp * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    if (!odev) {
+        HIP_TRY(hipMemcpyAsync(rec, d_rec.p, nrec * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+        if (out->taps) HIP_TRY(hipMemcpyAsync(tp, d_taps.p, ntp * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    }
     HIP_TRY(hipMemcpyAsync(cn1.data(), d_cn1.p, cn1.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipMemcpyAsync(cn10.data(), d_cn10.p, cn10.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
@@ -1254,7 +1258,23 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
     }
     // the MATLAB layout: one row per millisecond, each 10-ms step's value on its ten rows
     const int nrf = out->rec ? GNSS_NFIELDS : 0, ntf = out->taps ? 2 * ntaps : 0;
-    parallel_for(nch * (nrf + ntf), [&](int task) {
+    if (odev) {  // expanded on the GPU straight into the caller's device arrays
+        std::vector<int64_t> job(2 * (size_t)nch);
+        for (int i = 0; i < nch; i++) {
+            job[2 * i] = n1_of(i);
+            job[2 * i + 1] = chans[i];
+        }
+        DevBuf d_job;
+        HIP_TRY(d_job.alloc(ctx, "trk.d_job", sizeof(int64_t) * job.size()));
+        HIP_TRY(hipMemcpyAsync(d_job.p, job.data(), sizeof(int64_t) * job.size(), hipMemcpyHostToDevice, ctx->stream));
+        if (nrf)
+            HIP_TRY(launch_track_expand(d_rec.as<double>(), P.rec_cap, GNSS_NFIELDS, GNSS_NFIELDS, nch,
+                                        d_job.as<int64_t>(), out->rec, ML, n10, 0, ctx->stream));
+        if (ntf)
+            HIP_TRY(launch_track_expand(d_taps.as<double>(), P.rec_cap, 2 * ntaps, 2 * ntaps, nch,
+                                        d_job.as<int64_t>(), out->taps, ML, n10, ntaps, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+    } else parallel_for(nch * (nrf + ntf), [&](int task) {
         const int i = task / (nrf + ntf), f = task % (nrf + ntf);
         const int c = chans[i];
         const int64_t n1 = n1_of(i);

@@ -231,6 +231,12 @@ hipError_t launch_track_snapshot(const TrkParams& p, const TrkBuffers& b, const 
 hipError_t launch_track_bitedge(const TrkParams& p, const TrkBuffers& b, const TrkDev& d, hipStream_t s);
 hipError_t launch_track_phase_c_init(const TrkParams& p, const TrkBuffers& b, const TrkDev& d,
                                      int64_t skip, hipStream_t s);
+// GNSS_OUT_DEVICE: expand the compact records [i][rec_cap][stride] (field f of nf) into the
+// caller's device array [chan][nf][ML]; job[2i] = rows before the 10-ms values, job[2i+1] =
+// output channel index (device array).
+hipError_t launch_track_expand(const double* src, int64_t rec_cap, int stride, int nf, int nch,
+                               const int64_t* job, double* dst, int64_t ML, int64_t n10, int ntaps,
+                               hipStream_t s);
 
 constexpr int kTrkThreads = 256;
 constexpr int kArriveStride = 64;   // words: one 256-B line per counter

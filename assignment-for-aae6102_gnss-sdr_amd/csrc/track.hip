@@ -1659,6 +1659,39 @@ int track_run_blocks_per_cu(const TrkParams& p, int sub)
     return 0;
 }
 
+// Device-resident outputs (gnss_track_out.flags & GNSS_OUT_DEVICE): the MATLAB layout of
+// the compact per-step records, expanded on the GPU — one row per millisecond with each
+// 10-ms step's value on its ten rows (trackingCT.m:507-524), a zeroed tail. Channel i's
+// field f: src[(slot * stride) + f] -> dst[(chan * nf + f) * ML + k]. grid: (x: row chunks,
+// y: nch * nf).
+// ntaps > 0: the taps array, compact field f = 2 * tap + (I 0 / Q 1) -> [chan][I/Q][tap].
+__global__ void track_expand_kernel(const double* __restrict__ src, int64_t rec_cap, int stride, int nf,
+                                    const int64_t* __restrict__ job, double* __restrict__ dst, int64_t ML,
+                                    int64_t n10, int ntaps)
+{
+    const int i = blockIdx.y / nf, f = blockIdx.y - i * nf;
+    const int64_t n1 = job[2 * i], c = job[2 * i + 1];
+    const double* s = src + (int64_t)i * rec_cap * stride + f;
+    const int fo = ntaps ? (f & 1) * ntaps + (f >> 1) : f;
+    double* o = dst + (c * nf + fo) * ML;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < ML; k += (int64_t)gridDim.x * blockDim.x) {
+        double v = 0.0;
+        if (k < n1) v = s[k * stride];
+        else if (k < n1 + 10 * n10) v = s[(n1 + (k - n1) / 10) * stride];
+        o[k] = v;
+    }
+}
+
+hipError_t launch_track_expand(const double* src, int64_t rec_cap, int stride, int nf, int nch,
+                               const int64_t* job, double* dst, int64_t ML, int64_t n10, int ntaps,
+                               hipStream_t s)
+{
+    const int64_t chunks = (ML + 255) / 256;
+    hipLaunchKernelGGL(track_expand_kernel, dim3((unsigned)(chunks < 64 ? chunks : 64), (unsigned)(nch * nf)),
+                       dim3(256), 0, s, src, rec_cap, stride, nf, job, dst, ML, n10, ntaps);
+    return hipGetLastError();
+}
+
 hipError_t launch_track_prepare(const TrkParams& p, const TrkBuffers& b, const TrkDev& d, int pdi,
                                 int phaseC, hipStream_t s)
 {

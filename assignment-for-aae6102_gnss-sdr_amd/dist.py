@@ -87,7 +87,72 @@ def gather_tracking_rows(buf, shards, group=None, device=None):
         buf.len[ch] = pm[: len(ch), 0]
         buf.countinx[ch] = pm[: len(ch), 1]
         buf.CN0[:, ch] = pc[:, : len(ch)]
+    if buf.taps is not None:  # the ACF taps (config 5): the largest per-channel payload
+        taps = np.zeros((width,) + buf.taps.shape[1:], dtype=buf.taps.dtype)
+        taps[: len(mine)] = buf.taps[mine]
+        for r, pt in enumerate(_all_gather_array(taps, group, device)):
+            if r != me:
+                buf.taps[list(shards[r])] = pt[: len(shards[r])]
     buf.c.cn0_rows = int(max(_all_gather_array(rows, group, device))[0])
+    return buf
+
+
+def _gather_into(out, t, group):
+    """all_gather_into_tensor; gloo with device tensors (the one-GPU rehearsal) takes the
+    list form."""
+    import torch.distributed as dist
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        dist.all_gather(list(out.chunk(dist.get_world_size(group))), t, group=group)
+    else:
+        dist.all_gather_into_tensor(out, t, group=group)
+
+
+def gather_tracking_rows_device(buf, shards, group=None):
+    """gather_tracking_rows for DeviceTrackOutBuffers: the TckResultCT series (rec, and
+    taps when present) never leave HBM -- each rank packs its own channels' rows on the GPU
+    and one all_gather_into_tensor (RCCL over xGMI on MI355X) delivers every rank's rows,
+    scattered back in place. The small host arrays (len, countinx, CN0 columns, cn0_rows)
+    travel in one packed device tensor of their own."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    me = dist.get_rank(group)
+    width = max(len(s) for s in shards)
+    dev = buf.rec.device
+    mine = torch.tensor(list(shards[me]), dtype=torch.long, device=dev)
+
+    def rows(t):
+        own = torch.zeros((width,) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+        own[: len(shards[me])] = t.index_select(0, mine)
+        allr = torch.empty((world * width,) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+        _gather_into(allr, own, group)
+        for r in range(world):
+            if r != me and len(shards[r]):
+                idx = torch.tensor(list(shards[r]), dtype=torch.long, device=dev)
+                t.index_copy_(0, idx, allr[r * width: r * width + len(shards[r])])
+
+    rows(buf.rec)
+    if buf.taps is not None:
+        rows(buf.taps)
+    # small per-channel metadata: [len, countinx, CN0 column ...] per owned channel
+    nc = buf.CN0.shape[0]
+    meta = np.zeros((width, 3 + nc))
+    for j, c in enumerate(shards[me]):
+        meta[j, 0], meta[j, 1], meta[j, 2] = buf.len[c], buf.countinx[c], buf.c.cn0_rows
+        meta[j, 3:] = buf.CN0[:, c]
+    mt = torch.from_numpy(meta).to(dev)
+    allm = torch.empty((world * width, 3 + nc), dtype=mt.dtype, device=dev)
+    _gather_into(allm, mt, group)
+    allm = allm.cpu().numpy()
+    crows = buf.c.cn0_rows
+    for r in range(world):
+        for j, c in enumerate(shards[r]):
+            m = allm[r * width + j]
+            crows = max(crows, int(m[2]))
+            if r != me:
+                buf.len[c], buf.countinx[c] = int(m[0]), int(m[1])
+                buf.CN0[:, c] = m[3:]
+    buf.c.cn0_rows = crows
     return buf
 
 

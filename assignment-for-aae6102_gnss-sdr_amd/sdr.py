@@ -258,6 +258,39 @@ class TrackOutBuffers:
         return self.shape == (nsv, max_len, ntaps, cn0_cap)
 
 
+class DeviceTrackOutBuffers(TrackOutBuffers):
+    """TrackOutBuffers whose rec / taps live in HBM (gnss_track_out.flags = GNSS_OUT_DEVICE):
+    torch float64 tensors on `device`, filled by the library's expansion kernel; len,
+    countinx and CN0 stay host arrays. The multi-GPU path all-gathers these rows over
+    RCCL without a host round trip (dist.gather_tracking_rows_device)."""
+
+    def __init__(self, nsv: int, track, ntaps: int = 0, device="cuda:0", ctPOS: int | None = None):
+        import torch
+        super().__init__(nsv, track, 0, ctPOS)
+        self.device = torch.device(device)
+        self.rec = torch.zeros((nsv, abi.NFIELDS, self.max_len), dtype=torch.float64, device=self.device)
+        self.taps = (torch.zeros((nsv, 2, ntaps, self.max_len), dtype=torch.float64, device=self.device)
+                     if ntaps else None)
+        self.c.rec = C.cast(C.c_void_p(self.rec.data_ptr()), C.POINTER(C.c_double))
+        self.c.taps = C.cast(C.c_void_p(self.taps.data_ptr()), C.POINTER(C.c_double)) if ntaps else None
+        self.c.flags = abi.OUT_DEVICE
+        self.shape = (nsv, self.max_len, ntaps, self.cn0_cap)
+
+    def sync_producer(self):
+        """The library writes on its own stream: torch's pending work on these tensors
+        (allocation fill, an all-gather) must be done first."""
+        import torch
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def host(self) -> TrackOutBuffers:
+        """A host copy (TrackOutBuffers) of the same result."""
+        h = TrackOutBuffers.__new__(TrackOutBuffers)
+        h.__dict__.update({k: v for k, v in self.__dict__.items() if k not in ("device",)})
+        h.rec = self.rec.cpu().numpy()
+        h.taps = self.taps.cpu().numpy() if self.taps is not None else None
+        return h
+
+
 class StructArray:
     """MATLAB struct array indexed by PRN: TckResultCT(prn).P_i (trackingCT.m:153)."""
 
@@ -351,6 +384,8 @@ def trackingCT(file, signal, track, Acquired, *, ctx: Context | None = None, tap
         buf.countinx[:] = 0
     else:
         buf = TrackOutBuffers(nsv, track, ntaps)
+    if isinstance(buf, DeviceTrackOutBuffers):
+        buf.sync_producer()
     st = ctx.lib.gnss_tracking_ct(ctx.h, C.byref(f), C.byref(s), C.byref(t), C.byref(a),
                                   C.byref(buf.c))
     if st == abi.ENODATA:
@@ -364,7 +399,8 @@ def trackingCT(file, signal, track, Acquired, *, ctx: Context | None = None, tap
         import scipy.io as sio
         sio.savemat(save_countinx, {"countinx": countinx.reshape(1, -1)})
     cn0 = buf.CN0[: buf.c.cn0_rows].copy()
-    return build_tck_result(Acquired, buf, channels), cn0, countinx
+    hb = buf.host() if isinstance(buf, DeviceTrackOutBuffers) else buf
+    return build_tck_result(Acquired, hb, channels), cn0, countinx
 
 
 def trackingCT_POS(file, signal, track, Acquired, countinx, *, ctx: Context | None = None,

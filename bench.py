@@ -9,9 +9,12 @@ record resident in HBM, exactly as SDR_main.m:17-45 runs it:
 Units: acquisition hypothesis-samples (PRN x bin x ms x Sample) + tracking
 channel-samples (one IF sample correlated by one channel, all taps).
 
-Multi-GPU (torchrun, one process per GPU): every rank owns an independent
-record (seed 6102 + rank) — weak scaling, no data-path collective; timing is
-bracketed by barriers and the max over ranks is reported.
+Multi-GPU (torchrun, one process per GPU): strong scaling of ONE job -- every rank
+holds the same record in its HBM, the 32 PRNs of the acquisition and then the
+acquired channels are sharded round-robin over the ranks, and every step ends with
+the result gathers (RCCL over xGMI; the TckResultCT rows never leave HBM), so every
+rank holds the full outputs. Timing is bracketed by barriers, the max over ranks
+is reported, `value` = all ranks' units / that time.
 """
 from __future__ import annotations
 
@@ -31,6 +34,7 @@ pkg = importlib.import_module("assignment-for-aae6102_gnss-sdr_amd")
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SAMPLES_PER_MS = 58000  # Opensky Fs 58 MHz
+TRAFFIC_FILE = "traffic_r01.json"  # PMC bytes per launch of the dominant kernel (this round's pass)
 
 
 def parse():
@@ -240,6 +244,8 @@ def main():
         return run_cfg5(args, rank, world, local, dist, ctx)
     if args.workload == "cfg4":
         return run_cfg4(args, rank, world, local, dist, ctx)
+    import importlib as _il
+    D = _il.import_module("assignment-for-aae6102_gnss-sdr_amd.dist")
     file, signal, acq, track, _, _ = pkg.initParameters()
     S = signal.Sample
     file.skip = args.skip
@@ -247,22 +253,36 @@ def main():
     acq.freqNum = int(2 * abs(acq.freqMin) / acq.freqStep + 1)
     track.msToProcessCT_1ms, track.msToProcessCT_10ms = 1000, args.n10
 
-    # IF record in HBM: byte 0 .. skip + 1000 + 19 + n10 (+ margin) ms
+    # ONE record (the same bytes on every rank: each rank's HBM holds its own copy, made by
+    # the HIP generator outside the timed region): byte 0 .. skip + 1000 + 19 + n10 (+ margin) ms
     rec_ms = args.skip + 1000 + 19 + args.n10 + 3
-    cfg = pkg.synth.opensky(skip_ms=args.skip, seed=6102 + rank)
+    cfg = pkg.synth.opensky(skip_ms=args.skip, seed=6102)
     dev = pkg.DeviceRecord(ctx, rec_ms * S * 2)
     pkg.synth.generate_device(ctx, cfg, dev)
     file.dev = dev
 
-    outs = [None]  # the trackingCT output buffers, reused from step to step
+    # strong scaling of one job: acquisition PRNs 1..32 and then the acquired
+    # channels round-robin over the ranks; every step ends with the result gathers (RCCL
+    # over xGMI on the node, device-resident TckResultCT rows), so every rank holds the
+    # full Acquired and TckResultCT. N = 1: the same step without the gathers.
+    prns = list(range(1, 33))
+    my_prns = [prns[i] for i in D.shard(len(prns), world, rank)]
+    outs = [None]  # the trackingCT output buffers (HBM), reused from step to step
 
     def one_step():
-        A = pkg.acquisition(file, signal, acq, ctx=ctx)
+        A = pkg.acquisition(file, signal, acq, ctx=ctx, prn_list=my_prns)
         ta = ctx.timing()
-        buf = pkg.trackingCT(file, signal, track, A, ctx=ctx, raw=True, out=outs[0])
-        outs[0] = buf
+        if dist is not None:
+            A = D.gather_acquired(A, my_prns, prns, device=f"cuda:{local}")
+        nsv = len(A.sv)
+        shards = [D.shard(nsv, world, r) for r in range(world)]
+        if outs[0] is None or not outs[0].fits(nsv, track, 0):
+            outs[0] = pkg.DeviceTrackOutBuffers(nsv, track, 0, device=f"cuda:{local}")
+        buf = pkg.trackingCT(file, signal, track, A, ctx=ctx, channels=shards[rank], raw=True, out=outs[0])
         tt = ctx.timing()
-        return A, ta, tt, buf
+        if dist is not None:
+            D.gather_tracking_rows_device(buf, shards)
+        return A, ta, tt, buf, shards
 
     for _ in range(args.warmup):
         one_step()
@@ -271,7 +291,7 @@ def main():
     acq_units = trk_units = 0
     acq_ms = trk_ms = acq_corr_ms = acq_fine_ms = 0.0
     for _ in range(args.steps):
-        A, ta, tt, buf = one_step()
+        A, ta, tt, buf, shards = one_step()
         acq_units += ta["acq_hypothesis_samples"]
         trk_units += tt["track_channel_samples"]
         acq_ms += ta["acq_ms"]
@@ -283,16 +303,24 @@ def main():
     elapsed = max_over_ranks(dist, local, elapsed)
     units = sum_over_ranks(dist, local, float(acq_units + trk_units))
     nch = len(A.sv)
+    mine = shards[rank]
+    # the step's outputs, checked (not timed): the scenario's 8 SVs acquired, every channel
+    # tracked to full length, the gathered TckResultCT complete on this rank
+    full_len = [1000 + int(c) + args.n10 for c in buf.countinx]
+    outputs_ok = (sorted(int(x) for x in A.sv) == sorted(pkg.synth.OPENSKY_SV)
+                  and [int(x) for x in buf.len] == full_len
+                  and bool((buf.rec[:, abi_f("numSample"), 0] > 0).all().item()))
 
     # roofline of the dominant kernel: the tracking correlator of the 10-ms phase (most
     # of the time): the persistent track_run_kernel<3, 3, false> (one launch runs the
     # whole phase; 24-sample lanes) or, where its grid cannot be resident,
-    # track_step_kernel<3, 3, false> (one launch per step). A profiling pass brackets every launch with hipEvents on the
-    # ctx stream; algorithmic bytes = 2 B (int8 I + Q) per channel-sample of the launch.
+    # track_step_kernel<3, 3, false> (one launch per step). A profiling pass brackets every
+    # launch with hipEvents on the ctx stream; algorithmic bytes = 2 B (int8 I + Q) per
+    # channel-sample of the launch.
     roof = None
     if not args.no_profile_pass:
         ctx.set_profiling(True)
-        pkg.trackingCT(file, signal, track, A, ctx=ctx, raw=True)
+        pkg.trackingCT(file, signal, track, A, ctx=ctx, channels=mine, raw=True, out=outs[0])
         tp = ctx.timing()
         ctx.set_profiling(False)
         launches = tp["track10_launches"]
@@ -302,23 +330,24 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
                 "kernel": ("track_run_kernel<3, 3, false> (persistent: every step of the 10-ms phase, "
-                           "all channels)" if launches <= 2 else
+                           "all channels of the rank)" if launches <= 2 else
                            "track_step_kernel<3, 3, false> (10-ms phase step, all channels)"),
                 "steps_per_launch": round(tp["track10_channel_samples"] / max(1, launches) /
-                                          (nch * 10 * SAMPLES_PER_MS), 1),
+                                          (len(mine) * 10 * SAMPLES_PER_MS), 1),
                 "launches": int(launches), "avg_launch_us": round(avg_ms * 1e3, 3),
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "all_steps_avg_launch_us": round(tp["track_kernel_ms"] * 1e3 / max(1, tp["track_launches"]), 3),
                 "track_wall_ms_profiling": round(tp["track_ms"], 3)}
-        tf = os.path.join(ROOT, "profiles", "traffic_r01.json")
-        if os.path.exists(tf):
+        tf = os.path.join(ROOT, "profiles", TRAFFIC_FILE)
+        if world == 1 and os.path.exists(tf):
             try:
                 with open(tf) as fh:
                     tj = json.load(fh)
-                # PMC HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE) and the same kernel's
-                # rocprofv3 kernel-trace average (kernel only; the events above also hold
-                # each launch's dispatch latency)
+                # PMC HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE) of the same kernel and its
+                # rocprofv3 kernel-trace average, from the separate rocprofv3 passes of this
+                # round (tools/gpu_round.sh; a PMC pass cannot run inside this process)
                 roof["traffic"] = tj.get("bytes_per_launch")
+                roof["traffic_source"] = f"profiles/{TRAFFIC_FILE} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)"
                 roof["rocprof_avg_launch_us"] = tj.get("rocprof_avg_launch_us")
             except Exception:
                 pass
@@ -328,6 +357,7 @@ def main():
         cpu = cpu_baseline(file, signal, acq, track, A, dev, args, ta, tt)
 
     value = units / elapsed / 1e6
+    step_ms = elapsed / args.steps * 1e3
     line = {
         "metric": "correlator Msamples/s (acq+track), whole job",
         "value": round(value, 2),
@@ -335,20 +365,28 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "ms_per_step": round(step_ms, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "int8 in, f64 compute",
+        "dtype": "int8 in; acquisition: f32 correlation + f64 fine search; tracking: f64",
+        "dtype_per_leg": {"acquisition_correlation": "f32", "acquisition_fine_frequency": "f64",
+                          "tracking": "f64"},
         "data": "synthetic Opensky-shape IF (int8 I/Q, Fs 58 MHz, IF 4.58 MHz), resident in HBM",
         "config": {"workload": "acquisition cfg2 (32 PRN, +-7kHz/500Hz, 20 ms) + trackingCT cfg3 "
                                f"({nch} ch, 1000 ms @1ms + {args.n10} ms @10ms, E/P/L)",
-                   "per_rank": "independent record", "parallelism": f"records x{world}"},
+                   "parallelism": f"PRNs and channels x{world} (one record, strong scaling)",
+                   "prns_per_rank": len(my_prns), "channels_per_rank": len(mine)},
+        "outputs_ok": outputs_ok,
+        "acquired": [int(x) for x in A.sv],
         "per_gpu_Msamples_s": round(value / world, 2),
         "acq_Msamples_s": round(acq_units / (acq_ms * 1e-3) / 1e6, 2) if acq_ms else None,
         "track_Msamples_s": round(trk_units / (trk_ms * 1e-3) / 1e6, 2) if trk_ms else None,
         "acq_ms": round(acq_ms / args.steps, 3),
         "track_ms": round(trk_ms / args.steps, 3),
+        # device-busy evidence of the timed steps: the ctx stream's event-timed acquisition +
+        # tracking spans over the step's wall time (rank 0)
+        "device_busy_frac": round((acq_ms + trk_ms) / args.steps / step_ms, 4),
         "roofline": roof,
         # the acquisition's own line (16 B per hypothesis-sample over the
         # correlation time, the fine-frequency FFTs timed separately)
@@ -366,47 +404,98 @@ def main():
         dist.destroy_process_group()
 
 
+def abi_f(name):
+    return pkg.abi.FIELDS.index(name)
+
+
+def host_cpu():
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for ln in fh:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model, os.cpu_count()
+
+
 def cpu_baseline(file, signal, acq, track, A, dev, args, ta, tt):
-    """The CPU fp64 restatement (oracle/) timed on a bounded sample of the same
-    workload, extrapolated per unit and combined with the GPU step's unit mix."""
+    """The CPU fp64 restatement (oracle/, C, -O2) timed on a bounded sample of the same
+    workload (SURVEY 8d / BASELINE.md 2): one thread and all usable cores (OpenMP across
+    PRNs / channels), median of 5 runs each, plus the numpy restatement (the "MATLAB-like
+    vectorised" proxy, tests/numpy_twin.py) on one tracking step set. Per-unit rates are
+    extrapolated to the GPU step's unit mix. Labelled "restatement", never "MATLAB"."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
     import pyoracle as po
     from types import SimpleNamespace
     S = signal.Sample
-    nt = args.cpu_threads
+    allc = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     # bounded sample: IF window [skip, skip + 1000 + 19 + n10s + 2] ms
-    n10s = 1000
+    n10s = 200
     lo = file.skip * S * 2
     nbytes = (1000 + 19 + n10s + 4) * S * 2
     win = dev.download(lo, nbytes)
     f2 = SimpleNamespace(skip=0, dataType=2, dataPrecision=1, data=win, fileRoute=None, dev=None)
-    # acquisition sample: one PRN over the full grid (units = 1 x bins x ms x S)
     a1 = SimpleNamespace(**vars(acq))
-    t = time.perf_counter()
-    po.acquisition(f2, signal, a1, prn_list=[int(A.sv[0])], nthreads=nt)
-    acq_s = time.perf_counter() - t
-    acq_units = a1.freqNum * a1.datalen * S
-    # tracking sample: one channel, 1000 ms @1 ms (+ phase-B re-run) + n10s ms @10 ms
+    a1.datalen = 4  # the same grid (29 bins x S) over 4 non-coherent ms
     tr = SimpleNamespace(**vars(track))
     tr.msToProcessCT_10ms = n10s
-    A1 = SimpleNamespace(sv=A.sv[:1], SNR=A.SNR[:1], Doppler=A.Doppler[:1],
-                         codedelay=A.codedelay[:1], fineFreq=A.fineFreq[:1])
-    t = time.perf_counter()
-    po.trackingCT(f2, signal, tr, A1, nthreads=nt)
-    trk_s = time.perf_counter() - t
-    trk_units = (1000 + n10s) * S  # counted like the GPU (phase A once)
-    r_acq = acq_units / acq_s
-    r_trk = trk_units / trk_s
-    U_acq, U_trk = ta["acq_hypothesis_samples"], tt["track_channel_samples"]
-    step_s = U_acq / r_acq + U_trk / r_trk
-    return {"value": round((U_acq + U_trk) / step_s / 1e6, 4), "unit": "Msamples/s",
-            "cores": nt, "kind": "port",
-            "sample": f"oracle/ C fp64 restatement: acquisition of PRN {int(A.sv[0])} over "
-                      f"{a1.freqNum} bins x {a1.datalen} ms + fine FFT ({acq_s:.1f} s), trackingCT of 1 "
-                      f"channel 1000 ms @1ms (+phase-B rerun) + {n10s} ms @10ms ({trk_s:.1f} s); "
+
+    def leg(nt):
+        np_ = nt  # one PRN / channel per thread
+        prn_list = [int(p) for p in (list(A.sv) + [p for p in range(1, 33) if p not in A.sv])[:np_]]
+        nch = min(nt, len(A.sv))
+        A1 = SimpleNamespace(sv=A.sv[:nch], SNR=A.SNR[:nch], Doppler=A.Doppler[:nch],
+                             codedelay=A.codedelay[:nch], fineFreq=A.fineFreq[:nch])
+        ra, rt = [], []
+        for _ in range(5):
+            t = time.perf_counter()
+            po.acquisition(f2, signal, a1, prn_list=prn_list, nthreads=nt)
+            ra.append(len(prn_list) * a1.freqNum * a1.datalen * S / (time.perf_counter() - t))
+            t = time.perf_counter()
+            po.trackingCT(f2, signal, tr, A1, nthreads=nt)
+            rt.append(nch * (1000 + n10s) * S / (time.perf_counter() - t))
+        r_acq, r_trk = float(np.median(ra)), float(np.median(rt))
+        U_acq, U_trk = ta["acq_hypothesis_samples"], tt["track_channel_samples"]
+        return r_acq, r_trk, (U_acq + U_trk) / (U_acq / r_acq + U_trk / r_trk)
+
+    a_1, t_1, v_1 = leg(1)
+    a_n, t_n, v_n = leg(allc)
+    # numpy restatement (one thread, vectorised like the MATLAB code): 10 correlator steps
+    # of 10 ms (trackingCT.m:96-118) and one PRN's 29-bin x 1 ms acquisition (:40-78)
+    np_trk = np_acq = None
+    try:
+        import numpy_twin as tw
+        ca = tw.ca_code(int(A.sv[0]))
+        t = time.perf_counter()
+        for k in range(10):
+            tw.correlate_step(win[2 * 10 * S * k:], 10 * S, 0.0, 1.023e6, signal.Fs, float(A.fineFreq[0]),
+                              0.0, ca, [-0.5, 0.0, 0.5])
+        np_trk = 10 * 10 * S / (time.perf_counter() - t)
+        t = time.perf_counter()
+        tw.acquisition(win[: 2 * S], S, signal.Fs, signal.IF, signal.codeFreqBasis, acq.freqMin, acq.freqStep,
+                       acq.freqNum, 1, [int(A.sv[0])])
+        np_acq = acq.freqNum * S / (time.perf_counter() - t)
+    except Exception:
+        pass
+    model, ncpu = host_cpu()
+    return {"value": round(v_n / 1e6, 4), "unit": "Msamples/s", "cores": allc, "kind": "port",
+            "sample": f"oracle/ C fp64 restatement (median of 5): acquisition of {allc} PRNs (1 per "
+                      f"thread) over {a1.freqNum} bins x {a1.datalen} ms + fine FFT, trackingCT of "
+                      f"{min(allc, len(A.sv))} channels 1000 ms @1ms (+phase-B rerun) + {n10s} ms @10ms; "
                       "per-unit rates extrapolated to the GPU step's unit mix",
-            "acq_Msamples_s": round(r_acq / 1e6, 4), "track_Msamples_s": round(r_trk / 1e6, 4),
-            "host_cpu": os.uname().machine}
+            "one_thread": {"value": round(v_1 / 1e6, 4), "acq_Msamples_s": round(a_1 / 1e6, 4),
+                           "track_Msamples_s": round(t_1 / 1e6, 4)},
+            "all_cores": {"threads": allc, "value": round(v_n / 1e6, 4), "acq_Msamples_s": round(a_n / 1e6, 4),
+                          "track_Msamples_s": round(t_n / 1e6, 4)},
+            "numpy_restatement": {"track_Msamples_s": round(np_trk / 1e6, 4) if np_trk else None,
+                                  "acq_Msamples_s": round(np_acq / 1e6, 4) if np_acq else None,
+                                  "threads": 1},
+            "host_cpu": model, "nproc": ncpu,
+            "label": "CPU restatement of acquisition.m / trackingCT.m (MATLAB itself is absent)"}
 
 
 if __name__ == "__main__":

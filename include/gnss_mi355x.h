@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define GNSS_ABI_VERSION 6
+#define GNSS_ABI_VERSION 7
 
 /* ---- status codes (SURVEY §8b "Error conventions") --------------------- */
 #define GNSS_OK         0
@@ -159,7 +159,15 @@ enum gnss_track_field {
  *   countinx [nsv]  bit-edge result (trackingCT.m:207)
  *   CN0_Eph  [cn0_cap][nsv] row-major (row = snrIndex-1); rows never written are 0
  *   cn0_rows  out: rows of the MATLAB CN0_Eph matrix
+ *   flags     GNSS_OUT_DEVICE: rec and taps are DEVICE pointers (HIP memory of the
+ *             ctx's device, e.g. gnss_dev_alloc or a framework tensor); the series are
+ *             expanded into them on the GPU and never cross PCIe, so a multi-GPU caller
+ *             can all-gather them over RCCL/xGMI as they lie. The call returns after the
+ *             writes have completed (ctx stream synchronised). len, countinx and CN0_Eph
+ *             stay host arrays. Not for gnss_tracking_ct_multicorr (its codedelay
+ *             post-pass runs on the host): GNSS_EARG there.
  * max_len must be >= msToProcessCT_1ms + 19 + msToProcessCT_10ms.             */
+#define GNSS_OUT_DEVICE 1
 typedef struct gnss_track_out {
     int64_t  max_len;
     double  *rec;
@@ -169,6 +177,8 @@ typedef struct gnss_track_out {
     double  *CN0_Eph;
     int32_t  cn0_cap;
     int32_t  cn0_rows;
+    int32_t  flags;     /* GNSS_OUT_DEVICE or 0 (ABI v7)                           */
+    int32_t  reserved;
 } gnss_track_out;
 
 /* Device-side timing of the last call (hipEvents on the ctx stream). */

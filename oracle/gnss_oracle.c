@@ -546,6 +546,12 @@ static void correlate_cpx(const cpx *x, int64_t n, double remChip, double codeFr
                           double carrierFreq, double remPhase, const int8_t *ca, int pdi, int ntaps,
                           const double *taps, const double *post, int chip_off, double *sums);
 
+/* Carrier evaluation mode (TEST EXPERIMENT ONLY): 0 = the reference's rounded Wave (default);
+ * 1 = the same phase without the per-sample fp64 roundings (long double), to measure how
+ * much the closed loop depends on reproducing them. */
+static int g_carrier_mode = 0;
+void or_set_carrier_mode(int mode) { g_carrier_mode = mode; }
+
 void or_correlate_step(const int8_t *iq, int64_t n, double remChip, double codeFreq, double Fs,
                        double carrierFreq, double remPhase, const int8_t *ca, int pdi, int ntaps,
                        const double *taps, double *sums)
@@ -583,6 +589,13 @@ static void correlate_cpx(const cpx *x, int64_t n, double remChip, double codeFr
         /* CarrTime = (0:numSample)./Fs; Wave = (2*pi*(carrierFreq.*CarrTime)) + remPhase */
         double W = TWO_PI * (carrierFreq * ((double)k / Fs)) + remPhase;
         double cw = cos(W), sw = sin(W);
+        if (g_carrier_mode == 1) {
+            /* experiment only: the carrier phase without MATLAB's per-sample roundings */
+            long double Wl = (long double)TWO_PI * (long double)carrierFreq * (long double)k /
+                             (long double)Fs + (long double)remPhase;
+            cw = (double)cosl(Wl);
+            sw = (double)sinl(Wl);
+        }
         double xr = x[k].re, xi = x[k].im;
         double I = xr * sw + xi * cw; /* imag(raw.*carrsig) */
         double Q = xr * cw - xi * sw; /* real(raw.*carrsig) */

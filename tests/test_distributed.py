@@ -50,11 +50,24 @@ def _worker(rank, world, port, out_dir):
     chans = D.shard(3, world, rank)
     buf = po.trackingCT(file, signal, track, Aq, channels=chans, nthreads=1, raw=True)
     G = D.gather_tracking(buf, 3)
-    B = D.gather_tracking_rows(buf, [D.shard(3, world, r) for r in range(world)])  # (in place)
+    shards = [D.shard(3, world, r) for r in range(world)]
+    B = D.gather_tracking_rows(buf, shards)  # (in place)
+    # ACF taps (config 5 shape, 11 taps) through the row-packed gathers: host arrays, and the
+    # tensor form the GPU path uses (rec / taps as torch tensors, all_gather_into_tensor)
+    import torch
+    taps = pkg.colon(-0.5, 0.1, 0.5)
+    bt = po.trackingCT(file, signal, track, Aq, taps=taps, channels=chans, nthreads=1, raw=True)
+    tv = SimpleNamespace(rec=torch.from_numpy(bt.rec.copy()), taps=torch.from_numpy(bt.taps.copy()),
+                         len=bt.len.copy(), countinx=bt.countinx.copy(), CN0=bt.CN0.copy(),
+                         c=SimpleNamespace(cn0_rows=bt.c.cn0_rows))
+    D.gather_tracking_rows(bt, shards)
+    D.gather_tracking_rows_device(tv, shards)
     if rank == 0:
         np.savez(os.path.join(out_dir, "dist.npz"), sv=A.sv, codedelay=A.codedelay,
                  fineFreq=A.fineFreq, SNR=A.SNR, rec=G.rec, len=G.len, countinx=G.countinx, CN0=G.CN0,
-                 rec_rows=B.rec, len_rows=B.len, cx_rows=B.countinx, CN0_rows=B.CN0[: B.c.cn0_rows])
+                 rec_rows=B.rec, len_rows=B.len, cx_rows=B.countinx, CN0_rows=B.CN0[: B.c.cn0_rows],
+                 taps_rows=bt.taps, trec_rows=bt.rec, tv_rec=tv.rec.numpy(), tv_taps=tv.taps.numpy(),
+                 tv_len=tv.len, tv_cx=tv.countinx, tv_CN0=tv.CN0[: tv.c.cn0_rows])
     dist.barrier()
     dist.destroy_process_group()
 
@@ -84,3 +97,9 @@ def test_sharded_equals_single_process(tmp_path, pkg, po):
     assert np.array_equal(z["rec_rows"], buf.rec) and np.array_equal(z["len_rows"], buf.len)
     assert np.array_equal(z["cx_rows"], buf.countinx)
     assert np.array_equal(z["CN0_rows"], buf.CN0[: buf.c.cn0_rows])
+    # 11 taps: host row gather (taps included) and the tensor gather equal the full run
+    full = po.trackingCT(file, signal, track, Aq, taps=pkg.colon(-0.5, 0.1, 0.5), raw=True)
+    assert np.array_equal(z["taps_rows"], full.taps) and np.array_equal(z["trec_rows"], full.rec)
+    assert np.array_equal(z["tv_taps"], full.taps) and np.array_equal(z["tv_rec"], full.rec)
+    assert np.array_equal(z["tv_len"], full.len) and np.array_equal(z["tv_cx"], full.countinx)
+    assert np.array_equal(z["tv_CN0"], full.CN0[: full.c.cn0_rows])

@@ -105,3 +105,28 @@ def test_config4_bench_record_parity(pkg, po, ctx):
     g, gd = pkg.acquisition(file, signal, acq, ctx=ctx, prn_list=prns, diag=True)
     r, rd = po.acquisition(file, signal, acq, prn_list=prns, diag=True)
     compare(g, gd, r, rd)
+
+
+def test_config2_datalen20_against_oracle(pkg, po, ctx):
+    """BASELINE config 2 at its own length (datalen 20, +-7 kHz / 500 Hz, L = 10) against
+    the oracle: the 8 present SVs and 4 absent PRNs. Decisions bit-exact, SNR within
+    1e-3 dB, and the fp32 decision margins reported and asserted: every acquired PRN's
+    peak clears the largest off-window value by > 1e-4 relative (the fp32 surface's error
+    is ~1e-6) and every PRN's SNR is > 0.01 dB from the 12 dB gate."""
+    skip = 2
+    cfg = pkg.synth.opensky(skip_ms=skip)
+    data = po.synth_if(cfg, 0, (skip + 20 + 12) * 58000)
+    file, signal, acq, track = params(pkg, skip, data)
+    acq.freqMin, acq.freqNum, acq.freqStep, acq.datalen, acq.L = -7000, 29, 500, 20, 10
+    prns = sorted(pkg.synth.OPENSKY_SV + [1, 2, 5, 6])
+    g, gd = pkg.acquisition(file, signal, acq, ctx=ctx, prn_list=prns, diag=True)
+    r, rd = po.acquisition(file, signal, acq, prn_list=prns, diag=True, nthreads=16)
+    compare(g, gd, r, rd)
+    assert list(g.sv) == sorted(pkg.synth.OPENSKY_SV)
+    acq_mask = np.isin(gd.prn, g.sv)
+    margin = (gd.peak - gd.peak2) / gd.peak
+    gate = np.abs(gd.SNR - 12.0)
+    print("peak margins", dict(zip(gd.prn[acq_mask].tolist(), np.round(margin[acq_mask], 4).tolist())),
+          "min |SNR-12|", float(gate.min()))
+    assert margin[acq_mask].min() > 1e-4
+    assert gate.min() > 0.01

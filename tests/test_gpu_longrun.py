@@ -1,0 +1,65 @@
+"""Long-run parity at the benchmarked length: the bench's own step --
+its record (HIP generator, skip 5000 ms), the config-2 acquisition of it and the config-3
+trackingCT of all 8 acquired channels (1000 ms @1 ms + countinx + 40 000 ms @10 ms: the
+persistent 10-ms loop's 4 000 closed-loop steps) -- against the oracle's run of the same
+record for two channels (tests/golden/golden_track_long.npz, made on the GPU box by
+tests/golden/make_golden_long.py; the record's xxh64 digest proves the bytes are the same).
+Integer fields bit-exact over all ~5 000 distinct steps, P/E/L within 1e-8 of the series
+RMS (north-star 1e-5), NCO state 1e-7 relative, C/N0 1e-6 dB."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+PATH = os.path.join(GOLDEN, "golden_track_long.npz")
+
+
+@pytest.mark.skipif(not os.path.exists(PATH), reason="golden_track_long.npz not generated yet")
+def test_bench_shape_full_length_against_oracle(pkg, ctx):
+    import sys
+    sys.path.insert(0, GOLDEN)
+    import make_golden_long as mg
+    from test_gpu_tracking import INT_FIELDS, NCO_FIELDS
+    z = np.load(PATH)
+    file, signal, acq, track, _, _ = pkg.initParameters()
+    S = signal.Sample
+    skip, N1, N10 = int(z["skip"]), int(z["N1"]), int(z["N10"])
+    cfg = pkg.synth.opensky(skip_ms=skip, seed=int(z["seed"]))
+    dev = pkg.DeviceRecord(ctx, mg.record_bytes(S))
+    pkg.synth.generate_device(ctx, cfg, dev)
+    assert mg.digest(dev.download()) == str(z["digest"])
+    file.skip, file.dev = skip, dev
+    acq.freqMin, acq.freqStep, acq.datalen, acq.L = -7000, 500, 20, 10
+    acq.freqNum = 29
+    A = pkg.acquisition(file, signal, acq, ctx=ctx)
+    for f in ("sv", "codedelay", "Doppler", "fineFreq"):
+        assert np.array_equal(getattr(A, f), z[f]), f
+    assert np.max(np.abs(A.SNR - z["SNR"])) < 1e-3
+    track.msToProcessCT_1ms, track.msToProcessCT_10ms = N1, N10
+    b = pkg.trackingCT(file, signal, track, A, ctx=ctx, raw=True)
+    assert ctx.timing()["track_launches"] <= 4  # the persistent loop ran
+    F = pkg.abi.FIELDS
+    for j, c in enumerate(z["channels"]):
+        n1 = N1 + int(z["countinx"][j])
+        assert int(b.countinx[c]) == int(z["countinx"][j])
+        assert int(b.len[c]) == n1 + N10
+        rec = b.rec[c, :, : n1 + N10]
+        got = np.concatenate([rec[:, :n1], rec[:, n1::10]], axis=1)
+        ref = z[f"rec_{j}"]
+        for k, f in enumerate(F):
+            if f in INT_FIELDS:
+                bad = np.nonzero(got[k] != ref[k])[0]
+                assert len(bad) == 0, (int(c), f, bad[:5])
+        scale = np.sqrt(np.mean(ref[0] ** 2 + ref[1] ** 2))
+        for k in range(6):
+            err = np.max(np.abs(got[k] - ref[k])) / scale
+            print(f"channel {int(c)} {F[k]}: max err / rms {err:.3e}")
+            assert err < 1e-8, (int(c), F[k], err)
+        for f in NCO_FIELDS:
+            k = F.index(f)
+            assert np.allclose(got[k], ref[k], rtol=1e-7, atol=1e-9), (int(c), f)
+        ref_cn0 = z[f"CN0_{j}"]
+        assert np.allclose(b.CN0[: len(ref_cn0), c], ref_cn0, rtol=0, atol=1e-6)
