@@ -64,6 +64,21 @@ GNSS_HD Colon colon_make_hint(double a, double d, double b, int64_t hint)
     return o;
 }
 
+// colon_make_hint with the hint also as an exact double hd (== hint): no integer
+// conversion on the tracking tail's critical path, the interval count by a select.
+GNSS_HD Colon colon_make_hint2(double a, double d, double b, int64_t hint, double hd)
+{
+    const double X = b - a;
+    const double r = fma(-hd, d, X);
+    if (!(d > 0) || !(fabs(r) < 0.4 * d) || a == floor(a)) return colon_make(a, d, b);
+    const double tol = 2.0 * 2.220446049250313e-16 * fmax(fabs(a), fabs(b));
+    const bool dec = a + hd * d - b > tol;
+    const double nd = dec ? hd - 1 : hd;
+    double c = a + nd * d;
+    if (c - b > -tol) c = b;
+    return Colon{a, d, c, dec ? hint - 1 : hint};
+}
+
 GNSS_HD double colon_elem(const Colon& r, int64_t k)
 {
     if (2 * k == r.n) return (r.a + r.c) / 2;
@@ -99,6 +114,19 @@ GNSS_HD double fmod_pos(double x, double y)
 
 constexpr double kTwoPi = 2.0 * 3.14159265358979323846;  // MATLAB 2*pi
 constexpr double kTwoPiLo = 2.4492935982947064e-16;      // 2*pi - kTwoPi
+constexpr double kInvTwoPi = 1.0 / kTwoPi;               // RN(1/kTwoPi)
+
+// x / b for a divisor known ahead (Fs, 2*pi) with rb = RN(1/b): Markstein's correction
+// q' = RN(q + r*rb), q = RN(x*rb), r = x - q*b (exact by FMA), is the IEEE quotient (rb
+// within half an ulp of 1/b, q within an ulp of x/b); three dependent FMA-class ops
+// instead of the ~10 of a general division on the tracking loop's critical path.
+// Checked against the IEEE division on 3.5e8 operands (tests/native/markstein.c).
+GNSS_HD double div_const(double x, double b, double rb)
+{
+    const double q = x * rb;
+    const double r = __builtin_fma(-q, b, x);
+    return __builtin_fma(r, rb, q);
+}
 
 // ----------------------------------------------------------------------------
 // Tracking state (one per channel, fp64), lives in HBM across step launches.
@@ -182,7 +210,10 @@ struct StepDesc {
     double phi[kLaneMax];
     double2 rcs[kLaneMax];
     double tap_a[GNSS_MAX_TAPS], tap_c[GNSS_MAX_TAPS];  // colon start / end per tap
-    int32_t pdi, phaseC, bad, pad;
+    double rc0;          // remChip at the step's start (for remSample)
+    int32_t pdi, phaseC;
+    int32_t bad;         // GNSS_* of the step (file / staging / numSample checks)
+    int32_t bad_tap;     // GNSS_EINDEX: a replica index out of range (checked after bad)
 };
 
 struct TrkBuffers {

@@ -144,7 +144,7 @@ __device__ __forceinline__ NcoState nco_of(const TrkChan& c)
 // below 8 in magnitude), so the FMA and the correction are exact.
 __device__ __forceinline__ double rem_2pi(double x)
 {
-    const double q = trunc(x / kTwoPi);
+    const double q = trunc(div_const(x, kTwoPi, kInvTwoPi));
     double r = __builtin_fma(-q, kTwoPi, x);
     if (x >= 0) {
         if (r < 0) r += kTwoPi;
@@ -161,9 +161,16 @@ __device__ __forceinline__ double rem_2pi(double x)
 // round, an integer for ceil), where the IEEE division decides: the same n, without a
 // division on the critical path. remSample (a record field only) is step_rem_sample().
 struct StepSize {
-    double cps, inv_cps;
+    double cps, inv_cps, nd;  // nd = (double)n, exact
     int64_t n, dv;
 };
+
+// codeFreq / Fs and k / Fs: the IEEE quotient by Markstein's correction, or a true division
+// where the host could not verify the correction for this Fs (TrkParams.exact_div)
+__device__ __forceinline__ double over_fs(const TrkParams& p, double x)
+{
+    return p.exact_div ? x / p.Fs : div_const(x, p.Fs, p.inv_Fs);
+}
 
 // 1/x to about 1 ulp: hardware reciprocal and two Newton steps (the lanes' boundary search
 // only needs 1e-9 relative; exactness never depends on it)
@@ -179,18 +186,21 @@ __device__ __forceinline__ double fast_rcp(double x)
 __device__ __forceinline__ StepSize step_size(const TrkParams& p, const NcoState& c, int pdi, int phaseC)
 {
     StepSize z;
-    z.cps = c.codeFreq / p.Fs;
-    z.inv_cps = fast_rcp(z.cps);
+    z.cps = over_fs(p, c.codeFreq);
+    // 1/cps = Fs/codeFreq from the reciprocal of codeFreq (beside the quotient, not after it)
+    z.inv_cps = p.Fs * fast_rcp(c.codeFreq);
     const double num = p.codelength * pdi - c.remChip;
     const double qa = num * z.inv_cps;
     if (p.conv || p.given) {  // ceil
-        z.n = fabs(qa - rint(qa)) > 1e-7 ? (int64_t)ceil(qa) : (int64_t)ceil(num / z.cps);
+        z.nd = fabs(qa - rint(qa)) > 1e-7 ? ceil(qa) : ceil(num / z.cps);
+        z.n = (int64_t)z.nd;
         z.dv = z.n - (int64_t)(p.S * pdi);
         return z;
     }
     // round (half away from zero; q > 0)
     const double fr = qa - floor(qa);
-    z.n = fabs(fr - 0.5) > 1e-7 ? (int64_t)floor(qa + 0.5) : (int64_t)round(num / z.cps);
+    z.nd = fabs(fr - 0.5) > 1e-7 ? floor(qa + 0.5) : round(num / z.cps);
+    z.n = (int64_t)z.nd;
     z.dv = phaseC ? c.numSample - (int64_t)(p.S * pdi)  // :411 (the previous step's numSample)
                   : z.n - (int64_t)(p.S * pdi);         // :82
     return z;
@@ -200,7 +210,7 @@ __device__ __forceinline__ StepSize step_size(const TrkParams& p, const NcoState
 __device__ __forceinline__ double step_rem_sample(const TrkParams& p, const NcoState& c, int pdi, int phaseC)
 {
     if (p.conv) return 0.0;  // (trackingCT_POS_updated.m has none)
-    const double cps = c.codeFreq / p.Fs;
+    const double cps = over_fs(p, c.codeFreq);
     return phaseC ? (p.codelength * pdi - c.remChip) / cps : (p.codelength - c.remChip) / cps;
 }
 
@@ -211,88 +221,29 @@ __device__ __forceinline__ double step_rem_sample(const TrkParams& p, const NcoS
 //   role 1 (carrier): lanes < 32 the rotation table e^{i phi_m} (depends on f only);
 //   role 2: lane 63 the next remPhase (needs numSample).
 // `taps` = the tap spacings (a copy in LDS where the caller has one).
-__device__ __forceinline__ void prepare_desc_i(const TrkParams& p, const NcoState& c, int pdi, int phaseC, int role,
-                             int lane, StepDesc* d, const double* taps = nullptr,
-                             unsigned long long* dbg = nullptr)
+// An LDS double through a generic pointer known to point into LDS (a flat load would also
+// wait on vmcnt, i.e. on this wave's outstanding global traffic).
+__device__ __forceinline__ double lds_at(const double* q, int i)
 {
-    if (role == 1) {
-        // carrier increment delta = 2*pi*f/Fs as a double-double; dhi has 48 bits so
-        // m*dhi (m < 32) is exact
-        const double f = c.carrierFreq;
-        double dhi, dlo;
-        {
-            const double p0 = kTwoPi * f;
-            double pe = __builtin_fma(kTwoPi, f, -p0);
-            pe = pe + kTwoPiLo * f;
-            const double q = p0 / p.Fs;
-            const double r = __builtin_fma(-q, p.Fs, p0);
-            const double ql = (r + pe) / p.Fs;
-            dhi = __longlong_as_double(__double_as_longlong(q) & ~0x1FLL);
-            dlo = (q - dhi) + ql;
-        }
-        if (lane < kLaneMax) {
-            // phi[m] rounds once (m*dhi is exact)
-            const double ph = (double)lane * dhi + (double)lane * dlo;
-            double sn, cs;
-            sincos(ph, &sn, &cs);
-            d->phi[lane] = ph;
-            d->rcs[lane] = make_double2(cs, sn);
-            if (lane == 0) {
-                d->f = f;
-                d->phi0 = c.remPhase;
-                d->dhi = dhi;
-                d->dlo = dlo;
-            }
-        }
-        return;
-    }
-    const StepSize z = step_size(p, c, pdi, phaseC);
+    return ((__attribute__((address_space(3))) const double*)q)[i];
+}
+
+// The step's scalar fields and its numSample / file / staging checks (trackingCT.m:79-82,
+// 108-112, 442): lane 0 writes them; GNSS_* or GNSS_OK returned in every lane.
+__device__ __forceinline__ int desc_scalars(const TrkParams& p, const NcoState& c, const StepSize& z, int pdi,
+                                            int phaseC, int lane, StepDesc* d)
+{
     const int64_t n = z.n;
-    const double cps = z.cps;
-    if (role == 2) {
-        if (lane == 63) {
-            // remPhase = rem(Wave(numSample+1), 2*pi) (:104-106)
-            d->remPhase_next = rem_2pi(kTwoPi * (c.carrierFreq * ((double)n / p.Fs)) + c.remPhase);
-        } else if (lane == 62) {
-            d->remSample = step_rem_sample(p, c, pdi, phaseC);  // (off the code role's path)
-        }
-        return;
-    }
-    if (dbg && lane == 0) dbg[0] = wall_clock64();
-    const int64_t A = c.pos / p.bps;  // first sample of the fread (ftell / bytes per sample)
+    // first sample of the fread (ftell / bytes per sample; bps = 1, 2 or 4 divides pos)
+    const int64_t A = c.pos >> (p.bps == 4 ? 2 : p.bps == 2 ? 1 : 0);
     const int64_t sb = p.fmt ? 4 : 2;  // staged bytes per sample
     int bad = GNSS_OK;
-    if (n <= 0 || n > (int64_t)(p.S * pdi * 1.01) + 64) bad = GNSS_EINDEX;
+    if (!(z.nd > 0) || z.nd > floor(p.S * pdi * 1.01) + 64) bad = GNSS_EINDEX;
     else if (p.bps * (A + n) > p.file_len) bad = (phaseC || p.conv || p.given) ? GNSS_EIO : GNSS_ENODATA;  // :108-112 / :442
     else if (sb * A < p.buf_base || sb * (A + n) > p.buf_base + p.buf_len) bad = GNSS_EIO;
-    if (lane < p.ntaps) {
-        // t = (0 + Spacing + remChip) : cps : ((numSample-1)*cps + Spacing + remChip) (:96-98)
-        const double tap = taps ? taps[lane] : p.taps[lane];
-        const double a = (0 + tap) + c.remChip;
-        const double bb = ((double)(n - 1) * cps + tap) + c.remChip;
-        const Colon col = colon_make_hint(a, cps, bb, n - 1);
-        d->tap_a[lane] = col.a;
-        d->tap_c[lane] = col.c;
-        const double post = p.tap_post[lane];
-        const int64_t c0 = (int64_t)ceil(colon_elem(col, 0) + post);
-        const int64_t c1 = (int64_t)ceil(colon_elem(col, n - 1) + post);
-        // Code index ceil(t) + 1 + chip_off within [1, 1023*pdi + 2 + chip_off]
-        int tb = (col.n != n - 1 || c0 + p.chip_off < 0 || c1 > 1023LL * pdi + 1) ? GNSS_EINDEX : GNSS_OK;
-        if (lane == p.iP) {
-            // remChip = (t_CodePrompt(numSample) + codeFreq/Fs) - codeFreqBasis*ms*pdi (:102);
-            // trackingCT_POS_updated.m:220: ... - signal.codelength*pdi
-            d->remChip_next = (colon_elem(col, n - 1) + c.codeFreq / p.Fs) -
-                              (p.conv ? p.codelength * pdi : p.codeFreqBasis * p.ms * pdi);
-        }
-        if (tb != GNSS_OK && bad == GNSS_OK) bad = tb;
-    }
-    if (dbg && lane == 0) dbg[1] = wall_clock64();
-    // the first failing lane's code wins
-    const unsigned long long fails = __ballot(bad != GNSS_OK);
-    const int badw = fails ? __builtin_amdgcn_readlane(bad, __ffsll((long long)fails) - 1) : GNSS_OK;
     if (lane == 0) {
         double mr = 0.0, mi = 0.0;
-        if (p.fmt == 1 && badw == GNSS_OK) {
+        if (p.fmt == 1 && bad == GNSS_OK) {
             // rawsignal0DC = I - mean(I) + 1i*(Q - mean(Q)) over the n samples read
             // (trackingCT.m:84-88 / :417-421): integer sums, exact, from the group prefix
             // sums plus the samples of the partial group; mean = sum / n rounded once
@@ -320,11 +271,132 @@ __device__ __forceinline__ void prepare_desc_i(const TrkParams& p, const NcoStat
         d->g_first = A >> 3;
         d->g_last = (A + n - 1) >> 3;
         d->Index = c.Index;
-        d->d = cps;
+        d->d = z.cps;
         d->inv_d = z.inv_cps;
+        d->rc0 = c.remChip;
         d->pdi = pdi;
         d->phaseC = phaseC;
-        d->bad = badw;
+        d->bad = bad;
+    }
+    return bad;
+}
+
+// The replica colons of the taps (trackingCT.m:96-102): lane s < ntaps stores tap s's colon
+// start / end (all the correlator lanes need), then checks its replica index range and, for
+// the prompt, the next remChip. Returns GNSS_EINDEX in a lane whose index range fails.
+__device__ __forceinline__ int desc_taps(const TrkParams& p, const NcoState& c, const StepSize& z, int pdi,
+                                         int lane, StepDesc* d, const double* taps, const double* posts)
+{
+    if (lane >= p.ntaps) return GNSS_OK;
+    // t = (0 + Spacing + remChip) : cps : ((numSample-1)*cps + Spacing + remChip) (:96-98);
+    // n - 1 as the exact double z.nd - 1 (no integer round trip on the critical path)
+    const double cps = z.cps;
+    const double tap = taps ? lds_at(taps, lane) : p.taps[lane];
+    const double post = posts ? lds_at(posts, lane) : p.tap_post[lane];
+    const double a = (0 + tap) + c.remChip;
+    const double bb = ((z.nd - 1) * cps + tap) + c.remChip;
+    const Colon col = colon_make_hint2(a, cps, bb, z.n - 1, z.nd - 1);
+    d->tap_a[lane] = col.a;
+    d->tap_c[lane] = col.c;
+    // (after the stores: the lanes need only a, c) elements 0 and n-1 of a colon of n - 1
+    // intervals are a and c
+    const bool whole = col.n == z.n - 1;
+    const double c0 = ceil(col.a + post);
+    const double c1 = ceil(col.c + post);
+    if (lane == p.iP) {
+        // remChip = (t_CodePrompt(numSample) + codeFreq/Fs) - codeFreqBasis*ms*pdi (:102);
+        // trackingCT_POS_updated.m:220: ... - signal.codelength*pdi (codeFreq/Fs = cps)
+        d->remChip_next = ((whole ? col.c : colon_elem(col, z.n - 1)) + cps) -
+                          (p.conv ? p.codelength * pdi : p.codeFreqBasis * p.ms * pdi);
+    }
+    // Code index ceil(t) + 1 + chip_off within [1, 1023*pdi + 2 + chip_off]
+    return (!whole || c0 + p.chip_off < 0 || c1 > 1023.0 * pdi + 1) ? GNSS_EINDEX : GNSS_OK;
+}
+
+// remPhase after the step (trackingCT.m:104-106) and remSample (:79 / :414, a record field),
+// from the descriptor alone
+__device__ __forceinline__ void desc_rem(const TrkParams& p, StepDesc* d)
+{
+    const double nd = (double)d->n;
+    d->remPhase_next = rem_2pi(kTwoPi * (d->f * over_fs(p, nd)) + d->phi0);
+    d->remSample = p.conv ? 0.0  // (trackingCT_POS_updated.m has none)
+                 : d->phaseC ? (p.codelength * d->pdi - d->rc0) / d->d : (p.codelength - d->rc0) / d->d;
+}
+
+// Prepare the descriptor of the step that follows state `c` (trackingCT.m:79-107 /
+// :411-441). Waves work on it side by side (divergent lanes of one wave would run one
+// after the other):
+//   role 0 (code): lanes < ntaps build the colon of their tap; without `split` lane 0 also
+//     the scalars and the checks, and the result folds into `bad`;
+//   role 1 (carrier): lanes < 32 the rotation table e^{i phi_m} (depends on f only);
+//   role 2: lane 63 the next remPhase and remSample (needs numSample and the table's f);
+//   role 3 (split only): the scalars and their checks.
+// split (the persistent loop): roles 0 / 1 / 3 on three waves in the tail, role 2 by the
+// flush wave during the next step (desc_rem): the tail's code chain is the colon alone.
+// `taps` / `posts` = the tap spacings / prompt offsets (copies in LDS where the caller has).
+__device__ __forceinline__ void prepare_desc_i(const TrkParams& p, const NcoState& c, int pdi, int phaseC, int role,
+                             int lane, StepDesc* d, const double* taps = nullptr,
+                             unsigned long long* dbg = nullptr, const double* posts = nullptr,
+                             bool split = false)
+{
+    if (role == 1) {
+        // carrier increment delta = 2*pi*f/Fs as a double-double; dhi has 48 bits so
+        // m*dhi (m < 32) is exact
+        const double f = c.carrierFreq;
+        double dhi, dlo;
+        {
+            const double p0 = kTwoPi * f;
+            double pe = __builtin_fma(kTwoPi, f, -p0);
+            pe = pe + kTwoPiLo * f;
+            const double q = over_fs(p, p0);
+            const double r = __builtin_fma(-q, p.Fs, p0);
+            const double ql = over_fs(p, r + pe);
+            dhi = __longlong_as_double(__double_as_longlong(q) & ~0x1FLL);
+            dlo = (q - dhi) + ql;
+        }
+        if (lane < kLaneMax) {
+            // phi[m] rounds once (m*dhi is exact)
+            const double ph = (double)lane * dhi + (double)lane * dlo;
+            double sn, cs;
+            sincos(ph, &sn, &cs);
+            d->phi[lane] = ph;
+            d->rcs[lane] = make_double2(cs, sn);
+            if (lane == 0) {
+                d->f = f;
+                d->phi0 = c.remPhase;
+                d->dhi = dhi;
+                d->dlo = dlo;
+            }
+        }
+        return;
+    }
+    const StepSize z = step_size(p, c, pdi, phaseC);
+    if (role == 2) {
+        if (lane == 63) {
+            // remPhase = rem(Wave(numSample+1), 2*pi) (:104-106)
+            d->remPhase_next = rem_2pi(kTwoPi * (c.carrierFreq * over_fs(p, z.nd)) + c.remPhase);
+        } else if (lane == 62) {
+            d->remSample = step_rem_sample(p, c, pdi, phaseC);  // (off the code role's path)
+        }
+        return;
+    }
+    if (role == 3) {
+        (void)desc_scalars(p, c, z, pdi, phaseC, lane, d);
+        return;
+    }
+    if (dbg && lane == 0) dbg[0] = wall_clock64();
+    const int tb = desc_taps(p, c, z, pdi, lane, d, taps, posts);
+    if (dbg && lane == 0) dbg[1] = wall_clock64();
+    // the first failing lane's code wins (every failing tap lane has GNSS_EINDEX)
+    const int btap = __ballot(tb != GNSS_OK) ? GNSS_EINDEX : GNSS_OK;
+    if (split) {
+        if (lane == 0) d->bad_tap = btap;
+        return;
+    }
+    const int bs = desc_scalars(p, c, z, pdi, phaseC, lane, d);
+    if (lane == 0) {
+        d->bad = bs != GNSS_OK ? bs : btap;
+        d->bad_tap = GNSS_OK;
     }
 }
 // out-of-line copy for the persistent kernel (keeps its register budget)
@@ -411,7 +483,7 @@ __device__ __forceinline__ LoopUpd loop_update_i(const TrkParams& p, const TrkCh
         u.codeFreq = p.conv ? p.codeFreqBasis + u.code_output : p.codeFreqBasis - u.code_output;
     }
     if (which & 2) {
-        u.PLLdiscri = atan_tab(P_q / P_i) / kTwoPi;
+        u.PLLdiscri = div_const(atan_tab(P_q / P_i), kTwoPi, kInvTwoPi);
         u.carrier_output = c.carrier_outputLast +
                            p.pll_r * (u.PLLdiscri - c.PLLdiscriLast) +
                            u.PLLdiscri * (pdi == 1 ? p.pll_t1 : (phaseC || p.conv) ? p.pll_t10 : T / p.tau1carr);
@@ -443,8 +515,8 @@ __device__ __forceinline__ int64_t record_cols(const TrkParams& p, const TrkChan
     const int64_t Index = c.Index + (phaseC ? 10 : 1);
     const int64_t nstep = c.nstep + 1;
     if (p.conv) return nstep;  // sum(delayValue(svIndex,(1:Index))), trackingCT_POS_updated.m:290
-    int64_t cols = 0;
-    if (Index >= c.sv1) cols = (Index - c.sv1) / p.nsv + 1;
+    int64_t cols = 0;  // (32-bit quotient: Index < 2^31; a 64-bit one is ~150 scalar ops)
+    if (Index >= c.sv1) cols = (int64_t)((uint32_t)(Index - c.sv1) / (uint32_t)p.nsv) + 1;
     return cols > nstep ? nstep : cols;
 }
 
@@ -954,7 +1026,7 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(const TrkParams
     const int64_t g0 = g_first + ((int64_t)blk * T + tid) * SUB;  // first group of the lane
     // issue the IF loads first (clamped so every lane loads something valid)
     const int8_t* iq = b.iq - p.buf_base;  // absolute-byte addressing
-    const int bad = dp->bad;
+    const int bad = dp->bad ? dp->bad : dp->bad_tap;
     constexpr int GB = FMT == 1 ? 2 : 1;  // 16-B loads per 8-sample group
     int4 raw[SUB * GB];
 #pragma unroll
@@ -1289,7 +1361,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
     __shared__ StepOut s_o;                                        // the step whose state and
     __shared__ LoopUpd s_u;                                        //   record are pending
     __shared__ double s_fin[NV];
-    __shared__ double s_taps[GNSS_MAX_TAPS];
+    __shared__ double s_taps[GNSS_MAX_TAPS], s_post[GNSS_MAX_TAPS];
     __shared__ double2 s_zero;
 
     if (!census(b.run_err, tid)) return;
@@ -1309,9 +1381,12 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         reinterpret_cast<unsigned*>(&s_d[0])[e] = ((const g_u32*)(b.desc + ch))[e];
     if (tid < kChanWords) reinterpret_cast<uint64_t*>(&s_c)[tid] = ((const g_u64*)cp)[tid];
     if (tid == 0) s_zero = make_double2(0.0, 0.0);
-    if (tid < NT) s_taps[tid] = p.taps[tid];
+    if (tid < NT) {
+        s_taps[tid] = p.taps[tid];
+        s_post[tid] = p.tap_post[tid];
+    }
     __syncthreads();
-    if (!s_d[0].bad)
+    if (!s_d[0].bad && !s_d[0].bad_tap)
         prefetch_raw<SUB>(iq, s_d[0].g_first + ((int64_t)blk * T + tid) * SUB, gmax, s_raw, tid);
 
     int cur = 0;   // s_d[cur]: this step
@@ -1337,10 +1412,11 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
     const unsigned long long t_start = wall_clock64();
     for (int s = 0; s < nsteps; s++) {
         const StepDesc& D = s_d[cur];
-        const int bad = D.bad;
+        const int bad = D.bad ? D.bad : D.bad_tap;
         const bool stop = !D.phaseC && D.Index + 1 > n1_target;  // 1-ms run of this channel done
         if (bad || stop || D.d * M >= 1.0) {  // (a code rate beyond Fs/M breaks the one-boundary lane)
             if (pend) flush();
+            if (io && tid == 64) desc_rem(p, &s_d[cur]);  // (complete for a step-kernel follow-up)
             __syncthreads();
             if (io) {  // leave the state and this (unused) descriptor for the host / next launch
                 if (tid == 0 && !stop) s_c.status = bad ? bad : GNSS_EINDEX;
@@ -1399,6 +1475,9 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
             }
         }
 
+        // the step's remPhase / remSample (role 2 of the descriptor, off the tail: the
+        // next tail reads them after the sweep's closing barrier)
+        if (wv == 1 && lane == 0) desc_rem(p, &s_d[cur]);
         if (pend) {
             if (srow && tid == 64) srow[16] = wall_clock64();
             flush();  // (the sweep's closing barrier publishes it)
@@ -1452,7 +1531,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         o.phaseC = phaseC;
         const LoopUpd u = loop_update_i(p, c, s_fin[2 * p.iE], s_fin[2 * p.iE + 1], s_fin[2 * p.iP],
                                       s_fin[2 * p.iP + 1], s_fin[2 * p.iL], s_fin[2 * p.iL + 1], o.pdi,
-                                      o.phaseC, wv == 0 ? 1 : wv == 3 ? 2 : 3);  // (each role's half)
+                                      o.phaseC, wv == 0 || wv == 2 ? 1 : wv == 3 ? 2 : 3);  // (each role's half)
         if (srow && io && tid == 0) srow[11] = wall_clock64();
         NcoState nx;
         nx.remChip = o.remChip;
@@ -1462,17 +1541,17 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         nx.numSample = o.n;
         nx.pos = c.pos + p.bps * o.n;
         nx.Index = c.Index + (o.phaseC ? 10 : 1);
-        if (wv == 0 || wv == 3) {  // the code half / the carrier table of the next descriptor
+        if (wv == 0 || wv == 3) {  // the tap colons / the carrier table of the next descriptor
             prepare_desc_i(p, nx, o.pdi, o.phaseC, wv == 0 ? 0 : 1, lane, &s_d[cur ^ 1], s_taps,
-                           srow && io ? srow + 14 : nullptr);
+                           srow && io ? srow + 14 : nullptr, s_post, true);
             if (srow && io && lane == 0) srow[wv == 0 ? 12 : 13] = wall_clock64();
         } else if (wv == 1) {
             if (lane == 0) {
                 s_o = o;
                 s_u = u;
             }
-        } else {  // wave 2: remPhase of the next step, then its IF has landed
-            prepare_desc_i(p, nx, o.pdi, o.phaseC, 2, lane, &s_d[cur ^ 1], s_taps);  // lane 63
+        } else {  // wave 2: the next step's scalars and checks, then its IF has landed
+            prepare_desc_i(p, nx, o.pdi, o.phaseC, 3, lane, &s_d[cur ^ 1], s_taps, nullptr, s_post, true);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         pend = true;
@@ -1486,6 +1565,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         b.stamps[22 + 3 * ch] = (unsigned long long)nsteps;
     }
     if (pend) flush();
+    if (io && tid == 64) desc_rem(p, &s_d[cur]);  // (complete for a step-kernel follow-up)
     __syncthreads();
     if (io) {  // the state and the next step's descriptor for the next launch
         if (tid < kChanWords)

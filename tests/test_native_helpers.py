@@ -31,3 +31,16 @@ def test_fmod_pos_equals_c_fmod(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches 0" in r.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_div_const_equals_ieee_division(tmp_path):
+    """The tracking tail's divisions by Fs and 2*pi (div_const, Markstein's correction)
+    return the IEEE quotient the reference's `/` computes (trackingCT.m:80,102,106,146)."""
+    src = os.path.join(ROOT, "tests", "native", "markstein.cpp")
+    exe = tmp_path / "markstein"
+    subprocess.run([HIPCC, "-O2", "-std=c++17", "-ffp-contract=off", "-o", str(exe), src],
+                   check=True, capture_output=True)
+    r = subprocess.run([str(exe), "2000000"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches 0" in r.stdout
