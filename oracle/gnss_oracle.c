@@ -551,6 +551,12 @@ static void correlate_cpx(const cpx *x, int64_t n, double remChip, double codeFr
  * much the closed loop depends on reproducing them. */
 static int g_carrier_mode = 0;
 void or_set_carrier_mode(int mode) { g_carrier_mode = mode; }
+/* mode >= 2 (experiment only): the carrier of the lane-table correlator -- lanes of g_lane_w
+ * samples aligned to the 8-sample groups of the file (first lane starts g_lane_a7 = A mod 8
+ * samples before the window), e^{i Wave(lane start)} (the reference's rounding) times the
+ * table e^{i m delta} quantised to `mode` fractional bits. */
+static int g_lane_w = 24, g_lane_a7 = 0;
+void or_set_lane_geometry(int w, int a7) { g_lane_w = w; g_lane_a7 = a7; }
 
 void or_correlate_step(const int8_t *iq, int64_t n, double remChip, double codeFreq, double Fs,
                        double carrierFreq, double remPhase, const int8_t *ca, int pdi, int ntaps,
@@ -595,6 +601,17 @@ static void correlate_cpx(const cpx *x, int64_t n, double remChip, double codeFr
                              (long double)Fs + (long double)remPhase;
             cw = (double)cosl(Wl);
             sw = (double)sinl(Wl);
+        } else if (g_carrier_mode >= 2) {
+            const int64_t L = (k + g_lane_a7) / g_lane_w;
+            const int64_t ks = L * g_lane_w - g_lane_a7;
+            const double Wb = TWO_PI * (carrierFreq * ((double)ks / Fs)) + remPhase;
+            const long double dl = 2.0L * 3.14159265358979323846264338327950288L * (long double)carrierFreq / (long double)Fs;
+            const long double sc = ldexpl(1.0L, g_carrier_mode);
+            const long double tr = roundl(cosl(dl * (long double)(k - ks)) * sc) / sc;
+            const long double ti = roundl(sinl(dl * (long double)(k - ks)) * sc) / sc;
+            const long double br = cosl((long double)Wb), bi = sinl((long double)Wb);
+            cw = (double)(br * tr - bi * ti);
+            sw = (double)(br * ti + bi * tr);
         }
         double xr = x[k].re, xi = x[k].im;
         double I = xr * sw + xi * cw; /* imag(raw.*carrsig) */
@@ -759,6 +776,8 @@ static int trk_step(const trk_ctx *t, chan_state *c, int ch, int sv1, int pdi, i
     }
 
     double sums[2 * GNSS_MAX_TAPS];
+    g_lane_w = pdi == 1 ? 8 : 24;
+    g_lane_a7 = (int)(((c->pos - got) / (t->file->dataType * t->file->dataPrecision)) & 7);
     correlate_cpx(buf, n, c->remChip, c->codeFreq, sg->Fs, c->carrierFreq, c->remPhase, ca, pdi,
                   t->ntaps, t->taps, NULL, 0, sums);
     if (phaseC)

@@ -70,6 +70,7 @@ int or_tracking_ct_mc(const gnss_file *file, const gnss_signal *signal, const gn
  * trackingCT.m:96-118 / :429-449 without the negation): sums[2*ntaps] =
  * (I, Q) per tap. Exposed for per-step parity tests. */
 void or_set_carrier_mode(int mode);
+void or_set_lane_geometry(int w, int a7);
 void or_correlate_step(const int8_t *iq, int64_t numSample, double remChip, double codeFreq,
                        double Fs, double carrierFreq, double remPhase, const int8_t *ca1023,
                        int pdi, int ntaps, const double *taps, double *sums);

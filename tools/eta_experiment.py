@@ -28,22 +28,24 @@ Acq = pkg.sdr.from_c_acquired(pkg.sdr.to_c_acquired(type("A", (), dict(
     codedelay=S.OPENSKY_CODEDELAY[:nch], fineFreq=[float(f) for f in S.OPENSKY_FINEFREQ[:nch]]))))
 track.msToProcessCT_1ms, track.msToProcessCT_10ms = 1000, ms10
 res = []
-for mode in (0, 1):
+for mode in [int(m) for m in os.environ.get("MODES", "0,1").split(",")]:
     po.load().or_set_carrier_mode(mode)
     t0 = time.time()
     res.append(po.trackingCT(file, signal, track, Acq, nthreads=8))
     print("mode", mode, "oracle s", time.time() - t0, flush=True)
-(T0, c0, x0), (T1, c1, x1) = res
-print("countinx", list(x0), list(x1))
-for prn in Acq.sv:
-    a, b = T0(prn), T1(prn)
-    first = None
-    for f in ("numSample", "absoluteSample", "delayValue"):
-        d = np.nonzero(np.asarray(getattr(a, f)) != np.asarray(getattr(b, f)))[0]
-        if len(d):
-            first = d[0] if first is None else min(first, d[0])
-    scale = np.sqrt(np.mean(a.P_i ** 2 + a.P_q ** 2))
-    err = max(np.max(np.abs(a.P_i - b.P_i)), np.max(np.abs(a.P_q - b.P_q))) / scale
-    dll = np.max(np.abs(a.DLLdiscri - b.DLLdiscri))
-    print(f"PRN {prn}: len {len(a.P_i)} first int diff {first} P err/rms {err:.3e} "
-          f"max dDLL {dll:.3e} max dremChip {np.max(np.abs(a.remChip - b.remChip)):.3e}", flush=True)
+modes = [int(m) for m in os.environ.get("MODES", "0,1").split(",")]
+T0, c0, x0 = res[0]
+for mode, (T1, c1, x1) in zip(modes[1:], res[1:]):
+    print("== mode", modes[0], "vs", mode, "countinx", list(x0), list(x1))
+    for prn in Acq.sv:
+        a, b = T0(prn), T1(prn)
+        first = None
+        for f in ("numSample", "absoluteSample", "delayValue"):
+            d = np.nonzero(np.asarray(getattr(a, f)) != np.asarray(getattr(b, f)))[0]
+            if len(d):
+                first = d[0] if first is None else min(first, d[0])
+        scale = np.sqrt(np.mean(a.P_i ** 2 + a.P_q ** 2))
+        err = max(np.max(np.abs(a.P_i - b.P_i)), np.max(np.abs(a.P_q - b.P_q))) / scale
+        dll = np.max(np.abs(a.DLLdiscri - b.DLLdiscri))
+        print(f"PRN {prn}: len {len(a.P_i)} first int diff {first} P err/rms {err:.3e} "
+              f"max dDLL {dll:.3e} max dremChip {np.max(np.abs(a.remChip - b.remChip)):.3e}", flush=True)
