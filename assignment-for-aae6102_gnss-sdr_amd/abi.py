@@ -124,6 +124,7 @@ PROTOTYPES = {
     "gnss_last_error": (C.c_char_p, [C.c_void_p]),
     "gnss_last_timing": (C.c_int, [C.c_void_p, C.POINTER(GnssTiming)]),
     "gnss_ctx_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
+    "gnss_ctx_set_acq_precision": (C.c_int, [C.c_void_p, C.c_int]),
     "gnss_dev_alloc": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
     "gnss_dev_free": (C.c_int, [C.c_void_p, C.c_void_p]),
     "gnss_dev_upload": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),

@@ -16,13 +16,29 @@ namespace {
 __device__ __forceinline__ float sin_rev(float x) { return __builtin_amdgcn_sinf(x); }
 __device__ __forceinline__ float cos_rev(float x) { return __builtin_amdgcn_cosf(x); }
 
+// The rocFFT path's kernels, in fp32 (fast mode) or fp64 (the reference's precision):
+// V = float2 / double2, R its scalar.
+template <class V> struct ScalarOf;
+template <> struct ScalarOf<float2> { using T = float; };
+template <> struct ScalarOf<double2> { using T = double; };
+
+template <class V>
+__device__ __forceinline__ V mkv(typename ScalarOf<V>::T x, typename ScalarOf<V>::T y)
+{
+    V r;
+    r.x = x;
+    r.y = y;
+    return r;
+}
+
 // temp1 = rawsignal(ms idx) .* carrier(freqband,:)  (acquisition.m:41-44,56)
 // carrier(b, n) = exp(1i*2*pi*(IF + freqMin + freqStep*(b-1))*n/Fs), n = 1..S
-template <class Src>
+template <class Src, class V>
 __global__ void acq_wipe_kernel(const Src src, int64_t S, int datalen, int nbins,
                                 double IF, double freqMin, double freqStep, double Fs,
-                                float2* __restrict__ out)
+                                V* __restrict__ out)
 {
+    using R = typename ScalarOf<V>::T;
     const int j = blockIdx.y;  // (idx, b) pair: j = idx*nbins + b
     const int idx = j / nbins, b = j - idx * nbins;
     const double f = (IF + (freqMin + freqStep * (double)b)) / Fs;  // cycles per sample
@@ -30,65 +46,78 @@ __global__ void acq_wipe_kernel(const Src src, int64_t S, int datalen, int nbins
          n += (int64_t)gridDim.x * blockDim.x) {
         double cyc = f * (double)(n + 1);
         cyc -= floor(cyc);
-        const float ph = (float)cyc;
-        const float c = cos_rev(ph), s = sin_rev(ph);
+        R c, s;
+        if constexpr (sizeof(R) == 4) {
+            const float ph = (float)cyc;
+            c = cos_rev(ph);
+            s = sin_rev(ph);
+        } else {
+            sincospi(2.0 * cyc, &s, &c);
+        }
         const double2 x = src.at((int64_t)idx * S + n);
-        const float xr = (float)x.x, xi = (float)x.y;
-        out[(int64_t)j * S + n] = make_float2(xr * c - xi * s, xr * s + xi * c);
+        const R xr = (R)x.x, xi = (R)x.y;
+        out[(int64_t)j * S + n] = mkv<V>(xr * c - xi * s, xr * s + xi * c);
     }
 }
 
 // scode = [CA CA](ceil(n*(codeFreqBasis/Fs))), n = 1..S  (acquisition.m:49-51)
+template <class V>
 __global__ void acq_code_kernel(const float* __restrict__ ca, int nprn, int64_t S, double step,
-                                float2* __restrict__ out)
+                                V* __restrict__ out)
 {
+    using R = typename ScalarOf<V>::T;
     const int p = blockIdx.y;
     for (int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; n < S;
          n += (int64_t)gridDim.x * blockDim.x) {
         const int64_t ci = (int64_t)ceil((double)(n + 1) * step);  // 1-based into [CA CA]
-        out[(int64_t)p * S + n] = make_float2(ca[(int64_t)p * 1023 + (ci - 1) % 1023], 0.f);
+        out[(int64_t)p * S + n] = mkv<V>((R)ca[(int64_t)p * 1023 + (ci - 1) % 1023], (R)0);
     }
 }
 
 // temp3 .* conj(fft(temp1))  (acquisition.m:57-59): y[p][j][k] = C[p][k] * conj(X[j][k])
-__global__ void acq_mul_kernel(const float2* __restrict__ C, const float2* __restrict__ X,
-                               int nsig, int64_t S, float2* __restrict__ y)
+template <class V>
+__global__ void acq_mul_kernel(const V* __restrict__ C, const V* __restrict__ X,
+                               int nsig, int64_t S, V* __restrict__ y)
 {
     const int j = blockIdx.y, p = blockIdx.z;
-    const float2* c = C + (int64_t)p * S;
-    const float2* x = X + (int64_t)j * S;
-    float2* o = y + ((int64_t)p * nsig + j) * S;
+    const V* c = C + (int64_t)p * S;
+    const V* x = X + (int64_t)j * S;
+    V* o = y + ((int64_t)p * nsig + j) * S;
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < S;
          k += (int64_t)gridDim.x * blockDim.x) {
-        const float2 a = c[k], b = x[k];
+        const V a = c[k], b = x[k];
         // (ar + i ai)(br - i bi)
-        o[k] = make_float2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
+        o[k] = mkv<V>(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
     }
 }
 
 // correlation(b,:) = sum over ms of abs(ifft(.)).^2 (acquisition.m:53-61), ms order fixed
-__global__ void acq_power_kernel(const float2* __restrict__ y, int nbins, int datalen, int64_t S,
-                                 float scale, float* __restrict__ corr)
+template <class V>
+__global__ void acq_power_kernel(const V* __restrict__ y, int nbins, int datalen, int64_t S,
+                                 typename ScalarOf<V>::T scale, typename ScalarOf<V>::T* __restrict__ corr)
 {
+    using R = typename ScalarOf<V>::T;
     const int b = blockIdx.y, p = blockIdx.z;
     const int nsig = nbins * datalen;
     for (int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; n < S;
          n += (int64_t)gridDim.x * blockDim.x) {
-        float acc = 0.f;
+        R acc = 0;
         for (int idx = 0; idx < datalen; idx++) {
-            const float2 v = y[((int64_t)p * nsig + (int64_t)idx * nbins + b) * S + n];
+            const V v = y[((int64_t)p * nsig + (int64_t)idx * nbins + b) * S + n];
             acc += (v.x * v.x + v.y * v.y) * scale;
         }
         corr[((int64_t)p * nbins + b) * S + n] = acc;
     }
 }
 
-struct PeakPart {
-    float m;
-    int32_t bin, col, pad;
+// (the surface is fp32 in the fast mode, fp64 at the reference's precision)
+template <class R> struct PeakPart {
+    R m;
+    int32_t bin, col;
 };
 
-__device__ __forceinline__ void peak_merge(float& m, int& bin, int& col, float m2, int b2, int c2)
+template <class R>
+__device__ __forceinline__ void peak_merge(R& m, int& bin, int& col, R m2, int b2, int c2)
 {
     if (m2 > m) { m = m2; bin = b2; col = c2; }
     else if (m2 == m) { bin = min(bin, b2); col = min(col, c2); }
@@ -108,12 +137,13 @@ __device__ __forceinline__ int64_t storage_of(int64_t col, int perm)
     return perm ? (col % perm) * 2000 + col / perm : col;
 }
 
-__global__ void acq_peak_part_kernel(const float* __restrict__ corr, int nbins, int64_t S,
-                                     int nblk, int perm, PeakPart* __restrict__ part)
+template <class R>
+__global__ void acq_peak_part_kernel(const R* __restrict__ corr, int nbins, int64_t S,
+                                     int nblk, int perm, PeakPart<R>* __restrict__ part)
 {
     const int p = blockIdx.y, blk = blockIdx.x;
-    const float* c = corr + (int64_t)p * nbins * S;
-    float m = -1.f;
+    const R* c = corr + (int64_t)p * nbins * S;
+    R m = (R)-1;
     int bin = 0x7fffffff, col = 0x7fffffff;
     for (int b = 0; b < nbins; b++)
         for (int64_t k = (int64_t)blk * blockDim.x + threadIdx.x; k < S;
@@ -121,35 +151,36 @@ __global__ void acq_peak_part_kernel(const float* __restrict__ corr, int nbins, 
             peak_merge(m, bin, col, c[(int64_t)b * S + k], b, (int)natural_col(k, perm));
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-        const float m2 = __shfl_xor(m, o, 64);
+        const R m2 = __shfl_xor(m, o, 64);
         const int b2 = __shfl_xor(bin, o, 64), c2 = __shfl_xor(col, o, 64);
         peak_merge(m, bin, col, m2, b2, c2);
     }
-    __shared__ PeakPart s[16];
+    __shared__ PeakPart<R> s[16];
     const int wv = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) s[wv] = PeakPart{m, bin, col, 0};
+    if ((threadIdx.x & 63) == 0) s[wv] = PeakPart<R>{m, bin, col};
     __syncthreads();
     if (threadIdx.x == 0) {
         for (int w = 1; w < (int)(blockDim.x >> 6); w++) peak_merge(m, bin, col, s[w].m, s[w].bin, s[w].col);
-        part[(int64_t)p * nblk + blk] = PeakPart{m, bin, col, 0};
+        part[(int64_t)p * nblk + blk] = PeakPart<R>{m, bin, col};
     }
 }
 
 // Merge the partials, then SNR = 10*log10(peak^2 / mean(corr(fbin, off-peak).^2))
 // with the off-peak range [1:cp-cshift, cp+cshift:end] (acquisition.m:66-68).
-__global__ void acq_peak_final_kernel(const float* __restrict__ corr, int nbins, int64_t S,
-                                      int nblk, int cshift, int perm, const PeakPart* __restrict__ part,
+template <class R>
+__global__ void acq_peak_final_kernel(const R* __restrict__ corr, int nbins, int64_t S,
+                                      int nblk, int cshift, int perm, const PeakPart<R>* __restrict__ part,
                                       AcqPeak* __restrict__ out)
 {
     const int p = blockIdx.x;
-    __shared__ float s_m;
+    __shared__ R s_m;
     __shared__ int s_bin, s_col;
     __shared__ double s_sum[16], s_cnt[16], s_mx[16];
     if (threadIdx.x == 0) {
-        float m = -1.f;
+        R m = (R)-1;
         int bin = 0x7fffffff, col = 0x7fffffff;
         for (int k = 0; k < nblk; k++) {
-            const PeakPart q = part[(int64_t)p * nblk + k];
+            const PeakPart<R> q = part[(int64_t)p * nblk + k];
             peak_merge(m, bin, col, q.m, q.bin, q.col);
         }
         s_m = m; s_bin = bin; s_col = col;
@@ -157,7 +188,7 @@ __global__ void acq_peak_final_kernel(const float* __restrict__ corr, int nbins,
     __syncthreads();
     const int fbin = s_bin;
     const int64_t cp1 = (int64_t)s_col + 1;  // 1-based codePhase
-    const float* row = corr + ((int64_t)p * nbins + fbin) * S;
+    const R* row = corr + ((int64_t)p * nbins + fbin) * S;
     double sum = 0, cnt = 0, mx = 0;
     for (int64_t k = threadIdx.x + 1; k <= S; k += blockDim.x) {
         if (k <= cp1 - cshift || k >= cp1 + cshift) {
@@ -182,10 +213,9 @@ __global__ void acq_peak_final_kernel(const float* __restrict__ corr, int nbins,
         }
         const double pk = (double)s_m;
         AcqPeak r;
-        r.peak = s_m;
+        r.peak = (double)s_m;
         r.fbin = fbin;
         r.cp = s_col;
-        r.pad = 0;
         r.snr = 10.0 * log10((pk * pk) / (sum / cnt));
         r.peak2 = mx;
         out[p] = r;
@@ -279,53 +309,112 @@ constexpr int kFineBlocks = 512;
 
 }  // namespace
 
-hipError_t launch_acq_wipe(const int8_t* iq, const double2* xs, int64_t S, int datalen, int nbins, double IF,
-                           double freqMin, double freqStep, double Fs, float2* out, hipStream_t s)
+template <class V>
+static hipError_t launch_acq_wipe_t(const int8_t* iq, const double2* xs, int64_t S, int datalen, int nbins,
+                                    double IF, double freqMin, double freqStep, double Fs, V* out, hipStream_t s)
 {
     dim3 grid((unsigned)((S + 255) / 256), (unsigned)(datalen * nbins));
     if (xs)
-        hipLaunchKernelGGL(acq_wipe_kernel<SrcC64>, grid, dim3(256), 0, s, SrcC64{xs}, S, datalen, nbins, IF,
+        hipLaunchKernelGGL((acq_wipe_kernel<SrcC64, V>), grid, dim3(256), 0, s, SrcC64{xs}, S, datalen, nbins, IF,
                            freqMin, freqStep, Fs, out);
     else
-        hipLaunchKernelGGL(acq_wipe_kernel<SrcIQ8>, grid, dim3(256), 0, s, SrcIQ8{iq}, S, datalen, nbins, IF,
+        hipLaunchKernelGGL((acq_wipe_kernel<SrcIQ8, V>), grid, dim3(256), 0, s, SrcIQ8{iq}, S, datalen, nbins, IF,
                            freqMin, freqStep, Fs, out);
     return hipGetLastError();
 }
 
+template <class V>
+static hipError_t launch_acq_code_t(const float* ca, int nprn, int64_t S, double codeFreqBasis, double Fs, V* out,
+                                    hipStream_t s)
+{
+    dim3 grid((unsigned)((S + 255) / 256), (unsigned)nprn);
+    hipLaunchKernelGGL(acq_code_kernel<V>, grid, dim3(256), 0, s, ca, nprn, S, codeFreqBasis / Fs, out);
+    return hipGetLastError();
+}
+
+template <class V>
+static hipError_t launch_acq_mul_t(const V* code_spec, const V* sig_spec, int nprn, int nsig, int64_t S, V* out,
+                                   hipStream_t s)
+{
+    dim3 grid((unsigned)((S + 1023) / 1024), (unsigned)nsig, (unsigned)nprn);
+    hipLaunchKernelGGL(acq_mul_kernel<V>, grid, dim3(256), 0, s, code_spec, sig_spec, nsig, S, out);
+    return hipGetLastError();
+}
+
+template <class V>
+static hipError_t launch_acq_power_t(const V* y, int nprn, int nbins, int datalen, int64_t S,
+                                     typename ScalarOf<V>::T* corr, hipStream_t s)
+{
+    using R = typename ScalarOf<V>::T;
+    dim3 grid((unsigned)((S + 255) / 256), (unsigned)nbins, (unsigned)nprn);
+    const R scale = (R)(1.0 / ((double)S * (double)S));  // ifft's 1/N, squared
+    hipLaunchKernelGGL(acq_power_kernel<V>, grid, dim3(256), 0, s, y, nbins, datalen, S, scale, corr);
+    return hipGetLastError();
+}
+
+hipError_t launch_acq_wipe(const int8_t* iq, const double2* xs, int64_t S, int datalen, int nbins, double IF,
+                           double freqMin, double freqStep, double Fs, float2* out, hipStream_t s)
+{
+    return launch_acq_wipe_t(iq, xs, S, datalen, nbins, IF, freqMin, freqStep, Fs, out, s);
+}
+hipError_t launch_acq_wipe(const int8_t* iq, const double2* xs, int64_t S, int datalen, int nbins, double IF,
+                           double freqMin, double freqStep, double Fs, double2* out, hipStream_t s)
+{
+    return launch_acq_wipe_t(iq, xs, S, datalen, nbins, IF, freqMin, freqStep, Fs, out, s);
+}
 hipError_t launch_acq_code(const float* ca, const int32_t* /*prn_slot*/, int nprn, int64_t S,
                            double codeFreqBasis, double Fs, float2* out, hipStream_t s)
 {
-    dim3 grid((unsigned)((S + 255) / 256), (unsigned)nprn);
-    hipLaunchKernelGGL(acq_code_kernel, grid, dim3(256), 0, s, ca, nprn, S, codeFreqBasis / Fs, out);
-    return hipGetLastError();
+    return launch_acq_code_t(ca, nprn, S, codeFreqBasis, Fs, out, s);
 }
-
+hipError_t launch_acq_code(const float* ca, const int32_t* /*prn_slot*/, int nprn, int64_t S,
+                           double codeFreqBasis, double Fs, double2* out, hipStream_t s)
+{
+    return launch_acq_code_t(ca, nprn, S, codeFreqBasis, Fs, out, s);
+}
 hipError_t launch_acq_mul(const float2* code_spec, const float2* sig_spec, int nprn, int nsig,
                           int64_t S, float2* out, hipStream_t s)
 {
-    dim3 grid((unsigned)((S + 1023) / 1024), (unsigned)nsig, (unsigned)nprn);
-    hipLaunchKernelGGL(acq_mul_kernel, grid, dim3(256), 0, s, code_spec, sig_spec, nsig, S, out);
-    return hipGetLastError();
+    return launch_acq_mul_t(code_spec, sig_spec, nprn, nsig, S, out, s);
 }
-
+hipError_t launch_acq_mul(const double2* code_spec, const double2* sig_spec, int nprn, int nsig,
+                          int64_t S, double2* out, hipStream_t s)
+{
+    return launch_acq_mul_t(code_spec, sig_spec, nprn, nsig, S, out, s);
+}
 hipError_t launch_acq_power(const float2* y, int nprn, int nbins, int datalen, int64_t S,
                             int /*first_ms*/, float* corr, hipStream_t s)
 {
-    dim3 grid((unsigned)((S + 255) / 256), (unsigned)nbins, (unsigned)nprn);
-    const float scale = (float)(1.0 / ((double)S * (double)S));  // ifft's 1/N, squared
-    hipLaunchKernelGGL(acq_power_kernel, grid, dim3(256), 0, s, y, nbins, datalen, S, scale, corr);
+    return launch_acq_power_t(y, nprn, nbins, datalen, S, corr, s);
+}
+hipError_t launch_acq_power(const double2* y, int nprn, int nbins, int datalen, int64_t S,
+                            int /*first_ms*/, double* corr, hipStream_t s)
+{
+    return launch_acq_power_t(y, nprn, nbins, datalen, S, corr, s);
+}
+
+template <class R>
+static hipError_t launch_acq_peak_t(const R* corr, int nprn, int nbins, int64_t S, int cshift,
+                                    int perm, AcqPeak* out, void* scratch, hipStream_t s)
+{
+    PeakPart<R>* part = reinterpret_cast<PeakPart<R>*>(scratch);
+    hipLaunchKernelGGL(acq_peak_part_kernel<R>, dim3(kPeakBlocks, nprn), dim3(256), 0, s, corr, nbins, S,
+                       kPeakBlocks, perm, part);
+    hipLaunchKernelGGL(acq_peak_final_kernel<R>, dim3(nprn), dim3(256), 0, s, corr, nbins, S,
+                       kPeakBlocks, cshift, perm, part, out);
     return hipGetLastError();
 }
 
 hipError_t launch_acq_peak(const float* corr, int nprn, int nbins, int64_t S, int cshift,
                            int perm, AcqPeak* out, void* scratch, hipStream_t s)
 {
-    PeakPart* part = reinterpret_cast<PeakPart*>(scratch);
-    hipLaunchKernelGGL(acq_peak_part_kernel, dim3(kPeakBlocks, nprn), dim3(256), 0, s, corr, nbins, S,
-                       kPeakBlocks, perm, part);
-    hipLaunchKernelGGL(acq_peak_final_kernel, dim3(nprn), dim3(256), 0, s, corr, nbins, S,
-                       kPeakBlocks, cshift, perm, part, out);
-    return hipGetLastError();
+    return launch_acq_peak_t(corr, nprn, nbins, S, cshift, perm, out, scratch, s);
+}
+
+hipError_t launch_acq_peak(const double* corr, int nprn, int nbins, int64_t S, int cshift,
+                           int perm, AcqPeak* out, void* scratch, hipStream_t s)
+{
+    return launch_acq_peak_t(corr, nprn, nbins, S, cshift, perm, out, scratch, s);
 }
 
 hipError_t launch_fine_build(const int8_t* iq, const double2* xs, int64_t S, int L, const int32_t* codedelay,
@@ -354,7 +443,7 @@ hipError_t launch_fine_argmax(const double2* F, int nsv, int64_t N, int shifted,
 
 size_t acq_scratch_bytes(int nprn, int nsv)
 {
-    size_t a = sizeof(PeakPart) * (size_t)kPeakBlocks * (size_t)nprn;
+    size_t a = sizeof(PeakPart<double>) * (size_t)kPeakBlocks * (size_t)nprn;
     size_t b = sizeof(FinePart) * (size_t)kFineBlocks * (size_t)nsv;
     return a > b ? a : b;
 }

@@ -1,6 +1,7 @@
 // acq_fft.hip — acquisition.m's FFT work for gfx950 without rocFFT's Bluestein path:
 //  (1) the parallel-code-phase search (acquisition.m:47-61) as a two-pass mixed-radix FFT
-//      correlator in fp32 for S = P * 2000 with P prime (Opensky 58000 = 29 * 2000,
+//      correlator in fp64 (the reference's precision) or fp32 (fast mode) for S = P * 2000
+//      with P prime (Opensky 58000 = 29 * 2000,
 //      Urban 26000 = 13 * 2000);
 //  (2) the fine-frequency search (acquisition.m:103-116) in fp64: the zero-padded
 //      N = L*S*datalen point FFT of the 10-ms code-wiped block, split into datalen
@@ -342,19 +343,22 @@ __device__ __forceinline__ void load_row_tw(V* s_tw, const V* tw_row, int tid)
     for (int i = tid; i < kRow; i += kRowThreads) s_tw[i] = tw_row[i];
 }
 
-// ============================== correlator (fp32) =================================
+// ============================== correlator ========================================
+// V = float2: the fast fp32 mode; V = double2: the reference's precision (acquisition.m's
+// MATLAB FFTs are fp64), every product, transform and power sum in fp64.
 
 // ---- F1: forward rows. Transform s < nsig: rawsignal(ms) .* carrier(bin) (acquisition.m:41-44,56);
 // s >= nsig: the code replica of PRN s - nsig (acquisition.m:49-51). Row n2 holds
 // x[P*n1 + n2]; output B[s][n2][k1] * w_S^(-n2*k1).
-template <int P, class Src>
+template <int P, class Src, class V>
 __global__ __launch_bounds__(kRowThreads) void fwd_rows_kernel(
     const Src src, int nbins, int nsig, double IF, double freqMin, double freqStep,
-    double Fs, const float* __restrict__ ca, double code_step, const float2* __restrict__ tw_row,
-    const float2* __restrict__ tw_col, float2* __restrict__ B)
+    double Fs, const float* __restrict__ ca, double code_step, const V* __restrict__ tw_row,
+    const V* __restrict__ tw_col, V* __restrict__ B)
 {
+    using R = Re<V>;
     constexpr int64_t S = (int64_t)P * kRow;
-    __shared__ float2 s_a[kRow], s_tw[kRow];
+    __shared__ V s_a[kRow], s_tw[kRow];
     const int n2 = blockIdx.x, s = blockIdx.y, tid = threadIdx.x;
     load_row_tw(s_tw, tw_row, tid);
     if (s < nsig) {
@@ -364,61 +368,66 @@ __global__ __launch_bounds__(kRowThreads) void fwd_rows_kernel(
             const int64_t n = (int64_t)P * n1 + n2;
             double cyc = f * (double)(n + 1);  // n is 1-based in the reference
             cyc -= floor(cyc);
-            const float ph = (float)cyc;
-            const float c = __builtin_amdgcn_cosf(ph), sn = __builtin_amdgcn_sinf(ph);
+            R c, sn;
+            if constexpr (sizeof(R) == 4) {
+                const float ph = (float)cyc;
+                c = __builtin_amdgcn_cosf(ph);
+                sn = __builtin_amdgcn_sinf(ph);
+            } else {
+                sincospi(2.0 * cyc, &sn, &c);
+            }
             const double2 r = src.at((int64_t)idx * S + n);
-            const float xr = (float)r.x, xi = (float)r.y;
-            s_a[n1] = make_float2(xr * c - xi * sn, xr * sn + xi * c);
+            const R xr = (R)r.x, xi = (R)r.y;
+            s_a[n1] = mk<V>(xr * c - xi * sn, xr * sn + xi * c);
         }
     } else {
         const float* cp = ca + (int64_t)(s - nsig) * 1023;
         for (int n1 = tid; n1 < kRow; n1 += kRowThreads) {
             const int64_t n = (int64_t)P * n1 + n2;
             const int64_t ci = (int64_t)ceil((double)(n + 1) * code_step);  // 1-based into [CA CA]
-            s_a[n1] = make_float2(cp[(ci - 1) % 1023], 0.f);
+            s_a[n1] = mk<V>((R)cp[(ci - 1) % 1023], (R)0);
         }
     }
     __syncthreads();
     fft2000<-1>(s_a, s_tw, tid);
-    float2* o = B + ((int64_t)s * P + n2) * kRow;
-    const float2* twc = tw_col + (int64_t)n2 * kRow;
+    V* o = B + ((int64_t)s * P + n2) * kRow;
+    const V* twc = tw_col + (int64_t)n2 * kRow;
     for (int k1 = tid; k1 < kRow; k1 += kRowThreads) o[k1] = cmul(s_a[k1], twc[k1]);
 }
 
 // ---- F2: forward columns: X[s][k1 + 2000*k2] = DFT_P over n2 of B[s][n2][k1]
-template <int P>
-__global__ __launch_bounds__(kColThreads) void fwd_cols_kernel(const float2* __restrict__ B,
-                                                              float2* __restrict__ X)
+template <int P, class V>
+__global__ __launch_bounds__(kColThreads) void fwd_cols_kernel(const V* __restrict__ B, V* __restrict__ X)
 {
     const int k1 = blockIdx.x * kColThreads + threadIdx.x, s = blockIdx.y;
     if (k1 >= kRow) return;
-    const float2* b = B + (int64_t)s * P * kRow + k1;
-    float2 v[P];
+    const V* b = B + (int64_t)s * P * kRow + k1;
+    V v[P];
 #pragma unroll
     for (int i = 0; i < P; i++) v[i] = b[(int64_t)i * kRow];
-    float2* x = X + (int64_t)s * P * kRow + k1;
-    dft_prime<P, -1>(v, [&](int k, float2 y) { x[(int64_t)k * kRow] = y; });
+    V* x = X + (int64_t)s * P * kRow + k1;
+    dft_prime<P, -1>(v, [&](int k, V y) { x[(int64_t)k * kRow] = y; });
 }
 
 // ---- I1: inverse columns of Z = C_p .* conj(X_{ms,bin}) for transform t = (pair, ms)
 // of this batch; pair q = first_pair + t / datalen -> bin = q / nprn, p = q % nprn.
-template <int P>
+template <int P, class V>
 __global__ __launch_bounds__(kColThreads) void inv_cols_kernel(
-    const float2* __restrict__ C, const float2* __restrict__ X, int nbins, int nprn, int datalen,
-    int first_pair, const float2* __restrict__ tw_col, float2* __restrict__ A)
+    const V* __restrict__ C, const V* __restrict__ X, int nbins, int nprn, int datalen,
+    int first_pair, const V* __restrict__ tw_col, V* __restrict__ A)
 {
     const int k1 = blockIdx.x * kColThreads + threadIdx.x, t = blockIdx.y;
     if (k1 >= kRow) return;
     const int q = first_pair + t / datalen, idx = t % datalen;
     const int bin = q / nprn, p = q - bin * nprn;
-    const float2* c = C + (int64_t)p * P * kRow + k1;
-    const float2* x = X + ((int64_t)idx * nbins + bin) * P * kRow + k1;
-    float2 v[P];
+    const V* c = C + (int64_t)p * P * kRow + k1;
+    const V* x = X + ((int64_t)idx * nbins + bin) * P * kRow + k1;
+    V v[P];
 #pragma unroll
     for (int i = 0; i < P; i++) v[i] = cmulc(c[(int64_t)i * kRow], x[(int64_t)i * kRow]);
-    float2* a = A + (int64_t)t * P * kRow + k1;
-    const float2* tw = tw_col + k1;
-    dft_prime<P, 1>(v, [&](int k, float2 y) {
+    V* a = A + (int64_t)t * P * kRow + k1;
+    const V* tw = tw_col + k1;
+    dft_prime<P, 1>(v, [&](int k, V y) {
         a[(int64_t)k * kRow] = cmulc(y, tw[(int64_t)k * kRow]);
     });
 }
@@ -479,6 +488,59 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel(
     const int q = first_pair + g;
     const int bin = q / nprn, p = q - bin * nprn;
     float* o = corr + (((int64_t)p * nbins + bin) * P + tau2) * kRow;
+#pragma unroll
+    for (int i = 0; i < Q; i++) {
+        const int t1 = tid + i * kRowThreads;
+        if (t1 < kRow) o[t1] = acc[i];
+    }
+}
+
+// The fp64 inverse rows: the same transform and sum order, one ms per pass (two fp64
+// rows and their table would take 96 KB of LDS), the next ms's row prefetched into
+// registers while this one transforms. (Twiddles read from the global table instead of
+// this LDS copy: 634 -> 721 us per batch, dropped.)
+template <int P>
+__global__ __launch_bounds__(kRowThreads) void inv_rows_kernel_f64(
+    const double2* __restrict__ A, int nprn, int datalen, int first_pair, double scale,
+    const double2* __restrict__ tw_row, double* __restrict__ corr, int nbins)
+{
+    constexpr int Q = (kRow + kRowThreads - 1) / kRowThreads;
+    __shared__ double2 s_a[kRow], s_tw[kRow];
+    const int tau2 = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
+    load_row_tw(s_tw, tw_row, tid);
+    double acc[Q];
+    double2 nx[Q];
+#pragma unroll
+    for (int i = 0; i < Q; i++) acc[i] = 0.0;
+    const double2* src = A + ((int64_t)g * datalen * P + tau2) * kRow;
+    auto ld = [&](int idx) {
+#pragma unroll
+        for (int i = 0; i < Q; i++) {
+            const int e = tid + i * kRowThreads;
+            nx[i] = src[(int64_t)idx * P * kRow + (e < kRow ? e : kRow - 1)];
+        }
+    };
+    ld(0);
+    for (int idx = 0; idx < datalen; idx++) {
+#pragma unroll
+        for (int i = 0; i < Q; i++) {
+            const int e = tid + i * kRowThreads;
+            if (e < kRow) s_a[e] = nx[i];
+        }
+        if (idx + 1 < datalen) ld(idx + 1);
+        __syncthreads();
+        fft2000<1>(s_a, s_tw, tid);
+#pragma unroll
+        for (int i = 0; i < Q; i++) {  // the ms in order (acquisition.m:53-61)
+            const int t1 = tid + i * kRowThreads, t = t1 < kRow ? t1 : kRow - 1;
+            const double2 v = s_a[t];
+            acc[i] += (v.x * v.x + v.y * v.y) * scale;
+        }
+        __syncthreads();
+    }
+    const int q = first_pair + g;
+    const int bin = q / nprn, p = q - bin * nprn;
+    double* o = corr + (((int64_t)p * nbins + bin) * P + tau2) * kRow;
 #pragma unroll
     for (int i = 0; i < Q; i++) {
         const int t1 = tid + i * kRowThreads;
@@ -640,23 +702,24 @@ __global__ void fine_best_final_kernel(const FineBest* __restrict__ part, int nb
 bool acq_fft_supported(int64_t S) { return S == 13 * kRow || S == 29 * kRow; }
 
 // The forward spectra: X[s] for s < nsig ((ms, bin) signals, s = ms*nbins + bin) and the
-// code spectra C[p] (stored after them: X + nsig*S).
+// code spectra C[p] (stored after them: X + nsig*S). V = float2 or double2.
+template <class V>
 hipError_t launch_acq_fft_forward(const int8_t* iq, const double2* xs, int64_t S, int datalen, int nbins,
                                   double IF, double freqMin, double freqStep, double Fs, const float* ca,
-                                  int nprn, double codeFreqBasis, const float2* tw_row,
-                                  const float2* tw_col, float2* B, float2* X, hipStream_t s)
+                                  int nprn, double codeFreqBasis, const V* tw_row,
+                                  const V* tw_col, V* B, V* X, hipStream_t s)
 {
     const int nsig = datalen * nbins, ntr = nsig + nprn;
     const double step = codeFreqBasis / Fs;
 #define GNSS_FWD(P_)                                                                            \
     if (S == (int64_t)P_ * kRow) {                                                              \
         if (xs)                                                                                 \
-            hipLaunchKernelGGL((fwd_rows_kernel<P_, SrcC64>), dim3(P_, ntr), dim3(kRowThreads), 0, s, \
+            hipLaunchKernelGGL((fwd_rows_kernel<P_, SrcC64, V>), dim3(P_, ntr), dim3(kRowThreads), 0, s, \
                                SrcC64{xs}, nbins, nsig, IF, freqMin, freqStep, Fs, ca, step, tw_row, tw_col, B); \
         else                                                                                    \
-            hipLaunchKernelGGL((fwd_rows_kernel<P_, SrcIQ8>), dim3(P_, ntr), dim3(kRowThreads), 0, s, \
+            hipLaunchKernelGGL((fwd_rows_kernel<P_, SrcIQ8, V>), dim3(P_, ntr), dim3(kRowThreads), 0, s, \
                                SrcIQ8{iq}, nbins, nsig, IF, freqMin, freqStep, Fs, ca, step, tw_row, tw_col, B); \
-        hipLaunchKernelGGL(fwd_cols_kernel<P_>, dim3((kRow + kColThreads - 1) / kColThreads, ntr), \
+        hipLaunchKernelGGL((fwd_cols_kernel<P_, V>), dim3((kRow + kColThreads - 1) / kColThreads, ntr), \
                            dim3(kColThreads), 0, s, B, X);                                      \
         return hipGetLastError();                                                               \
     }
@@ -664,6 +727,13 @@ hipError_t launch_acq_fft_forward(const int8_t* iq, const double2* xs, int64_t S
 #undef GNSS_FWD
     return hipErrorInvalidValue;
 }
+template hipError_t launch_acq_fft_forward<float2>(const int8_t*, const double2*, int64_t, int, int, double,
+                                                   double, double, double, const float*, int, double,
+                                                   const float2*, const float2*, float2*, float2*, hipStream_t);
+template hipError_t launch_acq_fft_forward<double2>(const int8_t*, const double2*, int64_t, int, int, double,
+                                                    double, double, double, const float*, int, double,
+                                                    const double2*, const double2*, double2*, double2*,
+                                                    hipStream_t);
 
 // Correlation of (bin, PRN) pairs [first_pair, first_pair + npair) (pair = bin*nprn + p)
 // over every ms: corr[p][bin] (tau2-major) = sum_ms |ifft(C_p .* conj(X_{ms,bin}))|^2.
@@ -675,11 +745,32 @@ hipError_t launch_acq_fft_correlate(const float2* C, const float2* X, int64_t S,
     const float scale = (float)(1.0 / ((double)S * (double)S));  // ifft's 1/N, squared
 #define GNSS_INV(P_)                                                                            \
     if (S == (int64_t)P_ * kRow) {                                                              \
-        hipLaunchKernelGGL(inv_cols_kernel<P_>,                                                 \
+        hipLaunchKernelGGL((inv_cols_kernel<P_, float2>),                                       \
                            dim3((kRow + kColThreads - 1) / kColThreads, npair * datalen),       \
                            dim3(kColThreads), 0, s, C, X, nbins, nprn, datalen, first_pair,     \
                            tw_col, A);                                                          \
         hipLaunchKernelGGL(inv_rows_kernel<P_>, dim3(P_, npair), dim3(kRowThreads), 0, s, A, nprn, \
+                           datalen, first_pair, scale, tw_row, corr, nbins);                    \
+        return hipGetLastError();                                                               \
+    }
+    GNSS_INV(13) GNSS_INV(29)
+#undef GNSS_INV
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_acq_fft_correlate(const double2* C, const double2* X, int64_t S, int datalen,
+                                    int nbins, int nprn, int first_pair, int npair,
+                                    const double2* tw_row, const double2* tw_col, double2* A,
+                                    double* corr, hipStream_t s)
+{
+    const double scale = 1.0 / ((double)S * (double)S);
+#define GNSS_INV(P_)                                                                            \
+    if (S == (int64_t)P_ * kRow) {                                                              \
+        hipLaunchKernelGGL((inv_cols_kernel<P_, double2>),                                      \
+                           dim3((kRow + kColThreads - 1) / kColThreads, npair * datalen),       \
+                           dim3(kColThreads), 0, s, C, X, nbins, nprn, datalen, first_pair,     \
+                           tw_col, A);                                                          \
+        hipLaunchKernelGGL(inv_rows_kernel_f64<P_>, dim3(P_, npair), dim3(kRowThreads), 0, s, A, nprn, \
                            datalen, first_pair, scale, tw_row, corr, nbins);                    \
         return hipGetLastError();                                                               \
     }

@@ -47,6 +47,8 @@ struct gnss_ctx {
     // (pointer, bytes); a pageable std::vector re-faults and bounces every call
     std::map<std::string, std::pair<void*, size_t>> pinned;
     int64_t acq_tw_S = 0;  // the acquisition twiddle tables in the pool are for this S
+    int acq_tw_dbl = -1;   //   ... and this precision
+    int acq_fp64 = 1;      // acquisition correlation precision: 1 = fp64 (reference), 0 = fp32
 };
 
 namespace {
@@ -327,6 +329,113 @@ void generate_ca(int prn, float* out)
 
 }  // namespace
 
+namespace {
+template <class V> struct CplxReal;
+template <> struct CplxReal<float2> { using T = float; };
+template <> struct CplxReal<double2> { using T = double; };
+
+// The PRN x bin x ms search of acquisition.m:47-61 into corr[p][bin][.] (sum over the ms of
+// |ifft(fft(code) .* conj(fft(signal .* carrier)))|^2), V = float2 (fast mode) or double2
+// (the reference's precision): the own P x 2000 FFT correlator (acq_fft.hip) where S = P * 2000,
+// batched rocFFT otherwise. e_all.a is recorded when the timed work starts; *perm = P for
+// the own correlator's tau2-major surface, 0 for natural order.
+template <class V>
+int acq_search(gnss_ctx* ctx, const int8_t* blk, const double2* xa, int64_t S, int dl, int nb, int np,
+               const gnss_signal* sg, const gnss_acq* acq, const float* ca, typename CplxReal<V>::T* corr,
+               Events& e_all, int* perm)
+{
+    const int dbl = sizeof(V) == sizeof(double2) ? 1 : 0;
+    const size_t csz = sizeof(V);
+    const int nsig = dl * nb;
+    int st = GNSS_OK;
+    if (acq_fft_supported(S) && !getenv("GNSS_ACQ_ROCFFT")) {
+        DevBuf d_twr, d_twc, B, X, A;  // (freed after the stream drains)
+        const int P = (int)(S / 2000);
+        *perm = P;
+        // twiddles (fp64 on the host; rounded to fp32 in the fast mode), kept in the
+        // context per S and precision
+        const bool have_tw = ctx->acq_tw_S == S && ctx->acq_tw_dbl == dbl;
+        HIP_TRY(d_twr.alloc(ctx, "acq.d_twr", 2000 * csz));
+        HIP_TRY(d_twc.alloc(ctx, "acq.d_twc", (size_t)P * 2000 * csz));
+        if (!have_tw) {
+            std::vector<V> twr(2000), twc((size_t)P * 2000);
+            for (int m = 0; m < 2000; m++) {
+                const double a = -2.0 * M_PI * (double)m / 2000.0;
+                twr[m].x = std::cos(a);
+                twr[m].y = std::sin(a);
+            }
+            for (int m = 0; m < P; m++)
+                for (int k = 0; k < 2000; k++) {
+                    const double a = -2.0 * M_PI * (double)((int64_t)m * k % S) / (double)S;
+                    twc[(size_t)m * 2000 + k].x = std::cos(a);
+                    twc[(size_t)m * 2000 + k].y = std::sin(a);
+                }
+            HIP_TRY(hipMemcpyAsync(d_twr.p, twr.data(), twr.size() * csz, hipMemcpyHostToDevice, ctx->stream));
+            HIP_TRY(hipMemcpyAsync(d_twc.p, twc.data(), twc.size() * csz, hipMemcpyHostToDevice, ctx->stream));
+            HIP_TRY(hipStreamSynchronize(ctx->stream));  // (the host vectors go out of scope)
+            ctx->acq_tw_S = S;
+            ctx->acq_tw_dbl = dbl;
+        }
+        const size_t ntr = (size_t)nsig + np;
+        HIP_TRY(B.alloc(ctx, "acq.B", csz * ntr * S));
+        HIP_TRY(X.alloc(ctx, "acq.X", csz * ntr * S));
+        const int npairs = nb * np;
+        // (bin, PRN) pairs per batch: the inverse intermediate round-trips through HBM
+        // anyway (PMC, profiles/acq_traffic_r01.json), so batches of ~1 GiB, balanced (no
+        // small tail batch that leaves the chip idle): config 2 (fp32) measured 7.94 ms of
+        // correlation at 28 pairs per batch (256 MB), 7.09-7.29 at 112, 7.15-7.30 at 232
+        // (tools/gpu_acq_batch.sh). Pairs are independent: the bits do not depend on it.
+        const int target = (int)std::max<int64_t>(1, ((int64_t)1 << 30) / ((int64_t)dl * S * (int64_t)csz));
+        const int nbat = (npairs + target - 1) / target;
+        int batch = (npairs + nbat - 1) / nbat;
+        if (const char* e = getenv("GNSS_ACQ_BATCH")) batch = std::max(1, atoi(e));
+        batch = std::min(batch, npairs);
+        HIP_TRY(A.alloc(ctx, "acq.A", csz * (size_t)batch * dl * S));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        HIP_TRY(hipEventRecord(e_all.a, ctx->stream));
+        HIP_TRY(launch_acq_fft_forward<V>(blk, xa, S, dl, nb, sg->IF, acq->freqMin, acq->freqStep, sg->Fs, ca, np,
+                                          sg->codeFreqBasis, d_twr.as<V>(), d_twc.as<V>(), B.as<V>(), X.as<V>(),
+                                          ctx->stream));
+        const V* C = X.as<V>() + (size_t)nsig * S;
+        for (int q0 = 0; q0 < npairs; q0 += batch) {
+            const int nq = std::min(batch, npairs - q0);
+            HIP_TRY(launch_acq_fft_correlate(C, X.as<V>(), S, dl, nb, np, q0, nq, d_twr.as<V>(), d_twc.as<V>(),
+                                             A.as<V>(), corr, ctx->stream));
+        }
+        return GNSS_OK;
+    }
+    // batched rocFFT (sample counts that are not P x 2000)
+    *perm = 0;
+    DevBuf sig, code, y;
+    HIP_TRY(sig.alloc(ctx, "acq.sig", csz * (size_t)nsig * S));
+    HIP_TRY(code.alloc(ctx, "acq.code", csz * (size_t)np * S));
+    // PRN chunk so the product/IFFT buffer stays <= ~4 GB
+    const size_t per_prn = csz * (size_t)nsig * S;
+    const int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)np, ((size_t)4 << 30) / per_prn));
+    HIP_TRY(y.alloc(ctx, "acq.y", per_prn * (size_t)chunk));
+    // plans outside the timed region
+    rocfft_plan pl;
+    if ((st = get_plan(ctx, S, nsig, dbl, 0, &pl))) return st;
+    if ((st = get_plan(ctx, S, np, dbl, 0, &pl))) return st;
+    for (int p0 = 0; p0 < np; p0 += chunk) {
+        const int pc = std::min(chunk, np - p0);
+        if ((st = get_plan(ctx, S, (size_t)pc * nsig, dbl, 1, &pl))) return st;
+    }
+    HIP_TRY(hipEventRecord(e_all.a, ctx->stream));
+    HIP_TRY(launch_acq_wipe(blk, xa, S, dl, nb, sg->IF, acq->freqMin, acq->freqStep, sg->Fs, sig.as<V>(), ctx->stream));
+    if ((st = run_fft(ctx, sig.p, S, nsig, dbl, 0))) return st;
+    HIP_TRY(launch_acq_code(ca, nullptr, np, S, sg->codeFreqBasis, sg->Fs, code.as<V>(), ctx->stream));
+    if ((st = run_fft(ctx, code.p, S, np, dbl, 0))) return st;
+    for (int p0 = 0; p0 < np; p0 += chunk) {
+        const int pc = std::min(chunk, np - p0);
+        HIP_TRY(launch_acq_mul(code.as<V>() + (size_t)p0 * S, sig.as<V>(), pc, nsig, S, y.as<V>(), ctx->stream));
+        if ((st = run_fft(ctx, y.p, S, (size_t)pc * nsig, dbl, 1))) return st;
+        HIP_TRY(launch_acq_power(y.as<V>(), pc, nb, dl, S, 0, corr + (size_t)p0 * nb * S, ctx->stream));
+    }
+    return GNSS_OK;
+}
+}  // namespace
+
 extern "C" {
 
 int gnss_abi_version(void) { return GNSS_ABI_VERSION; }
@@ -391,6 +500,13 @@ int gnss_ctx_set_profiling(gnss_ctx* ctx, int enable)
 {
     if (!ctx) return GNSS_EARG;
     ctx->profiling = enable;
+    return GNSS_OK;
+}
+
+int gnss_ctx_set_acq_precision(gnss_ctx* ctx, int fp64)
+{
+    if (!ctx || (fp64 != 0 && fp64 != 1)) return GNSS_EARG;
+    ctx->acq_fp64 = fp64;
     return GNSS_OK;
 }
 
@@ -489,98 +605,32 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
 
     std::vector<float> cah((size_t)np * 1023);
     for (int i = 0; i < np; i++) generate_ca(prns[i], &cah[(size_t)i * 1023]);
-    DevBuf ca, sig, code, y, corr, peaks, scratch;
-    DevBuf d_twr, d_twc, B, X, A;  // own FFT correlator buffers (freed after the stream drains)
+    DevBuf ca, corr, peaks, scratch;
     HIP_TRY(ca.alloc(ctx, "acq.ca", cah.size() * sizeof(float)));
     HIP_TRY(hipMemcpyAsync(ca.p, cah.data(), cah.size() * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
-    const int nsig = dl * nb;
-    HIP_TRY(corr.alloc(ctx, "acq.corr", sizeof(float) * (size_t)np * nb * S));
+    // correlation precision: fp64 = the reference's (MATLAB's fft / ifft / abs().^2 in
+    // double, acquisition.m:56-61), the default; fp32 = the fast mode
+    // (gnss_ctx_set_acq_precision)
+    const int dbl = ctx->acq_fp64 ? 1 : 0;
+    HIP_TRY(corr.alloc(ctx, "acq.corr", (dbl ? sizeof(double) : sizeof(float)) * (size_t)np * nb * S));
     HIP_TRY(peaks.alloc(ctx, "acq.peaks", sizeof(AcqPeak) * (size_t)np));
     HIP_TRY(scratch.alloc(ctx, "acq.scratch", acq_scratch_bytes(np, np)));
-    const bool own_fft = acq_fft_supported(S) && !getenv("GNSS_ACQ_ROCFFT");
-    int perm = 0;
     Events e_all, e_corr;  // e_corr.b marks the end of the PRN search
-    if (own_fft) {
-        // two-pass FFT correlator (acq_fft.hip): S = P * 2000
-        const int P = (int)(S / 2000);
-        perm = P;
-        // twiddles (fp64 on the host, rounded to fp32), kept in the context per S
-        const bool have_tw = ctx->acq_tw_S == S;
-        HIP_TRY(d_twr.alloc(ctx, "acq.d_twr", 2000 * sizeof(float2)));
-        HIP_TRY(d_twc.alloc(ctx, "acq.d_twc", (size_t)P * 2000 * sizeof(float2)));
-        if (!have_tw) {
-            std::vector<float2> twr(2000), twc((size_t)P * 2000);
-            for (int m = 0; m < 2000; m++) {
-                const double a = -2.0 * M_PI * (double)m / 2000.0;
-                twr[m] = make_float2((float)std::cos(a), (float)std::sin(a));
-            }
-            for (int m = 0; m < P; m++)
-                for (int k = 0; k < 2000; k++) {
-                    const double a = -2.0 * M_PI * (double)((int64_t)m * k % S) / (double)S;
-                    twc[(size_t)m * 2000 + k] = make_float2((float)std::cos(a), (float)std::sin(a));
-                }
-            HIP_TRY(hipMemcpyAsync(d_twr.p, twr.data(), twr.size() * sizeof(float2), hipMemcpyHostToDevice, ctx->stream));
-            HIP_TRY(hipMemcpyAsync(d_twc.p, twc.data(), twc.size() * sizeof(float2), hipMemcpyHostToDevice, ctx->stream));
-            HIP_TRY(hipStreamSynchronize(ctx->stream));  // (the host vectors go out of scope)
-            ctx->acq_tw_S = S;
-        }
-        const size_t ntr = (size_t)nsig + np;
-        HIP_TRY(B.alloc(ctx, "acq.B", sizeof(float2) * ntr * S));
-        HIP_TRY(X.alloc(ctx, "acq.X", sizeof(float2) * ntr * S));
-        const int npairs = nb * np;
-        // (bin, PRN) pairs per batch: the inverse intermediate round-trips through HBM
-        // anyway (PMC, profiles/acq_traffic_r01.json), so batches of ~1 GiB, balanced (no
-        // small tail batch that leaves the chip idle): config 2 measured 7.94 ms of
-        // correlation at 28 pairs per batch (256 MB), 7.09-7.29 at 112, 7.15-7.30 at 232
-        // (tools/gpu_acq_batch.sh). Pairs are independent: the bits do not depend on it.
-        const int target = (int)std::max<int64_t>(1, ((int64_t)1 << 30) / ((int64_t)dl * S * 8));
-        const int nbat = (npairs + target - 1) / target;
-        int batch = (npairs + nbat - 1) / nbat;
-        if (const char* e = getenv("GNSS_ACQ_BATCH")) batch = std::max(1, atoi(e));
-        batch = std::min(batch, npairs);
-        HIP_TRY(A.alloc(ctx, "acq.A", sizeof(float2) * (size_t)batch * dl * S));
-        HIP_TRY(hipStreamSynchronize(ctx->stream));
-        HIP_TRY(hipEventRecord(e_all.a, ctx->stream));
-        HIP_TRY(launch_acq_fft_forward(blk, xa, S, dl, nb, sg->IF, acq->freqMin, acq->freqStep, sg->Fs,
-                                       ca.as<float>(), np, sg->codeFreqBasis, d_twr.as<float2>(),
-                                       d_twc.as<float2>(), B.as<float2>(), X.as<float2>(), ctx->stream));
-        const float2* C = X.as<float2>() + (size_t)nsig * S;
-        for (int q0 = 0; q0 < npairs; q0 += batch) {
-            const int nq = std::min(batch, npairs - q0);
-            HIP_TRY(launch_acq_fft_correlate(C, X.as<float2>(), S, dl, nb, np, q0, nq, d_twr.as<float2>(),
-                                             d_twc.as<float2>(), A.as<float2>(), corr.as<float>(), ctx->stream));
-        }
-    } else {
-    HIP_TRY(sig.alloc(ctx, "acq.sig", sizeof(float2) * (size_t)nsig * S));
-    HIP_TRY(code.alloc(ctx, "acq.code", sizeof(float2) * (size_t)np * S));
-    // PRN chunk so the product/IFFT buffer stays <= ~4 GB
-    const size_t per_prn = sizeof(float2) * (size_t)nsig * S;
-    int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)np, ((size_t)4 << 30) / per_prn));
-    HIP_TRY(y.alloc(ctx, "acq.y", per_prn * (size_t)chunk));
-
-    // plans outside the timed region
-    rocfft_plan pl;
-    if ((st = get_plan(ctx, S, nsig, 0, 0, &pl))) return st;
-    if ((st = get_plan(ctx, S, np, 0, 0, &pl))) return st;
-    for (int p0 = 0; p0 < np; p0 += chunk) {
-        const int pc = std::min(chunk, np - p0);
-        if ((st = get_plan(ctx, S, (size_t)pc * nsig, 0, 1, &pl))) return st;
-    }
-
-    HIP_TRY(hipEventRecord(e_all.a, ctx->stream));
-    HIP_TRY(launch_acq_wipe(blk, xa, S, dl, nb, sg->IF, acq->freqMin, acq->freqStep, sg->Fs, sig.as<float2>(), ctx->stream));
-    if ((st = run_fft(ctx, sig.p, S, nsig, 0, 0))) return st;
-    HIP_TRY(launch_acq_code(ca.as<float>(), nullptr, np, S, sg->codeFreqBasis, sg->Fs, code.as<float2>(), ctx->stream));
-    if ((st = run_fft(ctx, code.p, S, np, 0, 0))) return st;
-    for (int p0 = 0; p0 < np; p0 += chunk) {
-        const int pc = std::min(chunk, np - p0);
-        HIP_TRY(launch_acq_mul(code.as<float2>() + (size_t)p0 * S, sig.as<float2>(), pc, nsig, S, y.as<float2>(), ctx->stream));
-        if ((st = run_fft(ctx, y.p, S, (size_t)pc * nsig, 0, 1))) return st;
-        HIP_TRY(launch_acq_power(y.as<float2>(), pc, nb, dl, S, 0, corr.as<float>() + (size_t)p0 * nb * S, ctx->stream));
-    }
-    }
+    int perm = 0;
+    if (dbl)
+        st = acq_search<double2>(ctx, blk, xa, S, dl, nb, np, sg, acq, ca.as<float>(), corr.as<double>(), e_all,
+                                 &perm);
+    else
+        st = acq_search<float2>(ctx, blk, xa, S, dl, nb, np, sg, acq, ca.as<float>(), corr.as<float>(), e_all,
+                                &perm);
+    if (st) return st;
     const int cshift = (int)std::ceil(sg->Fs / sg->codeFreqBasis);  // :66
-    HIP_TRY(launch_acq_peak(corr.as<float>(), np, nb, S, cshift, perm, peaks.as<AcqPeak>(), scratch.p, ctx->stream));
+    if (dbl)
+        HIP_TRY(launch_acq_peak(corr.as<double>(), np, nb, S, cshift, perm, peaks.as<AcqPeak>(), scratch.p,
+                                ctx->stream));
+    else
+        HIP_TRY(launch_acq_peak(corr.as<float>(), np, nb, S, cshift, perm, peaks.as<AcqPeak>(), scratch.p,
+                                ctx->stream));
     HIP_TRY(hipEventRecord(e_corr.b, ctx->stream));
     std::vector<AcqPeak> ph((size_t)np);
     HIP_TRY(hipMemcpyAsync(ph.data(), peaks.p, sizeof(AcqPeak) * (size_t)np, hipMemcpyDeviceToHost, ctx->stream));

@@ -281,10 +281,9 @@ constexpr int kDescWords = (int)(sizeof(StepDesc) / 4);
 // Acquisition (acq.hip)
 // ----------------------------------------------------------------------------
 struct AcqPeak {           // per-PRN detector result
-    float peak;
+    double peak;
     int32_t fbin;          // 0-based
     int32_t cp;            // 0-based code phase
-    int32_t pad;
     double snr;
     double peak2;
 };
@@ -297,19 +296,36 @@ hipError_t launch_acq_mul(const float2* code_spec, const float2* sig_spec, int n
                           int64_t S, float2* out, hipStream_t s);
 hipError_t launch_acq_power(const float2* y, int nprn, int nbins, int datalen, int64_t S,
                             int first_ms, float* corr, hipStream_t s);
+// the same at fp64 (the reference's precision)
+hipError_t launch_acq_wipe(const int8_t* iq, const double2* xs, int64_t S, int datalen, int nbins, double IF,
+                           double freqMin, double freqStep, double Fs, double2* out, hipStream_t s);
+hipError_t launch_acq_code(const float* ca, const int32_t* prn_slot, int nprn, int64_t S,
+                           double codeFreqBasis, double Fs, double2* out, hipStream_t s);
+hipError_t launch_acq_mul(const double2* code_spec, const double2* sig_spec, int nprn, int nsig,
+                          int64_t S, double2* out, hipStream_t s);
+hipError_t launch_acq_power(const double2* y, int nprn, int nbins, int datalen, int64_t S,
+                            int first_ms, double* corr, hipStream_t s);
 hipError_t launch_acq_peak(const float* corr, int nprn, int nbins, int64_t S, int cshift,
+                           int perm, AcqPeak* out, void* scratch, hipStream_t s);
+hipError_t launch_acq_peak(const double* corr, int nprn, int nbins, int64_t S, int cshift,
                            int perm, AcqPeak* out, void* scratch, hipStream_t s);
 
 // Two-pass FFT correlator for S = P * 2000 (acq_fft.hip)
 bool acq_fft_supported(int64_t S);
+// V = float2 (fp32 fast mode) or double2 (fp64, the reference's precision)
+template <class V>
 hipError_t launch_acq_fft_forward(const int8_t* iq, const double2* xs, int64_t S, int datalen, int nbins, double IF,
                                   double freqMin, double freqStep, double Fs, const float* ca,
-                                  int nprn, double codeFreqBasis, const float2* tw_row,
-                                  const float2* tw_col, float2* B, float2* X, hipStream_t s);
+                                  int nprn, double codeFreqBasis, const V* tw_row,
+                                  const V* tw_col, V* B, V* X, hipStream_t s);
 hipError_t launch_acq_fft_correlate(const float2* C, const float2* X, int64_t S, int datalen,
                                     int nbins, int nprn, int first_pair, int npair,
                                     const float2* tw_row, const float2* tw_col, float2* A,
                                     float* corr, hipStream_t s);
+hipError_t launch_acq_fft_correlate(const double2* C, const double2* X, int64_t S, int datalen,
+                                    int nbins, int nprn, int first_pair, int npair,
+                                    const double2* tw_row, const double2* tw_col, double2* A,
+                                    double* corr, hipStream_t s);
 bool fine_fft_supported(int64_t S, int L);
 size_t fine_fft_scratch_bytes(int64_t S, int L, int datalen);
 hipError_t launch_fine_fft_tables(int64_t S, int L, int datalen, void* scratch, hipStream_t s);

@@ -92,6 +92,11 @@ class Context:
     def set_profiling(self, on: bool):
         self.check(self.lib.gnss_ctx_set_profiling(self.h, 1 if on else 0))
 
+    def set_acq_precision(self, fp64: bool):
+        """Acquisition correlation at fp64 (the reference's precision, default) or the fp32
+        fast mode (gnss_ctx_set_acq_precision)."""
+        self.check(self.lib.gnss_ctx_set_acq_precision(self.h, 1 if fp64 else 0))
+
 
 class DeviceRecord:
     """An IF record resident in this context's HBM (bytes = file bytes)."""

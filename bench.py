@@ -223,7 +223,7 @@ def run_cfg4(args, rank, world, local, dist, ctx):
             "value": round(total / elapsed / 1e6, 2), "unit": "Msamples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
-            "dtype": "int8 in, f32 correlation / f64 fine search",
+            "dtype": "int8 in, f64 correlation / f64 fine search",
             "data": "synthetic Urban-shape IF (int8 I/Q, Fs 26 MHz, IF 0), resident in HBM",
             "config": {"workload": "acquisition cfg4 (32 PRN, +-10kHz/250Hz, 10 ms, L 10)",
                        "parallelism": f"PRNs x{world}", "prns_per_rank": len(mine)},
@@ -352,6 +352,28 @@ def main():
             except Exception:
                 pass
 
+    # the acquisition's fp32 fast mode (gnss_ctx_set_acq_precision(ctx, 0)) on the same
+    # record, after the timed region: its time and whether its decisions equal the fp64 ones
+    fast = None
+    if not args.no_profile_pass:
+        ctx.set_acq_precision(False)
+        try:
+            pkg.acquisition(file, signal, acq, ctx=ctx, prn_list=my_prns)
+            f_ms = f_corr = 0.0
+            for _ in range(2):
+                Af = pkg.acquisition(file, signal, acq, ctx=ctx, prn_list=my_prns)
+                tf_ = ctx.timing()
+                f_ms += tf_["acq_ms"] / 2
+                f_corr += tf_["acq_corr_ms"] / 2
+        finally:
+            ctx.set_acq_precision(True)
+        Ad = pkg.acquisition(file, signal, acq, ctx=ctx, prn_list=my_prns)
+        same = all(np_equal(getattr(Af, f), getattr(Ad, f)) for f in ("sv", "codedelay", "Doppler", "fineFreq"))
+        fast = {"dtype": "f32 correlation + f64 fine search", "acq_ms": round(f_ms, 3),
+                "corr_ms": round(f_corr, 3),
+                "acq_Msamples_s": round(ta["acq_hypothesis_samples"] / (f_ms * 1e-3) / 1e6, 2),
+                "decisions_equal_fp64": bool(same)}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(file, signal, acq, track, A, dev, args, ta, tt)
@@ -369,8 +391,8 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "int8 in; acquisition: f32 correlation + f64 fine search; tracking: f64",
-        "dtype_per_leg": {"acquisition_correlation": "f32", "acquisition_fine_frequency": "f64",
+        "dtype": "int8 in; acquisition: f64 correlation + f64 fine search; tracking: f64",
+        "dtype_per_leg": {"acquisition_correlation": "f64", "acquisition_fine_frequency": "f64",
                           "tracking": "f64"},
         "data": "synthetic Opensky-shape IF (int8 I/Q, Fs 58 MHz, IF 4.58 MHz), resident in HBM",
         "config": {"workload": "acquisition cfg2 (32 PRN, +-7kHz/500Hz, 20 ms) + trackingCT cfg3 "
@@ -395,6 +417,7 @@ def main():
                           "frac": round(16.0 * acq_units / (acq_corr_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
                           "corr_ms": round(acq_corr_ms / args.steps, 3),
                           "fine_ms": round(acq_fine_ms / args.steps, 3)} if acq_corr_ms else None),
+        "acq_fp32_fast_mode": fast,
         "cpu_baseline": cpu,
     }
     if rank == 0:
@@ -402,6 +425,11 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def np_equal(a, b):
+    import numpy as np
+    return bool(np.array_equal(np.asarray(a), np.asarray(b)))
 
 
 def abi_f(name):

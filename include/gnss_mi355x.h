@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define GNSS_ABI_VERSION 7
+#define GNSS_ABI_VERSION 8
 
 /* ---- status codes (SURVEY §8b "Error conventions") --------------------- */
 #define GNSS_OK         0
@@ -213,6 +213,12 @@ int  gnss_last_timing(const gnss_ctx *ctx, gnss_timing *out);
 /* Profiling mode: every correlator-step launch is bracketed by hipEvents (no
  * step graphs) so gnss_timing.track_kernel_ms is the sum of kernel durations. */
 int  gnss_ctx_set_profiling(gnss_ctx *ctx, int enable);
+/* Precision of the acquisition's PRN x bin x ms correlation (ABI v8; replaces nothing in
+ * the reference, whose fft/ifft/abs().^2 are MATLAB doubles, acquisition.m:56-61):
+ * fp64 = 1 (default) runs it at the reference's precision; fp64 = 0 is the fp32 fast mode
+ * (the same decisions in every parity test, SNR within 1e-3 dB). The fine-frequency FFT
+ * (acquisition.m:103-116) is fp64 in both. GNSS_EARG for other values. */
+int  gnss_ctx_set_acq_precision(gnss_ctx *ctx, int fp64);
 
 /* Device memory owned by the ctx, for callers that keep an IF record resident
  * in HBM (gnss_file.dev_data) across calls. */

@@ -1,5 +1,6 @@
 """Acquisition-only driver for profiling: BASELINE config 2 (32 PRNs, +-7 kHz / 500 Hz,
-20 ms) on a device-resident synthetic Opensky record. Args: [datalen] [freqNum]."""
+20 ms) on a device-resident synthetic Opensky record, fp64 correlation (ACQ_FP32=1: the
+fp32 fast mode). Args: [datalen] [freqNum]."""
 import importlib, os, sys, time
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -8,6 +9,7 @@ pkg = importlib.import_module("assignment-for-aae6102_gnss-sdr_amd")
 dl = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 nb = int(sys.argv[2]) if len(sys.argv) > 2 else 29
 ctx = pkg.Context(0)
+ctx.set_acq_precision(os.environ.get("ACQ_FP32") is None)  # ACQ_FP32=1: the fp32 fast mode
 file, signal, acq, track, _, _ = pkg.initParameters()
 skip = 5000
 cfg = pkg.synth.opensky(skip_ms=skip)
