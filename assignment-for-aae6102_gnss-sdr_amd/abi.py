@@ -104,6 +104,18 @@ class GnssTiming(C.Structure):
                 ("track10_channel_samples", C.c_int64)]
 
 
+class GnssVtChan(C.Structure):
+    _fields_ = [("prn", C.c_int32), ("pad", C.c_int32), ("file_ptr", C.c_int64), ("remChip", C.c_double),
+                ("remCarrPhase", C.c_double), ("codeFreq", C.c_double), ("carrFreq", C.c_double),
+                ("carrFreqBasis", C.c_double), ("oldCarrNco", C.c_double), ("oldCarrError", C.c_double)]
+
+
+class GnssVtOut(C.Structure):
+    _fields_ = [(f, C.c_double) for f in ("E_i", "E_q", "P_i", "P_q", "L_i", "L_q", "carrError", "codeError",
+                                          "carrNco", "remChip", "remCarrPhase", "codeFreq", "carrFreq")] + \
+               [("numSample", C.c_int64), ("absoluteSample", C.c_int64), ("codedelay", C.c_double)]
+
+
 class GnssSynthSv(C.Structure):
     _fields_ = [("prn", C.c_int32), ("doppler_hz", C.c_double), ("code_phase0", C.c_double),
                 ("carr_phase0", C.c_double), ("cn0_dbhz", C.c_double), ("bit_seed", C.c_uint64),
@@ -154,6 +166,14 @@ PROTOTYPES = {
                                       C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "gnss_synth_if_device": (C.c_int, [C.c_void_p, C.POINTER(GnssSynth), C.c_uint64, C.c_uint64,
                                        C.c_void_p]),
+    "gnss_tracking_vt_step": (C.c_int, [C.c_void_p, C.POINTER(GnssFile), C.POINTER(GnssSignal),
+                                        C.POINTER(GnssTrack), C.c_int32, C.c_int32, C.POINTER(GnssVtChan),
+                                        C.POINTER(C.c_double), C.POINTER(GnssVtOut)]),
+    "gnss_vt_nco_step": (C.c_int, [C.POINTER(GnssSignal), C.POINTER(GnssTrack), C.c_int32,
+                                   C.POINTER(GnssVtChan), C.c_double, C.c_double, C.c_double,
+                                   C.POINTER(GnssVtOut)]),
+    "gnss_vt_prepare": (C.c_int, [C.POINTER(GnssSignal), C.c_int32, C.POINTER(GnssVtChan), C.c_double,
+                                  C.POINTER(C.c_int32), C.POINTER(C.c_int64)]),
 }
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libgnss_mi355x.so")

@@ -1502,6 +1502,74 @@ int gnss_correlate_step(gnss_ctx* ctx, const gnss_file* file, const gnss_signal*
     return GNSS_OK;
 }
 
+}  // extern "C"
+
+// generateCAcode.m chips for the other host translation units (vt.cpp)
+void gnss::ca_chips(int prn, float* out) { generate_ca(prn, out); }
+
+extern "C" {
+
+// trackingVT_POS_updated.m:157-349, one step of n channels (include/gnss_mi355x.h): the
+// reads and replica chips sized on the host (gnss_vt_prepare), the carrier-wiped sums on
+// the GPU (vt.hip), the NCO / PLL / DLL discriminator on the host (gnss_vt_nco_step).
+int gnss_tracking_vt_step(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg, const gnss_track* tr,
+                          int32_t pdi, int32_t n, gnss_vt_chan* chans, const double* codeFreq_new,
+                          gnss_vt_out* out)
+{
+    if (!ctx || !file || !sg || !tr || !chans || !codeFreq_new || !out || n < 1 || n > GNSS_MAX_SV || pdi < 1)
+        return fail(ctx, GNSS_EARG, "bad arguments");
+    ctx->err.clear();
+    ctx->timing = gnss_timing{};
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (file->dataPrecision != 1 || file->dataType != 2)
+        return fail(ctx, GNSS_EARG, "vector tracking: int8 I/Q records only");
+    std::vector<int64_t> ns((size_t)n);
+    int64_t lo = INT64_MAX, hi = 0;
+    for (int i = 0; i < n; i++) {
+        int32_t code[3];
+        const int st = gnss_vt_prepare(sg, pdi, &chans[i], codeFreq_new[i], code, &ns[i]);
+        if (st) return fail(ctx, st, "channel %d: read size / replica index (trackingVT_POS_updated.m:161,240)", i);
+        if (chans[i].file_ptr < 0 || (chans[i].file_ptr & 1)) return fail(ctx, GNSS_EARG, "file_ptr");
+        lo = std::min(lo, chans[i].file_ptr);
+        hi = std::max(hi, chans[i].file_ptr + 2 * ns[i]);
+    }
+    if (hi > file_length(file)) return fail(ctx, GNSS_EIO, "read past the end of the IF record");
+    IfWindow w;
+    int st = stage_window(ctx, file, lo, hi, w);
+    if (st) return st;
+    std::vector<VtDesc> dh((size_t)n);
+    int64_t nmax = 0;
+    for (int i = 0; i < n; i++) {
+        dh[i] = VtDesc{chans[i].file_ptr - w.base, ns[i], chans[i].carrFreq, chans[i].remCarrPhase};
+        nmax = std::max(nmax, ns[i]);
+    }
+    const int nblk = vt_blocks(nmax);
+    DevBuf d_desc, d_part;
+    HIP_TRY(d_desc.alloc(ctx, "vt.desc", sizeof(VtDesc) * (size_t)n));
+    HIP_TRY(d_part.alloc(ctx, "vt.part", sizeof(double) * 2 * (size_t)n * nblk));
+    HIP_TRY(hipMemcpyAsync(d_desc.p, dh.data(), sizeof(VtDesc) * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+    Events ev;
+    HIP_TRY(hipEventRecord(ev.a, ctx->stream));
+    HIP_TRY(launch_vt_sums(w.ptr, 1, d_desc.as<VtDesc>(), n, sg->Fs, nblk, d_part.as<double>(), ctx->stream));
+    HIP_TRY(hipEventRecord(ev.b, ctx->stream));
+    std::vector<double> ph((size_t)2 * n * nblk);
+    HIP_TRY(hipMemcpyAsync(ph.data(), d_part.p, ph.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    ctx->timing.track_ms = ev.ms();
+    ctx->timing.track_launches = 1;
+    for (int i = 0; i < n; i++) {
+        double sI = 0.0, sQ = 0.0;
+        for (int b = 0; b < nblk; b++) {  // block order
+            sI += ph[((size_t)i * nblk + b) * 2];
+            sQ += ph[((size_t)i * nblk + b) * 2 + 1];
+        }
+        ctx->timing.track_channel_samples += ns[i];
+        const int s2 = gnss_vt_nco_step(sg, tr, pdi, &chans[i], codeFreq_new[i], sI, sQ, &out[i]);
+        if (s2) return fail(ctx, s2, "channel %d: NCO step", i);
+    }
+    return GNSS_OK;
+}
+
 int gnss_ca_code(int prn, int8_t* out1023)
 {
     if (prn < 1 || prn > 51 || !out1023) return GNSS_EARG;

@@ -369,6 +369,19 @@ struct SrcC64 {
     __device__ __forceinline__ double2 at(int64_t n) const { return p[n]; }
 };
 
+// Vector-tracking sums (vt.hip): channel i reads d.n samples from window byte d.A of `iq`
+// (int8 I/Q pairs, or int8 real with iq_pairs = 0) with carrier frequency f, phase phi0;
+// part[i][blk] = (sum I, sum Q) of block blk, nblk blocks per channel (vt_blocks).
+struct VtDesc {
+    int64_t A, n;
+    double f, phi0;
+};
+int vt_blocks(int64_t nmax);
+// generateCAcode.m's 1023 +-1 chips of `prn` (host)
+void ca_chips(int prn, float* out);
+hipError_t launch_vt_sums(const int8_t* iq, int iq_pairs, const VtDesc* desc, int nch, double Fs, int nblk,
+                          double* part, hipStream_t s);
+
 // Synthetic IF (synth.hip)
 hipError_t launch_synth_if(const gnss_synth& cfg, const float* ca, uint64_t sample0,
                            uint64_t nsamples, int8_t* dst, hipStream_t s);

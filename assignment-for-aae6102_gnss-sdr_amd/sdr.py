@@ -600,6 +600,38 @@ def ca_code(prn: int) -> np.ndarray:
     return out
 
 
+def vt_channel(prn, file_ptr, remChip, remCarrPhase, codeFreq, carrFreq, carrFreqBasis, oldCarrNco=0.0,
+               oldCarrError=0.0):
+    """A vector-tracking channel state (gnss_vt_chan): the initialisation of
+    trackingVT_POS_updated.m:108-125 (from TckResultCT at msStartTckVT in the reference)."""
+    return abi.GnssVtChan(prn=int(prn), pad=0, file_ptr=int(file_ptr), remChip=float(remChip),
+                          remCarrPhase=float(remCarrPhase), codeFreq=float(codeFreq), carrFreq=float(carrFreq),
+                          carrFreqBasis=float(carrFreqBasis), oldCarrNco=float(oldCarrNco),
+                          oldCarrError=float(oldCarrError))
+
+
+def trackingVT_step(file, signal, track, chans, codeFreq_new, pdi=1, *, ctx: Context | None = None):
+    """One step of trackingVT_POS_updated.m's tracking half (:157-349) for every channel on the
+    GPU (gnss_tracking_vt_step): `chans` = a sequence of vt_channel states, advanced in place;
+    codeFreq_new[i] = channel i's code frequency for this step, the caller's EKF prediction
+    (:211-215). Returns one dict per channel: TckResultVT(prn).*(msIndex) (:319-346)."""
+    ctx = ctx or default_context()
+    n = len(chans)
+    arr = (abi.GnssVtChan * n)(*chans)
+    cf = np.ascontiguousarray(codeFreq_new, dtype=np.float64)
+    if len(cf) != n:
+        raise ValueError("one code frequency per channel")
+    outs = (abi.GnssVtOut * n)()
+    f, keep = to_c_file(file)
+    s = to_c_signal(signal)
+    t, keep2 = to_c_track(track)
+    ctx.check(ctx.lib.gnss_tracking_vt_step(ctx.h, C.byref(f), C.byref(s), C.byref(t), int(pdi), n, arr,
+                                            cf.ctypes.data_as(C.POINTER(C.c_double)), outs))
+    for i in range(n):
+        C.memmove(C.byref(chans[i]), C.byref(arr[i]), C.sizeof(abi.GnssVtChan))
+    return [{k: getattr(o, k) for k, _ in abi.GnssVtOut._fields_} for o in outs]
+
+
 def correlate_step(file, signal, prn, pdi, remChip, codeFreq, carrierFreq, remPhase, pos_bytes,
                    taps, *, ctx: Context | None = None):
     """One trackingCT correlation step on the GPU at an arbitrary NCO state

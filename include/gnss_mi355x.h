@@ -336,6 +336,60 @@ int gnss_correlate_step(gnss_ctx *ctx, const gnss_file *file, const gnss_signal 
                         double remPhase, int64_t pos_bytes, int n_taps, const double *taps,
                         double *sums_out, int64_t *numSample_out);
 
+/* ---- trackingVT_POS_updated.m, the tracking half (ABI v8) -----------
+ * One vector-tracking step of the loop at trackingVT_POS_updated.m:157-349 for n
+ * channels: read sizing (:161), the three replica chips, the carrier wipe and sums
+ * (:217-281), the remaining code / carrier phase (:284-285), C/N0 is the caller's, the
+ * PLL (:305-311) and the DLL discriminator (:314-316). The vector half -- satellite
+ * position, iono / tropo, the predicted code frequency and the Kalman filter (:166-215,
+ * :350-420) -- stays with the caller, which passes each step's predicted code frequency.
+ * The reference's replica quirk is kept: Code(svindex, ceil_mx(1)) linear-indexes ONE
+ * element of the 3 x n matrix ceil_mx (the first sample's chip of each of the E / P / L
+ * rows, the 1025 clamp of :240-246 applied to it alone), so E / P / L = that chip times
+ * the whole sum(InphaseSignal) / sum(QuadratureSignal). Spacing = 0.7:-0.05:-0.7 (:27):
+ * E / P / L at Spacing(5) / (15) / (25) = +0.5 / 0 / -0.5. */
+typedef struct gnss_vt_chan {
+    int32_t prn;
+    int32_t pad;
+    int64_t file_ptr;       /* bytes: the fseek position of the next read (:162)          */
+    double  remChip;        /* chips (:284)                                               */
+    double  remCarrPhase;   /* rad (:285)                                                 */
+    double  codeFreq;       /* the last step's code frequency: sizes the next read (:161) */
+    double  carrFreq;       /* carrier NCO frequency (:310)                               */
+    double  carrFreqBasis;  /* (:121)                                                     */
+    double  oldCarrNco, oldCarrError;  /* PLL filter state (:307-308)                    */
+} gnss_vt_chan;
+
+/* TckResultVT(prn).*(msIndex) of one channel and step (:319-346). */
+typedef struct gnss_vt_out {
+    double  E_i, E_q, P_i, P_q, L_i, L_q;
+    double  carrError, codeError, carrNco;
+    double  remChip, remCarrPhase, codeFreq, carrFreq;
+    int64_t numSample, absoluteSample;
+    double  codedelay;
+} gnss_vt_out;
+
+/* The step on the GPU: the IF as in gnss_tracking_ct (int8 records; int16: GNSS_EARG),
+ * codeFreq_new[i] = channel i's code frequency for this step (:211-215), pdi =
+ * track.pdi. chans[] are advanced in place; out[i] = channel i's record.
+ * GNSS_EINDEX: a replica chip index MATLAB would reject; GNSS_EIO: read past EOF. */
+int gnss_tracking_vt_step(gnss_ctx *ctx, const gnss_file *file, const gnss_signal *signal,
+                          const gnss_track *track, int32_t pdi, int32_t n, gnss_vt_chan *chans,
+                          const double *codeFreq_new, gnss_vt_out *out);
+
+/* The same step's host half alone (no GPU): from the channel state, this step's code
+ * frequency and the step's carrier-wiped sums (sumI = sum(InphaseSignal), sumQ =
+ * sum(QuadratureSignal)), the record and the advanced state -- what gnss_tracking_vt_step
+ * applies after its kernels. numSample_out (may be NULL): the read size, :161. */
+int gnss_vt_nco_step(const gnss_signal *signal, const gnss_track *track, int32_t pdi,
+                     gnss_vt_chan *chan, double codeFreq_new, double sumI, double sumQ,
+                     gnss_vt_out *out);
+
+/* The replica chips and read size of a VT step (host, no GPU): code[3] = the E / P / L
+ * chip values (+-1) the quirk multiplies the sums by, *numSample = ceil(...) (:161). */
+int gnss_vt_prepare(const gnss_signal *signal, int32_t pdi, const gnss_vt_chan *chan,
+                    double codeFreq_new, int32_t code_out[3], int64_t *numSample);
+
 /* generateCAcode.m:16-64: the 1023 +-1 chips of PRN 1..51 used by the kernels. */
 int gnss_ca_code(int prn, int8_t *out1023);
 

@@ -670,6 +670,86 @@ double or_loop_filter(double outLast, double discri, double discriLast, double t
     return outLast + (tau2 / tau1) * (discri - discriLast) + discri * (T / tau1);
 }
 
+/* ---- trackingVT_POS_updated.m:157-349, the tracking half of one step ----
+ * st[0..7] = {file_ptr (bytes), remChip, remCarrPhase, codeFreq (last step), carrFreq,
+ * carrFreqBasis, oldCarrNco, oldCarrError}, advanced in place; rec[16] = {E_i, E_q, P_i, P_q,
+ * L_i, L_q, carrError, codeError, carrNco, remChip, remCarrPhase, codeFreq, carrFreq, numSample,
+ * absoluteSample, codedelay}. iq = the int8 I/Q record from byte 0 (NULL: sums given in
+ * sums[2] = {sum I, sum Q}, the replay of a recorded step); ca = the PRN's 1023 chips.
+ * Returns GNSS_* (EINDEX: a replica index MATLAB rejects; EIO: read past nbytes). */
+static double or_vt_spacing(int i1)
+{
+    or_colon c;
+    or_colon_init(&c, 0.7, -0.05, -0.7); /* Spacing = 0.7:-0.05:-0.7 (:27) */
+    return or_colon_elem(&c, i1 - 1);
+}
+
+int or_vt_step(const int8_t *iq, int64_t nbytes, double *st, double codeFreq_new, const int8_t *ca,
+               double Fs, double codelength, double ms, int pdi, double tau1carr, double tau2carr,
+               const double *sums, double *rec)
+{
+    const double remChip0 = st[1];
+    const int64_t n = (int64_t)ceil((codelength * pdi - remChip0) / (st[3] / Fs)); /* :161 */
+    if (n < 1) return GNSS_EINDEX;
+    const int64_t ptr = (int64_t)st[0];
+    /* Code = [CA(end) repmat(CA,1,pdi) CA(1)] (:110): ceil_mx(idx) = the first element of
+     * row idx = ceil(0 + Spacing + remChip) + 1, the 1025 clamp on it alone (:218-249) */
+    int code[3];
+    const int sp[3] = {5, 15, 25};
+    for (int s = 0; s < 3; s++) {
+        double j = ceil((0 + or_vt_spacing(sp[s])) + remChip0) + 1;
+        if (j > 1025) j = 1025;
+        const int64_t len = 1023 * (int64_t)pdi + 2, ji = (int64_t)j;
+        if (ji < 1 || ji > len) return GNSS_EINDEX;
+        code[s] = ji == 1 ? ca[1022] : ji == len ? ca[0] : ca[(ji - 2) % 1023];
+    }
+    double sI, sQ;
+    if (iq) {
+        if (ptr < 0 || ptr + 2 * n > nbytes) return GNSS_EIO;
+        long double aI = 0, aQ = 0;
+        for (int64_t k = 0; k < n; k++) {
+            /* Wave = (2*pi*(carrFreq .* CarrTime)) + remCarrPhase, CarrTime = (0:n)/Fs (:275-276) */
+            const double W = TWO_PI * (st[4] * ((double)k / Fs)) + st[2];
+            const double xr = iq[ptr + 2 * k], xi = iq[ptr + 2 * k + 1];
+            aI += xr * sin(W) + xi * cos(W); /* imag(rawsignal .* carrsig) (:279) */
+            aQ += xr * cos(W) - xi * sin(W); /* real(...) (:280) */
+        }
+        sI = (double)aI;
+        sQ = (double)aQ;
+    } else {
+        sI = sums[0];
+        sQ = sums[1];
+    }
+    const double cps = codeFreq_new / Fs; /* :218 */
+    or_colon col;
+    const double sp15 = or_vt_spacing(15);
+    or_colon_init(&col, (0 + sp15) + remChip0, cps, ((double)(n - 1) * cps + sp15) + remChip0);
+    if (col.n != n - 1) return GNSS_EINDEX;
+    const double remChip = (or_colon_elem(&col, n - 1) + cps) - 1023 * pdi;          /* :284 */
+    const double remCarrPhase = fmod(TWO_PI * (st[4] * ((double)n / Fs)) + st[2], TWO_PI); /* :285 */
+    const double Ei = code[0] * sI, Eq = code[0] * sQ, Pi = code[1] * sI, Pq = code[1] * sQ;
+    const double Li = code[2] * sI, Lq = code[2] * sQ;
+    const double carrError = atan(Pq / Pi) / (2.0 * M_PI);                              /* :306 */
+    const double carrNco = st[6] + (tau2carr / tau1carr) * (carrError - st[7]) +
+                           carrError * (pdi * 1e-3 / tau1carr);                         /* :307 */
+    const double carrFreq = st[5] + carrNco;                                            /* :310 */
+    const double E = sqrt(Ei * Ei + Eq * Eq), L = sqrt(Li * Li + Lq * Lq);
+    const double codeError = -0.5 * (E - L) / (E + L);                                  /* :316 */
+    const int64_t absS = ptr + 2 * n;                                                   /* ftell */
+    const double r[16] = {Ei, Eq, Pi, Pq, Li, Lq, carrError, codeError, carrNco, remChip, remCarrPhase,
+                          codeFreq_new, carrFreq, (double)n, (double)absS,
+                          fmod((double)absS / 2, Fs * ms)};                             /* :347 */
+    memcpy(rec, r, sizeof r);
+    st[0] = (double)absS;
+    st[1] = remChip;
+    st[2] = remCarrPhase;
+    st[3] = codeFreq_new;
+    st[4] = carrFreq;
+    st[6] = carrNco;
+    st[7] = carrError;
+    return GNSS_OK;
+}
+
 typedef struct chan_state {
     double remChip, remPhase, remSample;
     double carrier_output, carrier_outputLast, PLLdiscriLast;

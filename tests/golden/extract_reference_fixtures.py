@@ -16,6 +16,10 @@ are data (inputs + expected outputs), committed under tests/golden/:
                                arrays) and sbf_Opensky_90.mat (nav1, sfb1); and the 40-s
                                run's eph/sbf_Opensky_40.mat (its P_i = the first 1000 +
                                countinx + 40000 values of the same series).
+  ref_tckRstVT_Opensky.npz     subset of SDR_MATLAB-main/tckRstVT_Opensky_updated.mat (output of
+                               trackingVT_POS_updated.m on the real Opensky IF, 5 PRNs x 5000
+                               1-ms steps): the correlator outputs and the NCO / loop state of
+                               steps 1..1200 (the vector-tracking NCO replay, tests/test_vt_kat.py).
 
 Only scipy.io.loadmat (a MAT-v5 parser that executes nothing) is used.
 """
@@ -62,6 +66,21 @@ def main():
                               for p in prns])
     np.savez_compressed(os.path.join(HERE, "ref_tckRstCT_10ms_Opensky.npz"), **arrs)
     print("prns", prns, "wrote fixtures")
+    vt_fixture()
+
+
+def vt_fixture(nsteps=1200):
+    d = sio.loadmat(os.path.join(REF, "tckRstVT_Opensky_updated.mat"), squeeze_me=True,
+                    struct_as_record=False)
+    T = d["TckResultVT"]
+    prns = [i + 1 for i, t in enumerate(T) if np.asarray(getattr(t, "P_i", np.array([]))).size > 0]
+    fields = ["E_i", "E_q", "P_i", "P_q", "L_i", "L_q", "carrError", "codeError", "remChip",
+              "remCarrPhase", "codeFreq", "carrFreq", "carrNco", "absoluteSample", "codedelay"]
+    arrs = {"prns": np.array(prns)}
+    for fld in fields:
+        arrs[fld] = np.stack([np.asarray(getattr(T[p - 1], fld), dtype=np.float64)[:nsteps] for p in prns])
+    np.savez_compressed(os.path.join(HERE, "ref_tckRstVT_Opensky.npz"), **arrs)
+    print("VT prns", prns)
 
 
 def fig_series(path):
