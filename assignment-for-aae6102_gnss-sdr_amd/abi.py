@@ -101,7 +101,8 @@ class GnssTiming(C.Structure):
                 ("track_launches", C.c_int64), ("track_channel_samples", C.c_int64),
                 ("acq_hypothesis_samples", C.c_int64), ("h2d_ms", C.c_double),
                 ("track10_kernel_ms", C.c_double), ("track10_launches", C.c_int64),
-                ("track10_channel_samples", C.c_int64)]
+                ("track10_channel_samples", C.c_int64), ("h2d_bytes", C.c_int64),
+                ("track_segments", C.c_int64)]
 
 
 class GnssVtChan(C.Structure):
@@ -137,6 +138,7 @@ PROTOTYPES = {
     "gnss_last_timing": (C.c_int, [C.c_void_p, C.POINTER(GnssTiming)]),
     "gnss_ctx_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
     "gnss_ctx_set_acq_precision": (C.c_int, [C.c_void_p, C.c_int]),
+    "gnss_ctx_set_window": (C.c_int, [C.c_void_p, C.c_uint64]),
     "gnss_dev_alloc": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
     "gnss_dev_free": (C.c_int, [C.c_void_p, C.c_void_p]),
     "gnss_dev_upload": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),

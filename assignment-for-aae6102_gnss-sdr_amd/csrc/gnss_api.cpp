@@ -49,6 +49,7 @@ struct gnss_ctx {
     int64_t acq_tw_S = 0;  // the acquisition twiddle tables in the pool are for this S
     int acq_tw_dbl = -1;   //   ... and this precision
     int acq_fp64 = 1;      // acquisition correlation precision: 1 = fp64 (reference), 0 = fp32
+    uint64_t window = 0;   // trackingCT: max IF bytes resident in HBM (0: the whole read range)
 };
 
 namespace {
@@ -180,6 +181,63 @@ struct IfWindow {
     int64_t base = 0, len = 0;
 };
 
+// The file bytes [lo, hi) into device memory dst (returns once they have landed). Streaming staging (trackingCT.m:84-93 reads each step's block from the file;
+// here windows are staged whole): chunks of kStageChunk bytes through two pinned host buffers
+// of the context -- the disk read (or host copy) of chunk i+1 runs while the DMA engine moves
+// chunk i into HBM; a buffer is refilled only after its previous DMA has completed.
+int stage_into(gnss_ctx* ctx, const gnss_file* f, int64_t lo, int64_t hi, int8_t* dst)
+{
+    const int64_t n = hi - lo;
+    if (n <= 0) return GNSS_OK;
+    Events ev;
+    HIP_TRY(hipEventRecord(ev.a, ctx->stream));
+    constexpr int64_t kStageChunk = (int64_t)64 << 20;
+    int8_t* pb[2] = {pinned_buffer<int8_t>(ctx, "stage.0", (size_t)kStageChunk),
+                     pinned_buffer<int8_t>(ctx, "stage.1", (size_t)kStageChunk)};
+    if (!pb[0] || !pb[1]) return fail(ctx, GNSS_EDEVICE, "pinned staging buffers");
+    hipEvent_t done[2] = {nullptr, nullptr};
+    HIP_TRY(hipEventCreateWithFlags(&done[0], hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&done[1], hipEventDisableTiming));
+    struct EvGuard {
+        hipEvent_t* e;
+        ~EvGuard() { (void)hipEventDestroy(e[0]); (void)hipEventDestroy(e[1]); }
+    } guard{done};
+    int fd = -1;
+    if (!f->data) {
+        fd = open(f->path, O_RDONLY);
+        if (fd < 0) return fail(ctx, GNSS_EIO, "cannot open '%s'", f->path);
+    }
+    int64_t off = 0;
+    for (int i = 0; off < n; i++, off += kStageChunk) {
+        const int64_t len = std::min(kStageChunk, n - off);
+        int8_t* buf = pb[i & 1];
+        if (i >= 2) HIP_TRY(hipEventSynchronize(done[i & 1]));  // its last DMA has drained
+        if (f->data) {
+            memcpy(buf, f->data + lo + off, (size_t)len);
+        } else {
+            int64_t got = 0;
+            while (got < len) {
+                const ssize_t r = pread(fd, buf + got, (size_t)(len - got), lo + off + got);
+                if (r <= 0) break;
+                got += r;
+            }
+            if (got != len) {
+                close(fd);
+                (void)hipStreamSynchronize(ctx->stream);
+                return fail(ctx, GNSS_EIO, "short read of '%s'", f->path);
+            }
+        }
+        HIP_TRY(hipMemcpyAsync(dst + off, buf, (size_t)len, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipEventRecord(done[i & 1], ctx->stream));
+    }
+    if (fd >= 0) close(fd);
+    ctx->timing.h2d_bytes += n;
+    HIP_TRY(hipEventRecord(ev.b, ctx->stream));
+    HIP_TRY(hipEventSynchronize(ev.b));
+    ctx->timing.h2d_ms += ev.ms();
+    return GNSS_OK;
+}
+
 int stage_window(gnss_ctx* ctx, const gnss_file* f, int64_t lo, int64_t hi, IfWindow& w)
 {
     const int64_t flen = file_length(f);
@@ -197,28 +255,8 @@ int stage_window(gnss_ctx* ctx, const gnss_file* f, int64_t lo, int64_t hi, IfWi
     }
     const int64_t n = hi - lo;
     HIP_TRY(w.own.alloc((size_t)n + 64));
-    Events ev;
-    HIP_TRY(hipEventRecord(ev.a, ctx->stream));
-    if (f->data) {
-        HIP_TRY(hipMemcpyAsync(w.own.p, f->data + lo, (size_t)n, hipMemcpyHostToDevice, ctx->stream));
-    } else {
-        std::vector<int8_t> tmp((size_t)n);
-        int fd = open(f->path, O_RDONLY);
-        if (fd < 0) return fail(ctx, GNSS_EIO, "cannot open '%s'", f->path);
-        int64_t got = 0;
-        while (got < n) {
-            ssize_t r = pread(fd, tmp.data() + got, (size_t)(n - got), lo + got);
-            if (r <= 0) break;
-            got += r;
-        }
-        close(fd);
-        if (got != n) return fail(ctx, GNSS_EIO, "short read of '%s'", f->path);
-        HIP_TRY(hipMemcpyAsync(w.own.p, tmp.data(), (size_t)n, hipMemcpyHostToDevice, ctx->stream));
-        HIP_TRY(hipStreamSynchronize(ctx->stream));
-    }
-    HIP_TRY(hipEventRecord(ev.b, ctx->stream));
-    HIP_TRY(hipEventSynchronize(ev.b));
-    ctx->timing.h2d_ms += ev.ms();
+    const int st = stage_into(ctx, f, lo, hi, w.own.as<int8_t>());
+    if (st) return st;
     w.ptr = w.own.as<int8_t>();
     w.base = lo;
     w.len = n;
@@ -500,6 +538,13 @@ int gnss_ctx_set_profiling(gnss_ctx* ctx, int enable)
 {
     if (!ctx) return GNSS_EARG;
     ctx->profiling = enable;
+    return GNSS_OK;
+}
+
+int gnss_ctx_set_window(gnss_ctx* ctx, uint64_t bytes)
+{
+    if (!ctx) return GNSS_EARG;
+    ctx->window = bytes;
     return GNSS_OK;
 }
 
@@ -913,7 +958,7 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
     // IF window resident in HBM: from the earliest channel start to the latest
     // possible phase-C end (countinx <= 18, numSample within 1%)
     const int64_t bps = file->dataPrecision * file->dataType;
-    int64_t lo = INT64_MAX, hi = 0;
+    int64_t lo = INT64_MAX, hi = 0, hiA = 0;  // hiA: the end of the 1-ms phases' reads
     for (int c : chans) {
         const int64_t cd = acq->codedelay[c];
         lo = std::min(lo, (S - cd + 1 + file->skip * S) * bps);
@@ -932,13 +977,29 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
         const int64_t c0 = (S - cd + 1 + (file->skip + N1 + 18) * S) * bps;
         const int64_t a1 = (S - cd + 1 + file->skip * S) * bps + (int64_t)((N1 + 18) * S * 1.01 + 64) * bps;
         hi = std::max(hi, std::max(c0 + (int64_t)(n10 * 10 * S * 1.01 + 4096) * bps, a1));
+        hiA = std::max(hiA, a1);
     }
     P.file_len = file_length(file);
     if (P.file_len < 0) return fail(ctx, GNSS_EIO, "cannot open IF record");
     IfWindow w;
     lo &= ~(int64_t)31;  // whole 8-sample groups of any format
-    int st = stage_window(ctx, file, lo, hi, w);
-    if (st) return st;
+    // Streaming (gnss_ctx_set_window): with a window budget below the read range, the 1-ms
+    // phases' range is staged first and the 10-ms phase in segments, each staged (through the
+    // pinned double buffer) into the same HBM window before its launch
+    const bool seg = ctx->window > 0 && !file->dev_data && !pos && !gv && prec == 1 && dtyp == 2 && n10 > 0 &&
+                     (uint64_t)(hi - lo) > ctx->window;
+    int st;
+    if (seg) {
+        if ((uint64_t)(hiA - lo) > ctx->window || ctx->window < (uint64_t)(12 * S * bps * 1.01 + 8192))
+            return fail(ctx, GNSS_EARG, "window budget below the 1-ms phases' span");
+        HIP_TRY(w.own.alloc(ctx->window + 64));
+        w.ptr = w.own.as<int8_t>();
+        w.base = lo;
+        w.len = std::min<int64_t>(hiA, P.file_len) - lo;
+        if ((st = stage_into(ctx, file, w.base, w.base + w.len, w.own.as<int8_t>()))) return st;
+    } else if ((st = stage_window(ctx, file, lo, hi, w))) {
+        return st;
+    }
     const int8_t* iq_dev = w.ptr;
     P.buf_base = w.base;
     P.buf_len = w.len;
@@ -1240,7 +1301,45 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
         if ((st = run_steps(1, cxmax))) return st;
         HIP_TRY(launch_track_phase_c_init(P, B, TD, file->skip, ctx->stream));
         // phase C
-        if ((st = run_steps(10, n10))) return st;
+        if (!seg) {
+            if ((st = run_steps(10, n10))) return st;
+        } else {
+            // segments: from the channels' file positions, as many 10-ms steps as the window
+            // holds (numSample <= 10*S*1.01 + 64 per step, the kernels' own bound), staged
+            // into the window before their launch (the stream orders the previous launch's
+            // reads before the new bytes land)
+            const int64_t per_step = (int64_t)(10 * S * 1.01 + 64) * bps;
+            for (int done = 0; done < n10;) {
+                HIP_TRY(hipMemcpyAsync(chh.data(), d_chan.p, sizeof(TrkChan) * nch, hipMemcpyDeviceToHost,
+                                       ctx->stream));
+                HIP_TRY(hipStreamSynchronize(ctx->stream));
+                int64_t pmin = INT64_MAX, pmax = 0;
+                for (auto& t : chh) {
+                    if (t.status != GNSS_OK) continue;
+                    pmin = std::min(pmin, t.pos);
+                    pmax = std::max(pmax, t.pos);
+                }
+                if (pmin == INT64_MAX) break;  // no channel left
+                const int64_t base = (pmin & ~(int64_t)31);
+                const int64_t room = (int64_t)ctx->window - (pmax - base) - 4096;
+                int k = (int)std::min<int64_t>(n10 - done, room / per_step);
+                if (k < 1) return fail(ctx, GNSS_EARG, "window budget below one 10-ms step of every channel");
+                const int64_t end = std::min<int64_t>(P.file_len, pmax + (int64_t)k * per_step + 4096);
+                if ((st = stage_into(ctx, file, base, end, w.own.as<int8_t>()))) return st;
+                P.buf_base = base;
+                P.buf_len = end - base;
+                B.iq = w.own.as<int8_t>();
+                HIP_TRY(hipMemcpyAsync(d_args.p, &P, sizeof(TrkParams), hipMemcpyHostToDevice, ctx->stream));
+                HIP_TRY(hipMemcpyAsync(static_cast<char*>(d_args.p) + sizeof(TrkParams), &B, sizeof(TrkBuffers),
+                                       hipMemcpyHostToDevice, ctx->stream));
+                // the pending descriptors were checked against the previous window: rebuild
+                // them from the channels' state (the same fields, the new staging check)
+                HIP_TRY(launch_track_prepare(P, B, TD, 10, 1, ctx->stream));
+                if ((st = run_steps(10, k))) return st;
+                done += k;
+                ctx->timing.track_segments += 1;
+            }
+        }
     }
     HIP_TRY(hipEventRecord(e_all.b, ctx->stream));
     HIP_TRY(hipEventSynchronize(e_all.b));

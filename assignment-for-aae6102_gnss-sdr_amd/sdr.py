@@ -92,6 +92,11 @@ class Context:
     def set_profiling(self, on: bool):
         self.check(self.lib.gnss_ctx_set_profiling(self.h, 1 if on else 0))
 
+    def set_window(self, nbytes: int):
+        """Streaming: at most nbytes of IF resident in HBM per trackingCT call (0: the whole
+        read range), gnss_ctx_set_window."""
+        self.check(self.lib.gnss_ctx_set_window(self.h, int(nbytes)))
+
     def set_acq_precision(self, fp64: bool):
         """Acquisition correlation at fp64 (the reference's precision, default) or the fp32
         fast mode (gnss_ctx_set_acq_precision)."""

@@ -197,6 +197,8 @@ typedef struct gnss_timing {
     double  track10_kernel_ms;
     int64_t track10_launches;
     int64_t track10_channel_samples;
+    int64_t h2d_bytes;        /* bytes staged host/disk -> HBM in h2d_ms (ABI v8)  */
+    int64_t track_segments;   /* 10-ms phase segments staged (gnss_ctx_set_window) */
 } gnss_timing;
 
 typedef struct gnss_ctx gnss_ctx;
@@ -219,6 +221,14 @@ int  gnss_ctx_set_profiling(gnss_ctx *ctx, int enable);
  * (the same decisions in every parity test, SNR within 1e-3 dB). The fine-frequency FFT
  * (acquisition.m:103-116) is fp64 in both. GNSS_EARG for other values. */
 int  gnss_ctx_set_acq_precision(gnss_ctx *ctx, int fp64);
+/* Streaming (ABI v8): at most `bytes` of IF resident in HBM per trackingCT call (0 = the
+ * call's whole read range, the default). A record read from `path` or host `data` whose read
+ * range exceeds it is staged in windows: the 1-ms phases' range first, then the 10-ms phase
+ * (trackingCT.m:377-525) in segments of as many steps as the window holds, each staged through
+ * the context's pinned double buffer before its launch (trackingCT.m:416-426 reads every step
+ * from the file; the outputs are bit-identical to the unsegmented call). GNSS_EARG from the
+ * call if the budget cannot hold the 1-ms phases' span or one 10-ms step of every channel. */
+int  gnss_ctx_set_window(gnss_ctx *ctx, uint64_t bytes);
 
 /* Device memory owned by the ctx, for callers that keep an IF record resident
  * in HBM (gnss_file.dev_data) across calls. */

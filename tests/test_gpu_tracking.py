@@ -271,3 +271,32 @@ def test_config5_shape_32_channels_11_taps(pkg, po, ctx):
     r = po.trackingCT(file, signal, track, A, taps=taps, raw=True)
     assert r.status == 0
     compare(pkg, g, r)
+
+
+@pytest.mark.parametrize("route", ["host", "path"])
+def test_streamed_windows_equal_resident(pkg, ctx, opensky_short, tmp_path, route):
+    """Streaming (gnss_ctx_set_window): a 100 MB HBM window over a ~200 MB read range -- the
+    1-ms phases' range staged first, the 10-ms phase in segments staged through the pinned
+    double buffer -- gives the same bits as the whole range resident, from host memory and
+    from the file (trackingCT.m:84-93,416-426 read every step from the file)."""
+    skip, cfg, data = opensky_short
+    file, signal, acq, track = params(pkg, skip, data)
+    track.msToProcessCT_1ms, track.msToProcessCT_10ms = 700, 1000
+    A = acquired_of([16, 26, 31], [26051, 57908, 39064], [4579675.0, 4581800.0, 4581025.0])
+    g0 = pkg.trackingCT(file, signal, track, A, ctx=ctx, raw=True)
+    if route == "path":
+        p = tmp_path / "if.bin"
+        p.write_bytes(np.asarray(data, dtype=np.int8).tobytes())
+        file.data, file.fileRoute = None, str(p)
+    ctx.set_window(100 * 1000 * 1000)
+    try:
+        g1 = pkg.trackingCT(file, signal, track, A, ctx=ctx, raw=True)
+        t = ctx.timing()
+    finally:
+        ctx.set_window(0)
+    assert t["track_segments"] >= 2 and t["h2d_bytes"] > 0
+    assert np.array_equal(g0.len, g1.len) and np.array_equal(g0.countinx, g1.countinx)
+    for c in range(3):
+        n = int(g0.len[c])
+        assert np.array_equal(g0.rec[c, :, :n], g1.rec[c, :, :n]), c
+    assert np.array_equal(g0.CN0, g1.CN0)
