@@ -200,8 +200,8 @@ __device__ __forceinline__ void dft_prime(V (&v)[P], Put put)
 // ---- 2000-point Stockham in LDS (one buffer: every stage reads to registers, syncs,
 // writes): radices 5, 5, 5, 16 (Ns = 1, 5, 25, 125), natural order at the end.
 // tw[m] = e^{-j 2 pi m / 2000}. Callers sync after filling `a`.
-template <int DIR, int NS, class V>
-__device__ __forceinline__ void stage5(V* a, const V* tw, int tid)
+template <int DIR, int NS, class V, class TW>
+__device__ __forceinline__ void stage5(V* a, const TW& tw, int tid)
 {
     constexpr int NB = kRow / 5, PER = (NB + kRowThreads - 1) / kRowThreads;
     V v[PER][5];
@@ -230,8 +230,8 @@ __device__ __forceinline__ void stage5(V* a, const V* tw, int tid)
     __syncthreads();
 }
 
-template <int DIR, class V>
-__device__ __forceinline__ void fft2000(V* a, const V* tw, int tid)
+template <int DIR, class V, class TW>
+__device__ __forceinline__ void fft2000(V* a, const TW& tw, int tid)
 {
     stage5<DIR, 1>(a, tw, tid);
     stage5<DIR, 5>(a, tw, tid);
@@ -296,8 +296,8 @@ template <int R, int DIR, class V> __device__ __forceinline__ void dft_r(V (&v)[
 
 // ---- BATCH 2000-point transforms side by side in LDS (transform b at a + b*2000), one
 // radix-R Stockham stage; every butterfly of the batch is spread over the block's threads.
-template <int DIR, int R, int NS, int BATCH, class V>
-__device__ __forceinline__ void stage_batch(V* a, const V* tw, int tid)
+template <int DIR, int R, int NS, int BATCH, class V, class TW>
+__device__ __forceinline__ void stage_batch(V* a, const TW& tw, int tid)
 {
     constexpr int NB = kRow / R, TOT = NB * BATCH, PER = (TOT + kRowThreads - 1) / kRowThreads;
     V v[PER][R];
@@ -329,8 +329,8 @@ __device__ __forceinline__ void stage_batch(V* a, const V* tw, int tid)
 }
 
 // 2000 = 10 x 10 x 20: three LDS passes per batch of transforms (natural order at the end).
-template <int DIR, int BATCH, class V>
-__device__ __forceinline__ void fft2000_batch(V* a, const V* tw, int tid)
+template <int DIR, int BATCH, class V, class TW>
+__device__ __forceinline__ void fft2000_batch(V* a, const TW& tw, int tid)
 {
     stage_batch<DIR, 10, 1, BATCH>(a, tw, tid);
     stage_batch<DIR, 10, 10, BATCH>(a, tw, tid);
@@ -495,10 +495,12 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel(
     }
 }
 
-// The fp64 inverse rows: the same transform and sum order, one ms per pass (two fp64
-// rows and their table would take 96 KB of LDS), the next ms's row prefetched into
-// registers while this one transforms. (Twiddles read from the global table instead of
-// this LDS copy: 634 -> 721 us per batch, dropped.)
+// The fp64 inverse rows: the same sum order, one ms per pass (two fp64 rows and their
+// table would take 96 KB of LDS), the next ms's row prefetched into registers while this
+// one transforms, radices 10-10-20 (three LDS passes; 5-5-5-16: correlation 19.7 ->
+// 18.5 ms at config 2). Measured and dropped: twiddles from the global table (634 -> 721
+// us per batch); a 90-entry split table w^m = w^(m mod 50) w^(50 (m div 50)) (33 KB of
+// LDS, twice the blocks per CU; the extra complex product per twiddle: 19.7 -> 29.0 ms).
 template <int P>
 __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel_f64(
     const double2* __restrict__ A, int nprn, int datalen, int first_pair, double scale,
@@ -529,7 +531,7 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel_f64(
         }
         if (idx + 1 < datalen) ld(idx + 1);
         __syncthreads();
-        fft2000<1>(s_a, s_tw, tid);
+        fft2000_batch<1, 1>(s_a, s_tw, tid);  // (radices 10, 10, 20)
 #pragma unroll
         for (int i = 0; i < Q; i++) {  // the ms in order (acquisition.m:53-61)
             const int t1 = tid + i * kRowThreads, t = t1 < kRow ? t1 : kRow - 1;

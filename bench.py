@@ -34,7 +34,7 @@ pkg = importlib.import_module("assignment-for-aae6102_gnss-sdr_amd")
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SAMPLES_PER_MS = 58000  # Opensky Fs 58 MHz
-TRAFFIC_FILE = "traffic_r01.json"  # PMC bytes per launch of the dominant kernel (this round's pass)
+TRAFFIC_FILE = "traffic_r02.json"  # PMC bytes per launch of the dominant kernel (this round's pass)
 
 
 def parse():

@@ -1,0 +1,27 @@
+"""SQ / TCC counters per kernel from rocprofv3 --pmc passes (counter_collection.csv).
+Median per dispatch of every counter found, for each kernel substring given.
+Args: out.json dir [dir ...] -- ksub [ksub ...]"""
+import csv, glob, json, sys
+import numpy as np
+
+args = sys.argv[1:]
+out_path, rest = args[0], args[1:]
+cut = rest.index("--")
+dirs, ksubs = rest[:cut], rest[cut + 1:]
+res = {}
+for k in ksubs:
+    per = {}
+    for d in dirs:
+        for p in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
+            for r in csv.DictReader(open(p)):
+                if k not in r.get("Kernel_Name", ""):
+                    continue
+                key = (p, r.get("Dispatch_Id", r.get("Correlation_Id")))
+                c = r.get("Counter_Name")
+                per.setdefault(c, {}).setdefault(key, 0.0)
+                per[c][key] += float(r["Counter_Value"])
+    res[k] = {c: {"median_per_dispatch": float(np.median(list(v.values()))), "dispatches": len(v)}
+              for c, v in sorted(per.items())}
+json.dump(res, open(out_path, "w"), indent=1)
+for k, v in res.items():
+    print(k, {c: round(x["median_per_dispatch"], 1) for c, x in v.items()})
