@@ -337,6 +337,16 @@ __device__ __forceinline__ void fft2000_batch(V* a, const TW& tw, int tid)
     stage_batch<DIR, 20, 100, BATCH>(a, tw, tid);
 }
 
+// 2000 = 20 x 10 x 10 with the radix-20 pass first (Ns = 1: no twiddles), so the widest
+// butterfly never holds twiddles in registers (the fp64 row kernel stays within 256 VGPRs)
+template <int DIR, int BATCH, class V, class TW>
+__device__ __forceinline__ void fft2000_batch_r20first(V* a, const TW& tw, int tid)
+{
+    stage_batch<DIR, 20, 1, BATCH>(a, tw, tid);
+    stage_batch<DIR, 10, 20, BATCH>(a, tw, tid);
+    stage_batch<DIR, 10, 200, BATCH>(a, tw, tid);
+}
+
 template <class V>
 __device__ __forceinline__ void load_row_tw(V* s_tw, const V* tw_row, int tid)
 {
@@ -427,8 +437,11 @@ __global__ __launch_bounds__(kColThreads) void inv_cols_kernel(
     for (int i = 0; i < P; i++) v[i] = cmulc(c[(int64_t)i * kRow], x[(int64_t)i * kRow]);
     V* a = A + (int64_t)t * P * kRow + k1;
     const V* tw = tw_col + k1;
+    // A is streamed once (to the row pass): non-temporal stores keep C and X in the caches
     dft_prime<P, 1>(v, [&](int k, V y) {
-        a[(int64_t)k * kRow] = cmulc(y, tw[(int64_t)k * kRow]);
+        const V z = cmulc(y, tw[(int64_t)k * kRow]);
+        __builtin_nontemporal_store(z.x, &a[(int64_t)k * kRow].x);
+        __builtin_nontemporal_store(z.y, &a[(int64_t)k * kRow].y);
     });
 }
 
@@ -511,27 +524,30 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel_f64(
     const int tau2 = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
     load_row_tw(s_tw, tw_row, tid);
     double acc[Q];
-    double2 nx[Q];
 #pragma unroll
     for (int i = 0; i < Q; i++) acc[i] = 0.0;
     const double2* src = A + ((int64_t)g * datalen * P + tau2) * kRow;
-    auto ld = [&](int idx) {
-#pragma unroll
-        for (int i = 0; i < Q; i++) {
-            const int e = tid + i * kRowThreads;
-            nx[i] = src[(int64_t)idx * P * kRow + (e < kRow ? e : kRow - 1)];
-        }
-    };
-    ld(0);
+    // the next ms's row in named registers (an indexed array here is kept in scratch)
+    static_assert(Q == 8, "row prefetch is written for 8 values per lane");
+    const int e7 = tid + 7 * kRowThreads < kRow ? tid + 7 * kRowThreads : kRow - 1;
+    double2 n0, n1, n2, n3, n4, n5, n6, n7;
+#define GNSS_LD(IDX)                                                                         \
+    {                                                                                        \
+        const double2* r = src + (int64_t)(IDX) * P * kRow + tid;                              \
+        n0 = r[0]; n1 = r[kRowThreads]; n2 = r[2 * kRowThreads]; n3 = r[3 * kRowThreads];     \
+        n4 = r[4 * kRowThreads]; n5 = r[5 * kRowThreads]; n6 = r[6 * kRowThreads];             \
+        n7 = r[e7 - tid];                                                                    \
+    }
+    GNSS_LD(0)
     for (int idx = 0; idx < datalen; idx++) {
-#pragma unroll
-        for (int i = 0; i < Q; i++) {
-            const int e = tid + i * kRowThreads;
-            if (e < kRow) s_a[e] = nx[i];
-        }
-        if (idx + 1 < datalen) ld(idx + 1);
+        s_a[tid] = n0; s_a[tid + kRowThreads] = n1; s_a[tid + 2 * kRowThreads] = n2;
+        s_a[tid + 3 * kRowThreads] = n3; s_a[tid + 4 * kRowThreads] = n4;
+        s_a[tid + 5 * kRowThreads] = n5; s_a[tid + 6 * kRowThreads] = n6;
+        if (tid + 7 * kRowThreads < kRow) s_a[tid + 7 * kRowThreads] = n7;
+        if (idx + 1 < datalen) GNSS_LD(idx + 1)
+#undef GNSS_LD
         __syncthreads();
-        fft2000_batch<1, 1>(s_a, s_tw, tid);  // (radices 10, 10, 20)
+        fft2000_batch_r20first<1, 1>(s_a, s_tw, tid);
 #pragma unroll
         for (int i = 0; i < Q; i++) {  // the ms in order (acquisition.m:53-61)
             const int t1 = tid + i * kRowThreads, t = t1 < kRow ? t1 : kRow - 1;
