@@ -347,6 +347,15 @@ __device__ __forceinline__ void fft2000_batch_r20first(V* a, const TW& tw, int t
     stage_batch<DIR, 10, 200, BATCH>(a, tw, tid);
 }
 
+// a value read once (the column pass's intermediate): non-temporal load
+__device__ __forceinline__ double2 ld_nt(const double2* p)
+{
+    double2 v;
+    v.x = __builtin_nontemporal_load(&p->x);
+    v.y = __builtin_nontemporal_load(&p->y);
+    return v;
+}
+
 template <class V>
 __device__ __forceinline__ void load_row_tw(V* s_tw, const V* tw_row, int tid)
 {
@@ -471,7 +480,13 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel(
     auto ld = [&](int idx, int i) {
         const int e = tid + i * kRowThreads;
         const int r = idx < datalen ? idx : datalen - 1;
-        return src[(int64_t)r * P * V4 + (e < V4 ? e : V4 - 1)];
+        const float4* q = src + (int64_t)r * P * V4 + (e < V4 ? e : V4 - 1);
+        float4 v;  // (read once: non-temporal)
+        v.x = __builtin_nontemporal_load(&q->x);
+        v.y = __builtin_nontemporal_load(&q->y);
+        v.z = __builtin_nontemporal_load(&q->z);
+        v.w = __builtin_nontemporal_load(&q->w);
+        return v;
     };
     auto st = [&](int h, int i, float4 v) {
         const int e = tid + i * kRowThreads;
@@ -534,9 +549,9 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel_f64(
 #define GNSS_LD(IDX)                                                                         \
     {                                                                                        \
         const double2* r = src + (int64_t)(IDX) * P * kRow + tid;                              \
-        n0 = r[0]; n1 = r[kRowThreads]; n2 = r[2 * kRowThreads]; n3 = r[3 * kRowThreads];     \
-        n4 = r[4 * kRowThreads]; n5 = r[5 * kRowThreads]; n6 = r[6 * kRowThreads];             \
-        n7 = r[e7 - tid];                                                                    \
+        n0 = ld_nt(r); n1 = ld_nt(r + kRowThreads); n2 = ld_nt(r + 2 * kRowThreads);           \
+        n3 = ld_nt(r + 3 * kRowThreads); n4 = ld_nt(r + 4 * kRowThreads);                      \
+        n5 = ld_nt(r + 5 * kRowThreads); n6 = ld_nt(r + 6 * kRowThreads); n7 = ld_nt(r + e7 - tid); \
     }
     GNSS_LD(0)
     for (int idx = 0; idx < datalen; idx++) {
