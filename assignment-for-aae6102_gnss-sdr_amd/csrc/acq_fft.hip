@@ -595,13 +595,15 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel_f64(
 constexpr int kFineT = 10;
 constexpr int kFineJC = 16;  // j1 columns per FC block
 
-__global__ void fine_twiddle_kernel(double2* __restrict__ t, int64_t len)
+// t[x] = w_div^(m), m = x (row = 0) or (x / row) * (x % row) (the [n2][k] product table)
+__global__ void fine_twiddle_kernel(double2* __restrict__ t, int64_t len, int64_t div, int64_t row)
 {
-    const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (m >= len) return;
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= len) return;
+    const int64_t m = row ? (x / row) * (x % row) : x;
     double s, c;
-    sincospi(-2.0 * (double)m / (double)len, &s, &c);
-    t[m] = make_double2(c, s);
+    sincospi(-2.0 * (double)m / (double)div, &s, &c);
+    t[x] = make_double2(c, s);
 }
 
 template <int P, class Src>
@@ -648,11 +650,10 @@ __device__ __forceinline__ void best_merge(double& m, int64_t& i, double m2, int
 
 template <int P>
 __global__ __launch_bounds__(kColThreads) void fine_cols_kernel(
-    const double2* __restrict__ E, int D, int64_t N, int shifted, const double2* __restrict__ tabM,
-    FineBest* __restrict__ part)
+    const double2* __restrict__ E, int D, int64_t N, int shifted, const double2* __restrict__ tabK,
+    const double2* __restrict__ tabS, FineBest* __restrict__ part)
 {
     constexpr int T = kFineT, JC = kFineJC;
-    constexpr int64_t M = (int64_t)P * T * kRow;
     __shared__ double2 s_e[P * T * JC];  // [n2][m2 -> j2][jj]
     __shared__ FineBest s_b[kColThreads / 64];
     const int r = blockIdx.y, j10 = blockIdx.x * JC, tid = threadIdx.x;
@@ -661,18 +662,20 @@ __global__ __launch_bounds__(kColThreads) void fine_cols_kernel(
         s_e[e] = E[((int64_t)r * P * T + nm) * kRow + j10 + jj];
     }
     __syncthreads();
-    // DFT_T over m2 for each (n2, jj), twiddle w_M^(-n2*k1)
+    // DFT_T over m2 for each (n2, jj), twiddle w_M^(-n2*k1), k1 = k + 2000*j2:
+    // w_M^(-n2*k) (the [n2][k] table, 16 consecutive k per block: coalesced) times
+    // w_{P*T}^(-n2*j2) (a 290-entry table). (A gather from the full w_M table fetched
+    // ~4x the bytes of E from L2 / MALL.)
     for (int pr = tid; pr < P * JC; pr += kColThreads) {
         const int n2 = pr / JC, jj = pr - n2 * JC;
         double2 v[T];
 #pragma unroll
         for (int m2 = 0; m2 < T; m2++) v[m2] = s_e[(n2 * T + m2) * JC + jj];
         dft10<-1>(v);
+        const double2 tk = tabK[n2 * kRow + j10 + jj];
 #pragma unroll
-        for (int j2 = 0; j2 < T; j2++) {
-            const int64_t k1 = j10 + jj + (int64_t)kRow * j2;
-            s_e[(n2 * T + j2) * JC + jj] = cmul(v[j2], tabM[((int64_t)n2 * k1) % M]);
-        }
+        for (int j2 = 0; j2 < T; j2++)
+            s_e[(n2 * T + j2) * JC + jj] = cmul(v[j2], j2 ? cmul(tk, tabS[(n2 * j2) % (P * T)]) : tk);
     }
     __syncthreads();
     double bm = -1.0;
@@ -830,12 +833,15 @@ hipError_t launch_fine_fft_tables(int64_t S, int L, int datalen, void* scratch, 
     double2* tw_row = E + M * datalen;
     double2* tabA = tw_row + kRow;
     double2* tabB = tabA + (int64_t)kRow * datalen;
-    double2* tabM = tabB + (int64_t)kFineT * kRow;
-    const int64_t lens[4] = {kRow, (int64_t)kRow * datalen, (int64_t)kFineT * kRow, M};
-    double2* tabs[4] = {tw_row, tabA, tabB, tabM};
-    for (int t = 0; t < 4; t++)
+    double2* tabK = tabB + (int64_t)kFineT * kRow;  // [P][2000] w_M^(-n2*k), then w_{P*T}
+    double2* tabS = tabK + S;
+    const int64_t lens[5] = {kRow, (int64_t)kRow * datalen, (int64_t)kFineT * kRow, S, M / kRow};
+    const int64_t divs[5] = {kRow, (int64_t)kRow * datalen, (int64_t)kFineT * kRow, M, M / kRow};
+    const int64_t rows[5] = {0, 0, 0, kRow, 0};
+    double2* tabs[5] = {tw_row, tabA, tabB, tabK, tabS};
+    for (int t = 0; t < 5; t++)
         hipLaunchKernelGGL(fine_twiddle_kernel, dim3((unsigned)((lens[t] + 255) / 256)), dim3(256), 0,
-                           s, tabs[t], lens[t]);
+                           s, tabs[t], lens[t], divs[t], rows[t]);
     return hipGetLastError();
 }
 
@@ -850,8 +856,9 @@ hipError_t launch_fine_fft_argmax(const int8_t* iq, const double2* xs, int64_t S
     double2* tw_row = E + M * datalen;
     double2* tabA = tw_row + kRow;
     double2* tabB = tabA + (int64_t)kRow * datalen;
-    double2* tabM = tabB + (int64_t)kFineT * kRow;
-    FineBest* part = reinterpret_cast<FineBest*>(tabM + M);
+    double2* tabK = tabB + (int64_t)kFineT * kRow;
+    double2* tabS = tabK + S;
+    FineBest* part = reinterpret_cast<FineBest*>(tabK + M);  // (tabK + tabS < M entries)
     const int nblk = kRow / kFineJC;
 #define GNSS_FINE(P_)                                                                           \
     if (S == (int64_t)P_ * kRow) {                                                              \
@@ -864,7 +871,7 @@ hipError_t launch_fine_fft_argmax(const int8_t* iq, const double2* xs, int64_t S
                                0, s, SrcIQ8{iq}, base, ca, 1 / Fs, 1 / codeFreqBasis, codelength, datalen, N, \
                                tw_row, tabA, tabB, E);                                          \
         hipLaunchKernelGGL(fine_cols_kernel<P_>, dim3(nblk, datalen), dim3(kColThreads), 0, s, E, \
-                           datalen, N, shifted, tabM, part);                                    \
+                           datalen, N, shifted, tabK, tabS, part);                                    \
         hipLaunchKernelGGL(fine_best_final_kernel, dim3(1), dim3(256), 0, s, part, nblk * datalen, \
                            kbest);                                                              \
         return hipGetLastError();                                                               \
