@@ -528,7 +528,9 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel(
 // one transforms, radices 10-10-20 (three LDS passes; 5-5-5-16: correlation 19.7 ->
 // 18.5 ms at config 2). Measured and dropped: twiddles from the global table (634 -> 721
 // us per batch); a 90-entry split table w^m = w^(m mod 50) w^(50 (m div 50)) (33 KB of
-// LDS, twice the blocks per CU; the extra complex product per twiddle: 19.7 -> 29.0 ms).
+// LDS, twice the blocks per CU; the extra complex product per twiddle: 19.7 -> 29.0 ms);
+// a padded layout x -> x + x/20 against the radix-20 pass's 2-way store conflicts (28 %
+// of the LDS cycles by SQ_LDS_BANK_CONFLICT): 350 -> 481 us per launch (index divisions).
 template <int P>
 __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel_f64(
     const double2* __restrict__ A, int nprn, int datalen, int first_pair, double scale,
