@@ -34,7 +34,8 @@ pkg = importlib.import_module("assignment-for-aae6102_gnss-sdr_amd")
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SAMPLES_PER_MS = 58000  # Opensky Fs 58 MHz
-TRAFFIC_FILE = "traffic_r02.json"  # PMC bytes per launch of the dominant kernel (this round's pass)
+TRAFFIC_FILE = "traffic_r02.json"
+ACQ_BOUND_FILE = "acq_bound_r02.json"  # counters of the fp64 acquisition kernels (tools/acq_bound.py)  # PMC bytes per launch of the dominant kernel (this round's pass)
 
 
 def parse():
@@ -417,6 +418,9 @@ def main():
                           "frac": round(16.0 * acq_units / (acq_corr_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
                           "corr_ms": round(acq_corr_ms / args.steps, 3),
                           "fine_ms": round(acq_fine_ms / args.steps, 3)} if acq_corr_ms else None),
+        # what bounds the acquisition kernels (PMC counters + rocprofv3 averages of this
+        # round's separate passes, tools/acq_bound.py; a PMC pass cannot run in this process)
+        "acq_kernel_bounds": acq_bounds(),
         "acq_fp32_fast_mode": fast,
         "cpu_baseline": cpu,
     }
@@ -425,6 +429,14 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def acq_bounds():
+    try:
+        with open(os.path.join(ROOT, "profiles", ACQ_BOUND_FILE)) as fh:
+            return {"source": f"profiles/{ACQ_BOUND_FILE}", "kernels": json.load(fh)}
+    except (OSError, ValueError):
+        return None
 
 
 def np_equal(a, b):
