@@ -1068,12 +1068,23 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
     // everything with GNSS_NO_PERSIST. Both paths give the same bits.
     int cus = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
-    auto persistent_ok = [&](int pdi, int sub) {
-        if (getenv("GNSS_NO_PERSIST") || P.fmt != 0 || bpc_for(pdi, sub) > kMaxBpcRun) return false;
+    // Virtual blocks per resident block (vpb): where nch x bpc blocks cannot all be
+    // resident (config 5: 32 channels x 11 taps), each block correlates vpb of the step's
+    // blocks in turn -- the lane geometry and so the bits stay those of bpc blocks.
+    // GNSS_FORCE_VPB (test hook) asks for at least that many.
+    auto vpb_for = [&](int pdi, int sub) {
+        if (getenv("GNSS_NO_PERSIST") || P.fmt != 0 || bpc_for(pdi, sub) > kMaxBpcRun) return 0;
         const int occ = std::min(track_run_blocks_per_cu(P, sub), 4);
-        return occ >= 1 && (int64_t)nch * bpc_for(pdi, sub) <= (int64_t)occ * cus;
+        if (occ < 1) return 0;
+        const int bpc = bpc_for(pdi, sub);
+        int v0 = 1;
+        if (const char* fv = getenv("GNSS_FORCE_VPB")) v0 = std::max(1, std::min(atoi(fv), kMaxVpb));
+        for (int v = v0; v <= kMaxVpb; v++)
+            if ((int64_t)nch * ((bpc + v - 1) / v) <= (int64_t)occ * cus) return v;
+        return 0;
     };
-    bool persist1 = persistent_ok(1, sub1), persist10 = persistent_ok(10, sub10);
+    const int vpb1 = vpb_for(1, sub1), vpb10 = vpb_for(10, sub10);
+    bool persist1 = vpb1 > 0, persist10 = vpb10 > 0;
     if (const char* pr = getenv("GNSS_PROBE")) P.probe = atoi(pr);
     const int bpc1 = bpc_for(1, sub1), bpc10 = bpc_for(10, sub10);
     if (bpc10 > kMaxBpc) return fail(ctx, GNSS_EARG, "Sample too large for the step geometry");
@@ -1189,7 +1200,7 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
                 HIP_TRY(hipEventRecord(a, ctx->stream));
             }
             HIP_TRY(hipMemsetAsync(d_err.p, 0, 16, ctx->stream));  // timeout word + census
-            HIP_TRY(launch_track_run(P, B, TD, bpc, sub, count, tag, ctx->stream));
+            HIP_TRY(launch_track_run(P, B, TD, bpc, pdi == 1 ? vpb1 : vpb10, sub, count, tag, ctx->stream));
             tag += (unsigned)count + 1;
             unsigned err[3] = {0, 0, 0};
             HIP_TRY(hipMemcpyAsync(err, d_err.p, sizeof err, hipMemcpyDeviceToHost, ctx->stream));

@@ -252,7 +252,8 @@ hipError_t launch_track_step(const TrkParams& p, const TrkBuffers& b, const TrkD
 // Persistent form: `nsteps` steps of every channel in one launch (all nch*bpc blocks
 // resident); tags of this launch's hand-offs are tag0 + 1 .. tag0 + nsteps.
 hipError_t launch_track_run(const TrkParams& p, const TrkBuffers& b, const TrkDev& d,
-                            int blocks_per_chan, int sub, int nsteps, unsigned tag0, hipStream_t s);
+                            int blocks_per_chan, int vblocks_per_block, int sub, int nsteps, unsigned tag0,
+                            hipStream_t s);
 // blocks of the persistent kernel one CU can hold (occupancy query), for the host's
 // residency check
 int track_run_blocks_per_cu(const TrkParams& p, int sub);
@@ -275,6 +276,7 @@ constexpr int kArrivePerChan = 9;   // 8 XCD-group counters + the channel counte
 constexpr int kStampSlots = 2200;
 constexpr int kMaxBpc = 1024; // blocks per channel per step (partial buffer)
 constexpr int kMaxBpcRun = 256;  // blocks per channel of the persistent kernel
+constexpr int kMaxVpb = 16;      // virtual blocks per resident block of the persistent kernel
 constexpr int kDescWords = (int)(sizeof(StepDesc) / 4);
 
 // ----------------------------------------------------------------------------

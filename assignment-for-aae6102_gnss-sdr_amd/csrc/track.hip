@@ -1336,7 +1336,7 @@ __device__ __forceinline__ void prefetch_raw(const int8_t* iq, int64_t g0, int64
 template <int NT, int SUB, bool DIVIDE>
 __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT > 3 ? 2 : 3, NT > 3 ? 2 : 3))) void track_run_kernel(const TrkParams* __restrict__ pp,
                                                                const TrkBuffers* __restrict__ bp, int bpc,
-                                                               int nsteps, unsigned tag0)
+                                                               int vpb, int nsteps, unsigned tag0)
 {
     const TrkParams& p = *pp;
     const TrkBuffers& b = *bp;
@@ -1344,10 +1344,17 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
     constexpr int NV = 2 * NT;
     constexpr int T = kTrkThreads;
     static_assert(M <= kLaneMax, "lane span exceeds the rotation table");
-    const int ch = blockIdx.x / bpc;
-    const int blk = blockIdx.x - ch * bpc;
+    // vpb virtual blocks per resident block (config 5: 32 channels x 11 taps on one GPU):
+    // block pblk correlates the channel's blocks blk .. blk + nvb - 1 of the step's lane
+    // geometry one after the other, each with the same lanes, reduction and granule as a
+    // block of its own, so the sums are the same bits whatever vpb is
+    const int pbpc = (bpc + vpb - 1) / vpb;
+    const int ch = blockIdx.x / pbpc;
+    const int pblk = blockIdx.x - ch * pbpc;
+    const int blk = pblk * vpb;
+    const int nvb = bpc - blk < vpb ? bpc - blk : vpb;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const bool io = blk == 0;
+    const bool io = pblk == 0;
 
     constexpr int kSlot = 8 * T * 2;                  // running sums [8][T] double2
     constexpr int kRed = NV * (T + 32);               // block reduction
@@ -1439,7 +1446,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         // timing probe (GNSS_STAMPS), channel 0, row s: [0] step start, [1] computed,
         // [2] partial out, [3] all partials in, [4] next descriptor ready (block 0);
         // [5..9] the same for the channel's last block
-        unsigned long long* srow = b.stamps && ch == 0 && (io || blk == bpc - 1)
+        unsigned long long* srow = b.stamps && ch == 0 && (io || pblk == pbpc - 1)
                                        ? b.stamps + (size_t)(s % kStampSlots) * kStampRow + (io ? 0 : 5) : nullptr;
         if (srow && tid == 0) srow[0] = wall_clock64();
 
@@ -1449,29 +1456,36 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         // low level rotates with the step (0..2) so the channels sharing a CU take turns
         // (by age alone the first-dispatched channel would always win and the last one set
         // the launch's length).
-        switch ((p.probe & 64) ? ch % 3 : (p.probe & 128) ? 0 : (s + ch) % 3) {
-        case 0: __builtin_amdgcn_s_setprio(0); break;
-        case 1: __builtin_amdgcn_s_setprio(1); break;
-        default: __builtin_amdgcn_s_setprio(2); break;
-        }
-        {
-            const int64_t g0 = uni(D.g_first) + ((int64_t)blk * T + tid) * SUB;
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's global_load_lds landed
-            double oI[NT], oQ[NT];
-            lane_correlate<NT, SUB, DIVIDE, true, 0>(p, &D, LdsRaw{s_raw + tid}, 8 * g0 - A, cabits,
-                                                  reinterpret_cast<double2*>(s_mem) + tid, &s_zero, oI, oQ);
-            __syncthreads();  // slots and s_raw free
-            __builtin_amdgcn_s_setprio(3);
-            if (srow && tid == 0) srow[1] = wall_clock64();
-            // block sum in a fixed order, published as granules
-            const double bsum = block_partial<NT>(s_mem, oI, oQ, tid);
-            if (tid < NV * 4 && (tid & 3) == 0)
-                publish16(pg, ((s & 1) * kMaxBpcRun + blk) * NV + (tid >> 2), bsum, tag0 + s + 1);
-            if (srow && tid == 0) srow[2] = wall_clock64();
-            if (b.stamps && ch == 0 && tid == 0) {  // latest partial of the channel (all blocks)
-                unsigned long long* r = b.stamps + (size_t)(s % kStampSlots) * kStampRow;
-                atomicMax(r + 23, wall_clock64());
-                atomicMax(r + 24, ~wall_clock64());  // (earliest, complemented)
+        for (int jv = 0; jv < nvb; jv++) {
+            const int vb = blk + jv;
+            switch ((p.probe & 64) ? ch % 3 : (p.probe & 128) ? 0 : (s + ch) % 3) {
+            case 0: __builtin_amdgcn_s_setprio(0); break;
+            case 1: __builtin_amdgcn_s_setprio(1); break;
+            default: __builtin_amdgcn_s_setprio(2); break;
+            }
+            {
+                const int64_t g0 = uni(D.g_first) + ((int64_t)vb * T + tid) * SUB;
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's global_load_lds landed
+                double oI[NT], oQ[NT];
+                lane_correlate<NT, SUB, DIVIDE, true, 0>(p, &D, LdsRaw{s_raw + tid}, 8 * g0 - A, cabits,
+                                                      reinterpret_cast<double2*>(s_mem) + tid, &s_zero, oI, oQ);
+                __syncthreads();  // slots and s_raw free
+                // the next virtual block's IF, every lane its own groups (waited for at the
+                // top of its iteration), in flight during this block's reduction
+                if (jv + 1 < nvb)
+                    prefetch_raw<SUB>(iq, uni(D.g_first) + ((int64_t)(vb + 1) * T + tid) * SUB, gmax, s_raw, tid);
+                __builtin_amdgcn_s_setprio(3);
+                if (srow && tid == 0) srow[1] = wall_clock64();
+                // block sum in a fixed order, published as granules
+                const double bsum = block_partial<NT>(s_mem, oI, oQ, tid);
+                if (tid < NV * 4 && (tid & 3) == 0)
+                    publish16(pg, ((s & 1) * kMaxBpcRun + vb) * NV + (tid >> 2), bsum, tag0 + s + 1);
+                if (srow && tid == 0) srow[2] = wall_clock64();
+                if (b.stamps && ch == 0 && tid == 0) {  // latest partial of the channel (all blocks)
+                    unsigned long long* r = b.stamps + (size_t)(s % kStampSlots) * kStampRow;
+                    atomicMax(r + 23, wall_clock64());
+                    atomicMax(r + 24, ~wall_clock64());  // (earliest, complemented)
+                }
             }
         }
 
@@ -1704,13 +1718,14 @@ hipError_t launch_track_step(const TrkParams& p, const TrkBuffers& b, const TrkD
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_track_run(const TrkParams& p, const TrkBuffers& b, const TrkDev& d, int bpc, int sub,
+hipError_t launch_track_run(const TrkParams& p, const TrkBuffers& b, const TrkDev& d, int bpc, int vpb, int sub,
                             int nsteps, unsigned tag0, hipStream_t s)
 {
-    dim3 grid(p.nch * bpc), block(kTrkThreads);
+    if (vpb < 1 || bpc < 1) return hipErrorInvalidValue;
+    dim3 grid(p.nch * ((bpc + vpb - 1) / vpb)), block(kTrkThreads);
 #define GNSS_RUN(NT_, SUB_, DIV_)                                                              \
     if (p.ntaps == NT_ && sub == SUB_ && (p.exact_div != 0) == DIV_) {                         \
-        hipLaunchKernelGGL((track_run_kernel<NT_, SUB_, DIV_>), grid, block, 0, s, d.p, d.b, bpc, \
+        hipLaunchKernelGGL((track_run_kernel<NT_, SUB_, DIV_>), grid, block, 0, s, d.p, d.b, bpc, vpb, \
                            nsteps, tag0);                                                      \
         return hipGetLastError();                                                              \
     }

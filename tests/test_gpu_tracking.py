@@ -253,8 +253,8 @@ def test_file_route_positioned_reads(pkg, ctx, opensky_short, tmp_path):
 
 def test_config5_shape_32_channels_11_taps(pkg, po, ctx):
     """BASELINE config 5's shape at reduced length: 32 channels (every PRN present), the 11
-    ACF taps -0.5:0.1:0.5, one GPU (the per-step path: the persistent grid is not resident
-    for 32 channels), against the oracle."""
+    ACF taps -0.5:0.1:0.5, one GPU (the persistent loop with several of the step's blocks
+    per resident block: 32 x 96 blocks would not all be resident), against the oracle."""
     from types import SimpleNamespace
     skip, N1, N10 = 0, 650, 20  # (the bit-edge search needs i >= 600, trackingCT.m:179-204)
     cfg = pkg.synth.all_prn(32, skip_ms=skip)
@@ -268,6 +268,7 @@ def test_config5_shape_32_channels_11_taps(pkg, po, ctx):
     taps = pkg.colon(-0.5, 0.1, 0.5)
     assert np.array_equal(taps, po.colon(-0.5, 0.1, 0.5))
     g = pkg.trackingCT(file, signal, track, A, ctx=ctx, taps=taps, raw=True)
+    assert ctx.timing()["track_launches"] <= 4  # persistent, not one launch per step
     r = po.trackingCT(file, signal, track, A, taps=taps, raw=True)
     assert r.status == 0
     compare(pkg, g, r)
@@ -300,3 +301,26 @@ def test_streamed_windows_equal_resident(pkg, ctx, opensky_short, tmp_path, rout
         n = int(g0.len[c])
         assert np.array_equal(g0.rec[c, :, :n], g1.rec[c, :, :n]), c
     assert np.array_equal(g0.CN0, g1.CN0)
+
+
+@pytest.mark.parametrize("ntaps,vpb", [(3, 4), (11, 3)])
+def test_virtual_blocks_bit_identical(pkg, ctx, opensky_short, monkeypatch, ntaps, vpb):
+    """The persistent loop with several of the step's blocks per resident block (how 32
+    channels x 11 taps stay persistent on one GPU) gives the same records as one block each
+    and as the per-step path."""
+    skip, cfg, data = opensky_short
+    file, signal, acq, track = params(pkg, skip, data)
+    track.msToProcessCT_1ms, track.msToProcessCT_10ms = 700, 300
+    taps = pkg.colon(-0.5, 0.1, 0.5) if ntaps == 11 else None
+    A = acquired_of([3, 16, 22], [3684, 26051, 2611], [4580975.0, 4579675.0, 4581525.0])
+    p = pkg.trackingCT(file, signal, track, A, ctx=ctx, taps=taps, raw=True)
+    monkeypatch.setenv("GNSS_FORCE_VPB", str(vpb))
+    v = pkg.trackingCT(file, signal, track, A, ctx=ctx, taps=taps, raw=True)
+    assert ctx.timing()["track_launches"] <= 4
+    monkeypatch.delenv("GNSS_FORCE_VPB")
+    monkeypatch.setenv("GNSS_NO_PERSIST", "1")
+    q = pkg.trackingCT(file, signal, track, A, ctx=ctx, taps=taps, raw=True)
+    for c in range(3):
+        assert np.array_equal(p.rec[c], v.rec[c]) and np.array_equal(q.rec[c], v.rec[c]), c
+        assert p.len[c] == v.len[c] and p.countinx[c] == v.countinx[c]
+    assert np.array_equal(p.CN0, v.CN0)
