@@ -35,7 +35,8 @@ pkg = importlib.import_module("assignment-for-aae6102_gnss-sdr_amd")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SAMPLES_PER_MS = 58000  # Opensky Fs 58 MHz
 TRAFFIC_FILE = "traffic_r02.json"
-ACQ_BOUND_FILE = "acq_bound_r02.json"  # counters of the fp64 acquisition kernels (tools/acq_bound.py)  # PMC bytes per launch of the dominant kernel (this round's pass)
+ACQ_BOUND_FILE = "acq_bound_r02.json"
+TRAFFIC_FILE_CFG5 = "traffic_cfg5_r02.json"  # PMC bytes per launch of the 11-tap 10-ms launch  # counters of the fp64 acquisition kernels (tools/acq_bound.py)  # PMC bytes per launch of the dominant kernel (this round's pass)
 
 
 def parse():
@@ -165,6 +166,18 @@ def run_cfg5(args, rank, world, local, dist, ctx):
                 "kernel": "10-ms phase correlator, 11 taps (persistent or per-step launches)",
                 "launches": int(launches), "avg_launch_us": round(avg_ms * 1e3, 3),
                 "algorithmic_bytes_per_launch": bpl}
+        tf = os.path.join(ROOT, "profiles", TRAFFIC_FILE_CFG5)
+        if world == 1 and os.path.exists(tf):
+            try:
+                with open(tf) as fh:
+                    tj = json.load(fh)
+                roof["traffic"] = tj.get("bytes_per_launch")
+                roof["traffic_source"] = f"profiles/{TRAFFIC_FILE_CFG5} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)"
+            except (OSError, ValueError):
+                pass
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline_cfg5(file, signal, track, A, taps, dev)
     line = {"metric": "correlator Msamples/s (trackingCT cfg5), whole job", "value": round(total / elapsed / 1e6, 2),
             "unit": "Msamples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
@@ -173,7 +186,7 @@ def run_cfg5(args, rank, world, local, dist, ctx):
             "config": {"workload": f"trackingCT cfg5 (32 ch, 11 taps -0.5:0.1:0.5, 1000 ms @1ms + "
                                    f"{args.n10_cfg5} ms @10ms)", "parallelism": f"channels x{world}",
                        "channels_per_rank": len(mine)},
-            "roofline": roof, "cpu_baseline": None}
+            "roofline": roof, "cpu_baseline": cpu}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:
@@ -459,6 +472,42 @@ def host_cpu():
     except OSError:
         pass
     return model, os.cpu_count()
+
+
+def cpu_baseline_cfg5(file, signal, track, A, taps, dev):
+    """Config 5's CPU leg: the oracle's trackingCT with the same 11 taps on a bounded sample
+    (1 000 ms @1 ms + 100 ms @10 ms; 1 channel on one thread, 16 channels on 16 threads,
+    median of 3), channel-samples per second."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as po
+    from types import SimpleNamespace
+    S = signal.Sample
+    n10s = 100
+    win = dev.download(0, (1000 + 19 + n10s + 3) * S * 2)
+    f2 = SimpleNamespace(skip=0, dataType=2, dataPrecision=1, data=win, fileRoute=None, dev=None)
+    tr = SimpleNamespace(**vars(track))
+    tr.msToProcessCT_10ms = n10s
+    allc = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+
+    def leg(nch, nt):
+        A1 = SimpleNamespace(sv=A.sv[:nch], SNR=A.SNR[:nch], Doppler=A.Doppler[:nch],
+                             codedelay=A.codedelay[:nch], fineFreq=A.fineFreq[:nch])
+        r = []
+        for _ in range(3):
+            t = time.perf_counter()
+            po.trackingCT(f2, signal, tr, A1, taps=np.asarray(taps), nthreads=nt)
+            r.append(nch * (1000 + n10s) * S / (time.perf_counter() - t))
+        return float(np.median(r))
+
+    one = leg(1, 1)
+    nall = min(allc, len(A.sv))
+    many = leg(nall, nall)
+    model, ncpu = host_cpu()
+    return {"value": round(many / 1e6, 4), "unit": "Msamples/s", "cores": nall, "kind": "port",
+            "sample": f"oracle/ C fp64 restatement, trackingCT with 11 taps, {nall} channels x (1000 ms @1ms "
+                      f"+ {n10s} ms @10ms) on {nall} threads (median of 3)",
+            "one_thread": {"value": round(one / 1e6, 4), "sample": "1 channel, same length"},
+            "host_cpu": model, "nproc": ncpu}
 
 
 def cpu_baseline(file, signal, acq, track, A, dev, args, ta, tt):
