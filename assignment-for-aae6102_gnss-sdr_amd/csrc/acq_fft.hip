@@ -656,6 +656,10 @@ __global__ __launch_bounds__(kColThreads) void fine_cols_kernel(
     const double2* __restrict__ tabS, FineBest* __restrict__ part)
 {
     constexpr int T = kFineT, JC = kFineJC;
+    // 29 x 10 x 16 x 16 B = 74 KB of LDS: two blocks per CU on gfx950's 160 KiB (above the
+    // 64 KiB per-workgroup limit of earlier gfx9 parts; this file is built for gfx950 only)
+    static_assert(P * T * JC * sizeof(double2) + (kColThreads / 64) * sizeof(double) * 2 <= 80 * 1024,
+                  "fine_cols LDS tile: two blocks per CU of gfx950's 160 KiB");
     __shared__ double2 s_e[P * T * JC];  // [n2][m2 -> j2][jj]
     __shared__ FineBest s_b[kColThreads / 64];
     const int r = blockIdx.y, j10 = blockIdx.x * JC, tid = threadIdx.x;
