@@ -530,7 +530,8 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel(
 // us per batch); a 90-entry split table w^m = w^(m mod 50) w^(50 (m div 50)) (33 KB of
 // LDS, twice the blocks per CU; the extra complex product per twiddle: 19.7 -> 29.0 ms);
 // a padded layout x -> x + x/20 against the radix-20 pass's 2-way store conflicts (28 %
-// of the LDS cycles by SQ_LDS_BANK_CONFLICT): 350 -> 481 us per launch (index divisions).
+// of the LDS cycles by SQ_LDS_BANK_CONFLICT): 350 -> 481 us per launch (index divisions);
+// radix 10-10-20 (conflict-free first pass, twiddles in the radix-20 pass): 350 -> 367 us.
 template <int P>
 __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel_f64(
     const double2* __restrict__ A, int nprn, int datalen, int first_pair, double scale,
