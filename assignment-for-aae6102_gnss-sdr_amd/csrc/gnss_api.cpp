@@ -1074,13 +1074,15 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
     // GNSS_FORCE_VPB (test hook) asks for at least that many.
     auto vpb_for = [&](int pdi, int sub) {
         if (getenv("GNSS_NO_PERSIST") || P.fmt != 0 || bpc_for(pdi, sub) > kMaxBpcRun) return 0;
-        const int occ = std::min(track_run_blocks_per_cu(P, sub), 4);
-        if (occ < 1) return 0;
         const int bpc = bpc_for(pdi, sub);
         int v0 = 1;
         if (const char* fv = getenv("GNSS_FORCE_VPB")) v0 = std::max(1, std::min(atoi(fv), kMaxVpb));
-        for (int v = v0; v <= kMaxVpb; v++)
-            if ((int64_t)nch * ((bpc + v - 1) / v) <= (int64_t)occ * cus) return v;
+        const int occ1 = std::min(track_run_blocks_per_cu(P, sub, false), 4);
+        if (v0 == 1 && occ1 >= 1 && (int64_t)nch * bpc <= (int64_t)occ1 * cus) return 1;
+        const int occv = std::min(track_run_blocks_per_cu(P, sub, true), 4);  // 0: no such form
+        if (occv < 1) return 0;
+        for (int v = std::max(v0, 2); v <= kMaxVpb; v++)
+            if ((int64_t)nch * ((bpc + v - 1) / v) <= (int64_t)occv * cus) return v;
         return 0;
     };
     const int vpb1 = vpb_for(1, sub1), vpb10 = vpb_for(10, sub10);

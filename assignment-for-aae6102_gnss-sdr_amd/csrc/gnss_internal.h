@@ -256,7 +256,7 @@ hipError_t launch_track_run(const TrkParams& p, const TrkBuffers& b, const TrkDe
                             hipStream_t s);
 // blocks of the persistent kernel one CU can hold (occupancy query), for the host's
 // residency check
-int track_run_blocks_per_cu(const TrkParams& p, int sub);
+int track_run_blocks_per_cu(const TrkParams& p, int sub, bool vblocks = false);
 hipError_t launch_track_prepare(const TrkParams& p, const TrkBuffers& b, const TrkDev& d, int pdi,
                                 int phaseC, hipStream_t s);
 hipError_t launch_track_snapshot(const TrkParams& p, const TrkBuffers& b, const TrkDev& d, hipStream_t s);

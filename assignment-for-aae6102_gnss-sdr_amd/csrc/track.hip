@@ -1333,7 +1333,7 @@ __device__ __forceinline__ void prefetch_raw(const int8_t* iq, int64_t g0, int64
 // (the same fp64 code on the same sums: bit-identical copies), so a step needs one
 // exchange only: each block publishes its partial sums and reads everyone's. Block 0
 // of the channel writes the records, C/N0 and, at the end, the state.
-template <int NT, int SUB, bool DIVIDE>
+template <int NT, int SUB, bool DIVIDE, bool VB = false>
 __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT > 3 ? 2 : 3, NT > 3 ? 2 : 3))) void track_run_kernel(const TrkParams* __restrict__ pp,
                                                                const TrkBuffers* __restrict__ bp, int bpc,
                                                                int vpb, int nsteps, unsigned tag0)
@@ -1347,12 +1347,14 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
     // vpb virtual blocks per resident block (config 5: 32 channels x 11 taps on one GPU):
     // block pblk correlates the channel's blocks blk .. blk + nvb - 1 of the step's lane
     // geometry one after the other, each with the same lanes, reduction and granule as a
-    // block of its own, so the sums are the same bits whatever vpb is
-    const int pbpc = (bpc + vpb - 1) / vpb;
+    // block of its own, so the sums are the same bits whatever vpb is. (VB = false: the
+    // one-block-per-block form, the loop compiled away -- the headline's 8 channels.)
+    const int vpb_ = VB ? vpb : 1;
+    const int pbpc = (bpc + vpb_ - 1) / vpb_;
     const int ch = blockIdx.x / pbpc;
     const int pblk = blockIdx.x - ch * pbpc;
-    const int blk = pblk * vpb;
-    const int nvb = bpc - blk < vpb ? bpc - blk : vpb;
+    const int blk = pblk * vpb_;
+    const int nvb = VB ? (bpc - blk < vpb_ ? bpc - blk : vpb_) : 1;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const bool io = pblk == 0;
 
@@ -1472,7 +1474,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
                 __syncthreads();  // slots and s_raw free
                 // the next virtual block's IF, every lane its own groups (waited for at the
                 // top of its iteration), in flight during this block's reduction
-                if (jv + 1 < nvb)
+                if (VB && jv + 1 < nvb)
                     prefetch_raw<SUB>(iq, uni(D.g_first) + ((int64_t)(vb + 1) * T + tid) * SUB, gmax, s_raw, tid);
                 __builtin_amdgcn_s_setprio(3);
                 if (srow && tid == 0) srow[1] = wall_clock64();
@@ -1724,32 +1726,44 @@ hipError_t launch_track_run(const TrkParams& p, const TrkBuffers& b, const TrkDe
     if (vpb < 1 || bpc < 1) return hipErrorInvalidValue;
     dim3 grid(p.nch * ((bpc + vpb - 1) / vpb)), block(kTrkThreads);
 #define GNSS_RUN(NT_, SUB_, DIV_)                                                              \
-    if (p.ntaps == NT_ && sub == SUB_ && (p.exact_div != 0) == DIV_) {                         \
-        hipLaunchKernelGGL((track_run_kernel<NT_, SUB_, DIV_>), grid, block, 0, s, d.p, d.b, bpc, vpb, \
+    if (p.ntaps == NT_ && sub == SUB_ && (p.exact_div != 0) == DIV_ && vpb == 1) {            \
+        hipLaunchKernelGGL((track_run_kernel<NT_, SUB_, DIV_, false>), grid, block, 0, s, d.p, d.b, bpc, vpb, \
+                           nsteps, tag0);                                                      \
+        return hipGetLastError();                                                              \
+    }
+#define GNSS_RUNV(NT_, SUB_, DIV_)                                                             \
+    if (p.ntaps == NT_ && sub == SUB_ && (p.exact_div != 0) == DIV_ && vpb > 1) {             \
+        hipLaunchKernelGGL((track_run_kernel<NT_, SUB_, DIV_, true>), grid, block, 0, s, d.p, d.b, bpc, vpb, \
                            nsteps, tag0);                                                      \
         return hipGetLastError();                                                              \
     }
     GNSS_RUN(3, 1, false) GNSS_RUN(3, 2, false) GNSS_RUN(3, 3, false) GNSS_RUN(3, 4, false)
     GNSS_RUN(11, 1, false) GNSS_RUN(11, 2, false) GNSS_RUN(11, 3, false) GNSS_RUN(11, 4, false)
     GNSS_RUN(3, 1, true) GNSS_RUN(11, 1, true)
+    GNSS_RUNV(3, 1, false) GNSS_RUNV(3, 3, false) GNSS_RUNV(11, 1, false) GNSS_RUNV(11, 3, false)
 #undef GNSS_RUN
+#undef GNSS_RUNV
     return hipErrorInvalidValue;
 }
 
-int track_run_blocks_per_cu(const TrkParams& p, int sub)
+int track_run_blocks_per_cu(const TrkParams& p, int sub, bool vb)
 {
     int nb = 0;
-#define GNSS_OCC(NT_, SUB_, DIV_)                                                              \
-    if (p.ntaps == NT_ && sub == SUB_ && (p.exact_div != 0) == DIV_) {                         \
+#define GNSS_OCC(NT_, SUB_, DIV_, VB_)                                                         \
+    if (p.ntaps == NT_ && sub == SUB_ && (p.exact_div != 0) == DIV_ && vb == VB_) {            \
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(                                      \
-                &nb, reinterpret_cast<const void*>(track_run_kernel<NT_, SUB_, DIV_>),          \
+                &nb, reinterpret_cast<const void*>(track_run_kernel<NT_, SUB_, DIV_, VB_>),     \
                 kTrkThreads, 0) != hipSuccess)                                                 \
             nb = 0;                                                                            \
         return nb;                                                                             \
     }
-    GNSS_OCC(3, 1, false) GNSS_OCC(3, 2, false) GNSS_OCC(3, 3, false) GNSS_OCC(3, 4, false)
-    GNSS_OCC(11, 1, false) GNSS_OCC(11, 2, false) GNSS_OCC(11, 3, false) GNSS_OCC(11, 4, false)
-    GNSS_OCC(3, 1, true) GNSS_OCC(11, 1, true)
+    GNSS_OCC(3, 1, false, false) GNSS_OCC(3, 2, false, false) GNSS_OCC(3, 3, false, false)
+    GNSS_OCC(3, 4, false, false) GNSS_OCC(11, 1, false, false) GNSS_OCC(11, 2, false, false)
+    GNSS_OCC(11, 3, false, false) GNSS_OCC(11, 4, false, false) GNSS_OCC(3, 1, true, false)
+    GNSS_OCC(11, 1, true, false)
+    // virtual-block forms (several of the step's blocks per resident block)
+    GNSS_OCC(3, 1, false, true) GNSS_OCC(3, 3, false, true) GNSS_OCC(11, 1, false, true)
+    GNSS_OCC(11, 3, false, true)
 #undef GNSS_OCC
     return 0;
 }
