@@ -628,7 +628,7 @@ __global__ __launch_bounds__(kRowThreads) void fine_rows_kernel(
         const double code = (double)ca[(int64_t)fmod(cvi, codelength)];
         const double2 raw = src.at(base + n);
         const double2 x = make_double2(raw.x * code, raw.y * code);
-        s_a[m1] = cmul(x, tabA[((int64_t)m1 * r) % RD]);
+        s_a[m1] = cmul(x, tabA[(int64_t)r * kRow + m1]);  // w_RD^(-m1*r), [r][m1]: coalesced
     }
     __syncthreads();
     fft2000<-1>(s_a, tw_row, tid);
@@ -638,7 +638,7 @@ __global__ __launch_bounds__(kRowThreads) void fine_rows_kernel(
     const double2 cb = make_double2(cs, sn);
     double2* o = E + (((int64_t)r * P + n2) * T + m2) * kRow;
     for (int j1 = tid; j1 < kRow; j1 += kRowThreads)
-        o[j1] = cmul(cmul(s_a[j1], cb), tabB[((int64_t)m2 * j1) % ((int64_t)T * kRow)]);
+        o[j1] = cmul(cmul(s_a[j1], cb), tabB[m2 * kRow + j1]);  // w_{T*2000}^(-m2*j1), [m2][j1]
 }
 
 struct FineBest {
@@ -832,7 +832,7 @@ size_t fine_fft_scratch_bytes(int64_t S, int L, int datalen)
            sizeof(FineBest) * (size_t)datalen * (kRow / kFineJC);
 }
 
-// Twiddle tables of the fine search, once per call: w_2000, w_{2000*D}, w_{T*2000}, w_M.
+// Twiddle tables of the fine search, once per call: w_2000, w_{2000*D}, w_{T*2000}, w_M, w_{P*T}.
 hipError_t launch_fine_fft_tables(int64_t S, int L, int datalen, void* scratch, hipStream_t s)
 {
     const int64_t M = (int64_t)L * S;
@@ -842,9 +842,12 @@ hipError_t launch_fine_fft_tables(int64_t S, int L, int datalen, void* scratch, 
     double2* tabB = tabA + (int64_t)kRow * datalen;
     double2* tabK = tabB + (int64_t)kFineT * kRow;  // [P][2000] w_M^(-n2*k), then w_{P*T}
     double2* tabS = tabK + S;
+    // tabA[r][m1] = w_{2000 D}^(m1 r), tabB[m2][j1] = w_{T 2000}^(m2 j1), tabK[n2][k] = w_M^(n2 k):
+    // the exponent products laid out so a row pass reads them contiguously (the same
+    // values as a gather from the plain tables: the same m through the same formula)
     const int64_t lens[5] = {kRow, (int64_t)kRow * datalen, (int64_t)kFineT * kRow, S, M / kRow};
     const int64_t divs[5] = {kRow, (int64_t)kRow * datalen, (int64_t)kFineT * kRow, M, M / kRow};
-    const int64_t rows[5] = {0, 0, 0, kRow, 0};
+    const int64_t rows[5] = {0, kRow, kRow, kRow, 0};
     double2* tabs[5] = {tw_row, tabA, tabB, tabK, tabS};
     for (int t = 0; t < 5; t++)
         hipLaunchKernelGGL(fine_twiddle_kernel, dim3((unsigned)((lens[t] + 255) / 256)), dim3(256), 0,
