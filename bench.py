@@ -343,7 +343,7 @@ def main():
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                "kernel": ("track_run_kernel<3, 3, false> (persistent: every step of the 10-ms phase, "
+                "kernel": ("track_run_kernel<3, 3, false, false> (persistent: every step of the 10-ms phase, "
                            "all channels of the rank)" if launches <= 2 else
                            "track_step_kernel<3, 3, false> (10-ms phase step, all channels)"),
                 "steps_per_launch": round(tp["track10_channel_samples"] / max(1, launches) /
