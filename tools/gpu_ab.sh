@@ -1,4 +1,4 @@
-# A/B of the headline tracking launch: the library before the virtual-block change vs now
+# A/B of the headline tracking launch: tmp_ab/libgnss_old.so = the library built from commit a2deb7b (before the virtual blocks; build it there and copy it in to re-run) vs now
 set -o pipefail
 mkdir -p gpurun_out
 for i in 1 2; do

@@ -1,4 +1,4 @@
-# A/B of the headline tracking launch (before the virtual blocks vs now), the virtual-block
+# A/B of the headline tracking launch (tmp_ab/libgnss_old.so = the library of commit a2deb7b, before the virtual blocks), the virtual-block
 # tests, and the cfg5 bench
 set -o pipefail
 mkdir -p gpurun_out
