@@ -1053,6 +1053,10 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
         return sub;
     };
     int sub1 = sub_for(1), sub10 = sub_for(10);
+    if (const char* fs = getenv("GNSS_FORCE_SUB10")) {  // probe hook: the 10-ms lane span alone
+        const int v = atoi(fs);
+        if (v >= 1 && v <= 4 && sub_ok(v) && P.fmt == 0 && ntaps != 25) sub10 = v;
+    }
     if (const char* fs = getenv("GNSS_FORCE_SUB")) {  // test hook: exercise every kernel variant
         const int v = atoi(fs);
         if (v >= 1 && v <= 4 && sub_ok(v) && ((P.fmt == 0 && ntaps != 25) || v == 1 || v == 3)) sub1 = sub10 = v;
