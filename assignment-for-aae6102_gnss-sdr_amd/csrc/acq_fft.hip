@@ -631,7 +631,7 @@ __global__ __launch_bounds__(kRowThreads) void fine_rows_kernel(
         s_a[m1] = cmul(x, tabA[(int64_t)r * kRow + m1]);  // w_RD^(-m1*r), [r][m1]: coalesced
     }
     __syncthreads();
-    fft2000<-1>(s_a, tw_row, tid);
+    fft2000_batch_r20first<-1, 1>(s_a, tw_row, tid);
     double sn, cs;
     const int64_t e = ((int64_t)(P * m2 + n2) * r) % N;
     sincospi(-2.0 * (double)e / (double)N, &sn, &cs);
