@@ -408,7 +408,7 @@ __global__ __launch_bounds__(kRowThreads) void fwd_rows_kernel(
         }
     }
     __syncthreads();
-    fft2000<-1>(s_a, s_tw, tid);
+    fft2000_batch_r20first<-1, 1>(s_a, s_tw, tid);
     V* o = B + ((int64_t)s * P + n2) * kRow;
     const V* twc = tw_col + (int64_t)n2 * kRow;
     for (int k1 = tid; k1 < kRow; k1 += kRowThreads) o[k1] = cmul(s_a[k1], twc[k1]);
