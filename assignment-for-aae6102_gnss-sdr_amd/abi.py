@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import sys
 
 MAX_SV = 64
 MAX_TAPS = 32
@@ -139,6 +140,7 @@ PROTOTYPES = {
     "gnss_ctx_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
     "gnss_ctx_set_acq_precision": (C.c_int, [C.c_void_p, C.c_int]),
     "gnss_ctx_set_window": (C.c_int, [C.c_void_p, C.c_uint64]),
+    "gnss_ctx_set_option": (C.c_int, [C.c_void_p, C.c_int, C.c_int64]),
     "gnss_dev_alloc": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
     "gnss_dev_free": (C.c_int, [C.c_void_p, C.c_void_p]),
     "gnss_dev_upload": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
@@ -180,6 +182,20 @@ PROTOTYPES = {
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libgnss_mi355x.so")
 _lib = None
+_torch_first = False
+
+# gnss_ctx_set_option keys (include/gnss_mi355x.h, ABI v9)
+OPT_FORCE_SUB, OPT_NO_PERSIST, OPT_FORCE_VPB, OPT_ACQ_ROCFFT, OPT_FINE_ROCFFT, OPT_ACQ_BATCH = range(6)
+
+
+def require_torch():
+    """torch, for the entry points that exchange device tensors with the library; raises if
+    the library was loaded before torch (torch would then see no GPU in this process)."""
+    import torch
+    if _lib is not None and not _torch_first:
+        raise RuntimeError("import torch before the first gnss Context / abi.load() "
+                           "(PyTorch-ROCm must bring up its HIP runtime first)")
+    return torch
 
 
 class GnssError(RuntimeError):
@@ -198,13 +214,13 @@ def load(path: str | None = None):
     if not os.path.exists(p):
         raise ImportError(f"{p} missing: the HIP extension is not built "
                           "(run `python -c 'import __graft_entry__ as g; g.build()'`)")
-    # PyTorch-ROCm ships its own HIP / HSA runtime: load it BEFORE this library's, or torch
-    # finds no GPU later in the same process (device-resident outputs and the RCCL gathers
-    # hand torch tensors to the library). The library then shares the process with both.
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    # PyTorch-ROCm ships its own HIP / HSA runtime and finds no GPU if this library's runtime
+    # came up first: callers that hand torch tensors to the library (device-resident outputs,
+    # the RCCL gathers) import torch before the first load; require_torch() checks that.
+    # Everyone else never pays for torch.
+    global _torch_first
+    if _lib is None:
+        _torch_first = "torch" in sys.modules
     lib = C.CDLL(p)
     for name, (res, args) in PROTOTYPES.items():
         fn = getattr(lib, name)

@@ -50,7 +50,18 @@ struct gnss_ctx {
     int acq_tw_dbl = -1;   //   ... and this precision
     int acq_fp64 = 1;      // acquisition correlation precision: 1 = fp64 (reference), 0 = fp32
     uint64_t window = 0;   // trackingCT: max IF bytes resident in HBM (0: the whole read range)
+    int64_t opt[GNSS_OPT_COUNT] = {};  // gnss_ctx_set_option (test hooks; all 0 by default)
 };
+
+// Timing-probe hooks read from the environment in probe builds only (tools/build_probe.sh
+// passes -DGNSS_PROBE_BUILD=1); the product library reads no environment variable.
+#ifndef GNSS_PROBE_BUILD
+#define GNSS_PROBE_BUILD 0
+#endif
+static const char* probe_env(const char* name)
+{
+    return GNSS_PROBE_BUILD ? getenv(name) : nullptr;
+}
 
 namespace {
 // The context's pinned host buffer `key`, at least `bytes` (contents undefined).
@@ -386,7 +397,7 @@ int acq_search(gnss_ctx* ctx, const int8_t* blk, const double2* xa, int64_t S, i
     const size_t csz = sizeof(V);
     const int nsig = dl * nb;
     int st = GNSS_OK;
-    if (acq_fft_supported(S) && !getenv("GNSS_ACQ_ROCFFT")) {
+    if (acq_fft_supported(S) && !ctx->opt[GNSS_OPT_ACQ_ROCFFT]) {
         DevBuf d_twr, d_twc, B, X, A;  // (freed after the stream drains)
         const int P = (int)(S / 2000);
         *perm = P;
@@ -426,7 +437,7 @@ int acq_search(gnss_ctx* ctx, const int8_t* blk, const double2* xa, int64_t S, i
         const int target = (int)std::max<int64_t>(1, ((int64_t)1 << 30) / ((int64_t)dl * S * (int64_t)csz));
         const int nbat = (npairs + target - 1) / target;
         int batch = (npairs + nbat - 1) / nbat;
-        if (const char* e = getenv("GNSS_ACQ_BATCH")) batch = std::max(1, atoi(e));
+        if (ctx->opt[GNSS_OPT_ACQ_BATCH] > 0) batch = (int)ctx->opt[GNSS_OPT_ACQ_BATCH];
         batch = std::min(batch, npairs);
         HIP_TRY(A.alloc(ctx, "acq.A", csz * (size_t)batch * dl * S));
         HIP_TRY(hipStreamSynchronize(ctx->stream));
@@ -545,6 +556,13 @@ int gnss_ctx_set_window(gnss_ctx* ctx, uint64_t bytes)
 {
     if (!ctx) return GNSS_EARG;
     ctx->window = bytes;
+    return GNSS_OK;
+}
+
+int gnss_ctx_set_option(gnss_ctx* ctx, int key, int64_t value)
+{
+    if (!ctx || key < 0 || key >= GNSS_OPT_COUNT) return GNSS_EARG;
+    ctx->opt[key] = value;
     return GNSS_OK;
 }
 
@@ -728,7 +746,7 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     HIP_TRY(kb.alloc(ctx, "acq.kb", sizeof(int64_t) * (size_t)na));
     HIP_TRY(hipMemcpyAsync(fca.p, caf.data(), caf.size() * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(fcd.p, cdh.data(), cdh.size() * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
-    const bool own_fine = fine_fft_supported(S, L) && !getenv("GNSS_FINE_ROCFFT");
+    const bool own_fine = fine_fft_supported(S, L) && !ctx->opt[GNSS_OPT_FINE_ROCFFT];
     Events e_fine;
     if (own_fine) {
         // per-SV zero-padded FFT as datalen three-level transforms (acq_fft.hip)
@@ -812,7 +830,7 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
                          const GivenCfg* gv = nullptr)
 {
     // GNSS_HOSTPROF: host-side phases of this call on stderr
-    const bool hp = getenv("GNSS_HOSTPROF") != nullptr;
+    const bool hp = probe_env("GNSS_HOSTPROF") != nullptr;
     const auto h0 = std::chrono::steady_clock::now();
     auto hms = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count(); };
     if (!ctx || !file || !sg || !tr || !acq || !out) return GNSS_EARG;
@@ -1053,12 +1071,11 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
         return sub;
     };
     int sub1 = sub_for(1), sub10 = sub_for(10);
-    if (const char* fs = getenv("GNSS_FORCE_SUB10")) {  // probe hook: the 10-ms lane span alone
+    if (const char* fs = probe_env("GNSS_FORCE_SUB10")) {  // probe hook: the 10-ms lane span alone
         const int v = atoi(fs);
         if (v >= 1 && v <= 4 && sub_ok(v) && P.fmt == 0 && ntaps != 25) sub10 = v;
     }
-    if (const char* fs = getenv("GNSS_FORCE_SUB")) {  // test hook: exercise every kernel variant
-        const int v = atoi(fs);
+    if (const int v = (int)ctx->opt[GNSS_OPT_FORCE_SUB]) {  // test hook: exercise every kernel variant
         if (v >= 1 && v <= 4 && sub_ok(v) && ((P.fmt == 0 && ntaps != 25) || v == 1 || v == 3)) sub1 = sub10 = v;
     }
     auto bpc_for = [&](int pdi, int sub) {
@@ -1075,12 +1092,12 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
     // Virtual blocks per resident block (vpb): where nch x bpc blocks cannot all be
     // resident (config 5: 32 channels x 11 taps), each block correlates vpb of the step's
     // blocks in turn -- the lane geometry and so the bits stay those of bpc blocks.
-    // GNSS_FORCE_VPB (test hook) asks for at least that many.
+    // GNSS_OPT_FORCE_VPB (test hook) asks for at least that many.
     auto vpb_for = [&](int pdi, int sub) {
-        if (getenv("GNSS_NO_PERSIST") || P.fmt != 0 || bpc_for(pdi, sub) > kMaxBpcRun) return 0;
+        if (ctx->opt[GNSS_OPT_NO_PERSIST] || P.fmt != 0 || bpc_for(pdi, sub) > kMaxBpcRun) return 0;
         const int bpc = bpc_for(pdi, sub);
         int v0 = 1;
-        if (const char* fv = getenv("GNSS_FORCE_VPB")) v0 = std::max(1, std::min(atoi(fv), kMaxVpb));
+        if (ctx->opt[GNSS_OPT_FORCE_VPB] > 0) v0 = (int)std::min<int64_t>(ctx->opt[GNSS_OPT_FORCE_VPB], kMaxVpb);
         const int occ1 = std::min(track_run_blocks_per_cu(P, sub, false), 4);
         if (v0 == 1 && occ1 >= 1 && (int64_t)nch * bpc <= (int64_t)occ1 * cus) return 1;
         const int occv = std::min(track_run_blocks_per_cu(P, sub, true), 4);  // 0: no such form
@@ -1091,7 +1108,7 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
     };
     const int vpb1 = vpb_for(1, sub1), vpb10 = vpb_for(10, sub10);
     bool persist1 = vpb1 > 0, persist10 = vpb10 > 0;
-    if (const char* pr = getenv("GNSS_PROBE")) P.probe = atoi(pr);
+    if (const char* pr = probe_env("GNSS_PROBE")) P.probe = atoi(pr);
     const int bpc1 = bpc_for(1, sub1), bpc10 = bpc_for(10, sub10);
     if (bpc10 > kMaxBpc) return fail(ctx, GNSS_EARG, "Sample too large for the step geometry");
 
@@ -1161,7 +1178,7 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
     B.n1 = N1;
 
     DevBuf d_stamps;  // timing probe: per-launch wall-clock stamps of channel 0
-    const char* stamp_path = getenv("GNSS_STAMPS");
+    const char* stamp_path = probe_env("GNSS_STAMPS");
     if (stamp_path) {
         HIP_TRY(d_stamps.alloc(ctx, "trk.d_stamps", sizeof(unsigned long long) * ((size_t)kStampSlots * (8 + 3 * kMaxBpc) + 1)));
         HIP_TRY(hipMemsetAsync(d_stamps.p, 0, d_stamps.n, ctx->stream));
@@ -1574,8 +1591,7 @@ int gnss_correlate_step(gnss_ctx* ctx, const gnss_file* file, const gnss_signal*
     unsigned cab[32];
     ca_bits(prn, cab);
     int sub = 1;
-    if (const char* fs = getenv("GNSS_FORCE_SUB")) {
-        const int v = atoi(fs);
+    if (const int v = (int)ctx->opt[GNSS_OPT_FORCE_SUB]) {
         if (v >= 2 && v <= 4 && !P.exact_div && 8.0 * v * codeFreq / sg->Fs < 1.0) sub = v;
     }
     const int bpc = (int)std::ceil(((S * pdi * 1.01 + 64) / 8.0 + 2) / ((double)kTrkThreads * sub));

@@ -97,6 +97,10 @@ class Context:
         read range), gnss_ctx_set_window."""
         self.check(self.lib.gnss_ctx_set_window(self.h, int(nbytes)))
 
+    def set_option(self, key: int, value: int):
+        """Test hook: force one engine path (abi.OPT_*, gnss_ctx_set_option)."""
+        self.check(self.lib.gnss_ctx_set_option(self.h, int(key), int(value)))
+
     def set_acq_precision(self, fp64: bool):
         """Acquisition correlation at fp64 (the reference's precision, default) or the fp32
         fast mode (gnss_ctx_set_acq_precision)."""
@@ -275,7 +279,7 @@ class DeviceTrackOutBuffers(TrackOutBuffers):
     RCCL without a host round trip (dist.gather_tracking_rows_device)."""
 
     def __init__(self, nsv: int, track, ntaps: int = 0, device="cuda:0", ctPOS: int | None = None):
-        import torch
+        torch = abi.require_torch()
         super().__init__(nsv, track, 0, ctPOS)
         self.device = torch.device(device)
         self.rec = torch.zeros((nsv, abi.NFIELDS, self.max_len), dtype=torch.float64, device=self.device)

@@ -253,6 +253,7 @@ def run_cfg4(args, rank, world, local, dist, ctx):
 def main():
     args = parse()
     rank, world, local, dist = setup_dist(args)
+    import torch  # noqa: F401  (before the library: device-resident outputs are torch tensors)
     ctx = pkg.Context(local)
     if args.workload == "cfg5":
         return run_cfg5(args, rank, world, local, dist, ctx)

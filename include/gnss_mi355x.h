@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define GNSS_ABI_VERSION 8
+#define GNSS_ABI_VERSION 9
 
 /* ---- status codes (SURVEY §8b "Error conventions") --------------------- */
 #define GNSS_OK         0
@@ -229,6 +229,17 @@ int  gnss_ctx_set_acq_precision(gnss_ctx *ctx, int fp64);
  * from the file; the outputs are bit-identical to the unsegmented call). GNSS_EARG from the
  * call if the budget cannot hold the 1-ms phases' span or one 10-ms step of every channel. */
 int  gnss_ctx_set_window(gnss_ctx *ctx, uint64_t bytes);
+/* Test hooks (ABI v9; replace nothing in the reference): force one code path of the engine
+ * so the parity tests can prove every path gives the reference's results. All default 0
+ * (the engine's own choice); GNSS_EARG for an unknown key.                               */
+#define GNSS_OPT_FORCE_SUB    0  /* lane span 8*v samples for both tracking phases (1..4) */
+#define GNSS_OPT_NO_PERSIST   1  /* != 0: one launch per tracking step (no persistent loop) */
+#define GNSS_OPT_FORCE_VPB    2  /* >= 2: virtual blocks per resident block of the loop     */
+#define GNSS_OPT_ACQ_ROCFFT   3  /* != 0: rocFFT instead of the own P x 2000 correlator     */
+#define GNSS_OPT_FINE_ROCFFT  4  /* != 0: rocFFT for the fine-frequency transform           */
+#define GNSS_OPT_ACQ_BATCH    5  /* > 0: (bin, PRN) pairs per correlator batch              */
+#define GNSS_OPT_COUNT        6
+int  gnss_ctx_set_option(gnss_ctx *ctx, int key, int64_t value);
 
 /* Device memory owned by the ctx, for callers that keep an IF record resident
  * in HBM (gnss_file.dev_data) across calls. */

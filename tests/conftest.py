@@ -32,9 +32,25 @@ def po():
 
 @pytest.fixture(scope="session")
 def ctx(pkg):
+    import torch  # noqa: F401  (before the library: some tests hand it torch device tensors)
     c = pkg.Context(0)
     yield c
     c.close()
+
+
+@pytest.fixture
+def opts(pkg, ctx):
+    """opts(key, value): a gnss_ctx_set_option test hook on the shared context, reset to the
+    engine's own choice (0) when the test ends."""
+    used = set()
+
+    def set_opt(key, value):
+        used.add(key)
+        ctx.set_option(key, value)
+
+    yield set_opt
+    for k in used:
+        ctx.set_option(k, 0)
 
 
 @pytest.fixture(scope="session")

@@ -30,10 +30,10 @@ def opensky_acq(pkg, po):
 
 @pytest.mark.parametrize("prec,dtyp", FORMATS, ids=FMT_IDS)
 @pytest.mark.parametrize("path", ["own-fft", "rocfft"])
-def test_acquisition_formats(pkg, po, ctx, opensky_acq, monkeypatch, prec, dtyp, path):
+def test_acquisition_formats(pkg, po, ctx, opensky_acq, opts, prec, dtyp, path):
     if path == "rocfft":
-        monkeypatch.setenv("GNSS_ACQ_ROCFFT", "1")
-        monkeypatch.setenv("GNSS_FINE_ROCFFT", "1")
+        opts(pkg.abi.OPT_ACQ_ROCFFT, 1)
+        opts(pkg.abi.OPT_FINE_ROCFFT, 1)
     skip, iq8 = opensky_acq
     rec = pkg.synth.convert_record(iq8, prec, dtyp)
     file = _file(pkg, rec, skip, prec, dtyp)
@@ -66,11 +66,11 @@ def opensky_trk(pkg, po):
 
 @pytest.mark.parametrize("prec,dtyp", FORMATS, ids=FMT_IDS)
 @pytest.mark.parametrize("sub", ["default", "1"])
-def test_tracking_formats(pkg, po, ctx, opensky_trk, monkeypatch, prec, dtyp, sub):
+def test_tracking_formats(pkg, po, ctx, opensky_trk, opts, prec, dtyp, sub):
     """300 ms @1 ms + 200 ms @10 ms, 3 channels; int16 runs the per-step kernel with the
     mean of every read from prefix sums, int8 real the int8 kernels on (x, 0) pairs."""
     if sub != "default":
-        monkeypatch.setenv("GNSS_FORCE_SUB", sub)
+        opts(pkg.abi.OPT_FORCE_SUB, int(sub))
     skip, iq8 = opensky_trk
     rec = pkg.synth.convert_record(iq8, prec, dtyp)
     file = _file(pkg, rec, skip, prec, dtyp)

@@ -63,10 +63,10 @@ def test_pos_parity_opensky_8ch(pkg, po, ctx, opensky_short):
 
 @pytest.mark.parametrize("persist", [True, False], ids=["persistent", "step"])
 @pytest.mark.parametrize("sub", ["1", "3"])
-def test_pos_parity_kernel_variants(pkg, po, ctx, opensky_short, monkeypatch, sub, persist):
-    monkeypatch.setenv("GNSS_FORCE_SUB", sub)
+def test_pos_parity_kernel_variants(pkg, po, ctx, opensky_short, opts, sub, persist):
+    opts(pkg.abi.OPT_FORCE_SUB, int(sub))
     if not persist:
-        monkeypatch.setenv("GNSS_NO_PERSIST", "1")
+        opts(pkg.abi.OPT_NO_PERSIST, 1)
     skip, cfg, data = opensky_short
     file, signal, acq, track = params(pkg, skip, data)
     track.msToProcessCT_1ms, track.ctPOS = 300, 360
@@ -77,7 +77,7 @@ def test_pos_parity_kernel_variants(pkg, po, ctx, opensky_short, monkeypatch, su
     compare_pos(pkg, g, r)
 
 
-def test_pos_persistent_and_step_paths_bit_identical(pkg, ctx, opensky_short, monkeypatch):
+def test_pos_persistent_and_step_paths_bit_identical(pkg, ctx, opensky_short, opts):
     skip, cfg, data = opensky_short
     file, signal, acq, track = params(pkg, skip, data)
     track.msToProcessCT_1ms, track.ctPOS = 300, 400
@@ -85,7 +85,7 @@ def test_pos_persistent_and_step_paths_bit_identical(pkg, ctx, opensky_short, mo
     cx = [12, 3, 13]
     p = pkg.trackingCT_POS(file, signal, track, A, cx, ctx=ctx, raw=True)
     assert ctx.timing()["track_launches"] <= 4
-    monkeypatch.setenv("GNSS_NO_PERSIST", "1")
+    opts(pkg.abi.OPT_NO_PERSIST, 1)
     q = pkg.trackingCT_POS(file, signal, track, A, cx, ctx=ctx, raw=True)
     assert ctx.timing()["track_launches"] > 100
     assert np.array_equal(p.rec, q.rec) and np.array_equal(p.CN0, q.CN0)

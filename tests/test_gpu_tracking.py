@@ -68,11 +68,11 @@ def test_tracking_parity_opensky_8ch(pkg, po, ctx, opensky_short):
 
 @pytest.mark.parametrize("persist", [True, False], ids=["persistent", "step"])
 @pytest.mark.parametrize("sub", ["1", "2", "3", "4"])
-def test_tracking_parity_every_kernel_variant(pkg, po, ctx, opensky_short, monkeypatch, sub, persist):
+def test_tracking_parity_every_kernel_variant(pkg, po, ctx, opensky_short, opts, sub, persist):
     """Every lane span, through the persistent step loop and through one launch per step."""
-    monkeypatch.setenv("GNSS_FORCE_SUB", sub)
+    opts(pkg.abi.OPT_FORCE_SUB, int(sub))
     if not persist:
-        monkeypatch.setenv("GNSS_NO_PERSIST", "1")
+        opts(pkg.abi.OPT_NO_PERSIST, 1)
     skip, cfg, data = opensky_short
     file, signal, acq, track = params(pkg, skip, data)
     track.msToProcessCT_1ms, track.msToProcessCT_10ms = 700, 300
@@ -184,7 +184,7 @@ def test_channel_shards_equal_full_run(pkg, ctx, opensky_short):
         assert full.len[c] == part.len[c] and full.countinx[c] == part.countinx[c]
 
 
-def test_persistent_and_step_paths_bit_identical(pkg, ctx, opensky_short, monkeypatch):
+def test_persistent_and_step_paths_bit_identical(pkg, ctx, opensky_short, opts):
     """The persistent loop and one launch per step share the lane geometry and both
     fixed-order reductions: the same records to the last bit."""
     skip, cfg, data = opensky_short
@@ -193,7 +193,7 @@ def test_persistent_and_step_paths_bit_identical(pkg, ctx, opensky_short, monkey
     A = acquired_of([3, 16, 22], [3684, 26051, 2611], [4580975.0, 4579675.0, 4581525.0])
     p = pkg.trackingCT(file, signal, track, A, ctx=ctx, raw=True)
     assert ctx.timing()["track_launches"] <= 4
-    monkeypatch.setenv("GNSS_NO_PERSIST", "1")
+    opts(pkg.abi.OPT_NO_PERSIST, 1)
     q = pkg.trackingCT(file, signal, track, A, ctx=ctx, raw=True)
     assert ctx.timing()["track_launches"] > 100
     for c in range(3):
@@ -304,7 +304,7 @@ def test_streamed_windows_equal_resident(pkg, ctx, opensky_short, tmp_path, rout
 
 
 @pytest.mark.parametrize("ntaps,vpb", [(3, 4), (11, 3)])
-def test_virtual_blocks_bit_identical(pkg, ctx, opensky_short, monkeypatch, ntaps, vpb):
+def test_virtual_blocks_bit_identical(pkg, ctx, opensky_short, opts, ntaps, vpb):
     """The persistent loop with several of the step's blocks per resident block (how 32
     channels x 11 taps stay persistent on one GPU) gives the same records as one block each
     and as the per-step path."""
@@ -314,11 +314,11 @@ def test_virtual_blocks_bit_identical(pkg, ctx, opensky_short, monkeypatch, ntap
     taps = pkg.colon(-0.5, 0.1, 0.5) if ntaps == 11 else None
     A = acquired_of([3, 16, 22], [3684, 26051, 2611], [4580975.0, 4579675.0, 4581525.0])
     p = pkg.trackingCT(file, signal, track, A, ctx=ctx, taps=taps, raw=True)
-    monkeypatch.setenv("GNSS_FORCE_VPB", str(vpb))
+    opts(pkg.abi.OPT_FORCE_VPB, vpb)
     v = pkg.trackingCT(file, signal, track, A, ctx=ctx, taps=taps, raw=True)
     assert ctx.timing()["track_launches"] <= 4
-    monkeypatch.delenv("GNSS_FORCE_VPB")
-    monkeypatch.setenv("GNSS_NO_PERSIST", "1")
+    opts(pkg.abi.OPT_FORCE_VPB, 0)
+    opts(pkg.abi.OPT_NO_PERSIST, 1)
     q = pkg.trackingCT(file, signal, track, A, ctx=ctx, taps=taps, raw=True)
     for c in range(3):
         assert np.array_equal(p.rec[c], v.rec[c]) and np.array_equal(q.rec[c], v.rec[c]), c

@@ -1,0 +1,63 @@
+# One MI355X check, run from the repo root via gpurun:
+#   gpurun --timeout 1200 -- bash tools/gpu.sh STEP [STEP ...]
+# Steps run in order, each under its own time limit; the first failure ends the call.
+#   tests        pytest -m gpu (PYTEST_K="-k expr" narrows it)
+#   bench        python bench.py (BENCH_ARGS adds flags) -> gpurun_out/bench.json
+#   prof         rocprofv3 --kernel-trace --stats of one bench step -> gpurun_out/prof_bench(_summary.txt)
+#   traffic      FETCH_SIZE / WRITE_SIZE passes of the 10-ms tracking launch -> gpurun_out/traffic.json
+#   tracksq      SQ counter passes (VALU / LDS / waits) of the tracking launches -> gpurun_out/track_sq.json
+#   acqpmc       FETCH / WRITE + SQ passes of the fp64 acquisition kernels -> gpurun_out/acq_counters.json
+#   cfg5         bench --workload cfg5 + its PMC traffic + SQ passes -> gpurun_out/cfg5*.json
+set -o pipefail
+mkdir -p gpurun_out
+R=$GRAFT_REPO_ROOT
+cd "$R" || exit 1
+HEAD_SHA=$(cat "$R/.head_sha" 2>/dev/null || echo unknown)
+SQ1="SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
+SQ2="SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_SALU SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM SQ_ACTIVE_INST_SCA"
+SQ3="SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU"
+pmc() {  # pmc OUTDIR "COUNTERS" cmd...
+  local out=$1 ctrs=$2; shift 2
+  ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc $ctrs --kernel-trace --output-format csv -d "$R/gpurun_out/$out" -o run -- "$@" ) > "gpurun_out/$out.log" 2>&1 || { tail -20 "gpurun_out/$out.log"; return 1; }
+}
+for step in "$@"; do
+  echo "== $step $(date +%T)"
+  case $step in
+    tests)
+      timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread $PYTEST_K > gpurun_out/pytest_gpu.log 2>&1 \
+        && echo "TESTS_OK $(tail -1 gpurun_out/pytest_gpu.log)" || { grep -E "FAIL|Error" gpurun_out/pytest_gpu.log | tail -30; tail -40 gpurun_out/pytest_gpu.log; exit 1; } ;;
+    bench)
+      timeout -k 10 400 python3 bench.py $BENCH_ARGS > gpurun_out/bench.json 2> gpurun_out/bench.err \
+        && tail -1 gpurun_out/bench.json | cut -c1-700 || { tail -20 gpurun_out/bench.err; exit 1; } ;;
+    prof)
+      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_bench" -o run -- python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu ) > gpurun_out/bench_prof.json 2>&1 || { tail -20 gpurun_out/bench_prof.json; exit 1; }
+      python3 tools/prof_summary.py gpurun_out/prof_bench > gpurun_out/prof_bench_summary.txt && head -14 gpurun_out/prof_bench_summary.txt ;;
+    traffic)
+      pmc pmc_fetch FETCH_SIZE python3 "$R/tools/track_only.py" 1000 40000 || exit 1
+      pmc pmc_write WRITE_SIZE python3 "$R/tools/track_only.py" 1000 40000 || exit 1
+      python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write "track_run_kernel<3, 3, false, false>" gpurun_out/traffic.json "$HEAD_SHA" || exit 1
+      rm -f gpurun_out/pmc_*/**/*kernel_trace.csv ;;
+    tracksq)
+      pmc trk_sq1 "$SQ1" python3 "$R/tools/track_only.py" 100 400 || exit 1
+      pmc trk_sq2 "$SQ2" python3 "$R/tools/track_only.py" 100 400 || exit 1
+      pmc trk_sq3 "$SQ3" python3 "$R/tools/track_only.py" 100 400 || exit 1
+      python3 tools/pmc_sq.py gpurun_out/track_sq.json gpurun_out/trk_sq1 gpurun_out/trk_sq2 gpurun_out/trk_sq3 -- "track_run_kernel<3, 3, false, false>" "track_run_kernel<3, 1, false, false>" || exit 1
+      rm -f gpurun_out/trk_sq*/**/*kernel_trace.csv ;;
+    acqpmc)
+      pmc acq_fetch FETCH_SIZE python3 "$R/tools/acq_only.py" || exit 1
+      pmc acq_write WRITE_SIZE python3 "$R/tools/acq_only.py" || exit 1
+      pmc acq_sq1 "$SQ1" python3 "$R/tools/acq_only.py" || exit 1
+      pmc acq_sq2 "$SQ2" python3 "$R/tools/acq_only.py" || exit 1
+      python3 tools/pmc_sq.py gpurun_out/acq_counters.json gpurun_out/acq_fetch gpurun_out/acq_write gpurun_out/acq_sq1 gpurun_out/acq_sq2 -- "inv_cols_kernel<29, HIP_vector_type<double" "inv_rows_kernel_f64<29>" "fwd_rows_kernel<29" "fine_rows_kernel<29" "fine_cols_kernel<29>" || exit 1
+      rm -f gpurun_out/acq_*/**/*kernel_trace.csv ;;
+    cfg5)
+      timeout -k 10 500 python3 bench.py --workload cfg5 $BENCH_ARGS > gpurun_out/bench_cfg5.json 2> gpurun_out/bench_cfg5.err \
+        && tail -1 gpurun_out/bench_cfg5.json | cut -c1-700 || { tail -20 gpurun_out/bench_cfg5.err; exit 1; }
+      pmc c5_sq1 "$SQ1" python3 "$R/tools/track_only.py" 100 400 11 32 || exit 1
+      pmc c5_sq3 "$SQ3" python3 "$R/tools/track_only.py" 100 400 11 32 || exit 1
+      python3 tools/pmc_sq.py gpurun_out/cfg5_sq.json gpurun_out/c5_sq1 gpurun_out/c5_sq3 -- "track_run_kernel<11, 3" || exit 1
+      rm -f gpurun_out/c5_*/**/*kernel_trace.csv ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "== done $(date +%T)"
