@@ -109,13 +109,15 @@ class GnssTiming(C.Structure):
 class GnssVtChan(C.Structure):
     _fields_ = [("prn", C.c_int32), ("pad", C.c_int32), ("file_ptr", C.c_int64), ("remChip", C.c_double),
                 ("remCarrPhase", C.c_double), ("codeFreq", C.c_double), ("carrFreq", C.c_double),
-                ("carrFreqBasis", C.c_double), ("oldCarrNco", C.c_double), ("oldCarrError", C.c_double)]
+                ("carrFreqBasis", C.c_double), ("oldCarrNco", C.c_double), ("oldCarrError", C.c_double),
+                ("index_int", C.c_int32), ("snrIndex", C.c_int32), ("Zk", C.c_double * 20)]
 
 
 class GnssVtOut(C.Structure):
     _fields_ = [(f, C.c_double) for f in ("E_i", "E_q", "P_i", "P_q", "L_i", "L_q", "carrError", "codeError",
                                           "carrNco", "remChip", "remCarrPhase", "codeFreq", "carrFreq")] + \
-               [("numSample", C.c_int64), ("absoluteSample", C.c_int64), ("codedelay", C.c_double)]
+               [("numSample", C.c_int64), ("absoluteSample", C.c_int64), ("codedelay", C.c_double),
+                ("CN0", C.c_double), ("cn0_row", C.c_int32), ("status", C.c_int32)]
 
 
 class GnssSynthSv(C.Structure):
@@ -170,6 +172,9 @@ PROTOTYPES = {
                                       C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "gnss_synth_if_device": (C.c_int, [C.c_void_p, C.POINTER(GnssSynth), C.c_uint64, C.c_uint64,
                                        C.c_void_p]),
+    "gnss_tracking_vt_run": (C.c_int, [C.c_void_p, C.POINTER(GnssFile), C.POINTER(GnssSignal),
+                                       C.POINTER(GnssTrack), C.c_int32, C.c_int32, C.c_int32,
+                                       C.POINTER(GnssVtChan), C.POINTER(C.c_double), C.POINTER(GnssVtOut)]),
     "gnss_tracking_vt_step": (C.c_int, [C.c_void_p, C.POINTER(GnssFile), C.POINTER(GnssSignal),
                                         C.POINTER(GnssTrack), C.c_int32, C.c_int32, C.POINTER(GnssVtChan),
                                         C.POINTER(C.c_double), C.POINTER(GnssVtOut)]),

@@ -621,7 +621,6 @@ __global__ __launch_bounds__(kRowThreads) void fine_rows_kernel(
     __shared__ double2 s_a[kRow];
     const int rho = blockIdx.x, r = blockIdx.y, tid = threadIdx.x;
     const int m2 = rho / P, n2 = rho - m2 * P;
-    const int64_t RD = (int64_t)kRow * D;
     for (int m1 = tid; m1 < kRow; m1 += kRowThreads) {
         const int64_t n = (int64_t)P * T * m1 + (int64_t)P * m2 + n2;
         const double cvi = floor((invFs * (double)(n + 1)) / invFc);

@@ -1644,62 +1644,106 @@ extern "C" {
 // trackingVT_POS_updated.m:157-349, one step of n channels (include/gnss_mi355x.h): the
 // reads and replica chips sized on the host (gnss_vt_prepare), the carrier-wiped sums on
 // the GPU (vt.hip), the NCO / PLL / DLL discriminator on the host (gnss_vt_nco_step).
-int gnss_tracking_vt_step(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg, const gnss_track* tr,
-                          int32_t pdi, int32_t n, gnss_vt_chan* chans, const double* codeFreq_new,
-                          gnss_vt_out* out)
+int gnss_tracking_vt_run(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg, const gnss_track* tr,
+                         int32_t pdi, int32_t n, int32_t nsteps, gnss_vt_chan* chans, const double* codeFreq_new,
+                         gnss_vt_out* out)
 {
-    if (!ctx || !file || !sg || !tr || !chans || !codeFreq_new || !out || n < 1 || n > GNSS_MAX_SV || pdi < 1)
+    if (!ctx || !file || !sg || !tr || !chans || !codeFreq_new || !out || n < 1 || n > GNSS_MAX_SV || pdi < 1 ||
+        nsteps < 1 || !(sg->Fs > 0) || !(sg->codeFreqBasis > 0))
         return fail(ctx, GNSS_EARG, "bad arguments");
     ctx->err.clear();
     ctx->timing = gnss_timing{};
     HIP_TRY(hipSetDevice(ctx->device));
-    if (file->dataPrecision != 1 || file->dataType != 2)
-        return fail(ctx, GNSS_EARG, "vector tracking: int8 I/Q records only");
-    std::vector<int64_t> ns((size_t)n);
+    // formats of trackingVT_POS_updated.m:163-176: int8 I/Q, int8 real, int16 I/Q (means removed)
+    const int prec = file->dataPrecision, dtyp = file->dataType;
+    if (!((prec == 1 && (dtyp == 1 || dtyp == 2)) || (prec == 2 && dtyp == 2)))
+        return fail(ctx, GNSS_EARG, "vector tracking: int8 I/Q, int8 real or int16 I/Q records");
+    const int bps = prec * dtyp;
+    const int64_t flen = file_length(file);
+    if (flen < 0) return fail(ctx, GNSS_EIO, "cannot open IF record");
+    // the read range of every step: from the earliest file_ptr, at most nsteps reads of the
+    // largest size any step can ask for (the slowest code frequency of the series)
+    double cf_min = 1e300;
+    for (int i = 0; i < n; i++) {
+        if (chans[i].prn < 1 || chans[i].prn > 51) return fail(ctx, GNSS_EARG, "bad PRN");
+        if (chans[i].file_ptr < 0 || chans[i].file_ptr % bps) return fail(ctx, GNSS_EARG, "file_ptr");
+        if (chans[i].index_int < 0 || chans[i].index_int > 19 || chans[i].snrIndex < 1)
+            return fail(ctx, GNSS_EARG, "C/N0 state (index_int 0..19, snrIndex >= 1)");
+        cf_min = std::min(cf_min, chans[i].codeFreq);
+    }
+    for (int64_t k = 0; k < (int64_t)nsteps * n; k++) cf_min = std::min(cf_min, codeFreq_new[k]);
+    if (!(cf_min > 0)) return fail(ctx, GNSS_EARG, "code frequencies must be positive");
+    const double nmax = std::ceil((sg->codelength * pdi + 2.0) / (cf_min / sg->Fs)) + 2;
     int64_t lo = INT64_MAX, hi = 0;
     for (int i = 0; i < n; i++) {
-        int32_t code[3];
-        const int st = gnss_vt_prepare(sg, pdi, &chans[i], codeFreq_new[i], code, &ns[i]);
-        if (st) return fail(ctx, st, "channel %d: read size / replica index (trackingVT_POS_updated.m:161,240)", i);
-        if (chans[i].file_ptr < 0 || (chans[i].file_ptr & 1)) return fail(ctx, GNSS_EARG, "file_ptr");
         lo = std::min(lo, chans[i].file_ptr);
-        hi = std::max(hi, chans[i].file_ptr + 2 * ns[i]);
+        hi = std::max(hi, chans[i].file_ptr + (int64_t)(nsteps * nmax) * bps);
     }
-    if (hi > file_length(file)) return fail(ctx, GNSS_EIO, "read past the end of the IF record");
     IfWindow w;
-    int st = stage_window(ctx, file, lo, hi, w);
+    int st = stage_window(ctx, file, lo, std::min(hi, flen), w);
     if (st) return st;
-    std::vector<VtDesc> dh((size_t)n);
-    int64_t nmax = 0;
-    for (int i = 0; i < n; i++) {
-        dh[i] = VtDesc{chans[i].file_ptr - w.base, ns[i], chans[i].carrFreq, chans[i].remCarrPhase};
-        nmax = std::max(nmax, ns[i]);
-    }
-    const int nblk = vt_blocks(nmax);
-    DevBuf d_desc, d_part;
-    HIP_TRY(d_desc.alloc(ctx, "vt.desc", sizeof(VtDesc) * (size_t)n));
-    HIP_TRY(d_part.alloc(ctx, "vt.part", sizeof(double) * 2 * (size_t)n * nblk));
-    HIP_TRY(hipMemcpyAsync(d_desc.p, dh.data(), sizeof(VtDesc) * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+    std::vector<unsigned> cab((size_t)n * 32);
+    for (int i = 0; i < n; i++) ca_bits(chans[i].prn, &cab[(size_t)i * 32]);
+    DevBuf d_chan, d_cf, d_out, d_ca;
+    const size_t nrec = (size_t)nsteps * n;
+    HIP_TRY(d_chan.alloc(ctx, "vt.chan", sizeof(gnss_vt_chan) * (size_t)n));
+    HIP_TRY(d_cf.alloc(ctx, "vt.cf", sizeof(double) * nrec));
+    HIP_TRY(d_out.alloc(ctx, "vt.out", sizeof(gnss_vt_out) * nrec));
+    HIP_TRY(d_ca.alloc(ctx, "vt.ca", sizeof(unsigned) * cab.size()));
+    HIP_TRY(hipMemcpyAsync(d_chan.p, chans, sizeof(gnss_vt_chan) * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(d_cf.p, codeFreq_new, sizeof(double) * nrec, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(d_ca.p, cab.data(), sizeof(unsigned) * cab.size(), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemsetAsync(d_out.p, 0, sizeof(gnss_vt_out) * nrec, ctx->stream));
+    double t1, t2;
+    calc_loop_coef(tr->PLLBW, tr->PLLDamp, tr->PLLGain, t1, t2);
+    VtRunArgs A{};
+    A.rec = reinterpret_cast<const uint8_t*>(w.ptr);
+    A.base = w.base;
+    A.len = w.len;
+    A.file_len = flen;
+    A.chans = d_chan.as<gnss_vt_chan>();
+    A.codeFreq = d_cf.as<double>();
+    A.out = d_out.as<gnss_vt_out>();
+    A.ca_bits = d_ca.as<unsigned>();
+    A.Fs = sg->Fs;
+    A.ms = sg->ms;
+    A.codelength = sg->codelength;
+    A.tau1carr = t1;
+    A.tau2carr = t2;
+    A.n = n;
+    A.nsteps = nsteps;
+    A.pdi = pdi;
+    A.prec = prec;
+    A.dtype = dtyp;
     Events ev;
     HIP_TRY(hipEventRecord(ev.a, ctx->stream));
-    HIP_TRY(launch_vt_sums(w.ptr, 1, d_desc.as<VtDesc>(), n, sg->Fs, nblk, d_part.as<double>(), ctx->stream));
+    HIP_TRY(launch_vt_run(A, ctx->stream));
     HIP_TRY(hipEventRecord(ev.b, ctx->stream));
-    std::vector<double> ph((size_t)2 * n * nblk);
-    HIP_TRY(hipMemcpyAsync(ph.data(), d_part.p, ph.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(out, d_out.p, sizeof(gnss_vt_out) * nrec, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(chans, d_chan.p, sizeof(gnss_vt_chan) * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     ctx->timing.track_ms = ev.ms();
+    ctx->timing.track_kernel_ms = ctx->timing.track_ms;
     ctx->timing.track_launches = 1;
-    for (int i = 0; i < n; i++) {
-        double sI = 0.0, sQ = 0.0;
-        for (int b = 0; b < nblk; b++) {  // block order
-            sI += ph[((size_t)i * nblk + b) * 2];
-            sQ += ph[((size_t)i * nblk + b) * 2 + 1];
+    int first = GNSS_OK;
+    for (int s = 0; s < nsteps; s++)
+        for (int i = 0; i < n; i++) {
+            const gnss_vt_out& o = out[(size_t)s * n + i];
+            if (o.status) {
+                if (!first) first = o.status;
+            } else if (o.numSample > 0) {
+                ctx->timing.track_channel_samples += o.numSample;
+            }
         }
-        ctx->timing.track_channel_samples += ns[i];
-        const int s2 = gnss_vt_nco_step(sg, tr, pdi, &chans[i], codeFreq_new[i], sI, sQ, &out[i]);
-        if (s2) return fail(ctx, s2, "channel %d: NCO step", i);
-    }
+    if (first) return fail(ctx, first, "a channel stopped (its record's status): replica index / read past EOF");
     return GNSS_OK;
+}
+
+int gnss_tracking_vt_step(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg, const gnss_track* tr,
+                          int32_t pdi, int32_t n, gnss_vt_chan* chans, const double* codeFreq_new,
+                          gnss_vt_out* out)
+{
+    return gnss_tracking_vt_run(ctx, file, sg, tr, pdi, n, 1, chans, codeFreq_new, out);
 }
 
 int gnss_ca_code(int prn, int8_t* out1023)

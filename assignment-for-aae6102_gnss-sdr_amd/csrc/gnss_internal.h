@@ -371,18 +371,177 @@ struct SrcC64 {
     __device__ __forceinline__ double2 at(int64_t n) const { return p[n]; }
 };
 
-// Vector-tracking sums (vt.hip): channel i reads d.n samples from window byte d.A of `iq`
-// (int8 I/Q pairs, or int8 real with iq_pairs = 0) with carrier frequency f, phase phi0;
-// part[i][blk] = (sum I, sum Q) of block blk, nblk blocks per channel (vt_blocks).
-struct VtDesc {
-    int64_t A, n;
-    double f, phi0;
+// ---- Vector tracking (trackingVT_POS_updated.m:157-349): the scalar arithmetic of a step,
+// one source for the host half (vt.cpp, gnss_vt_nco_step) and the kernel's scalar end
+// (vt.hip), compiled with -ffp-contract=off on both sides so every operation rounds as
+// MATLAB's does (libm calls aside: atan / log10 / atan2 / hypot within an ulp).
+
+// C/N0 of one K = 20 block of Zk = P_i^2 + P_q^2 (trackingCT.m:120-134 and
+// trackingVT_POS_updated.m:297-301, the same estimator): mean, var over N - 1,
+// NA2 = sqrt(mean^2 - var) (complex where negative, quirk A.16), |10 log10(NA2 / (2 varIQ) / T)|
+GNSS_HD double cn0_moment(const double* Z, double T)
+{
+    double mean = 0;
+    for (int k = 0; k < 20; k++) mean += Z[k];
+    mean = mean / 20;
+    double var = 0;
+    for (int k = 0; k < 20; k++) var += (Z[k] - mean) * (Z[k] - mean);
+    var = var / 19;
+    const double m2v = mean * mean - var;
+    const double scale = 1 / T;
+    if (m2v >= 0) {
+        const double NA2 = sqrt(m2v);
+        const double varIQ = 0.5 * (mean - NA2);
+        return fabs(10 * log10(scale * NA2 / (2 * varIQ)));
+    }
+    const double y = sqrt(-m2v);  // NA2 = i*y
+    const double nr = 0, ni = scale * y;
+    const double dr = 2 * (0.5 * mean), di = 2 * (0.5 * -y);
+    const double den = dr * dr + di * di;
+    const double zr = (nr * dr + ni * di) / den, zi = (ni * dr - nr * di) / den;
+    const double lr = 10 * (log(hypot(zr, zi)) / log(10.0));
+    const double li = 10 * (atan2(zi, zr) / log(10.0));
+    return hypot(lr, li);
+}
+
+// Spacing = 0.7:-0.05:-0.7 (:27) as MATLAB's colon builds it; element i1 (1-based)
+GNSS_HD double vt_spacing(int i1)
+{
+    return colon_elem(colon_make(0.7, -0.05, -0.7), i1 - 1);
+}
+
+// The step's read size and replica chips (:161, :217-249): numSample with the LAST step's
+// code frequency; the E / P / L colons (0 + Spacing + remChip) : cps : ((n-1)*cps + Spacing +
+// remChip) with the new one must each have n elements (ceil_mx's concatenation and
+// t_CodePrompt(numSample)); chip index j = ceil(t(1)) + 1, clamped to 1025 (:240-246
+// inspects that one element), within Code = [CA(end) repmat(CA,1,pdi) CA(1)] (:110).
+struct VtPrep {
+    int64_t n;
+    int64_t j[3];  // 1-based indices into Code for E / P / L
+    int bad;
 };
-int vt_blocks(int64_t nmax);
+GNSS_HD VtPrep vt_prepare(double Fs, double codelength, int pdi, double remChip, double codeFreq_old,
+                          double codeFreq_new)
+{
+    VtPrep p{0, {1, 1, 1}, GNSS_OK};
+    const double ns = ceil((codelength * pdi - remChip) / (codeFreq_old / Fs));
+    if (!(ns >= 1) || ns > 1e9) {
+        p.bad = GNSS_EINDEX;
+        return p;
+    }
+    p.n = (int64_t)ns;
+    const double cps = codeFreq_new / Fs;  // :218
+    const int sp[3] = {5, 15, 25};
+    const int64_t len = 1023 * (int64_t)pdi + 2;
+    for (int s = 0; s < 3; s++) {
+        const double spc = vt_spacing(sp[s]);
+        const double a = (0 + spc) + remChip;
+        const Colon c = colon_make(a, cps, ((double)(p.n - 1) * cps + spc) + remChip);
+        if (c.n != p.n - 1) p.bad = GNSS_EINDEX;
+        double j = ceil(a) + 1;
+        if (j > 1025) j = 1025;
+        if (!(j >= 1) || j > (double)len) p.bad = GNSS_EINDEX;
+        p.j[s] = p.bad ? 1 : (int64_t)j;
+    }
+    return p;
+}
+
+// Code(j) for Code = [CA(1023) CA ... CA CA(1)], from CA chip values ca(i) (i 0-based)
+template <class CaAt>
+GNSS_HD int vt_code_at(int64_t j, int pdi, CaAt ca)
+{
+    const int64_t len = 1023 * (int64_t)pdi + 2;
+    return j == 1 ? ca(1022) : j == len ? ca(0) : ca((int)((j - 2) % 1023));
+}
+
+// The rest of the step from its sums (:247-249, :284-347): E / P / L, remChip, remCarrPhase,
+// the C/N0 estimator, PLL, DLL discriminator, the record; advances `c`. bps = bytes per
+// sample (dataPrecision * dataType), code[3] = the E / P / L chip values.
+GNSS_HD int vt_finish(double Fs, double ms, int pdi, int bps, double tau1carr, double tau2carr,
+                      gnss_vt_chan* c, const VtPrep& p, const int* code, double codeFreq_new, double sI,
+                      double sQ, gnss_vt_out* o)
+{
+    const int64_t n = p.n;
+    const double cps = codeFreq_new / Fs;
+    const double sp = vt_spacing(15);
+    const Colon col = colon_make((0 + sp) + c->remChip, cps, ((double)(n - 1) * cps + sp) + c->remChip);
+    if (col.n != n - 1) return GNSS_EINDEX;
+    const double remChip = (colon_elem(col, n - 1) + cps) - 1023 * pdi;  // :284
+    // Wave(numSample+1) = 2*pi*(carrFreq * (numSample/Fs)) + remCarrPhase (:275-276, :285)
+    const double W = kTwoPi * (c->carrFreq * ((double)n / Fs)) + c->remCarrPhase;
+    const double remCarrPhase = fmod(W, kTwoPi);
+    o->E_i = code[0] * sI;
+    o->E_q = code[0] * sQ;
+    o->P_i = code[1] * sI;
+    o->P_q = code[1] * sQ;
+    o->L_i = code[2] * sI;
+    o->L_q = code[2] * sQ;
+    // C/N0 (:292-304; flag_snr is 1 throughout)
+    o->CN0 = 0;
+    o->cn0_row = 0;
+    c->index_int += 1;
+    c->Zk[c->index_int - 1] = o->P_i * o->P_i + o->P_q * o->P_q;
+    if (c->index_int % 20 == 0) {
+        o->CN0 = cn0_moment(c->Zk, 1 * ms * pdi);
+        o->cn0_row = c->snrIndex;
+        c->index_int = 0;
+        c->snrIndex += 1;
+    }
+    // PLL (:305-311)
+    const double carrError = atan(o->P_q / o->P_i) / (2.0 * 3.14159265358979323846);
+    const double carrNco = c->oldCarrNco + (tau2carr / tau1carr) * (carrError - c->oldCarrError) +
+                           carrError * (pdi * 1e-3 / tau1carr);
+    const double carrFreq = c->carrFreqBasis + carrNco;
+    // DLL discriminator (:314-316)
+    const double E = sqrt(o->E_i * o->E_i + o->E_q * o->E_q);
+    const double L = sqrt(o->L_i * o->L_i + o->L_q * o->L_q);
+    o->codeError = -0.5 * (E - L) / (E + L);
+    o->carrError = carrError;
+    o->carrNco = carrNco;
+    o->remChip = remChip;
+    o->remCarrPhase = remCarrPhase;
+    o->codeFreq = codeFreq_new;
+    o->carrFreq = carrFreq;
+    o->numSample = n;
+    // ftell after reading numSample samples (:162-176, :344); codedelay =
+    // mod(absoluteSample / (dataPrecision * dataType), Fs * ms) (:347)
+    const int64_t absS = c->file_ptr + n * bps;
+    o->absoluteSample = absS;
+    o->codedelay = fmod_pos((double)absS / bps, Fs * ms);
+    o->status = GNSS_OK;
+    c->file_ptr = absS;
+    c->remChip = remChip;
+    c->remCarrPhase = remCarrPhase;
+    c->codeFreq = codeFreq_new;
+    c->carrFreq = carrFreq;
+    c->oldCarrNco = carrNco;
+    c->oldCarrError = carrError;
+    return GNSS_OK;
+}
+
+// calcLoopCoef.m:41-45
+GNSS_HD void calc_loop_coef(double LBW, double zeta, double k, double& t1, double& t2)
+{
+    const double Wn = LBW * 8 * zeta / (4 * (zeta * zeta) + 1);
+    t1 = k / (Wn * Wn);
+    t2 = 2.0 * zeta / Wn;
+}
+
+// The multi-step kernel (vt.hip): one workgroup per channel loops over nsteps steps.
+struct VtRunArgs {
+    const uint8_t* rec;       // staged record window; byte b of the file at rec[b - base]
+    int64_t base, len;        // window [base, base + len) in file bytes
+    int64_t file_len;         // the file's length (bytes): EIO past it
+    gnss_vt_chan* chans;      // [n], advanced in place
+    const double* codeFreq;   // [nsteps][n]
+    gnss_vt_out* out;         // [nsteps][n]
+    const unsigned* ca_bits;  // [n][32] C/A chips as sign bits (bit set: -1)
+    double Fs, ms, codelength, tau1carr, tau2carr;
+    int n, nsteps, pdi, prec, dtype;
+};
+hipError_t launch_vt_run(const VtRunArgs& a, hipStream_t s);
 // generateCAcode.m's 1023 +-1 chips of `prn` (host)
 void ca_chips(int prn, float* out);
-hipError_t launch_vt_sums(const int8_t* iq, int iq_pairs, const VtDesc* desc, int nch, double Fs, int nblk,
-                          double* part, hipStream_t s);
 
 // Synthetic IF (synth.hip)
 hipError_t launch_synth_if(const gnss_synth& cfg, const float* ca, uint64_t sample0,

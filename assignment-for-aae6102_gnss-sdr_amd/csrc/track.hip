@@ -564,32 +564,11 @@ __device__ __noinline__ void write_record(const TrkParams& p, const TrkBuffers& 
 // C/N0 of one 20-sample window of |P|^2 (trackingCT.m:124-131; moment method), out of
 // line: it runs once every 20 steps and its log/hypot/atan2 would otherwise sit in the
 // registers of the persistent step loop.
+// (out of line: keeps the persistent step loop's register budget; the arithmetic is
+// cn0_moment's, shared with the vector-tracking steps)
 __device__ __noinline__ double cn0_estimate(const double (&Z)[20], double T)
 {
-    double mean = 0;
-#pragma unroll
-    for (int k = 0; k < 20; k++) mean += Z[k];
-    mean = mean / 20;
-    double var = 0;
-#pragma unroll
-    for (int k = 0; k < 20; k++) var += (Z[k] - mean) * (Z[k] - mean);
-    var = var / 19;
-    const double m2v = mean * mean - var;
-    const double scale = 1 / T;
-    if (m2v >= 0) {
-        const double NA2 = sqrt(m2v);
-        const double varIQ = 0.5 * (mean - NA2);
-        return fabs(10 * log10(scale * NA2 / (2 * varIQ)));
-    }
-    // complex sqrt branch of MATLAB (quirk A.16)
-    const double y = sqrt(-m2v);
-    const double nr = 0, ni = scale * y;
-    const double dr = 2 * (0.5 * mean), di = 2 * (0.5 * -y);
-    const double den = dr * dr + di * di;
-    const double zr = (nr * dr + ni * di) / den, zi = (ni * dr - nr * di) / den;
-    const double lr = 10 * (log(hypot(zr, zi)) / log(10.0));
-    const double li = 10 * (atan2(zi, zr) / log(10.0));
-    return hypot(lr, li);
+    return cn0_moment(Z, T);
 }
 
 // The channel state after the step, with the C/N0 estimator (trackingCT.m:120-134).
@@ -717,7 +696,8 @@ struct LdsRaw {
 
 // Timing-probe builds only (tools/build_probe.sh, never the product library): bit 1 drops
 // the lane's sincos, bit 2 the per-tap boundary search, bit 4 the per-sample Wave / eta
-// (the rotation table alone). Their sums are wrong; they time the correlator's parts.
+// (the rotation table alone), bit 8 the whole lane correlate. Their sums are wrong; they time
+// (and count the instructions of) the correlator's parts.
 #ifndef GNSS_CORR_PROBE
 #define GNSS_CORR_PROBE 0
 #endif
@@ -729,6 +709,11 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
 {
     constexpr int M = 8 * SUB;
     constexpr int T = kTrkThreads;
+    if constexpr ((GNSS_CORR_PROBE & 8) != 0) {  // (probe: no correlate at all)
+#pragma unroll
+        for (int s = 0; s < NT; s++) { oI[s] = 0.0; oQ[s] = 0.0; }
+        return;
+    }
     const int64_t n = uni(dp->n);
     const double d = uni(dp->d), inv_d = uni(dp->inv_d);
     const double f = uni(dp->f), phi0 = uni(dp->phi0);

@@ -1,70 +1,137 @@
-// vt.hip — the carrier wipe and sums of a vector-tracking step for gfx950
-// (trackingVT_POS_updated.m:262-272): sum(imag(rawsignal .* carrsig)) and
-// sum(real(rawsignal .* carrsig)) over each channel's numSample samples, with the
-// reference's own Wave(k) = (2*pi*(carrFreq .* ((0:numSample)/Fs))) + remCarrPhase rounding
-// per sample (exact IEEE division k/Fs) and an fp64 sincos of the 2*pi-reduced phase. The
-// reference's replica quirk multiplies these two sums by one chip value per tap (vt.cpp),
-// so no code replica is generated here. Each block reduces its lanes in a fixed order and
-// stores one partial; the host adds the partials in block order (bit-reproducible).
+// vt.hip — vector-tracking steps for gfx950 (trackingVT_POS_updated.m:157-349, the tracking
+// half): one workgroup per channel runs nsteps steps in one launch. Per step, lane 0 sizes
+// the read and finds the replica chips (vt_prepare), every lane sums its strided share of
+// the carrier-wiped samples -- sum(imag(rawsignal .* carrsig)), sum(real(rawsignal .*
+// carrsig)) with the reference's own Wave(k) = (2*pi*(carrFreq .* ((0:numSample)/Fs))) +
+// remCarrPhase rounding per sample (IEEE division k/Fs) and an fp64 sincos of the 2*pi-reduced
+// phase -- the workgroup reduces them in a fixed pairing (bit-reproducible), and lane 0 runs
+// the scalar end (vt_finish: remChip, remCarrPhase, C/N0, PLL, DLL discriminator, the record),
+// the same source as the host half (vt.cpp). The reference's replica quirk multiplies the two
+// sums by one chip value per tap, so no code replica is generated. Formats (:163-176): int8
+// I/Q, int8 real, int16 I/Q with each read's means removed. A step is latency-bound (one
+// channel's ~58 000 samples per ms on one CU); the entry point is the drop-in for the
+// reference's loop, which runs one step of one channel at a time.
 #include "gnss_internal.h"
 
 namespace gnss {
 
 namespace {
 
-constexpr int kVtThreads = 256;
+constexpr int kVtRun = 1024;
 
-__global__ __launch_bounds__(kVtThreads) void vt_sum_kernel(const int8_t* __restrict__ iq, int iq_pairs,
-                                                            const VtDesc* __restrict__ desc, double Fs,
-                                                            int nblk, double* __restrict__ part)
+__device__ __forceinline__ int16_t ld_i16(const uint8_t* p)
 {
-    const int ch = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x;
-    const VtDesc d = desc[ch];
-    double sI = 0.0, sQ = 0.0;
-    for (int64_t k = (int64_t)blk * kVtThreads + tid; k < d.n; k += (int64_t)nblk * kVtThreads) {
-        // Wave(k+1) in MATLAB's 1-based terms = 2*pi*(f*(k/Fs)) + phi0 (0-based k)
-        const double W = kTwoPi * (d.f * ((double)k / Fs)) + d.phi0;
-        const double q = rint(W * (1.0 / kTwoPi));
-        double r = __builtin_fma(-q, kTwoPi, W);  // exact: both multiples of 2^-50 below 8
-        r = __builtin_fma(-q, kTwoPiLo, r);
-        double sn, cs;
-        sincos(r, &sn, &cs);
-        double xr, xi;
-        if (iq_pairs) {
-            xr = (double)iq[d.A + 2 * k];
-            xi = (double)iq[d.A + 2 * k + 1];
-        } else {  // int8 real record: rawsignal is real (:172-175)
-            xr = (double)iq[d.A + k];
-            xi = 0.0;
-        }
-        sI += xr * sn + xi * cs;  // imag(raw .* carrsig)
-        sQ += xr * cs - xi * sn;  // real(raw .* carrsig)
-    }
-    __shared__ double s_i[kVtThreads], s_q[kVtThreads];
-    s_i[tid] = sI;
-    s_q[tid] = sQ;
-    __syncthreads();
-    for (int h = kVtThreads / 2; h > 0; h >>= 1) {  // fixed pairing
+    return (int16_t)((unsigned)p[0] | ((unsigned)p[1] << 8));
+}
+
+// Fixed-pairing tree over the workgroup: v[0] = the sum, the same bits for the same inputs
+__device__ __forceinline__ void tree2(double* r0, double* r1, int tid)
+{
+    for (int h = kVtRun / 2; h > 0; h >>= 1) {
+        __syncthreads();
         if (tid < h) {
-            s_i[tid] += s_i[tid + h];
-            s_q[tid] += s_q[tid + h];
+            r0[tid] += r0[tid + h];
+            r1[tid] += r1[tid + h];
+        }
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kVtRun) void vt_run_kernel(VtRunArgs a)
+{
+    const int ch = blockIdx.x, tid = threadIdx.x;
+    __shared__ gnss_vt_chan s_c;
+    __shared__ VtPrep s_p;
+    __shared__ int s_bad;
+    __shared__ double s_r0[kVtRun], s_r1[kVtRun];
+    if (tid == 0) s_c = a.chans[ch];
+    const int bps = a.prec * a.dtype;  // bytes per sample (ftell advance, :344)
+    const bool iq16 = a.prec == 2, real8 = a.prec == 1 && a.dtype == 1;
+    const unsigned* cab = a.ca_bits + 32 * ch;
+    for (int s = 0; s < a.nsteps; s++) {
+        gnss_vt_out* o = a.out + (int64_t)s * a.n + ch;
+        const double cf = a.codeFreq[(int64_t)s * a.n + ch];
+        if (tid == 0) {
+            VtPrep p = vt_prepare(a.Fs, a.codelength, a.pdi, s_c.remChip, s_c.codeFreq, cf);
+            int bad = !(cf > 0) ? GNSS_EARG : p.bad;
+            if (!bad) {
+                const int64_t A = s_c.file_ptr, need = p.n * bps;
+                // a short fread makes `rawsignal .* carrsig` fail in MATLAB (:172, :279)
+                if (A + need > a.file_len) bad = GNSS_EIO;
+                else if (A < a.base || A + need > a.base + a.len) bad = GNSS_EIO;  // (outside the window)
+            }
+            s_p = p;
+            s_bad = bad;
+            if (bad) o->status = bad;
         }
         __syncthreads();
+        if (s_bad) break;
+        const int64_t n = s_p.n;
+        const uint8_t* r = a.rec + (s_c.file_ptr - a.base);
+        const double f = s_c.carrFreq, phi0 = s_c.remCarrPhase;
+        // int16: rawsignal = (I - mean(I)) + 1i*(Q - mean(Q)) over this read (:166-170); the
+        // integer sums are exact in fp64, the mean one division as MATLAB's mean
+        double mu_i = 0.0, mu_q = 0.0;
+        if (iq16) {
+            double si = 0.0, sq = 0.0;
+            for (int64_t k = tid; k < n; k += kVtRun) {
+                si += (double)ld_i16(r + 4 * k);
+                sq += (double)ld_i16(r + 4 * k + 2);
+            }
+            s_r0[tid] = si;
+            s_r1[tid] = sq;
+            tree2(s_r0, s_r1, tid);
+            mu_i = s_r0[0] / (double)n;
+            mu_q = s_r1[0] / (double)n;
+            __syncthreads();
+        }
+        double sI = 0.0, sQ = 0.0;
+        for (int64_t k = tid; k < n; k += kVtRun) {
+            // Wave(k+1) in MATLAB's 1-based terms = 2*pi*(f*(k/Fs)) + phi0 (0-based k)
+            const double W = kTwoPi * (f * ((double)k / a.Fs)) + phi0;
+            const double q = rint(W * (1.0 / kTwoPi));
+            double rr = __builtin_fma(-q, kTwoPi, W);  // exact: both multiples of 2^-50 below 8
+            rr = __builtin_fma(-q, kTwoPiLo, rr);
+            double sn, cs;
+            sincos(rr, &sn, &cs);
+            double xr, xi;
+            if (iq16) {
+                xr = (double)ld_i16(r + 4 * k) - mu_i;
+                xi = (double)ld_i16(r + 4 * k + 2) - mu_q;
+            } else if (real8) {  // int8 real record: rawsignal is real (:172-175)
+                xr = (double)(int8_t)r[k];
+                xi = 0.0;
+            } else {
+                xr = (double)(int8_t)r[2 * k];
+                xi = (double)(int8_t)r[2 * k + 1];
+            }
+            sI += xr * sn + xi * cs;  // imag(raw .* carrsig) (:279)
+            sQ += xr * cs - xi * sn;  // real(raw .* carrsig) (:280)
+        }
+        s_r0[tid] = sI;
+        s_r1[tid] = sQ;
+        tree2(s_r0, s_r1, tid);
+        if (tid == 0) {
+            int code[3];
+            for (int t = 0; t < 3; t++)
+                code[t] = vt_code_at(s_p.j[t], a.pdi, [&](int i) { return ((cab[i >> 5] >> (i & 31)) & 1u) ? -1 : 1; });
+            const int st = vt_finish(a.Fs, a.ms, a.pdi, bps, a.tau1carr, a.tau2carr, &s_c, s_p, code, cf,
+                                     s_r0[0], s_r1[0], o);
+            s_bad = st;
+            if (st) o->status = st;
+        }
+        __syncthreads();
+        if (s_bad) break;
     }
-    if (tid == 0) {
-        part[((int64_t)ch * nblk + blk) * 2] = s_i[0];
-        part[((int64_t)ch * nblk + blk) * 2 + 1] = s_q[0];
-    }
+    __syncthreads();
+    if (tid == 0) a.chans[ch] = s_c;
 }
 
 }  // namespace
 
-int vt_blocks(int64_t nmax) { return (int)std::min<int64_t>(64, (nmax + 32 * kVtThreads - 1) / (32 * kVtThreads)); }
-
-hipError_t launch_vt_sums(const int8_t* iq, int iq_pairs, const VtDesc* desc, int nch, double Fs, int nblk,
-                          double* part, hipStream_t s)
+hipError_t launch_vt_run(const VtRunArgs& a, hipStream_t s)
 {
-    hipLaunchKernelGGL(vt_sum_kernel, dim3(nblk, nch), dim3(kVtThreads), 0, s, iq, iq_pairs, desc, Fs, nblk, part);
+    hipLaunchKernelGGL(vt_run_kernel, dim3(a.n), dim3(kVtRun), 0, s, a);
     return hipGetLastError();
 }
 

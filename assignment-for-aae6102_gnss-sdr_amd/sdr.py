@@ -612,11 +612,12 @@ def ca_code(prn: int) -> np.ndarray:
 def vt_channel(prn, file_ptr, remChip, remCarrPhase, codeFreq, carrFreq, carrFreqBasis, oldCarrNco=0.0,
                oldCarrError=0.0):
     """A vector-tracking channel state (gnss_vt_chan): the initialisation of
-    trackingVT_POS_updated.m:108-125 (from TckResultCT at msStartTckVT in the reference)."""
+    trackingVT_POS_updated.m:108-125 (from TckResultCT at msStartTckVT in the reference) and
+    of the C/N0 estimator (:78-81: index_int 0, snrIndex 1)."""
     return abi.GnssVtChan(prn=int(prn), pad=0, file_ptr=int(file_ptr), remChip=float(remChip),
                           remCarrPhase=float(remCarrPhase), codeFreq=float(codeFreq), carrFreq=float(carrFreq),
                           carrFreqBasis=float(carrFreqBasis), oldCarrNco=float(oldCarrNco),
-                          oldCarrError=float(oldCarrError))
+                          oldCarrError=float(oldCarrError), index_int=0, snrIndex=1)
 
 
 def trackingVT_step(file, signal, track, chans, codeFreq_new, pdi=1, *, ctx: Context | None = None):
@@ -639,6 +640,33 @@ def trackingVT_step(file, signal, track, chans, codeFreq_new, pdi=1, *, ctx: Con
     for i in range(n):
         C.memmove(C.byref(chans[i]), C.byref(arr[i]), C.sizeof(abi.GnssVtChan))
     return [{k: getattr(o, k) for k, _ in abi.GnssVtOut._fields_} for o in outs]
+
+
+def trackingVT_run(file, signal, track, chans, codeFreq_series, pdi=1, *, ctx: Context | None = None):
+    """nsteps steps of trackingVT_POS_updated.m's tracking half (:157-349) for every channel in
+    ONE launch (gnss_tracking_vt_run): codeFreq_series[s][i] = channel i's code frequency of
+    step s (the caller's EKF prediction, :211-215, or a recorded series); `chans` advanced in
+    place. Returns a dict of [nsteps][n] arrays: TckResultVT(prn).*(msIndex) (:319-346), CN0
+    and cn0_row (CN0_VT(cn0_row, svindex), :301), status."""
+    ctx = ctx or default_context()
+    n = len(chans)
+    cf = np.ascontiguousarray(codeFreq_series, dtype=np.float64)
+    if cf.ndim != 2 or cf.shape[1] != n:
+        raise ValueError("codeFreq_series: [nsteps][n]")
+    nsteps = cf.shape[0]
+    arr = (abi.GnssVtChan * n)(*chans)
+    outs = (abi.GnssVtOut * (nsteps * n))()
+    f, keep = to_c_file(file)
+    s = to_c_signal(signal)
+    t, keep2 = to_c_track(track)
+    st = ctx.lib.gnss_tracking_vt_run(ctx.h, C.byref(f), C.byref(s), C.byref(t), int(pdi), n, nsteps, arr,
+                                      cf.ctypes.data_as(C.POINTER(C.c_double)), outs)
+    for i in range(n):
+        C.memmove(C.byref(chans[i]), C.byref(arr[i]), C.sizeof(abi.GnssVtChan))
+    rec = np.frombuffer(outs, dtype=np.dtype([(k, {C.c_double: "f8", C.c_int64: "i8", C.c_int32: "i4"}[t_])
+                                              for k, t_ in abi.GnssVtOut._fields_])).reshape(nsteps, n)
+    ctx.check(st)
+    return {k: rec[k].copy() for k in rec.dtype.names}
 
 
 def correlate_step(file, signal, prn, pdi, remChip, codeFreq, carrierFreq, remPhase, pos_bytes,

@@ -33,10 +33,66 @@ sys.path.insert(0, ROOT)
 pkg = importlib.import_module("assignment-for-aae6102_gnss-sdr_amd")
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X vector fp64 (half the 157.3 TF fp32 vector rate: 4-cycle wave64 fp64 ops)
+N_SIMD = 1024  # 256 CUs x 4 SIMDs
+CLOCK_GHZ = 2.4
 SAMPLES_PER_MS = 58000  # Opensky Fs 58 MHz
-TRAFFIC_FILE = "traffic_r02.json"
-ACQ_BOUND_FILE = "acq_bound_r02.json"
-TRAFFIC_FILE_CFG5 = "traffic_cfg5_r02.json"  # PMC bytes per launch of the 11-tap 10-ms launch  # counters of the fp64 acquisition kernels (tools/acq_bound.py)  # PMC bytes per launch of the dominant kernel (this round's pass)
+# counter evidence read by the bench, newest first; each file carries the source digest it was
+# measured at (tools/srcdigest.py) and the line says whether it matches the running tree
+TRAFFIC_FILES = ("traffic_r03.json", "traffic_r02.json")          # PMC bytes per 10-ms launch
+TRACK_SQ_FILES = ("r03_track_sq.json",)                            # SQ counters of the tracking launches
+ACQ_BOUND_FILES = ("acq_bound_r03.json", "acq_bound_r02.json")     # fp64 acquisition kernels (tools/acq_bound.py)
+TRAFFIC_FILES_CFG5 = ("traffic_cfg5_r03.json", "traffic_cfg5_r02.json")  # the 11-tap 10-ms launch
+CFG5_SQ_FILES = ("r03_cfg5_sq.json",)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import srcdigest  # noqa: E402
+
+SRC_DIGEST = srcdigest.src_digest()
+
+
+def evidence(names):
+    """The first profiles/<name> that exists, and its provenance: the source digest / commit
+    it was measured at and whether that digest is the running tree's."""
+    for n in names:
+        try:
+            with open(os.path.join(ROOT, "profiles", n)) as fh:
+                d = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        meta = d.get("_meta", d) if isinstance(d, dict) else {}
+        dig = meta.get("src_digest")
+        return d, {"file": f"profiles/{n}", "src_digest": dig, "git_commit": meta.get("git_commit"),
+                   "matches_code": dig == SRC_DIGEST}
+    return None, None
+
+
+def valu_roofline(sq, kernel, steps_per_dispatch=None):
+    """fp64 VALU line of a kernel from its SQ counter passes (chip totals per dispatch,
+    tools/pmc_sq.py): achieved fp64 TFLOP/s (FMA = 2) against the 78.6 TF vector peak, and the
+    VALU issue fraction (fp64 ops 4 cycles, other VALU 2 cycles per wave64 instruction on a
+    SIMD-32, over 1024 SIMDs x the dispatch duration at 2.4 GHz)."""
+    if not sq:
+        return None
+    k = next((x for x in sq if x != "_meta" and kernel in x), None)
+    if k is None:
+        return None
+    c = {n: v["median_per_dispatch"] for n, v in sq[k].items()}
+    need = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU", "duration_us")
+    if not all(n in c for n in need):
+        return None
+    dur = c["duration_us"] * 1e-6
+    f64 = c["SQ_INSTS_VALU_FMA_F64"] + c["SQ_INSTS_VALU_MUL_F64"] + c["SQ_INSTS_VALU_ADD_F64"]
+    flops = 64 * (2 * c["SQ_INSTS_VALU_FMA_F64"] + c["SQ_INSTS_VALU_MUL_F64"] + c["SQ_INSTS_VALU_ADD_F64"])
+    cycles = 4 * (f64 + c.get("SQ_INSTS_VALU_TRANS_F64", 0)) + 2 * (c["SQ_INSTS_VALU"] - f64)
+    tf = flops / dur / 1e12
+    out = {"bound": "valu", "unit": "TFLOP/s", "achieved": round(tf, 3), "peak": FP64_VALU_PEAK_TFLOPS,
+           "frac": round(tf / FP64_VALU_PEAK_TFLOPS, 4),
+           "valu_issue_frac": round(cycles / (N_SIMD * dur * CLOCK_GHZ * 1e9), 4),
+           "fp64_share_of_valu_cycles": round(4 * f64 / cycles, 4),
+           "counter_dispatch_us": round(c["duration_us"], 1), "kernel": k}
+    if steps_per_dispatch:
+        out["valu_instr_per_step"] = round(c["SQ_INSTS_VALU"] / steps_per_dispatch)
+    return out
 
 
 def parse():
@@ -133,12 +189,15 @@ def run_cfg5(args, rank, world, local, dist, ctx):
     outs = [None]
 
     def one_step():
+        # TckResultCT rows (and the 11 taps) stay in HBM; N > 1: every rank ends with all 32
+        # channels by one RCCL all-gather of the ranks' own rows, without a host round trip
+        if outs[0] is None:
+            outs[0] = pkg.DeviceTrackOutBuffers(nsv, track, len(taps), device=f"cuda:{local}")
         buf = pkg.trackingCT(file, signal, track, A, ctx=ctx, taps=taps, channels=mine, raw=True,
                              out=outs[0])
-        outs[0] = buf
         tt = ctx.timing()
-        if dist is not None:  # every rank ends with all 32 channels (RCCL all-gather of own rows)
-            D.gather_tracking_rows(buf, shards, device=f"cuda:{local}")
+        if dist is not None:
+            D.gather_tracking_rows_device(buf, shards)
         return tt
 
     for _ in range(args.warmup):
@@ -166,15 +225,18 @@ def run_cfg5(args, rank, world, local, dist, ctx):
                 "kernel": "10-ms phase correlator, 11 taps (persistent or per-step launches)",
                 "launches": int(launches), "avg_launch_us": round(avg_ms * 1e3, 3),
                 "algorithmic_bytes_per_launch": bpl}
-        tf = os.path.join(ROOT, "profiles", TRAFFIC_FILE_CFG5)
-        if world == 1 and os.path.exists(tf):
-            try:
-                with open(tf) as fh:
-                    tj = json.load(fh)
-                roof["traffic"] = tj.get("bytes_per_launch")
-                roof["traffic_source"] = f"profiles/{TRAFFIC_FILE_CFG5} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)"
-            except (OSError, ValueError):
-                pass
+        tj, prov = evidence(TRAFFIC_FILES_CFG5)
+        if world == 1 and tj:
+            roof["traffic"] = tj.get("bytes_per_launch")
+            roof["traffic_source"] = prov
+        # what binds it: fp64 VALU (the 32 channels share record lines in L2 / MALL, so the HBM
+        # fraction overstates the memory work), from the SQ passes of the same launch shape
+        sq, sq_prov = evidence(CFG5_SQ_FILES)
+        v = valu_roofline(sq, "track_run_kernel<11, 3", steps_per_dispatch=40)
+        if v:
+            v["source"] = sq_prov
+            v["counter_workload"] = "tools/track_only.py 100 400 11 32 (32 channels x 11 taps, 40 10-ms steps)"
+            roof["valu"] = v
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline_cfg5(file, signal, track, A, taps, dev)
@@ -186,6 +248,7 @@ def run_cfg5(args, rank, world, local, dist, ctx):
             "config": {"workload": f"trackingCT cfg5 (32 ch, 11 taps -0.5:0.1:0.5, 1000 ms @1ms + "
                                    f"{args.n10_cfg5} ms @10ms)", "parallelism": f"channels x{world}",
                        "channels_per_rank": len(mine)},
+            "code": {"src_digest": SRC_DIGEST, "git_commit": srcdigest.head_commit()},
             "roofline": roof, "cpu_baseline": cpu}
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -227,12 +290,27 @@ def run_cfg4(args, rank, world, local, dist, ctx):
     barrier(dist, local)
     t0 = time.perf_counter()
     units = 0
+    corr_ms = 0.0
     for _ in range(args.steps):
         A, ta = one_step()
         units += ta["acq_hypothesis_samples"]
+        corr_ms += ta["acq_corr_ms"]
     barrier(dist, local)
     elapsed = max_over_ranks(dist, local, time.perf_counter() - t0)
     total = sum_over_ranks(dist, local, float(units))
+    # the acquisition model (16 B per hypothesis-sample) over this rank's correlation
+    # time (the fine-frequency FFTs excluded, timed in acq_ms)
+    roof = None
+    if corr_ms > 0:
+        ach = 16.0 * units / (corr_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
+                "kernel": "acquisition correlator (fwd/inv P x 2000 FFT passes, fp64), rank 0",
+                "corr_ms_per_step": round(corr_ms / args.steps, 3),
+                "algorithmic_bytes_per_step": 16.0 * units / args.steps}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline_cfg4(file, signal, acq, dev, prns, S)
     line = {"metric": "correlator Msamples/s (acquisition cfg4), whole job",
             "value": round(total / elapsed / 1e6, 2), "unit": "Msamples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -242,7 +320,8 @@ def run_cfg4(args, rank, world, local, dist, ctx):
             "config": {"workload": "acquisition cfg4 (32 PRN, +-10kHz/250Hz, 10 ms, L 10)",
                        "parallelism": f"PRNs x{world}", "prns_per_rank": len(mine)},
             "acquired": [int(x) for x in A.sv], "acq_ms_rank0": round(ta["acq_ms"], 3),
-            "roofline": None, "cpu_baseline": None}
+            "code": {"src_digest": SRC_DIGEST, "git_commit": srcdigest.head_commit()},
+            "roofline": roof, "cpu_baseline": cpu}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:
@@ -353,19 +432,21 @@ def main():
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "all_steps_avg_launch_us": round(tp["track_kernel_ms"] * 1e3 / max(1, tp["track_launches"]), 3),
                 "track_wall_ms_profiling": round(tp["track_ms"], 3)}
-        tf = os.path.join(ROOT, "profiles", TRAFFIC_FILE)
-        if world == 1 and os.path.exists(tf):
-            try:
-                with open(tf) as fh:
-                    tj = json.load(fh)
-                # PMC HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE) of the same kernel and its
-                # rocprofv3 kernel-trace average, from the separate rocprofv3 passes of this
-                # round (tools/gpu_round.sh; a PMC pass cannot run inside this process)
-                roof["traffic"] = tj.get("bytes_per_launch")
-                roof["traffic_source"] = f"profiles/{TRAFFIC_FILE} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)"
-                roof["rocprof_avg_launch_us"] = tj.get("rocprof_avg_launch_us")
-            except Exception:
-                pass
+        tj, prov = evidence(TRAFFIC_FILES)
+        if world == 1 and tj:
+            # PMC HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE) of the same kernel and its
+            # rocprofv3 kernel-trace average, from the separate rocprofv3 passes (tools/gpu.sh
+            # traffic; a PMC pass cannot run inside this process); prov says whether they were
+            # measured on the code this bench runs
+            roof["traffic"] = tj.get("bytes_per_launch")
+            roof["traffic_source"] = prov
+            roof["rocprof_avg_launch_us"] = tj.get("rocprof_avg_launch_us")
+        sq, sq_prov = evidence(TRACK_SQ_FILES)
+        v = valu_roofline(sq, "track_run_kernel<3, 3", steps_per_dispatch=40)
+        if v:
+            v["source"] = sq_prov
+            v["counter_workload"] = "tools/track_only.py 100 400 (8 channels, 40 10-ms steps per dispatch)"
+            roof["valu"] = v
 
     # the acquisition's fp32 fast mode (gnss_ctx_set_acq_precision(ctx, 0)) on the same
     # record, after the timed region: its time and whether its decisions equal the fp64 ones
@@ -436,6 +517,7 @@ def main():
         # round's separate passes, tools/acq_bound.py; a PMC pass cannot run in this process)
         "acq_kernel_bounds": acq_bounds(),
         "acq_fp32_fast_mode": fast,
+        "code": {"src_digest": SRC_DIGEST, "git_commit": srcdigest.head_commit()},
         "cpu_baseline": cpu,
     }
     if rank == 0:
@@ -446,11 +528,8 @@ def main():
 
 
 def acq_bounds():
-    try:
-        with open(os.path.join(ROOT, "profiles", ACQ_BOUND_FILE)) as fh:
-            return {"source": f"profiles/{ACQ_BOUND_FILE}", "kernels": json.load(fh)}
-    except (OSError, ValueError):
-        return None
+    d, prov = evidence(ACQ_BOUND_FILES)
+    return {"source": prov, "kernels": d.get("kernels", d)} if d else None
 
 
 def np_equal(a, b):
@@ -475,10 +554,41 @@ def host_cpu():
     return model, os.cpu_count()
 
 
+def cpu_baseline_cfg4(file, signal, acq, dev, prns, S):
+    """Config 4's CPU leg: the oracle's acquisition with the Urban grid (81 bins) on a bounded
+    sample (2 of the 10 non-coherent ms, + the fine search): 1 PRN on one thread and the 32
+    PRNs on a thread each, median of 3; hypothesis-samples per second."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as po
+    from types import SimpleNamespace
+    win = dev.download()
+    f2 = SimpleNamespace(**vars(file))
+    f2.data, f2.dev = win, None
+    a1 = SimpleNamespace(**vars(acq))
+    a1.datalen = 2
+
+    def leg(pl, nt):
+        r = []
+        for _ in range(3):
+            t = time.perf_counter()
+            po.acquisition(f2, signal, a1, prn_list=pl, nthreads=nt)
+            r.append(len(pl) * a1.freqNum * a1.datalen * S / (time.perf_counter() - t))
+        return float(np.median(r))
+
+    one = leg([prns[0]], 1)
+    many = leg(list(prns), len(prns))
+    model, ncpu = host_cpu()
+    return {"value": round(many / 1e6, 4), "unit": "Msamples/s", "cores": len(prns), "kind": "port",
+            "sample": f"oracle/ C fp64 restatement, acquisition of the {len(prns)} PRNs (one thread each) over "
+                      f"{a1.freqNum} bins x {a1.datalen} ms + fine FFT (median of 3)",
+            "one_thread": {"value": round(one / 1e6, 4), "sample": "1 PRN, same grid"},
+            "cpu_quota": cpu_quota(), "host_cpu": model, "nproc": ncpu}
+
+
 def cpu_baseline_cfg5(file, signal, track, A, taps, dev):
     """Config 5's CPU leg: the oracle's trackingCT with the same 11 taps on a bounded sample
-    (1 000 ms @1 ms + 100 ms @10 ms; 1 channel on one thread, 16 channels on 16 threads,
-    median of 3), channel-samples per second."""
+    (1 000 ms @1 ms + 100 ms @10 ms; 1 channel on one thread, every channel of the step on a
+    thread of its own, median of 3), channel-samples per second."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as po
     from types import SimpleNamespace
@@ -488,7 +598,6 @@ def cpu_baseline_cfg5(file, signal, track, A, taps, dev):
     f2 = SimpleNamespace(skip=0, dataType=2, dataPrecision=1, data=win, fileRoute=None, dev=None)
     tr = SimpleNamespace(**vars(track))
     tr.msToProcessCT_10ms = n10s
-    allc = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
 
     def leg(nch, nt):
         A1 = SimpleNamespace(sv=A.sv[:nch], SNR=A.SNR[:nch], Doppler=A.Doppler[:nch],
@@ -501,20 +610,21 @@ def cpu_baseline_cfg5(file, signal, track, A, taps, dev):
         return float(np.median(r))
 
     one = leg(1, 1)
-    nall = min(allc, len(A.sv))
+    nall = len(A.sv)
     many = leg(nall, nall)
     model, ncpu = host_cpu()
     return {"value": round(many / 1e6, 4), "unit": "Msamples/s", "cores": nall, "kind": "port",
             "sample": f"oracle/ C fp64 restatement, trackingCT with 11 taps, {nall} channels x (1000 ms @1ms "
                       f"+ {n10s} ms @10ms) on {nall} threads (median of 3)",
             "one_thread": {"value": round(one / 1e6, 4), "sample": "1 channel, same length"},
-            "host_cpu": model, "nproc": ncpu}
+            "cpu_quota": cpu_quota(), "host_cpu": model, "nproc": ncpu}
 
 
 def cpu_baseline(file, signal, acq, track, A, dev, args, ta, tt):
     """The CPU fp64 restatement (oracle/, C, -O2) timed on a bounded sample of the same
-    workload (SURVEY 8d / BASELINE.md 2): one thread and all usable cores (OpenMP across
-    PRNs / channels), median of 5 runs each, plus the numpy restatement (the "MATLAB-like
+    workload (SURVEY 8d / BASELINE.md 2): one thread, and every unit of the step on a thread of
+    its own (the 32 PRNs of the acquisition, the acquired channels of trackingCT; OpenMP across
+    PRNs / channels), median of 3 runs each, plus the numpy restatement (the "MATLAB-like
     vectorised" proxy, tests/numpy_twin.py) on one tracking step set. Per-unit rates are
     extrapolated to the GPU step's unit mix. Labelled "restatement", never "MATLAB"."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -522,7 +632,6 @@ def cpu_baseline(file, signal, acq, track, A, dev, args, ta, tt):
     import pyoracle as po
     from types import SimpleNamespace
     S = signal.Sample
-    allc = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     # bounded sample: IF window [skip, skip + 1000 + 19 + n10s + 2] ms
     n10s = 200
     lo = file.skip * S * 2
@@ -533,27 +642,27 @@ def cpu_baseline(file, signal, acq, track, A, dev, args, ta, tt):
     a1.datalen = 4  # the same grid (29 bins x S) over 4 non-coherent ms
     tr = SimpleNamespace(**vars(track))
     tr.msToProcessCT_10ms = n10s
+    U_acq, U_trk = ta["acq_hypothesis_samples"], tt["track_channel_samples"]
 
-    def leg(nt):
-        np_ = nt  # one PRN / channel per thread
-        prn_list = [int(p) for p in (list(A.sv) + [p for p in range(1, 33) if p not in A.sv])[:np_]]
-        nch = min(nt, len(A.sv))
+    def leg(nprn, nch, reps):
+        # one PRN / channel per thread: acquisition of nprn PRNs, trackingCT of nch channels
+        prn_list = [int(p) for p in (list(A.sv) + [p for p in range(1, 33) if p not in A.sv])[:nprn]]
         A1 = SimpleNamespace(sv=A.sv[:nch], SNR=A.SNR[:nch], Doppler=A.Doppler[:nch],
                              codedelay=A.codedelay[:nch], fineFreq=A.fineFreq[:nch])
         ra, rt = [], []
-        for _ in range(5):
+        for _ in range(reps):
             t = time.perf_counter()
-            po.acquisition(f2, signal, a1, prn_list=prn_list, nthreads=nt)
+            po.acquisition(f2, signal, a1, prn_list=prn_list, nthreads=nprn)
             ra.append(len(prn_list) * a1.freqNum * a1.datalen * S / (time.perf_counter() - t))
             t = time.perf_counter()
-            po.trackingCT(f2, signal, tr, A1, nthreads=nt)
+            po.trackingCT(f2, signal, tr, A1, nthreads=nch)
             rt.append(nch * (1000 + n10s) * S / (time.perf_counter() - t))
         r_acq, r_trk = float(np.median(ra)), float(np.median(rt))
-        U_acq, U_trk = ta["acq_hypothesis_samples"], tt["track_channel_samples"]
         return r_acq, r_trk, (U_acq + U_trk) / (U_acq / r_acq + U_trk / r_trk)
 
-    a_1, t_1, v_1 = leg(1)
-    a_n, t_n, v_n = leg(allc)
+    a_1, t_1, v_1 = leg(1, 1, 3)
+    n_prn, n_ch = 32, len(A.sv)
+    a_n, t_n, v_n = leg(n_prn, n_ch, 3)
     # numpy restatement (one thread, vectorised like the MATLAB code): 10 correlator steps
     # of 10 ms (trackingCT.m:96-118) and one PRN's 29-bin x 1 ms acquisition (:40-78)
     np_trk = np_acq = None
@@ -572,20 +681,37 @@ def cpu_baseline(file, signal, acq, track, A, dev, args, ta, tt):
     except Exception:
         pass
     model, ncpu = host_cpu()
-    return {"value": round(v_n / 1e6, 4), "unit": "Msamples/s", "cores": allc, "kind": "port",
-            "sample": f"oracle/ C fp64 restatement (median of 5): acquisition of {allc} PRNs (1 per "
-                      f"thread) over {a1.freqNum} bins x {a1.datalen} ms + fine FFT, trackingCT of "
-                      f"{min(allc, len(A.sv))} channels 1000 ms @1ms (+phase-B rerun) + {n10s} ms @10ms; "
-                      "per-unit rates extrapolated to the GPU step's unit mix",
+    return {"value": round(v_n / 1e6, 4), "unit": "Msamples/s", "cores": n_prn, "kind": "port",
+            "sample": f"oracle/ C fp64 restatement (median of 3): acquisition of the {n_prn} PRNs (one thread "
+                      f"each) over {a1.freqNum} bins x {a1.datalen} ms + fine FFT, trackingCT of the {n_ch} "
+                      f"channels (one thread each) 1000 ms @1ms (+phase-B rerun) + {n10s} ms @10ms; per-unit "
+                      "rates extrapolated to the GPU step's unit mix",
+            "threads": {"acquisition": n_prn, "tracking": n_ch}, "cpu_quota": cpu_quota(),
             "one_thread": {"value": round(v_1 / 1e6, 4), "acq_Msamples_s": round(a_1 / 1e6, 4),
-                           "track_Msamples_s": round(t_1 / 1e6, 4)},
-            "all_cores": {"threads": allc, "value": round(v_n / 1e6, 4), "acq_Msamples_s": round(a_n / 1e6, 4),
+                           "track_Msamples_s": round(t_1 / 1e6, 4), "sample": "1 PRN, 1 channel, same lengths"},
+            "all_units": {"value": round(v_n / 1e6, 4), "acq_Msamples_s": round(a_n / 1e6, 4),
                           "track_Msamples_s": round(t_n / 1e6, 4)},
             "numpy_restatement": {"track_Msamples_s": round(np_trk / 1e6, 4) if np_trk else None,
                                   "acq_Msamples_s": round(np_acq / 1e6, 4) if np_acq else None,
                                   "threads": 1},
             "host_cpu": model, "nproc": ncpu,
             "label": "CPU restatement of acquisition.m / trackingCT.m (MATLAB itself is absent)"}
+
+
+def cpu_quota():
+    """CPUs this process may use: the cgroup CPU quota (cpu.max) where one is set, else the
+    affinity mask (the GPU box shows the whole machine's CPUs to nproc)."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+            if q != "max":
+                return round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count()
 
 
 if __name__ == "__main__":

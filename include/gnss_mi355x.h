@@ -357,18 +357,22 @@ int gnss_correlate_step(gnss_ctx *ctx, const gnss_file *file, const gnss_signal 
                         double remPhase, int64_t pos_bytes, int n_taps, const double *taps,
                         double *sums_out, int64_t *numSample_out);
 
-/* ---- trackingVT_POS_updated.m, the tracking half (ABI v8) -----------
- * One vector-tracking step of the loop at trackingVT_POS_updated.m:157-349 for n
- * channels: read sizing (:161), the three replica chips, the carrier wipe and sums
- * (:217-281), the remaining code / carrier phase (:284-285), C/N0 is the caller's, the
- * PLL (:305-311) and the DLL discriminator (:314-316). The vector half -- satellite
- * position, iono / tropo, the predicted code frequency and the Kalman filter (:166-215,
- * :350-420) -- stays with the caller, which passes each step's predicted code frequency.
+/* ---- trackingVT_POS_updated.m, the tracking half (ABI v9) -----------
+ * Steps of the loop at trackingVT_POS_updated.m:157-349 for n channels: read sizing (:161),
+ * the three replica chips, the carrier wipe and sums (:217-281), the remaining code /
+ * carrier phase (:284-285), the C/N0 estimator (:292-304), the PLL (:305-311) and the DLL
+ * discriminator (:314-316). The vector half -- satellite position, iono / tropo, the
+ * predicted code frequency and the Kalman filter (:166-215, :350-420) -- stays with the
+ * caller, which passes each step's predicted code frequency.
  * The reference's replica quirk is kept: Code(svindex, ceil_mx(1)) linear-indexes ONE
  * element of the 3 x n matrix ceil_mx (the first sample's chip of each of the E / P / L
  * rows, the 1025 clamp of :240-246 applied to it alone), so E / P / L = that chip times
  * the whole sum(InphaseSignal) / sum(QuadratureSignal). Spacing = 0.7:-0.05:-0.7 (:27):
- * E / P / L at Spacing(5) / (15) / (25) = +0.5 / 0 / -0.5. */
+ * E / P / L at Spacing(5) / (15) / (25) = +0.5 / 0 / -0.5; the three colons must have
+ * numSample elements each (ceil_mx's vertical concatenation and t_CodePrompt(numSample),
+ * :217-228, :284), else GNSS_EINDEX as MATLAB raises.
+ * Formats (:163-176): int8 I/Q (dataPrecision 1, dataType 2), int8 real (1, 1), int16 I/Q
+ * with each read's means removed (2, 2); file_ptr in bytes. */
 typedef struct gnss_vt_chan {
     int32_t prn;
     int32_t pad;
@@ -379,29 +383,43 @@ typedef struct gnss_vt_chan {
     double  carrFreq;       /* carrier NCO frequency (:310)                               */
     double  carrFreqBasis;  /* (:121)                                                     */
     double  oldCarrNco, oldCarrError;  /* PLL filter state (:307-308)                    */
+    int32_t index_int;      /* C/N0 estimator (:78-81, :293-303): Zk entries filled, 0..19 */
+    int32_t snrIndex;       /*   the next CN0_VT row (1-based; starts at 1)                */
+    double  Zk[20];         /*   P_i^2 + P_q^2 of the current K = 20 block                 */
 } gnss_vt_chan;
 
-/* TckResultVT(prn).*(msIndex) of one channel and step (:319-346). */
+/* TckResultVT(prn).*(msIndex) of one channel and step (:319-346) and CN0_VT. */
 typedef struct gnss_vt_out {
     double  E_i, E_q, P_i, P_q, L_i, L_q;
     double  carrError, codeError, carrNco;
     double  remChip, remCarrPhase, codeFreq, carrFreq;
     int64_t numSample, absoluteSample;
     double  codedelay;
+    double  CN0;            /* CN0_VT(cn0_row, svindex) when cn0_row > 0 (:301)           */
+    int32_t cn0_row;        /* 1-based row written by this step, 0: none                  */
+    int32_t status;         /* GNSS_OK, or the channel's error at this step (vt_run)      */
 } gnss_vt_out;
 
-/* The step on the GPU: the IF as in gnss_tracking_ct (int8 records; int16: GNSS_EARG),
- * codeFreq_new[i] = channel i's code frequency for this step (:211-215), pdi =
- * track.pdi. chans[] are advanced in place; out[i] = channel i's record.
- * GNSS_EINDEX: a replica chip index MATLAB would reject; GNSS_EIO: read past EOF. */
+/* nsteps steps of the n channels in ONE launch (one workgroup per channel loops over the
+ * steps: read sizing, sums in a fixed order, the scalar end, all on the GPU):
+ * codeFreq_new[s * n + i] = channel i's code frequency for step s (:211-215; the caller's
+ * EKF prediction, or a recorded series), pdi = track.pdi. chans[] are advanced in place;
+ * out[s * n + i] = channel i's record of step s. A channel whose step fails (GNSS_EINDEX: a
+ * replica index MATLAB would reject; GNSS_EIO: read past EOF) stops there with
+ * out[..].status set; the call returns the first such status. */
+int gnss_tracking_vt_run(gnss_ctx *ctx, const gnss_file *file, const gnss_signal *signal,
+                         const gnss_track *track, int32_t pdi, int32_t n, int32_t nsteps,
+                         gnss_vt_chan *chans, const double *codeFreq_new, gnss_vt_out *out);
+
+/* One step: gnss_tracking_vt_run with nsteps = 1. */
 int gnss_tracking_vt_step(gnss_ctx *ctx, const gnss_file *file, const gnss_signal *signal,
                           const gnss_track *track, int32_t pdi, int32_t n, gnss_vt_chan *chans,
                           const double *codeFreq_new, gnss_vt_out *out);
 
 /* The same step's host half alone (no GPU): from the channel state, this step's code
  * frequency and the step's carrier-wiped sums (sumI = sum(InphaseSignal), sumQ =
- * sum(QuadratureSignal)), the record and the advanced state -- what gnss_tracking_vt_step
- * applies after its kernels. numSample_out (may be NULL): the read size, :161. */
+ * sum(QuadratureSignal)), the record and the advanced state -- the arithmetic the
+ * kernel's scalar end runs (the same source). int8 I/Q byte offsets. */
 int gnss_vt_nco_step(const gnss_signal *signal, const gnss_track *track, int32_t pdi,
                      gnss_vt_chan *chan, double codeFreq_new, double sumI, double sumQ,
                      gnss_vt_out *out);

@@ -684,33 +684,69 @@ static double or_vt_spacing(int i1)
     return or_colon_elem(&c, i1 - 1);
 }
 
-int or_vt_step(const int8_t *iq, int64_t nbytes, double *st, double codeFreq_new, const int8_t *ca,
-               double Fs, double codelength, double ms, int pdi, double tau1carr, double tau2carr,
-               const double *sums, double *rec)
+static double cn0_moment(const double *Zk, double T);
+
+/* trackingVT_POS_updated.m:157-349, the tracking half of one step of one channel.
+ * st (VT_STATE): [0] file_ptr (bytes), [1] remChip, [2] remCarrPhase, [3] codeFreq (the last
+ * step's), [4] carrFreq, [5] carrFreqBasis, [6] oldCarrNco, [7] oldCarrError, [8] index_int,
+ * [9] snrIndex, [10..29] Zk; advanced in place. rec (VT_REC, 18): E/P/L I/Q, carrError,
+ * codeError, carrNco, remChip, remCarrPhase, codeFreq, carrFreq, numSample, absoluteSample,
+ * codedelay, CN0, cn0_row. raw = the record's bytes (prec / dtype: dataPrecision /
+ * dataType, :163-176) or NULL with sums = (sum I, sum Q) given. */
+int or_vt_step(const uint8_t *raw, int64_t nbytes, int prec, int dtype, double *st, double codeFreq_new,
+               const int8_t *ca, double Fs, double codelength, double ms, int pdi, double tau1carr,
+               double tau2carr, const double *sums, double *rec)
 {
     const double remChip0 = st[1];
     const int64_t n = (int64_t)ceil((codelength * pdi - remChip0) / (st[3] / Fs)); /* :161 */
     if (n < 1) return GNSS_EINDEX;
     const int64_t ptr = (int64_t)st[0];
-    /* Code = [CA(end) repmat(CA,1,pdi) CA(1)] (:110): ceil_mx(idx) = the first element of
-     * row idx = ceil(0 + Spacing + remChip) + 1, the 1025 clamp on it alone (:218-249) */
+    const int bps = prec * dtype;
+    const double cps = codeFreq_new / Fs; /* :218 */
+    /* t_CodeEarly / Prompt / Late (:220-222): each must have numSample elements (ceil_mx's
+     * vertical concatenation, :227; t_CodePrompt(numSample), :284).
+     * Code = [CA(end) repmat(CA,1,pdi) CA(1)] (:110): ceil_mx(idx) = the first element of
+     * row idx = ceil(0 + Spacing + remChip) + 1, the 1025 clamp on it alone (:230-249) */
     int code[3];
     const int sp[3] = {5, 15, 25};
+    or_colon col[3];
     for (int s = 0; s < 3; s++) {
-        double j = ceil((0 + or_vt_spacing(sp[s])) + remChip0) + 1;
+        const double spc = or_vt_spacing(sp[s]);
+        or_colon_init(&col[s], (0 + spc) + remChip0, cps, ((double)(n - 1) * cps + spc) + remChip0);
+        if (col[s].n != n - 1) return GNSS_EINDEX;
+        double j = ceil((0 + spc) + remChip0) + 1;
         if (j > 1025) j = 1025;
         const int64_t len = 1023 * (int64_t)pdi + 2, ji = (int64_t)j;
         if (ji < 1 || ji > len) return GNSS_EINDEX;
         code[s] = ji == 1 ? ca[1022] : ji == len ? ca[0] : ca[(ji - 2) % 1023];
     }
     double sI, sQ;
-    if (iq) {
-        if (ptr < 0 || ptr + 2 * n > nbytes) return GNSS_EIO;
+    if (raw) {
+        if (ptr < 0 || ptr + (int64_t)bps * n > nbytes) return GNSS_EIO;
+        double mi = 0, mq = 0;
+        if (prec == 2) { /* rawsignal = (I - mean(I)) + 1i*(Q - mean(Q)) (:166-170) */
+            for (int64_t k = 0; k < n; k++) {
+                mi += (double)(int16_t)(raw[ptr + 4 * k] | (raw[ptr + 4 * k + 1] << 8));
+                mq += (double)(int16_t)(raw[ptr + 4 * k + 2] | (raw[ptr + 4 * k + 3] << 8));
+            }
+            mi = mi / (double)n;
+            mq = mq / (double)n;
+        }
         long double aI = 0, aQ = 0;
         for (int64_t k = 0; k < n; k++) {
             /* Wave = (2*pi*(carrFreq .* CarrTime)) + remCarrPhase, CarrTime = (0:n)/Fs (:275-276) */
             const double W = TWO_PI * (st[4] * ((double)k / Fs)) + st[2];
-            const double xr = iq[ptr + 2 * k], xi = iq[ptr + 2 * k + 1];
+            double xr, xi;
+            if (prec == 2) {
+                xr = (double)(int16_t)(raw[ptr + 4 * k] | (raw[ptr + 4 * k + 1] << 8)) - mi;
+                xi = (double)(int16_t)(raw[ptr + 4 * k + 2] | (raw[ptr + 4 * k + 3] << 8)) - mq;
+            } else if (dtype == 1) { /* int8 real (:172-175) */
+                xr = (int8_t)raw[ptr + k];
+                xi = 0;
+            } else {
+                xr = (int8_t)raw[ptr + 2 * k];
+                xi = (int8_t)raw[ptr + 2 * k + 1];
+            }
             aI += xr * sin(W) + xi * cos(W); /* imag(rawsignal .* carrsig) (:279) */
             aQ += xr * cos(W) - xi * sin(W); /* real(...) (:280) */
         }
@@ -720,25 +756,31 @@ int or_vt_step(const int8_t *iq, int64_t nbytes, double *st, double codeFreq_new
         sI = sums[0];
         sQ = sums[1];
     }
-    const double cps = codeFreq_new / Fs; /* :218 */
-    or_colon col;
-    const double sp15 = or_vt_spacing(15);
-    or_colon_init(&col, (0 + sp15) + remChip0, cps, ((double)(n - 1) * cps + sp15) + remChip0);
-    if (col.n != n - 1) return GNSS_EINDEX;
-    const double remChip = (or_colon_elem(&col, n - 1) + cps) - 1023 * pdi;          /* :284 */
+    const double remChip = (or_colon_elem(&col[1], n - 1) + cps) - 1023 * pdi;          /* :284 */
     const double remCarrPhase = fmod(TWO_PI * (st[4] * ((double)n / Fs)) + st[2], TWO_PI); /* :285 */
     const double Ei = code[0] * sI, Eq = code[0] * sQ, Pi = code[1] * sI, Pq = code[1] * sQ;
     const double Li = code[2] * sI, Lq = code[2] * sQ;
+    /* C/N0 (:292-304; flag_snr is 1 throughout) */
+    double cn0 = 0, cn0_row = 0;
+    int index_int = (int)st[8] + 1;
+    st[10 + index_int - 1] = Pi * Pi + Pq * Pq;
+    if (index_int % 20 == 0) {
+        cn0 = cn0_moment(st + 10, 1 * ms * pdi);
+        cn0_row = st[9];
+        index_int = 0;
+        st[9] += 1;
+    }
+    st[8] = index_int;
     const double carrError = atan(Pq / Pi) / (2.0 * M_PI);                              /* :306 */
     const double carrNco = st[6] + (tau2carr / tau1carr) * (carrError - st[7]) +
                            carrError * (pdi * 1e-3 / tau1carr);                         /* :307 */
     const double carrFreq = st[5] + carrNco;                                            /* :310 */
     const double E = sqrt(Ei * Ei + Eq * Eq), L = sqrt(Li * Li + Lq * Lq);
     const double codeError = -0.5 * (E - L) / (E + L);                                  /* :316 */
-    const int64_t absS = ptr + 2 * n;                                                   /* ftell */
-    const double r[16] = {Ei, Eq, Pi, Pq, Li, Lq, carrError, codeError, carrNco, remChip, remCarrPhase,
+    const int64_t absS = ptr + (int64_t)bps * n;                                        /* ftell */
+    const double r[18] = {Ei, Eq, Pi, Pq, Li, Lq, carrError, codeError, carrNco, remChip, remCarrPhase,
                           codeFreq_new, carrFreq, (double)n, (double)absS,
-                          fmod((double)absS / 2, Fs * ms)};                             /* :347 */
+                          fmod((double)absS / bps, Fs * ms), cn0, cn0_row};            /* :347 */
     memcpy(rec, r, sizeof r);
     st[0] = (double)absS;
     st[1] = remChip;

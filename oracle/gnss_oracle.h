@@ -86,9 +86,9 @@ void or_nco_replay(double remChip, double codeFreq, double carrFreq, double remC
                    double Fs, double codelength, int pdi, int use_ceil,
                    int64_t *numSample, double *remChipNext, double *remCarrPhaseNext);
 /* trackingCT.m:136-150 loop filter, one update: returns the new output. */
-int or_vt_step(const int8_t *iq, int64_t nbytes, double *st, double codeFreq_new, const int8_t *ca,
-               double Fs, double codelength, double ms, int pdi, double tau1carr, double tau2carr,
-               const double *sums, double *rec);
+int or_vt_step(const uint8_t *raw, int64_t nbytes, int prec, int dtype, double *st, double codeFreq_new,
+               const int8_t *ca, double Fs, double codelength, double ms, int pdi, double tau1carr,
+               double tau2carr, const double *sums, double *rec);
 double or_loop_filter(double outLast, double discri, double discriLast, double tau1, double tau2,
                       double T);
 

@@ -67,9 +67,9 @@ def load():
         lib.or_loop_filter.argtypes = [C.c_double] * 6
         lib.or_loop_filter.restype = C.c_double
         lib.or_synth_if.argtypes = [C.POINTER(abi.GnssSynth), C.c_uint64, C.c_uint64, C.c_void_p, C.c_int]
-        lib.or_vt_step.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_double, C.c_void_p, C.c_double,
-                                   C.c_double, C.c_double, C.c_int, C.c_double, C.c_double, C.c_void_p,
-                                   C.c_void_p]
+        lib.or_vt_step.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_void_p, C.c_double, C.c_void_p,
+                                   C.c_double, C.c_double, C.c_double, C.c_int, C.c_double, C.c_double,
+                                   C.c_void_p, C.c_void_p]
         _lib = lib
     return _lib
 
@@ -219,25 +219,35 @@ def correlate_step(iq, numSample, remChip, codeFreq, Fs, carrierFreq, remPhase, 
 
 
 VT_STATE = ["file_ptr", "remChip", "remCarrPhase", "codeFreq", "carrFreq", "carrFreqBasis",
-            "oldCarrNco", "oldCarrError"]
+            "oldCarrNco", "oldCarrError", "index_int", "snrIndex"] + [f"Zk{k}" for k in range(20)]
 VT_REC = ["E_i", "E_q", "P_i", "P_q", "L_i", "L_q", "carrError", "codeError", "carrNco", "remChip",
-          "remCarrPhase", "codeFreq", "carrFreq", "numSample", "absoluteSample", "codedelay"]
+          "remCarrPhase", "codeFreq", "carrFreq", "numSample", "absoluteSample", "codedelay", "CN0", "cn0_row"]
+
+
+def vt_state(file_ptr, remChip, remCarrPhase, codeFreq, carrFreq, carrFreqBasis, oldCarrNco=0.0,
+             oldCarrError=0.0):
+    """A VT_STATE vector (float64[30]); the C/N0 estimator starts at index_int 0, snrIndex 1 (:78-81)."""
+    st = np.zeros(len(VT_STATE))
+    st[:10] = [file_ptr, remChip, remCarrPhase, codeFreq, carrFreq, carrFreqBasis, oldCarrNco, oldCarrError, 0, 1]
+    return st
 
 
 def vt_step(st, codeFreq_new, prn, iq=None, sums=None, Fs=58e6, codelength=1023.0, ms=1e-3, pdi=1,
-            pll=(15, 0.707, 0.25)):
-    """One trackingVT_POS_updated.m step (tracking half, :157-349): st (float64[8], VT_STATE order)
-    is advanced in place; returns (status, rec float64[16] in VT_REC order). iq = the int8 I/Q
-    record (byte 0 = file byte 0) or None with sums = (sum I, sum Q) given."""
+            pll=(15, 0.707, 0.25), prec=1, dtype=2):
+    """One trackingVT_POS_updated.m step (tracking half, :157-349): st (float64[30], VT_STATE
+    order, vt_state()) is advanced in place; returns (status, rec float64[18] in VT_REC order).
+    iq = the record's bytes (byte 0 = file byte 0; prec / dtype = dataPrecision / dataType) or
+    None with sums = (sum I, sum Q) given."""
     t1, t2 = calc_loop_coef(*pll)
-    rec = np.zeros(16)
+    rec = np.zeros(len(VT_REC))
     ca = generate_ca(prn)
     sm = np.ascontiguousarray(sums if sums is not None else [0.0, 0.0], dtype=np.float64)
+    raw = None
     if iq is not None:
-        iq = np.ascontiguousarray(iq, dtype=np.int8)
-    st_ = load().or_vt_step(iq.ctypes.data if iq is not None else None, len(iq) if iq is not None else 0,
-                            st.ctypes.data, float(codeFreq_new), ca.ctypes.data, Fs, codelength, ms, pdi,
-                            t1, t2, sm.ctypes.data, rec.ctypes.data)
+        raw = np.ascontiguousarray(iq).view(np.uint8).reshape(-1)
+    st_ = load().or_vt_step(raw.ctypes.data if raw is not None else None, raw.size if raw is not None else 0,
+                            int(prec), int(dtype), st.ctypes.data, float(codeFreq_new), ca.ctypes.data, Fs,
+                            codelength, ms, pdi, t1, t2, sm.ctypes.data, rec.ctypes.data)
     return st_, rec
 
 

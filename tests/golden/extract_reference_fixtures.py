@@ -79,6 +79,8 @@ def vt_fixture(nsteps=1200):
     arrs = {"prns": np.array(prns)}
     for fld in fields:
         arrs[fld] = np.stack([np.asarray(getattr(T[p - 1], fld), dtype=np.float64)[:nsteps] for p in prns])
+    # CN0_VT(snrIndex, svindex) (:292-305): one row per K = 20 steps, columns in Acquired.sv order
+    arrs["CN0_VT"] = np.asarray(d["CN0_VT"], dtype=np.float64)[: nsteps // 20]
     np.savez_compressed(os.path.join(HERE, "ref_tckRstVT_Opensky.npz"), **arrs)
     print("VT prns", prns)
 

@@ -1,0 +1,124 @@
+"""Long-run golden of BASELINE config 5: the oracle's 11-tap trackingCT
+(taps -0.5:0.1:0.5, trackingCT_multiCorr-GIVEN.m:25 tap semantics on trackingCT.m's loop)
+over the FULL benchmarked length -- 1000 ms @1 ms + countinx + 90 000 ms @10 ms
+(trackingCT.m:73-171, :178-213, :377-525) -- on the bench's own 32-SV record, for three of
+the 32 channels.
+
+Runs ON THE GPU BOX (the record is the HIP synthetic generator's, resident in HBM: it is
+downloaded there and fed to the CPU oracle, one OpenMP thread per channel, ~13 min), e.g.
+    gpurun --timeout 1200 -- python -u tests/golden/make_golden_cfg5.py
+and writes gpurun_out/golden_cfg5_long.npz, committed as tests/golden/golden_cfg5_long.npz.
+The record's xxh64 digest is stored with it, so tests/test_gpu_longrun.py proves it
+regenerated the same bytes. Storage (compact(), ~3 MB): the integer fields exact, as their
+first value and int32 step differences; the 22 tap sums (E / P / L are taps 0 / 5 / 10) as
+int32 multiples of q = 2e-9 x the channel's P RMS (the test's tolerance is 1e-8 of the RMS,
+5 quanta); the NCO fields as float64. Test infrastructure only."""
+import importlib
+import os
+import sys
+import threading
+import time
+from types import SimpleNamespace
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle"), HERE]
+import make_golden_long as mgl  # noqa: E402  (digest, beat)
+import pyoracle as po  # noqa: E402
+
+pkg = importlib.import_module("assignment-for-aae6102_gnss-sdr_amd")
+
+SKIP, N1, N10, NSV = 0, 1000, 90000, 32
+CHANNELS = (2, 17, 31)  # PRN 3 (the weakest, 40.8 dB-Hz), PRN 18 (-3.9 kHz), PRN 32 (the grid's last)
+QREL = 2e-9
+
+
+def record_bytes(S=58000):
+    return (SKIP + N1 + 19 + N10 + 3) * S * 2
+
+
+def acquired(cfg, signal):
+    S = signal.Sample
+    cds = [int(round((-cfg.sv[i].code_phase0) % 1023 / (1.023e6 / signal.Fs))) % S for i in range(NSV)]
+    return SimpleNamespace(sv=np.array([cfg.sv[i].prn for i in range(NSV)]), SNR=np.zeros(NSV),
+                           Doppler=np.zeros(NSV), codedelay=np.array(cds),
+                           fineFreq=np.array([signal.IF + cfg.sv[i].doppler_hz for i in range(NSV)]))
+
+
+def distinct_steps(a, n1):
+    """The record's distinct steps: the 1-ms ones and one of each 10-fold 10-ms row."""
+    return np.concatenate([a[..., :n1], a[..., n1::10]], axis=-1)
+
+
+INT_FIELDS = ("codedelay", "numSample", "delayValue", "absoluteSample", "codedelay2")
+
+
+def field_rows(F):
+    ints = [F.index(f) for f in INT_FIELDS]
+    return ints, [i for i in range(6, len(F)) if i not in ints]
+
+
+def compact(j, r, tp, cn0, F):
+    """Channel j's arrays in the committed form: r = distinct-step record [18][steps],
+    tp = taps [2][11][steps]; E / P / L (r[:6]) must be taps 0 / 5 / 10."""
+    ints, nco = field_rows(F)
+    assert all(np.array_equal(r[k], tp[k % 2, (5, 5, 0, 0, 10, 10)[k]]) for k in range(6))
+    rms = float(np.sqrt(np.mean(r[0] ** 2 + r[1] ** 2)))
+    qt = np.rint(tp / (QREL * rms))
+    assert np.abs(qt).max() < 2 ** 31
+    iv = r[ints].astype(np.int64)
+    d = np.diff(iv, axis=1)
+    assert np.abs(d).max() < 2 ** 31
+    return {f"rms_{j}": rms, f"int0_{j}": iv[:, 0], f"intd_{j}": d.astype(np.int32),
+            f"taps_{j}": qt.astype(np.int32), f"nco_{j}": r[nco], f"CN0_{j}": cn0}
+
+
+def expand(z, j):
+    """(integer fields [5][steps], taps [2][11][steps] as floats, nco [7][steps], rms)."""
+    iv = np.concatenate([z[f"int0_{j}"][:, None], z[f"intd_{j}"].astype(np.int64)], axis=1).cumsum(axis=1)
+    rms = float(z[f"rms_{j}"])
+    return iv, z[f"taps_{j}"] * (float(z["qrel"]) * rms), z[f"nco_{j}"], rms
+
+
+def main(out):
+    ctx = pkg.Context(0)
+    file, signal, acq, track = pkg.initParameters()[:4]
+    cfg = pkg.synth.all_prn(NSV, skip_ms=SKIP)
+    dev = pkg.DeviceRecord(ctx, record_bytes(signal.Sample))
+    pkg.synth.generate_device(ctx, cfg, dev)
+    data = dev.download()
+    dg = mgl.digest(data)
+    print("record", len(data), "bytes, xxh64", dg, flush=True)
+    file.skip, file.data = SKIP, data
+    track.msToProcessCT_1ms, track.msToProcessCT_10ms = N1, N10
+    A = acquired(cfg, signal)
+    taps = pkg.colon(-0.5, 0.1, 0.5)
+    stop = threading.Event()
+    threading.Thread(target=mgl.beat, args=(stop,), daemon=True).start()
+    t = time.time()
+    b = po.trackingCT(file, signal, track, A, taps=taps, channels=list(CHANNELS), nthreads=len(CHANNELS),
+                      raw=True)
+    stop.set()
+    assert b.status == 0, b.status
+    print(f"oracle channels {CHANNELS}: {time.time() - t:.1f} s", flush=True)
+    save = dict(digest=dg, skip=SKIP, N1=N1, N10=N10, nsv=NSV, channels=np.array(CHANNELS), qrel=QREL,
+                taps=taps, countinx=np.array([int(b.countinx[c]) for c in CHANNELS]),
+                len=np.array([int(b.len[c]) for c in CHANNELS]))
+    for j, c in enumerate(CHANNELS):
+        n1 = N1 + int(b.countinx[c])
+        L = int(b.len[c])
+        assert L == n1 + N10
+        rec = b.rec[c, :, :L]
+        assert np.array_equal(rec[:, n1::10], rec[:, n1 + 9::10])  # 10x replication
+        r = distinct_steps(rec, n1)
+        tp = distinct_steps(b.taps[c, :, :, :L], n1)  # [2][11][steps]
+        save.update(compact(j, r, tp, b.CN0[: b.c.cn0_rows, c], pkg.abi.FIELDS))
+        print(f"channel {c} (PRN {int(A.sv[c])}): countinx {int(b.countinx[c])}", flush=True)
+    np.savez_compressed(out, **save)
+    print("wrote", out, os.path.getsize(out), "bytes", flush=True)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "golden_cfg5_long.npz"))

@@ -39,7 +39,7 @@ STRUCTS = {
     "gnss_file": "GnssFile", "gnss_signal": "GnssSignal", "gnss_acq": "GnssAcq",
     "gnss_acquired": "GnssAcquired", "gnss_acq_diag": "GnssAcqDiag", "gnss_track": "GnssTrack",
     "gnss_track_out": "GnssTrackOut", "gnss_timing": "GnssTiming", "gnss_synth_sv": "GnssSynthSv",
-    "gnss_synth": "GnssSynth",
+    "gnss_synth": "GnssSynth", "gnss_vt_chan": "GnssVtChan", "gnss_vt_out": "GnssVtOut",
 }
 
 

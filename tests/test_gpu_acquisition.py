@@ -142,3 +142,36 @@ def test_config2_datalen20_against_oracle(pkg, po, ctx, precision):
           "min |SNR-12|", float(gate.min()))
     assert margin[acq_mask].min() > 1e-4
     assert gate.min() > 0.01
+
+
+def test_config4_all_32_prns_against_oracle(pkg, po, ctx):
+    """BASELINE config 4 at its benchmarked shape: the bench's own Urban
+    record (the HIP generator's bytes, skip 1000 ms), all 32 PRNs, +-10 kHz / 250 Hz (81
+    bins), datalen 10, L 10, against the oracle on the same bytes (acquisition.m:47-80 and
+    the fine search :83-126). Decisions bit-exact, SNR within 1e-6 dB, and the margins
+    reported and asserted as in the config-2 test: every acquired PRN's peak clears the
+    largest off-window value by > 1e-4 relative, and every PRN's SNR is > 0.01 dB from the
+    12 dB gate (so no decision rests on round-off)."""
+    skip, S = 1000, 26000
+    cfg = pkg.synth.urban(skip_ms=skip, Fs=26e6)
+    dev = pkg.DeviceRecord(ctx, (skip + 30) * S * 2)
+    pkg.synth.generate_device(ctx, cfg, dev)
+    file = SimpleNamespace(skip=skip, dataType=2, dataPrecision=1, data=None, fileRoute=None, dev=dev)
+    signal = SimpleNamespace(IF=0.0, Fs=26e6, codeFreqBasis=1.023e6, ms=1e-3, Sample=S,
+                             codelength=1023.0)
+    acq = SimpleNamespace(freqNum=81, freqMin=-10000, freqStep=250, datalen=10, L=10)
+    g, gd = pkg.acquisition(file, signal, acq, ctx=ctx, diag=True)
+    hostf = SimpleNamespace(skip=skip, dataType=2, dataPrecision=1, data=dev.download(), fileRoute=None,
+                            dev=None)
+    r, rd = po.acquisition(hostf, signal, acq, diag=True, nthreads=16)
+    compare(g, gd, r, rd)
+    assert len(gd.prn) == 32
+    assert set(pkg.synth.URBAN_SV) <= set(g.sv)
+    acq_mask = np.isin(gd.prn, g.sv)
+    margin = (gd.peak - gd.peak2) / gd.peak
+    gate = np.abs(gd.SNR - 12.0)
+    print("acquired", list(g.sv), "peak margins",
+          dict(zip(gd.prn[acq_mask].tolist(), np.round(margin[acq_mask], 4).tolist())),
+          "min |SNR-12|", float(gate.min()))
+    assert margin[acq_mask].min() > 1e-4
+    assert gate.min() > 0.01

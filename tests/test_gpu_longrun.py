@@ -63,3 +63,57 @@ def test_bench_shape_full_length_against_oracle(pkg, ctx):
             assert np.allclose(got[k], ref[k], rtol=1e-7, atol=1e-9), (int(c), f)
         ref_cn0 = z[f"CN0_{j}"]
         assert np.allclose(b.CN0[: len(ref_cn0), c], ref_cn0, rtol=0, atol=1e-6)
+
+
+PATH5 = os.path.join(GOLDEN, "golden_cfg5_long.npz")
+
+
+@pytest.mark.skipif(not os.path.exists(PATH5), reason="golden_cfg5_long.npz not generated yet")
+def test_config5_full_length_against_oracle(pkg, ctx):
+    """BASELINE config 5 at its benchmarked length: the bench's 32-SV
+    record, all 32 channels x 11 taps (-0.5:0.1:0.5) tracked on one GPU exactly as the bench
+    runs them (the virtual-block persistent launch, one launch per phase: 1000 ms @1 ms +
+    countinx + 90 000 ms @10 ms), against the oracle's run of three of the channels
+    (tests/golden/golden_cfg5_long.npz, tests/golden/make_golden_cfg5.py). Integer fields
+    bit-exact over every step, E/P/L and all 22 tap sums within 1e-8 of the series RMS,
+    NCO state 1e-7 relative, C/N0 1e-6 dB. Reference: trackingCT.m:73-171,:178-213,:377-525;
+    tap semantics trackingCT_multiCorr-GIVEN.m:25."""
+    import sys
+    sys.path.insert(0, GOLDEN)
+    import make_golden_cfg5 as mg
+    import make_golden_long as mgl
+    z = np.load(PATH5)
+    file, signal, acq, track, _, _ = pkg.initParameters()
+    N1, N10, skip = int(z["N1"]), int(z["N10"]), int(z["skip"])
+    cfg = pkg.synth.all_prn(int(z["nsv"]), skip_ms=skip)
+    dev = pkg.DeviceRecord(ctx, mg.record_bytes(signal.Sample))
+    pkg.synth.generate_device(ctx, cfg, dev)
+    assert mgl.digest(dev.download()) == str(z["digest"])
+    file.skip, file.dev = skip, dev
+    track.msToProcessCT_1ms, track.msToProcessCT_10ms = N1, N10
+    A = mg.acquired(cfg, signal)
+    taps = pkg.colon(-0.5, 0.1, 0.5)
+    assert np.array_equal(taps, z["taps"])
+    b = pkg.trackingCT(file, signal, track, A, ctx=ctx, taps=taps, raw=True)
+    assert ctx.timing()["track_launches"] <= 4  # the persistent (virtual-block) loop ran
+    F = pkg.abi.FIELDS
+    ints, nco = mg.field_rows(F)
+    for j, c in enumerate(z["channels"]):
+        n1 = N1 + int(z["countinx"][j])
+        assert int(b.countinx[c]) == int(z["countinx"][j]) and int(b.len[c]) == int(z["len"][j])
+        L = int(b.len[c])
+        got = mg.distinct_steps(b.rec[c, :, :L], n1)
+        gtaps = mg.distinct_steps(b.taps[c, :, :, :L], n1)
+        iv, rtaps, rnco, rms = mg.expand(z, j)
+        for k, i in enumerate(ints):
+            bad = np.nonzero(got[i] != iv[k])[0]
+            assert len(bad) == 0, (int(c), F[i], bad[:5])
+        # E / P / L are taps 0 / 5 / 10 of the 11 (P_i, P_q, E_i, E_q, L_i, L_q)
+        repl = np.stack([rtaps[k % 2, (5, 5, 0, 0, 10, 10)[k]] for k in range(6)])
+        e_epl = np.max(np.abs(got[:6] - repl)) / rms
+        e_taps = np.max(np.abs(gtaps - rtaps)) / rms
+        print(f"channel {int(c)}: E/P/L max err / rms {e_epl:.2e}, taps {e_taps:.2e} (quantum 2e-9)")
+        assert e_epl < 1e-8 and e_taps < 1e-8, (int(c), e_epl, e_taps)
+        assert np.allclose(got[nco], rnco, rtol=1e-7, atol=1e-9), int(c)
+        ref_cn0 = z[f"CN0_{j}"]
+        assert np.allclose(b.CN0[: len(ref_cn0), c], ref_cn0, rtol=0, atol=1e-6)

@@ -7,12 +7,13 @@
 #   traffic      FETCH_SIZE / WRITE_SIZE passes of the 10-ms tracking launch -> gpurun_out/traffic.json
 #   tracksq      SQ counter passes (VALU / LDS / waits) of the tracking launches -> gpurun_out/track_sq.json
 #   acqpmc       FETCH / WRITE + SQ passes of the fp64 acquisition kernels -> gpurun_out/acq_counters.json
+#   probes       per timing-probe library (PROBES="0 1 2 8"): SQ fp64/VALU counts and GNSS_STAMPS
+#   cfg4         bench --workload cfg4 -> gpurun_out/bench_cfg4.json
 #   cfg5         bench --workload cfg5 + its PMC traffic + SQ passes -> gpurun_out/cfg5*.json
 set -o pipefail
 mkdir -p gpurun_out
 R=$GRAFT_REPO_ROOT
 cd "$R" || exit 1
-HEAD_SHA=$(cat "$R/.head_sha" 2>/dev/null || echo unknown)
 SQ1="SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
 SQ2="SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_SALU SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM SQ_ACTIVE_INST_SCA"
 SQ3="SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU"
@@ -35,7 +36,7 @@ for step in "$@"; do
     traffic)
       pmc pmc_fetch FETCH_SIZE python3 "$R/tools/track_only.py" 1000 40000 || exit 1
       pmc pmc_write WRITE_SIZE python3 "$R/tools/track_only.py" 1000 40000 || exit 1
-      python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write "track_run_kernel<3, 3, false, false>" gpurun_out/traffic.json "$HEAD_SHA" || exit 1
+      python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write "track_run_kernel<3, 3, false, false>" gpurun_out/traffic.json || exit 1
       rm -f gpurun_out/pmc_*/**/*kernel_trace.csv ;;
     tracksq)
       pmc trk_sq1 "$SQ1" python3 "$R/tools/track_only.py" 100 400 || exit 1
@@ -50,6 +51,9 @@ for step in "$@"; do
       pmc acq_sq2 "$SQ2" python3 "$R/tools/acq_only.py" || exit 1
       python3 tools/pmc_sq.py gpurun_out/acq_counters.json gpurun_out/acq_fetch gpurun_out/acq_write gpurun_out/acq_sq1 gpurun_out/acq_sq2 -- "inv_cols_kernel<29, HIP_vector_type<double" "inv_rows_kernel_f64<29>" "fwd_rows_kernel<29" "fine_rows_kernel<29" "fine_cols_kernel<29>" || exit 1
       rm -f gpurun_out/acq_*/**/*kernel_trace.csv ;;
+    cfg4)
+      timeout -k 10 400 python3 bench.py --workload cfg4 $BENCH_ARGS > gpurun_out/bench_cfg4.json 2> gpurun_out/bench_cfg4.err \
+        && tail -1 gpurun_out/bench_cfg4.json | cut -c1-500 || { tail -20 gpurun_out/bench_cfg4.err; exit 1; } ;;
     cfg5)
       timeout -k 10 500 python3 bench.py --workload cfg5 $BENCH_ARGS > gpurun_out/bench_cfg5.json 2> gpurun_out/bench_cfg5.err \
         && tail -1 gpurun_out/bench_cfg5.json | cut -c1-700 || { tail -20 gpurun_out/bench_cfg5.err; exit 1; }
@@ -57,6 +61,14 @@ for step in "$@"; do
       pmc c5_sq3 "$SQ3" python3 "$R/tools/track_only.py" 100 400 11 32 || exit 1
       python3 tools/pmc_sq.py gpurun_out/cfg5_sq.json gpurun_out/c5_sq1 gpurun_out/c5_sq3 -- "track_run_kernel<11, 3" || exit 1
       rm -f gpurun_out/c5_*/**/*kernel_trace.csv ;;
+    probes)  # timing-probe libraries (tools/build_probe.sh $PROBES): fp64 / VALU counts + stamps each
+      for n in ${PROBES:-0}; do
+        GNSS_LIB=$R/tools/probe_lib/libgnss_probe$n.so pmc pr${n}_sq "$SQ3" python3 "$R/tools/track_only.py" 100 400 || exit 1
+        python3 tools/pmc_sq.py gpurun_out/probe_sq_$n.json gpurun_out/pr${n}_sq -- "track_run_kernel<3, 3, false, false>" > /dev/null || exit 1
+        GNSS_LIB=$R/tools/probe_lib/libgnss_probe$n.so GNSS_STAMPS=gpurun_out/st_$n.bin timeout -k 10 120 python3 tools/track_only.py 100 2000 > gpurun_out/st_$n.log 2>&1 || { tail gpurun_out/st_$n.log; exit 1; }
+        echo "probe $n: $(python3 tools/stamps_run.py gpurun_out/st_$n.bin | grep -E 'period|computed|all partials|next desc' | tr -s ' ' | tr '\n' ';')"
+      done
+      rm -f gpurun_out/pr*_sq/**/*kernel_trace.csv ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
