@@ -1239,24 +1239,36 @@ __device__ __forceinline__ void publish16(__amdgpu_buffer_rsrc_t r, int unit, do
 }
 
 // Poll n 16-B granules until both tags of each equal `tag`; granule e's words land in
-// dst[2e], dst[2e+1]. Same protocol as sweep_words (pollers pid 0..np-1, n <= 64*np).
+// dst[2e], dst[2e+1]. Same protocol as sweep_words (pollers pid 0..np-1, n <= 64*np), but a
+// lane's loads go out CH at a time back to back and are checked after one wait: a poll round
+// costs one memory round trip, not one per granule (a load, its s_waitcnt and the tag check
+// per granule made the 10-ms exchange two to three serial round trips).
+template <int CH>
 __device__ bool sweep16(__amdgpu_buffer_rsrc_t r, int n, unsigned tag, unsigned* dst, int pid, int np,
                         unsigned* err, int base)
 {
-    unsigned long long todo = 0;
-    if (pid >= 0)
-        for (int k = 0, e = pid; e < n; k++, e += np) todo |= 1ull << k;
+    const int ng = (pid >= 0 && pid < n) ? (n - pid + np - 1) / np : 0;  // this lane's granules
+    unsigned long long todo = ng >= 64 ? ~0ull : (1ull << ng) - 1ull;
     unsigned long long t0 = 0;
     int late = 0;
     while (todo) {
-        for (int k = 0; (todo >> k) != 0; k++) {
-            if (!((todo >> k) & 1ull)) continue;
-            const int e = pid + k * np;
-            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (base + e) * 16, 0, kPolSc1);
-            if (v.y == tag && v.w == tag) {
-                dst[2 * e] = v.x;
-                dst[2 * e + 1] = v.z;
-                todo &= ~(1ull << k);
+        for (int k0 = 0; k0 < ng; k0 += CH) {
+            if (((todo >> k0) & ((1ull << CH) - 1ull)) == 0) continue;
+            u32x4 v[CH];
+#pragma unroll
+            for (int j = 0; j < CH; j++) {
+                const int e = k0 + j < ng ? pid + (k0 + j) * np : pid;  // (past the end: any own granule)
+                v[j] = __builtin_amdgcn_raw_buffer_load_b128(r, (base + e) * 16, 0, kPolSc1);
+            }
+#pragma unroll
+            for (int j = 0; j < CH; j++) {
+                const int k = k0 + j;
+                if (k < ng && ((todo >> k) & 1ull) && v[j].y == tag && v[j].w == tag) {
+                    const int e = pid + k * np;
+                    dst[2 * e] = v[j].x;
+                    dst[2 * e + 1] = v[j].z;
+                    todo &= ~(1ull << k);
+                }
             }
         }
         if (!todo) break;

@@ -58,6 +58,20 @@ def scenario(svs, codedelays, dopplers, cn0s, *, Fs=58e6, IF=4.58e6, skip_ms=500
     return cfg
 
 
+def codedelays(cfg, skip_ms):
+    """The code delays (samples, acquisition.m's codedelay convention) `scenario` placed each
+    SV at, recovered from its code phase: the inverse of code_phase0 = cd*d0 - n_ref*crate."""
+    S = math.ceil(cfg.Fs * 1e-3)
+    d0 = FC / cfg.Fs
+    n_ref = skip_ms * S - 1
+    out = []
+    for i in range(cfg.n_sv):
+        v = cfg.sv[i]
+        crate = FC * (1.0 + v.doppler_hz / FL1) / cfg.Fs
+        out.append(int(round((v.code_phase0 + n_ref * crate) / d0)) % S)
+    return out
+
+
 def opensky(skip_ms=5000, seed=6102, cn0=None):
     cn0s = cn0 or [40.0 + (s - 17.0) * 0.8 for s in OPENSKY_SNR]
     dop = [f - 4.58e6 for f in OPENSKY_FINEFREQ]

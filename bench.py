@@ -179,7 +179,7 @@ def run_cfg5(args, rank, world, local, dist, ctx):
     dev = pkg.DeviceRecord(ctx, (skip + 1000 + 19 + args.n10_cfg5 + 3) * S * 2)
     pkg.synth.generate_device(ctx, cfg, dev)
     file.skip, file.dev = skip, dev
-    cds = [int(round((-cfg.sv[i].code_phase0) % 1023 / (1.023e6 / signal.Fs))) % S for i in range(nsv)]
+    cds = pkg.synth.codedelays(cfg, skip)  # where the scenario put each SV (acquisition.m convention)
     A = SimpleNamespace(sv=np.array([cfg.sv[i].prn for i in range(nsv)]), SNR=np.zeros(nsv),
                         Doppler=np.zeros(nsv), codedelay=np.array(cds),
                         fineFreq=np.array([signal.IF + cfg.sv[i].doppler_hz for i in range(nsv)]))

@@ -41,7 +41,7 @@ def record_bytes(S=58000):
 
 def acquired(cfg, signal):
     S = signal.Sample
-    cds = [int(round((-cfg.sv[i].code_phase0) % 1023 / (1.023e6 / signal.Fs))) % S for i in range(NSV)]
+    cds = pkg.synth.codedelays(cfg, SKIP)  # where the scenario put each SV
     return SimpleNamespace(sv=np.array([cfg.sv[i].prn for i in range(NSV)]), SNR=np.zeros(NSV),
                            Doppler=np.zeros(NSV), codedelay=np.array(cds),
                            fineFreq=np.array([signal.IF + cfg.sv[i].doppler_hz for i in range(NSV)]))
@@ -115,7 +115,9 @@ def main(out):
         r = distinct_steps(rec, n1)
         tp = distinct_steps(b.taps[c, :, :, :L], n1)  # [2][11][steps]
         save.update(compact(j, r, tp, b.CN0[: b.c.cn0_rows, c], pkg.abi.FIELDS))
-        print(f"channel {c} (PRN {int(A.sv[c])}): countinx {int(b.countinx[c])}", flush=True)
+        lock = float(np.mean(np.abs(r[0, n1:]) > np.abs(r[1, n1:])))  # |P_i| > |P_q| in the 10-ms phase
+        save[f"lock_{j}"] = lock
+        print(f"channel {c} (PRN {int(A.sv[c])}): countinx {int(b.countinx[c])}, 10-ms lock {lock:.3f}", flush=True)
     np.savez_compressed(out, **save)
     print("wrote", out, os.path.getsize(out), "bytes", flush=True)
 

@@ -261,7 +261,7 @@ def test_config5_shape_32_channels_11_taps(pkg, po, ctx):
     data = po.synth_if(cfg, 0, (skip + N1 + 19 + N10 + 4) * 58000)
     file, signal, acq, track = params(pkg, skip, data)
     track.msToProcessCT_1ms, track.msToProcessCT_10ms = N1, N10
-    cds = [int(round((-cfg.sv[i].code_phase0) % 1023 / (1.023e6 / 58e6))) % 58000 for i in range(32)]
+    cds = pkg.synth.codedelays(cfg, skip)
     A = SimpleNamespace(sv=np.array([cfg.sv[i].prn for i in range(32)]), SNR=np.zeros(32),
                         Doppler=np.zeros(32), codedelay=np.array(cds),
                         fineFreq=np.array([4.58e6 + cfg.sv[i].doppler_hz for i in range(32)]))

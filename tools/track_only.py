@@ -18,7 +18,7 @@ pkg.synth.generate_device(ctx, cfg, dev)
 file.skip, file.dev = skip, dev
 from types import SimpleNamespace
 S = 58000
-cds = [int(round((cfg.sv[i].code_phase0 * -1) % 1023 / (1.023e6 / 58e6))) % S for i in range(cfg.n_sv)]
+cds = pkg.synth.codedelays(cfg, skip)
 A = SimpleNamespace(sv=np.array([cfg.sv[i].prn for i in range(nch)]), SNR=np.zeros(nch), Doppler=np.zeros(nch),
                     codedelay=np.array(cds[:nch]), fineFreq=np.array([4.58e6 + cfg.sv[i].doppler_hz for i in range(nch)]))
 track.msToProcessCT_1ms, track.msToProcessCT_10ms = N1, N10
