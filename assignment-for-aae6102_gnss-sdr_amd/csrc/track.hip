@@ -1502,7 +1502,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         // (waves 0, 2, 3 poll; wave 1 is flushing the previous step meanwhile)
         // (block 0: waves 0, 2, 3 poll while wave 1 writes the record; the other blocks'
         // wave 1 flush is short and it joins the polling after it)
-        if (!sweep16(pg, bpc * NV, tag0 + s + 1, pw, io ? (wv == 1 ? -1 : tid - (wv > 1 ? 64 : 0)) : tid,
+        if (!sweep16<(NT > 3 ? 12 : 4)>(pg, bpc * NV, tag0 + s + 1, pw, io ? (wv == 1 ? -1 : tid - (wv > 1 ? 64 : 0)) : tid,
                      io ? 3 * 64 : 4 * 64, b.run_err, (s & 1) * kMaxBpcRun * NV))
             return;
         if (srow && tid == 0) srow[3] = wall_clock64();
