@@ -1,7 +1,7 @@
 # One MI355X check, run from the repo root via gpurun:
 #   gpurun --timeout 1200 -- bash tools/gpu.sh STEP [STEP ...]
 # Steps run in order, each under its own time limit; the first failure ends the call.
-#   tests        pytest -m gpu (PYTEST_K="-k expr" narrows it)
+#   tests        pytest -m gpu (PYTEST_K="expr" narrows it to -k expr)
 #   bench        python bench.py (BENCH_ARGS adds flags) -> gpurun_out/bench.json
 #   prof         rocprofv3 --kernel-trace --stats of one bench step -> gpurun_out/prof_bench(_summary.txt)
 #   traffic      FETCH_SIZE / WRITE_SIZE passes of the 10-ms tracking launch -> gpurun_out/traffic.json
@@ -25,7 +25,7 @@ for step in "$@"; do
   echo "== $step $(date +%T)"
   case $step in
     tests)
-      timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread $PYTEST_K > gpurun_out/pytest_gpu.log 2>&1 \
+      timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu.log 2>&1 \
         && echo "TESTS_OK $(tail -1 gpurun_out/pytest_gpu.log)" || { grep -E "FAIL|Error" gpurun_out/pytest_gpu.log | tail -30; tail -40 gpurun_out/pytest_gpu.log; exit 1; } ;;
     bench)
       timeout -k 10 400 python3 bench.py $BENCH_ARGS > gpurun_out/bench.json 2> gpurun_out/bench.err \
