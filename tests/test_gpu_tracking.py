@@ -256,7 +256,8 @@ def test_config5_shape_32_channels_11_taps(pkg, po, ctx):
     ACF taps -0.5:0.1:0.5, one GPU (the persistent loop with several of the step's blocks
     per resident block: 32 x 96 blocks would not all be resident), against the oracle."""
     from types import SimpleNamespace
-    skip, N1, N10 = 0, 650, 20  # (the bit-edge search needs i >= 600, trackingCT.m:179-204)
+    skip, N1, N10 = 0, 1000, 20  # (the bit-edge search window of trackingCT.m:179-204: the channels
+    # are locked, the first data-bit edge after 600 ms can lie well past it)
     cfg = pkg.synth.all_prn(32, skip_ms=skip)
     data = po.synth_if(cfg, 0, (skip + N1 + 19 + N10 + 4) * 58000)
     file, signal, acq, track = params(pkg, skip, data)

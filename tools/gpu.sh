@@ -69,6 +69,8 @@ for step in "$@"; do
         echo "probe $n: $(python3 tools/stamps_run.py gpurun_out/st_$n.bin | grep -E 'period|computed|all partials|next desc' | tr -s ' ' | tr '\n' ';')"
       done
       rm -f gpurun_out/pr*_sq/**/*kernel_trace.csv ;;
+    lat)  # fp64 / fp32 dependent-latency micro-benchmark (tools/micro/lat2, built in-tree)
+      timeout -k 10 60 ./tools/micro/lat2 > gpurun_out/lat2.txt 2>&1 && cat gpurun_out/lat2.txt || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
