@@ -228,6 +228,8 @@ def load(path: str | None = None):
         _torch_first = "torch" in sys.modules
     lib = C.CDLL(p)
     for name, (res, args) in PROTOTYPES.items():
+        if p != LIB_PATH and not hasattr(lib, name):
+            continue  # (an A/B or probe build of another revision: entry points it lacks stay unbound)
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -1239,36 +1239,24 @@ __device__ __forceinline__ void publish16(__amdgpu_buffer_rsrc_t r, int unit, do
 }
 
 // Poll n 16-B granules until both tags of each equal `tag`; granule e's words land in
-// dst[2e], dst[2e+1]. Same protocol as sweep_words (pollers pid 0..np-1, n <= 64*np), but a
-// lane's loads go out CH at a time back to back and are checked after one wait: a poll round
-// costs one memory round trip, not one per granule (a load, its s_waitcnt and the tag check
-// per granule made the 10-ms exchange two to three serial round trips).
-template <int CH, bool SYNC = true>
+// dst[2e], dst[2e+1]. Same protocol as sweep_words (pollers pid 0..np-1, n <= 64*np).
 __device__ bool sweep16(__amdgpu_buffer_rsrc_t r, int n, unsigned tag, unsigned* dst, int pid, int np,
                         unsigned* err, int base)
 {
-    const int ng = (pid >= 0 && pid < n) ? (n - pid + np - 1) / np : 0;  // this lane's granules
-    unsigned long long todo = ng >= 64 ? ~0ull : (1ull << ng) - 1ull;
+    unsigned long long todo = 0;
+    if (pid >= 0)
+        for (int k = 0, e = pid; e < n; k++, e += np) todo |= 1ull << k;
     unsigned long long t0 = 0;
     int late = 0;
     while (todo) {
-        for (int k0 = 0; k0 < ng; k0 += CH) {
-            if (((todo >> k0) & ((1ull << CH) - 1ull)) == 0) continue;
-            u32x4 v[CH];
-#pragma unroll
-            for (int j = 0; j < CH; j++) {
-                const int e = k0 + j < ng ? pid + (k0 + j) * np : pid;  // (past the end: any own granule)
-                v[j] = __builtin_amdgcn_raw_buffer_load_b128(r, (base + e) * 16, 0, kPolSc1);
-            }
-#pragma unroll
-            for (int j = 0; j < CH; j++) {
-                const int k = k0 + j;
-                if (k < ng && ((todo >> k) & 1ull) && v[j].y == tag && v[j].w == tag) {
-                    const int e = pid + k * np;
-                    dst[2 * e] = v[j].x;
-                    dst[2 * e + 1] = v[j].z;
-                    todo &= ~(1ull << k);
-                }
+        for (int k = 0; (todo >> k) != 0; k++) {
+            if (!((todo >> k) & 1ull)) continue;
+            const int e = pid + k * np;
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (base + e) * 16, 0, kPolSc1);
+            if (v.y == tag && v.w == tag) {
+                dst[2 * e] = v.x;
+                dst[2 * e + 1] = v.z;
+                todo &= ~(1ull << k);
             }
         }
         if (!todo) break;
@@ -1279,7 +1267,6 @@ __device__ bool sweep16(__amdgpu_buffer_rsrc_t r, int n, unsigned tag, unsigned*
             late = 0;
         }
     }
-    if constexpr (!SYNC) return todo == 0;  // (the caller's barrier follows)
     return !__syncthreads_or(todo != 0);
 }
 
@@ -1367,11 +1354,9 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
     __shared__ __attribute__((aligned(16))) TrkChan s_c;           // the channel state
     __shared__ StepOut s_o;                                        // the step whose state and
     __shared__ LoopUpd s_u;                                        //   record are pending
-    __shared__ double s_fin2[2][NV];  // the channel sums, by step parity (the flush of step s
-                                      // reads its own while step s + 1's are written)
+    __shared__ double s_fin[NV];
     __shared__ double s_taps[GNSS_MAX_TAPS], s_post[GNSS_MAX_TAPS];
     __shared__ double2 s_zero;
-    __shared__ int s_timeout;
 
     if (!census(b.run_err, tid)) return;
     g_chan* cp = (g_chan*)(b.chan + ch);
@@ -1389,10 +1374,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
     for (int e = tid; e < kDescWords; e += T)
         reinterpret_cast<unsigned*>(&s_d[0])[e] = ((const g_u32*)(b.desc + ch))[e];
     if (tid < kChanWords) reinterpret_cast<uint64_t*>(&s_c)[tid] = ((const g_u64*)cp)[tid];
-    if (tid == 0) {
-        s_zero = make_double2(0.0, 0.0);
-        s_timeout = 0;
-    }
+    if (tid == 0) s_zero = make_double2(0.0, 0.0);
     if (tid < NT) {
         s_taps[tid] = p.taps[tid];
         s_post[tid] = p.tap_post[tid];
@@ -1402,25 +1384,20 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         prefetch_raw<SUB>(iq, s_d[0].g_first + ((int64_t)blk * T + tid) * SUB, gmax, s_raw, tid);
 
     int cur = 0;   // s_d[cur]: this step
-    bool pend = false;  // a finished step's state / record still to write (s_o, s_u, s_fin2[fpend])
-    int fpend = 0;
+    bool pend = false;  // a finished step's state / record still to write (s_o, s_u, s_fin)
     int64_t pre[2] = {0, 0};  // block 0: its record's delayValue prefix reads, issued early
     bool pre_ok = false;      //   (for the pending step)
     // The pending step's side effects, by wave 1 while the next step's partials are in
     // flight (off the critical path): the state replica (every block, in place) and, in
     // block 0, the record, C/N0 and taps.
-    // The channel sum's lanes (tid < CL * NV) poll the partials they add; the flush runs on
-    // wave 3, which none of them is in.
-    constexpr int CL = chan_lanes<NV>();
-    static_assert(CL * NV <= 3 * 64, "the flush wave (3) must not hold a channel-sum lane");
     auto flush = [&]() {
-        if (wv == 3) {
+        if (wv == 1) {
             if (io) {
-                if (lane == 0) write_record_i(p, b, ch, s_c, s_o, s_u, s_fin2[fpend], pre_ok ? pre : nullptr);
+                if (lane == 0) write_record_i(p, b, ch, s_c, s_o, s_u, s_fin, pre_ok ? pre : nullptr);
                 if (b.taps_rec && lane < NV && s_c.slot < p.rec_cap)
-                    b.taps_rec[((int64_t)ch * p.rec_cap + s_c.slot) * NV + lane] = s_fin2[fpend][lane];
+                    b.taps_rec[((int64_t)ch * p.rec_cap + s_c.slot) * NV + lane] = s_fin[lane];
             }
-            if (lane == 0) update_state_inplace(p, b, ch, s_c, s_o, s_u, s_fin2[fpend], io);
+            if (lane == 0) update_state_inplace(p, b, ch, s_c, s_o, s_u, s_fin, io);
         }
         pend = false;
         pre_ok = false;
@@ -1446,7 +1423,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
             return;
         }
         const int64_t A = uni(D.A), n = uni(D.n);
-        if (pend && io && wv == 3 && lane == 0) {  // (used by the flush below, after the compute)
+        if (pend && io && wv == 1 && lane == 0) {  // (used by the flush below, after the compute)
             const int64_t* dvp = b.dvpre + (int64_t)ch * (p.rec_cap + 1);
             const int64_t cols = record_cols(p, s_c, s_o.phaseC);
             pre[0] = dvp[s_c.nstep];
@@ -1501,48 +1478,45 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
 
         // the step's remPhase / remSample (role 2 of the descriptor, off the tail: the
         // next tail reads them after the sweep's closing barrier)
-        if (wv == 3 && lane == 0) desc_rem(p, &s_d[cur]);
+        if (wv == 1 && lane == 0) desc_rem(p, &s_d[cur]);
         if (pend) {
             if (srow && tid == 64) srow[16] = wall_clock64();
             flush();  // (the sweep's closing barrier publishes it)
             if (srow && tid == 64) srow[17] = wall_clock64();
         }
 
-        // ---- every block's partial, summed in a fixed order (bit-identical in all blocks):
-        // lane (v, q) of the channel sum (tid < CL*NV, v = tid / CL, q = tid % CL) polls the
-        // granules it adds -- value v of blocks q, q + CL, ... -- then adds them in block
-        // order and finishes with the DPP butterfly of its CL lanes (one wave): no block
-        // barrier between the hand-off and the sum. Wave 3 flushes the previous step meanwhile.
+        // ---- every block's partial, summed in a fixed order (bit-identical in all blocks)
         unsigned* pw = reinterpret_cast<unsigned*>(s_mem);
-        const bool sum_lane = tid < CL * NV;
-        const bool polled = sweep16<(NT > 3 ? 12 : 6), false>(
-            pg, bpc * NV, tag0 + s + 1, pw, sum_lane ? (tid % CL) * NV + tid / CL : -1, CL * NV, b.run_err,
-            (s & 1) * kMaxBpcRun * NV);
+        // (waves 0, 2, 3 poll; wave 1 is flushing the previous step meanwhile)
+        // (block 0: waves 0, 2, 3 poll while wave 1 writes the record; the other blocks'
+        // wave 1 flush is short and it joins the polling after it)
+        if (!sweep16(pg, bpc * NV, tag0 + s + 1, pw, io ? (wv == 1 ? -1 : tid - (wv > 1 ? 64 : 0)) : tid,
+                     io ? 3 * 64 : 4 * 64, b.run_err, (s & 1) * kMaxBpcRun * NV))
+            return;
         if (srow && tid == 0) srow[3] = wall_clock64();
-        if (sum_lane) {
-            const double a = channel_sum<NV>(bpc, tid, [&](int k, int v) {
-                const unsigned lo = pw[(k * NV + v) * 2], hi = pw[(k * NV + v) * 2 + 1];
-                return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-            });
-            if constexpr (GNSS_CORR_PROBE != 0)  // (probe builds: E = P = L = 1, a steady loop)
-                if (tid % CL == 0) s_fin2[s & 1][tid / CL] = ((tid / CL) & 1) ? 0.0 * a : 1.0 + 0.0 * a;
-            if constexpr (GNSS_CORR_PROBE == 0)
-                if (tid % CL == 0) s_fin2[s & 1][tid / CL] = D.phaseC ? -a : a;  // :447-449
-        }
-        if (!polled) s_timeout = 1;
-        const int phaseC = D.phaseC;
-        lds_barrier();
-        if (s_timeout) return;  // (run_err is set)
-        if (srow && io && tid == 0) srow[10] = wall_clock64();
         // wave 2 issues the whole block's next IF (it starts at A + n, ftell after this
-        // read; issued once every poll has returned, so no poll queued behind it) and waits
-        // for it at the end of the tail: the correlator waves never stall on it
+        // read; the polls above would have queued behind it) and waits for it at the end
+        // of the tail: the correlator waves never stall on it
         if (wv == 2 && s + 1 < nsteps) {
 #pragma unroll
             for (int h = 0; h < 4; h++)
                 prefetch_raw<SUB>(iq, ((A + n) >> 3) + ((int64_t)blk * T + h * 64 + lane) * SUB, gmax, s_raw,
                                   h * 64 + lane);
         }
+        constexpr int CL = chan_lanes<NV>();
+        if (tid < CL * NV) {
+            const double a = channel_sum<NV>(bpc, tid, [&](int k, int v) {
+                const unsigned lo = pw[(k * NV + v) * 2], hi = pw[(k * NV + v) * 2 + 1];
+                return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+            });
+            if constexpr (GNSS_CORR_PROBE != 0)  // (probe builds: E = P = L = 1, a steady loop)
+                if (tid % CL == 0) s_fin[tid / CL] = ((tid / CL) & 1) ? 0.0 * a : 1.0 + 0.0 * a;
+            if constexpr (GNSS_CORR_PROBE == 0)
+                if (tid % CL == 0) s_fin[tid / CL] = D.phaseC ? -a : a;  // :447-449
+        }
+        const int phaseC = D.phaseC;
+        lds_barrier();
+        if (srow && io && tid == 0) srow[10] = wall_clock64();
 
         // ---- the loop update and the next descriptor: wave 0 its code half (DLL half of
         // the update), wave 3 its carrier table (PLL half), wave 2 the next remPhase; wave 1
@@ -1556,7 +1530,6 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         o.remPhase = D.remPhase_next;
         o.pdi = D.pdi;
         o.phaseC = phaseC;
-        const double* s_fin = s_fin2[s & 1];
         const LoopUpd u = loop_update_i(p, c, s_fin[2 * p.iE], s_fin[2 * p.iE + 1], s_fin[2 * p.iP],
                                       s_fin[2 * p.iP + 1], s_fin[2 * p.iL], s_fin[2 * p.iL + 1], o.pdi,
                                       o.phaseC, wv == 0 || wv == 2 ? 1 : wv == 3 ? 2 : 3);  // (each role's half)
@@ -1583,7 +1556,6 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         pend = true;
-        fpend = s & 1;
         lds_barrier();
         if (srow && tid == 0) srow[4] = wall_clock64();
         cur ^= 1;

@@ -39,9 +39,9 @@ for step in "$@"; do
       python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write "track_run_kernel<3, 3, false, false>" gpurun_out/traffic.json || exit 1
       rm -f gpurun_out/pmc_*/**/*kernel_trace.csv ;;
     tracksq)
-      pmc trk_sq1 "$SQ1" python3 "$R/tools/track_only.py" 100 400 || exit 1
-      pmc trk_sq2 "$SQ2" python3 "$R/tools/track_only.py" 100 400 || exit 1
-      pmc trk_sq3 "$SQ3" python3 "$R/tools/track_only.py" 100 400 || exit 1
+      pmc trk_sq1 "$SQ1" python3 "$R/tools/track_only.py" 1000 400 || exit 1
+      pmc trk_sq2 "$SQ2" python3 "$R/tools/track_only.py" 1000 400 || exit 1
+      pmc trk_sq3 "$SQ3" python3 "$R/tools/track_only.py" 1000 400 || exit 1
       python3 tools/pmc_sq.py gpurun_out/track_sq.json gpurun_out/trk_sq1 gpurun_out/trk_sq2 gpurun_out/trk_sq3 -- "track_run_kernel<3, 3, false, false>" "track_run_kernel<3, 1, false, false>" || exit 1
       rm -f gpurun_out/trk_sq*/**/*kernel_trace.csv ;;
     acqpmc)
@@ -57,18 +57,27 @@ for step in "$@"; do
     cfg5)
       timeout -k 10 500 python3 bench.py --workload cfg5 $BENCH_ARGS > gpurun_out/bench_cfg5.json 2> gpurun_out/bench_cfg5.err \
         && tail -1 gpurun_out/bench_cfg5.json | cut -c1-700 || { tail -20 gpurun_out/bench_cfg5.err; exit 1; }
-      pmc c5_sq1 "$SQ1" python3 "$R/tools/track_only.py" 100 400 11 32 || exit 1
-      pmc c5_sq3 "$SQ3" python3 "$R/tools/track_only.py" 100 400 11 32 || exit 1
+      pmc c5_sq1 "$SQ1" python3 "$R/tools/track_only.py" 1000 400 11 32 || exit 1
+      pmc c5_sq3 "$SQ3" python3 "$R/tools/track_only.py" 1000 400 11 32 || exit 1
       python3 tools/pmc_sq.py gpurun_out/cfg5_sq.json gpurun_out/c5_sq1 gpurun_out/c5_sq3 -- "track_run_kernel<11, 3" || exit 1
       rm -f gpurun_out/c5_*/**/*kernel_trace.csv ;;
     probes)  # timing-probe libraries (tools/build_probe.sh $PROBES): fp64 / VALU counts + stamps each
       for n in ${PROBES:-0}; do
-        GNSS_LIB=$R/tools/probe_lib/libgnss_probe$n.so pmc pr${n}_sq "$SQ3" python3 "$R/tools/track_only.py" 100 400 || exit 1
+        GNSS_LIB=$R/tools/probe_lib/libgnss_probe$n.so pmc pr${n}_sq "$SQ3" python3 "$R/tools/track_only.py" 1000 400 || exit 1
         python3 tools/pmc_sq.py gpurun_out/probe_sq_$n.json gpurun_out/pr${n}_sq -- "track_run_kernel<3, 3, false, false>" > /dev/null || exit 1
-        GNSS_LIB=$R/tools/probe_lib/libgnss_probe$n.so GNSS_STAMPS=gpurun_out/st_$n.bin timeout -k 10 120 python3 tools/track_only.py 100 2000 > gpurun_out/st_$n.log 2>&1 || { tail gpurun_out/st_$n.log; exit 1; }
+        GNSS_LIB=$R/tools/probe_lib/libgnss_probe$n.so GNSS_STAMPS=gpurun_out/st_$n.bin timeout -k 10 120 python3 tools/track_only.py 1000 2000 > gpurun_out/st_$n.log 2>&1 || { tail gpurun_out/st_$n.log; exit 1; }
         echo "probe $n: $(python3 tools/stamps_run.py gpurun_out/st_$n.bin | grep -E 'period|computed|all partials|next desc' | tr -s ' ' | tr '\n' ';')"
       done
       rm -f gpurun_out/pr*_sq/**/*kernel_trace.csv ;;
+    ab)  # A/B of library builds (tools/build_commit_lib.sh / build_probe.sh): AB="name ..." ->
+         # tools/probe_lib/libgnss_<name>.so; 8-channel trackingCT (1000 ms + 4000 x 10 ms), per-launch
+         # hipEvents and GNSS_STAMPS of the 10-ms launch
+      for v in $AB; do
+        GNSS_LIB=$R/tools/probe_lib/libgnss_$v.so TRK_PROFILE=1 TRK_ITERS=3 timeout -k 10 120 python3 tools/track_only.py 1000 40000 > gpurun_out/ab_$v.log 2>&1 || { tail -5 gpurun_out/ab_$v.log; exit 1; }
+        GNSS_LIB=$R/tools/probe_lib/libgnss_$v.so GNSS_STAMPS=gpurun_out/abst_$v.bin TRK_ITERS=1 timeout -k 10 120 python3 tools/track_only.py 1000 2000 > /dev/null 2>&1 || exit 1
+        echo "ab $v: $(grep track10 gpurun_out/ab_$v.log | tail -2 | tr '\n' ' ')"
+        python3 tools/stamps_run.py gpurun_out/abst_$v.bin | grep -E "period|computed|all partials|next desc|tail" | sed "s/^/   /"
+      done ;;
     lat)  # fp64 / fp32 dependent-latency micro-benchmark (tools/micro/lat2, built in-tree)
       timeout -k 10 60 ./tools/micro/lat2 > gpurun_out/lat2.txt 2>&1 && cat gpurun_out/lat2.txt || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
