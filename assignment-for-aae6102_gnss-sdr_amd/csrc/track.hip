@@ -96,6 +96,54 @@ __device__ __forceinline__ unsigned long long load_agent(const unsigned long lon
     return __hip_atomic_load((g_u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The scalar tail's per-launch constants, held in registers for the whole step loop: built
+// once from TrkParams at the launch's start and laundered through a volatile asm, so the
+// compiler can neither re-load them from memory on every step (each reload was a scalar
+// load and its wait on the tail's dependent chain) nor hoist anything across. The tail's
+// functions take it in place of TrkParams (same field names; the int16 layout, fmt 1, never
+// runs in the persistent loop).
+struct TailK {
+    double Fs, inv_Fs, codelength, S, codeFreqBasis, ms;
+    double dll_r, dll_t1, dll_t10, pll_r, pll_t1, pll_t10, tau1code, tau1carr;
+    int32_t exact_div, conv, given, chip_off, ntaps, iE, iP, iL, bps;
+    int64_t file_len, buf_base, buf_len;
+    const double* taps;
+    const double* tap_post;
+    static constexpr int fmt = 0;
+    static constexpr const long long* pref_i = nullptr;
+    static constexpr const long long* pref_q = nullptr;
+    static constexpr const short* stage16 = nullptr;
+};
+
+template <class T>
+__device__ __forceinline__ void launder_s(T& v)
+{
+    asm volatile("" : "+s"(v));
+}
+
+__device__ __forceinline__ TailK tail_k(const TrkParams& p)
+{
+    TailK k;
+    k.Fs = p.Fs; k.inv_Fs = p.inv_Fs; k.codelength = p.codelength; k.S = p.S;
+    k.codeFreqBasis = p.codeFreqBasis; k.ms = p.ms;
+    k.dll_r = p.dll_r; k.dll_t1 = p.dll_t1; k.dll_t10 = p.dll_t10;
+    k.pll_r = p.pll_r; k.pll_t1 = p.pll_t1; k.pll_t10 = p.pll_t10;
+    k.tau1code = p.tau1code; k.tau1carr = p.tau1carr;
+    k.exact_div = p.exact_div; k.conv = p.conv; k.given = p.given; k.chip_off = p.chip_off;
+    k.ntaps = p.ntaps; k.iE = p.iE; k.iP = p.iP; k.iL = p.iL; k.bps = p.bps;
+    k.file_len = p.file_len; k.buf_base = p.buf_base; k.buf_len = p.buf_len;
+    k.taps = p.taps; k.tap_post = p.tap_post;
+    launder_s(k.Fs); launder_s(k.inv_Fs); launder_s(k.codelength); launder_s(k.S);
+    launder_s(k.codeFreqBasis); launder_s(k.ms);
+    launder_s(k.dll_r); launder_s(k.dll_t1); launder_s(k.dll_t10);
+    launder_s(k.pll_r); launder_s(k.pll_t1); launder_s(k.pll_t10);
+    launder_s(k.tau1code); launder_s(k.tau1carr);
+    launder_s(k.exact_div); launder_s(k.conv); launder_s(k.given); launder_s(k.chip_off);
+    launder_s(k.ntaps); launder_s(k.iE); launder_s(k.iP); launder_s(k.iL); launder_s(k.bps);
+    launder_s(k.file_len); launder_s(k.buf_base); launder_s(k.buf_len);
+    return k;
+}
+
 // CarrTime = k/Fs (trackingCT.m:104) as the IEEE quotient: one FMA-corrected
 // reciprocal (host-verified exact for this Fs and k range) or a true division.
 template <bool DIVIDE>
@@ -167,7 +215,8 @@ struct StepSize {
 
 // codeFreq / Fs and k / Fs: the IEEE quotient by Markstein's correction, or a true division
 // where the host could not verify the correction for this Fs (TrkParams.exact_div)
-__device__ __forceinline__ double over_fs(const TrkParams& p, double x)
+template <class P>
+__device__ __forceinline__ double over_fs(const P& p, double x)
 {
     return p.exact_div ? x / p.Fs : div_const(x, p.Fs, p.inv_Fs);
 }
@@ -183,7 +232,8 @@ __device__ __forceinline__ double fast_rcp(double x)
     return __builtin_fma(r, e, r);
 }
 
-__device__ __forceinline__ StepSize step_size(const TrkParams& p, const NcoState& c, int pdi, int phaseC)
+template <class P>
+__device__ __forceinline__ StepSize step_size(const P& p, const NcoState& c, int pdi, int phaseC)
 {
     StepSize z;
     z.cps = over_fs(p, c.codeFreq);
@@ -207,7 +257,8 @@ __device__ __forceinline__ StepSize step_size(const TrkParams& p, const NcoState
 }
 
 // remSample of the step (trackingCT.m:79 / :414), for the record
-__device__ __forceinline__ double step_rem_sample(const TrkParams& p, const NcoState& c, int pdi, int phaseC)
+template <class P>
+__device__ __forceinline__ double step_rem_sample(const P& p, const NcoState& c, int pdi, int phaseC)
 {
     if (p.conv) return 0.0;  // (trackingCT_POS_updated.m has none)
     const double cps = over_fs(p, c.codeFreq);
@@ -230,7 +281,8 @@ __device__ __forceinline__ double lds_at(const double* q, int i)
 
 // The step's scalar fields and its numSample / file / staging checks (trackingCT.m:79-82,
 // 108-112, 442): lane 0 writes them; GNSS_* or GNSS_OK returned in every lane.
-__device__ __forceinline__ int desc_scalars(const TrkParams& p, const NcoState& c, const StepSize& z, int pdi,
+template <class P>
+__device__ __forceinline__ int desc_scalars(const P& p, const NcoState& c, const StepSize& z, int pdi,
                                             int phaseC, int lane, StepDesc* d)
 {
     const int64_t n = z.n;
@@ -284,7 +336,8 @@ __device__ __forceinline__ int desc_scalars(const TrkParams& p, const NcoState& 
 // The replica colons of the taps (trackingCT.m:96-102): lane s < ntaps stores tap s's colon
 // start / end (all the correlator lanes need), then checks its replica index range and, for
 // the prompt, the next remChip. Returns GNSS_EINDEX in a lane whose index range fails.
-__device__ __forceinline__ int desc_taps(const TrkParams& p, const NcoState& c, const StepSize& z, int pdi,
+template <class P>
+__device__ __forceinline__ int desc_taps(const P& p, const NcoState& c, const StepSize& z, int pdi,
                                          int lane, StepDesc* d, const double* taps, const double* posts)
 {
     if (lane >= p.ntaps) return GNSS_OK;
@@ -315,7 +368,8 @@ __device__ __forceinline__ int desc_taps(const TrkParams& p, const NcoState& c, 
 
 // remPhase after the step (trackingCT.m:104-106) and remSample (:79 / :414, a record field),
 // from the descriptor alone
-__device__ __forceinline__ void desc_rem(const TrkParams& p, StepDesc* d)
+template <class P>
+__device__ __forceinline__ void desc_rem(const P& p, StepDesc* d)
 {
     const double nd = (double)d->n;
     d->remPhase_next = rem_2pi(kTwoPi * (d->f * over_fs(p, nd)) + d->phi0);
@@ -334,7 +388,8 @@ __device__ __forceinline__ void desc_rem(const TrkParams& p, StepDesc* d)
 // split (the persistent loop): roles 0 / 1 / 3 on three waves in the tail, role 2 by the
 // flush wave during the next step (desc_rem): the tail's code chain is the colon alone.
 // `taps` / `posts` = the tap spacings / prompt offsets (copies in LDS where the caller has).
-__device__ __forceinline__ void prepare_desc_i(const TrkParams& p, const NcoState& c, int pdi, int phaseC, int role,
+template <class P>
+__device__ __forceinline__ void prepare_desc_i(const P& p, const NcoState& c, int pdi, int phaseC, int role,
                              int lane, StepDesc* d, const double* taps = nullptr,
                              unsigned long long* dbg = nullptr, const double* posts = nullptr,
                              bool split = false)
@@ -414,26 +469,21 @@ __device__ __forceinline__ void prepare_desc_block(const TrkParams& p, const Nco
 
 
 // atan for the PLL discriminator. The classic four-interval reduction with an
-// 11-term odd polynomial (error < 1 ulp); its constants are read through a pointer the
-// compiler cannot see through, so inlined into the persistent step loop they are not
-// hoisted into registers that would stay live over the correlator (+40 VGPRs with the
-// library atan).
-__device__ const double kAtanTab[19] = {
-    4.63647609000806093515e-01, 7.85398163397448278999e-01, 9.82793723247329054082e-01,
-    1.57079632679489655800e+00,  // atan(0.5), atan(1), atan(1.5), atan(inf): high parts
-    2.26987774529616870924e-17, 3.06161699786838301793e-17, 1.39033110312309984516e-17,
-    6.12323399573676603587e-17,  // low parts
-    3.33333333333329318027e-01, -1.99999999998764832476e-01, 1.42857142725034663711e-01,
-    -1.11111104054623557880e-01, 9.09088713343650656196e-02, -7.69187620504482999495e-02,
-    6.66107313738753120669e-02, -5.83357013379057348645e-02, 4.97687799461593236017e-02,
-    -3.65315727442169155270e-02, 1.62858201153657823623e-02};
+// 11-term odd polynomial (error < 1 ulp). Its constants are literals materialised into
+// scalar registers at their use (kc(): a volatile asm the compiler can neither hoist out of
+// the step loop -- the library atan cost +40 VGPRs over the correlator -- nor turn into a
+// memory load: a table read here was a flat load of global memory on the PLL's critical
+// path, several hundred cycles).
+__device__ __forceinline__ double kc(double v)
+{
+    asm volatile("" : "+s"(v));
+    return v;
+}
 
 __device__ __forceinline__ double atan_tab(double x)
 {
-    const double* t = kAtanTab;
-    asm volatile("" : "+s"(t));
     const double ax = fabs(x);
-    if (!(ax < 0x1p66)) return x != x ? x : copysign(t[3] + t[7], x);
+    if (!(ax < 0x1p66)) return x != x ? x : copysign(kc(1.57079632679489655800e+00) + kc(6.12323399573676603587e-17), x);
     int id;
     double y;
     if (ax < 0.4375) {
@@ -449,11 +499,18 @@ __device__ __forceinline__ double atan_tab(double x)
         id = 3; y = -1.0 / ax;
     }
     const double z = y * y, w = z * z;
-    const double* a = t + 8;
-    const double s1 = z * (a[0] + w * (a[2] + w * (a[4] + w * (a[6] + w * (a[8] + w * a[10])))));
-    const double s2 = w * (a[1] + w * (a[3] + w * (a[5] + w * (a[7] + w * a[9]))));
+    const double s1 = z * (kc(3.33333333333329318027e-01) + w * (kc(1.42857142725034663711e-01) +
+                      w * (kc(9.09088713343650656196e-02) + w * (kc(6.66107313738753120669e-02) +
+                      w * (kc(4.97687799461593236017e-02) + w * kc(1.62858201153657823623e-02))))));
+    const double s2 = w * (kc(-1.99999999998764832476e-01) + w * (kc(-1.11111104054623557880e-01) +
+                      w * (kc(-7.69187620504482999495e-02) + w * (kc(-5.83357013379057348645e-02) +
+                      w * kc(-3.65315727442169155270e-02)))));
     if (id < 0) return y - y * (s1 + s2);
-    const double r = t[id] - ((y * (s1 + s2) - t[4 + id]) - y);
+    const double hi = id == 0 ? kc(4.63647609000806093515e-01) : id == 1 ? kc(7.85398163397448278999e-01)
+                    : id == 2 ? kc(9.82793723247329054082e-01) : kc(1.57079632679489655800e+00);
+    const double lo = id == 0 ? kc(2.26987774529616870924e-17) : id == 1 ? kc(3.06161699786838301793e-17)
+                    : id == 2 ? kc(1.39033110312309984516e-17) : kc(6.12323399573676603587e-17);
+    const double r = hi - ((y * (s1 + s2) - lo) - y);
     return x < 0 ? -r : r;
 }
 
@@ -464,7 +521,8 @@ struct LoopUpd {
     double DLLdiscri, code_output, codeFreq, PLLdiscri, carrier_output, carrierFreq;
 };
 
-__device__ __forceinline__ LoopUpd loop_update_i(const TrkParams& p, const TrkChan& c, double E_i,
+template <class P>
+__device__ __forceinline__ LoopUpd loop_update_i(const P& p, const TrkChan& c, double E_i,
                                                double E_q, double P_i, double P_q, double L_i,
                                                double L_q, int pdi, int phaseC, int which = 3)
 {
@@ -697,7 +755,8 @@ struct LdsRaw {
 // Timing-probe builds only (tools/build_probe.sh, never the product library): bit 1 drops
 // the lane's sincos, bit 2 the per-tap boundary search, bit 4 the per-sample Wave / eta
 // (the rotation table alone), bit 8 the whole lane correlate. Their sums are wrong; they time
-// (and count the instructions of) the correlator's parts.
+// (and count the instructions of) the correlator's parts. Bit 16 repeats the scalar tail
+// (right sums, the same descriptor) four extra times per step between stamps 18 and 19.
 #ifndef GNSS_CORR_PROBE
 #define GNSS_CORR_PROBE 0
 #endif
@@ -1324,6 +1383,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
                                                                int vpb, int nsteps, unsigned tag0)
 {
     const TrkParams& p = *pp;
+    const TailK tk = tail_k(p);  // (the scalar tail's constants, in registers)
     const TrkBuffers& b = *bp;
     constexpr int M = 8 * SUB;
     constexpr int NV = 2 * NT;
@@ -1410,7 +1470,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         const bool stop = !D.phaseC && D.Index + 1 > n1_target;  // 1-ms run of this channel done
         if (bad || stop || D.d * M >= 1.0) {  // (a code rate beyond Fs/M breaks the one-boundary lane)
             if (pend) flush();
-            if (io && tid == 64) desc_rem(p, &s_d[cur]);  // (complete for a step-kernel follow-up)
+            if (io && tid == 64) desc_rem(tk, &s_d[cur]);  // (complete for a step-kernel follow-up)
             __syncthreads();
             if (io) {  // leave the state and this (unused) descriptor for the host / next launch
                 if (tid == 0 && !stop) s_c.status = bad ? bad : GNSS_EINDEX;
@@ -1478,7 +1538,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
 
         // the step's remPhase / remSample (role 2 of the descriptor, off the tail: the
         // next tail reads them after the sweep's closing barrier)
-        if (wv == 1 && lane == 0) desc_rem(p, &s_d[cur]);
+        if (wv == 1 && lane == 0) desc_rem(tk, &s_d[cur]);
         if (pend) {
             if (srow && tid == 64) srow[16] = wall_clock64();
             flush();  // (the sweep's closing barrier publishes it)
@@ -1530,8 +1590,29 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         o.remPhase = D.remPhase_next;
         o.pdi = D.pdi;
         o.phaseC = phaseC;
-        const LoopUpd u = loop_update_i(p, c, s_fin[2 * p.iE], s_fin[2 * p.iE + 1], s_fin[2 * p.iP],
-                                      s_fin[2 * p.iP + 1], s_fin[2 * p.iL], s_fin[2 * p.iL + 1], o.pdi,
+        if constexpr ((GNSS_CORR_PROBE & 16) != 0) {
+            // (probe: the tail's loop update and descriptor four extra times -- the same values
+            // into the same descriptor -- between stamps 18 and 19: its cost in place, warm)
+            if (srow && io && tid == 0) srow[18] = wall_clock64();
+            for (int rep = 0; rep < 4; rep++) {
+                const LoopUpd ur = loop_update_i(tk, c, s_fin[2 * tk.iE], s_fin[2 * tk.iE + 1], s_fin[2 * tk.iP],
+                                                 s_fin[2 * tk.iP + 1], s_fin[2 * tk.iL], s_fin[2 * tk.iL + 1], o.pdi,
+                                                 o.phaseC, wv == 0 || wv == 2 ? 1 : wv == 3 ? 2 : 3);
+                NcoState nr{o.remChip, o.remPhase, ur.codeFreq, ur.carrierFreq, o.n, c.pos + tk.bps * o.n,
+                            c.Index + (o.phaseC ? 10 : 1)};
+                if (srow && io && rep == 0 && lane == 0) srow[29 + wv] = wall_clock64();  // (loop update done)
+                if (wv == 0 || wv == 3)
+                    prepare_desc_i(tk, nr, o.pdi, o.phaseC, wv == 0 ? 0 : 1, lane, &s_d[cur ^ 1], s_taps, nullptr,
+                                   s_post, true);
+                else if (wv == 2)
+                    prepare_desc_i(tk, nr, o.pdi, o.phaseC, 3, lane, &s_d[cur ^ 1], s_taps, nullptr, s_post, true);
+                if (srow && io && rep == 0 && lane == 0) srow[25 + wv] = wall_clock64();  // (role done)
+                lds_barrier();
+            }
+            if (srow && io && tid == 0) srow[19] = wall_clock64();
+        }
+        const LoopUpd u = loop_update_i(tk, c, s_fin[2 * tk.iE], s_fin[2 * tk.iE + 1], s_fin[2 * tk.iP],
+                                      s_fin[2 * tk.iP + 1], s_fin[2 * tk.iL], s_fin[2 * tk.iL + 1], o.pdi,
                                       o.phaseC, wv == 0 || wv == 2 ? 1 : wv == 3 ? 2 : 3);  // (each role's half)
         if (srow && io && tid == 0) srow[11] = wall_clock64();
         NcoState nx;
@@ -1540,10 +1621,10 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         nx.codeFreq = u.codeFreq;
         nx.carrierFreq = u.carrierFreq;
         nx.numSample = o.n;
-        nx.pos = c.pos + p.bps * o.n;
+        nx.pos = c.pos + tk.bps * o.n;
         nx.Index = c.Index + (o.phaseC ? 10 : 1);
         if (wv == 0 || wv == 3) {  // the tap colons / the carrier table of the next descriptor
-            prepare_desc_i(p, nx, o.pdi, o.phaseC, wv == 0 ? 0 : 1, lane, &s_d[cur ^ 1], s_taps,
+            prepare_desc_i(tk, nx, o.pdi, o.phaseC, wv == 0 ? 0 : 1, lane, &s_d[cur ^ 1], s_taps,
                            srow && io ? srow + 14 : nullptr, s_post, true);
             if (srow && io && lane == 0) srow[wv == 0 ? 12 : 13] = wall_clock64();
         } else if (wv == 1) {
@@ -1552,7 +1633,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
                 s_u = u;
             }
         } else {  // wave 2: the next step's scalars and checks, then its IF has landed
-            prepare_desc_i(p, nx, o.pdi, o.phaseC, 3, lane, &s_d[cur ^ 1], s_taps, nullptr, s_post, true);
+            prepare_desc_i(tk, nx, o.pdi, o.phaseC, 3, lane, &s_d[cur ^ 1], s_taps, nullptr, s_post, true);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         pend = true;
@@ -1566,7 +1647,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         b.stamps[22 + 3 * ch] = (unsigned long long)nsteps;
     }
     if (pend) flush();
-    if (io && tid == 64) desc_rem(p, &s_d[cur]);  // (complete for a step-kernel follow-up)
+    if (io && tid == 64) desc_rem(tk, &s_d[cur]);  // (complete for a step-kernel follow-up)
     __syncthreads();
     if (io) {  // the state and the next step's descriptor for the next launch
         if (tid < kChanWords)

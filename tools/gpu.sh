@@ -73,8 +73,8 @@ for step in "$@"; do
          # tools/probe_lib/libgnss_<name>.so; 8-channel trackingCT (1000 ms + 4000 x 10 ms), per-launch
          # hipEvents and GNSS_STAMPS of the 10-ms launch
       for v in $AB; do
-        GNSS_LIB=$R/tools/probe_lib/libgnss_$v.so TRK_PROFILE=1 TRK_ITERS=3 timeout -k 10 120 python3 tools/track_only.py 1000 40000 > gpurun_out/ab_$v.log 2>&1 || { tail -5 gpurun_out/ab_$v.log; exit 1; }
-        GNSS_LIB=$R/tools/probe_lib/libgnss_$v.so GNSS_STAMPS=gpurun_out/abst_$v.bin TRK_ITERS=1 timeout -k 10 120 python3 tools/track_only.py 1000 2000 > /dev/null 2>&1 || exit 1
+        GNSS_LIB=$R/tools/probe_lib/libgnss_$v.so TRK_PROFILE=1 TRK_ITERS=3 timeout -k 10 120 python3 tools/track_only.py 1000 40000 3 ${AB_NCH:-8} > gpurun_out/ab_$v.log 2>&1 || { tail -5 gpurun_out/ab_$v.log; exit 1; }
+        GNSS_LIB=$R/tools/probe_lib/libgnss_$v.so GNSS_STAMPS=gpurun_out/abst_$v.bin TRK_ITERS=1 timeout -k 10 120 python3 tools/track_only.py 1000 2000 3 ${AB_NCH:-8} > /dev/null 2>&1 || exit 1
         echo "ab $v: $(grep track10 gpurun_out/ab_$v.log | tail -2 | tr '\n' ' ')"
         python3 tools/stamps_run.py gpurun_out/abst_$v.bin | grep -E "period|computed|all partials|next desc|tail" | sed "s/^/   /"
       done ;;

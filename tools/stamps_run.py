@@ -21,6 +21,13 @@ for path in sys.argv[1:]:
     dp = np.diff(a[:, 0]) * 0.01
     dp = dp[dp < 1000]
     print(f"  {'step period (blk0)':32s} {np.median(dp):7.2f}  mean {dp.mean():6.2f}  p90 {np.percentile(dp, 90):6.2f}  p99 {np.percentile(dp, 99):6.2f}  max {dp.max():7.2f}")
+    print("  period tail: " + ", ".join(f">{t} us: {int((dp > t).sum())} steps {dp[dp > t].sum():.0f} us"
+                                        for t in (8, 10, 15, 30, 100)) + f" (of {dp.sum():.0f} us)")
+    big = np.argsort(dp)[-3:]
+    for i in big:  # where the slowest steps spent their time (blk0 stamps)
+        r, nx = a[i], a[i + 1]
+        print(f"   slow step: {dp[i]:.1f} us = corr {(r[1]-r[0])*0.01:.2f} part {(r[2]-r[1])*0.01:.2f} "
+              f"xchg {(r[3]-r[2])*0.01:.2f} tail {(r[4]-r[3])*0.01:.2f} gap {(nx[0]-r[4])*0.01:.2f}")
     b = np.fromfile(path, dtype=np.uint64)[:-1].reshape(-1, ROW)[:, :14].astype(np.int64)
     b = b[(b[:, 0] != 0) & (b[:, 5] != 0) & (b[:, 10] != 0)]
     if len(b):
@@ -46,3 +53,12 @@ for path in sys.argv[1:]:
     if len(e):
         lat = e[:, 23].astype(np.int64); ear = (~e[:, 24]).astype(np.int64)
         print(f"  all blocks: first->last partial out {us(lat - ear):6.2f}; latest partial -> blk0 all in {us(e[:, 3].astype(np.int64) - lat):6.2f}; blk0 partial -> latest {us(lat - e[:, 2].astype(np.int64)):6.2f}")
+    e = np.fromfile(path, dtype=np.uint64)[:-1].reshape(-1, ROW)[:, :20].astype(np.int64)
+    e = e[(e[:, 18] != 0) & (e[:, 19] != 0)]
+    if len(e):
+        print(f"  tail repeated in place (probe 16): {us(e[:, 19] - e[:, 18]) / 4:6.2f} us per repetition")
+        g = np.fromfile(path, dtype=np.uint64)[:-1].reshape(-1, ROW)[:, :33].astype(np.int64)
+        g = g[(g[:, 18] != 0) & (g[:, 25] != 0)]
+        if len(g):
+            print("   its first repetition by wave (loop update / role end, us from the start): " + ", ".join(
+                f"w{w} {us(g[:, 29 + w] - g[:, 18]):.2f}/{us(g[:, 25 + w] - g[:, 18]):.2f}" for w in range(4)))
