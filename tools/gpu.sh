@@ -67,16 +67,18 @@ for step in "$@"; do
         python3 tools/pmc_sq.py gpurun_out/probe_sq_$n.json gpurun_out/pr${n}_sq -- "track_run_kernel<3, 3, false, false>" > /dev/null || exit 1
         GNSS_LIB=$R/tools/probe_lib/libgnss_probe$n.so GNSS_STAMPS=gpurun_out/st_$n.bin timeout -k 10 120 python3 tools/track_only.py 1000 2000 > gpurun_out/st_$n.log 2>&1 || { tail gpurun_out/st_$n.log; exit 1; }
         echo "probe $n: $(python3 tools/stamps_run.py gpurun_out/st_$n.bin | grep -E 'period|computed|all partials|next desc' | tr -s ' ' | tr '\n' ';')"
+        rm -f gpurun_out/st_$n.bin  # (tens of MB: gpurun_out is copied back only below 64 MiB)
       done
       rm -f gpurun_out/pr*_sq/**/*kernel_trace.csv ;;
     ab)  # A/B of library builds (tools/build_commit_lib.sh / build_probe.sh): AB="name ..." ->
          # tools/probe_lib/libgnss_<name>.so; 8-channel trackingCT (1000 ms + 4000 x 10 ms), per-launch
-         # hipEvents and GNSS_STAMPS of the 10-ms launch
+         # hipEvents and GNSS_STAMPS of the 10-ms launch (AB_TAPS=11 AB_NCH=32: the config-5 shape)
       for v in $AB; do
-        GNSS_LIB=$R/tools/probe_lib/libgnss_$v.so TRK_PROFILE=1 TRK_ITERS=3 timeout -k 10 120 python3 tools/track_only.py 1000 40000 3 ${AB_NCH:-8} > gpurun_out/ab_$v.log 2>&1 || { tail -5 gpurun_out/ab_$v.log; exit 1; }
-        GNSS_LIB=$R/tools/probe_lib/libgnss_$v.so GNSS_STAMPS=gpurun_out/abst_$v.bin TRK_ITERS=1 timeout -k 10 120 python3 tools/track_only.py 1000 2000 3 ${AB_NCH:-8} > /dev/null 2>&1 || exit 1
+        GNSS_LIB=$R/tools/probe_lib/libgnss_$v.so TRK_PROFILE=1 TRK_ITERS=3 timeout -k 10 120 python3 tools/track_only.py 1000 40000 ${AB_TAPS:-3} ${AB_NCH:-8} > gpurun_out/ab_$v.log 2>&1 || { tail -5 gpurun_out/ab_$v.log; exit 1; }
+        GNSS_LIB=$R/tools/probe_lib/libgnss_$v.so GNSS_STAMPS=gpurun_out/abst_$v.bin TRK_ITERS=1 timeout -k 10 120 python3 tools/track_only.py 1000 2000 ${AB_TAPS:-3} ${AB_NCH:-8} > /dev/null 2>&1 || exit 1
         echo "ab $v: $(grep track10 gpurun_out/ab_$v.log | tail -2 | tr '\n' ' ')"
         python3 tools/stamps_run.py gpurun_out/abst_$v.bin | grep -E "period|computed|all partials|next desc|tail" | sed "s/^/   /"
+        rm -f gpurun_out/abst_$v.bin
       done ;;
     lat)  # fp64 / fp32 dependent-latency micro-benchmark (tools/micro/lat2, built in-tree)
       timeout -k 10 60 ./tools/micro/lat2 > gpurun_out/lat2.txt 2>&1 && cat gpurun_out/lat2.txt || exit 1 ;;
