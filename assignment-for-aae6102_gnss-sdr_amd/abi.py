@@ -190,7 +190,8 @@ _lib = None
 _torch_first = False
 
 # gnss_ctx_set_option keys (include/gnss_mi355x.h, ABI v9)
-OPT_FORCE_SUB, OPT_NO_PERSIST, OPT_FORCE_VPB, OPT_ACQ_ROCFFT, OPT_FINE_ROCFFT, OPT_ACQ_BATCH = range(6)
+(OPT_FORCE_SUB, OPT_NO_PERSIST, OPT_FORCE_VPB, OPT_ACQ_ROCFFT, OPT_FINE_ROCFFT, OPT_ACQ_BATCH, OPT_ACQ_FUSED,
+ OPT_ACQ_RING) = range(8)
 
 
 def require_torch():

@@ -33,6 +33,7 @@ namespace gnss {
 namespace {
 
 constexpr int kRow = 2000;      // row length, 5*5*5*16
+constexpr int kRowPad = 2100;   // LDS row of the radix-20-first transforms (stage_batch SW)
 constexpr int kRowThreads = 256;
 constexpr int kColThreads = 256;
 
@@ -296,18 +297,33 @@ template <int R, int DIR, class V> __device__ __forceinline__ void dft_r(V (&v)[
 
 // ---- BATCH 2000-point transforms side by side in LDS (transform b at a + b*2000), one
 // radix-R Stockham stage; every butterfly of the batch is spread over the block's threads.
-template <int DIR, int R, int NS, int BATCH, class V, class TW>
+// SW = 1 (the Ns = 1 radix-20 stage of a single transform): outputs stored padded, element
+// 20*j + i at 21*j + i, so the 16 lanes of an LDS cycle hit 16 different 16-B bank slots
+// (the plain order's 320-B lane stride put 4 lanes on each: 35 % of the fp64 row pass's LDS
+// cycles were conflicts, profiles/r02_acq_counters.json; 140 store cycles per transform
+// instead of 500 by the 16-lane model); SW = 2: the stage after it, reading that layout,
+// element x = j' + 200*i at (j' + j'/20) + 210*i (one division per thread, none per element).
+// The buffer holds kRowPad elements.
+template <int DIR, int R, int NS, int BATCH, class V, class TW, int SW = 0>
 __device__ __forceinline__ void stage_batch(V* a, const TW& tw, int tid)
 {
     constexpr int NB = kRow / R, TOT = NB * BATCH, PER = (TOT + kRowThreads - 1) / kRowThreads;
+    static_assert(SW == 0 || (BATCH == 1 && ((SW == 1 && R == 20 && NS == 1) || (SW == 2 && R == 10 && NS == 20))),
+                  "padded layout");
     V v[PER][R];
 #pragma unroll
     for (int q = 0; q < PER; q++) {
         const int u0 = tid + q * kRowThreads, u = u0 < TOT ? u0 : TOT - 1;
         const int b = u / NB, j = u - b * NB, k = j % NS;
         const V* src = a + b * kRow;
+        if constexpr (SW == 2) {
+            const V* s0 = src + j + j / 20;
 #pragma unroll
-        for (int i = 0; i < R; i++) v[q][i] = src[j + i * NB];
+            for (int i = 0; i < R; i++) v[q][i] = s0[210 * i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < R; i++) v[q][i] = src[j + i * NB];
+        }
         if (NS > 1) {
 #pragma unroll
             for (int i = 1; i < R; i++) v[q][i] = twid<DIR>(v[q][i], tw[i * k * (kRow / (NS * R))]);
@@ -321,8 +337,13 @@ __device__ __forceinline__ void stage_batch(V* a, const TW& tw, int tid)
         if (u < TOT) {
             const int b = u / NB, j = u - b * NB, k = j % NS, d = (j / NS) * NS * R + k;
             V* dst = a + b * kRow;
+            if constexpr (SW == 1) {
 #pragma unroll
-            for (int i = 0; i < R; i++) dst[d + i * NS] = v[q][i];
+                for (int i = 0; i < R; i++) dst[d + j + i] = v[q][i];
+            } else {
+#pragma unroll
+                for (int i = 0; i < R; i++) dst[d + i * NS] = v[q][i];
+            }
         }
     }
     __syncthreads();
@@ -338,12 +359,14 @@ __device__ __forceinline__ void fft2000_batch(V* a, const TW& tw, int tid)
 }
 
 // 2000 = 20 x 10 x 10 with the radix-20 pass first (Ns = 1: no twiddles), so the widest
-// butterfly never holds twiddles in registers (the fp64 row kernel stays within 256 VGPRs)
+// butterfly never holds twiddles in registers (the fp64 row kernel stays within 256 VGPRs);
+// one transform, its first stage's outputs padded (SW above): `a` holds kRowPad elements
 template <int DIR, int BATCH, class V, class TW>
 __device__ __forceinline__ void fft2000_batch_r20first(V* a, const TW& tw, int tid)
 {
-    stage_batch<DIR, 20, 1, BATCH>(a, tw, tid);
-    stage_batch<DIR, 10, 20, BATCH>(a, tw, tid);
+    static_assert(BATCH == 1, "one transform (padded layout)");
+    stage_batch<DIR, 20, 1, BATCH, V, TW, 1>(a, tw, tid);
+    stage_batch<DIR, 10, 20, BATCH, V, TW, 2>(a, tw, tid);
     stage_batch<DIR, 10, 200, BATCH>(a, tw, tid);
 }
 
@@ -377,7 +400,7 @@ __global__ __launch_bounds__(kRowThreads) void fwd_rows_kernel(
 {
     using R = Re<V>;
     constexpr int64_t S = (int64_t)P * kRow;
-    __shared__ V s_a[kRow], s_tw[kRow];
+    __shared__ V s_a[kRowPad], s_tw[kRow];
     const int n2 = blockIdx.x, s = blockIdx.y, tid = threadIdx.x;
     load_row_tw(s_tw, tw_row, tid);
     if (s < nsig) {
@@ -538,7 +561,7 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel_f64(
     const double2* __restrict__ tw_row, double* __restrict__ corr, int nbins)
 {
     constexpr int Q = (kRow + kRowThreads - 1) / kRowThreads;
-    __shared__ double2 s_a[kRow], s_tw[kRow];
+    __shared__ double2 s_a[kRowPad], s_tw[kRow];
     const int tau2 = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
     load_row_tw(s_tw, tw_row, tid);
     double acc[Q];
@@ -584,6 +607,173 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel_f64(
     }
 }
 
+// ---- I1 + I2 fused (fp64): one persistent launch, the intermediate kept in each XCD's L2.
+// The two-kernel path streams every transform's P x 2000 intermediate A (928 KB at config 2)
+// out to HBM and back, 2.2x the correlator's model bytes (profiles/acq_bound_r02.json). Here
+// each XCD (read from HW_REG_XCC_ID, not assumed from blockIdx) runs its own pipeline over
+// its share of the (bin, PRN) pairs, transform j = (pair, ms) of that share at a time:
+//   column workers  I1 of transform j, one 256-column chunk per item, into ring slot j % R
+//                   of the XCD's own region (plain stores: the lines stay in its L2);
+//   row workers     one row tau2 each for the whole launch; per transform they copy
+//                   their row out of the slot (L1-bypassing sc1 loads, served by the same
+//                   L2), free the slot, and run I2 (2000-point inverse + |.|^2 sum over the
+//                   ms in order).
+// Hand-off inside one L2: every storing wave drains its stores (s_waitcnt vmcnt(0)) before
+// the workgroup's counter add, and the reader polls the counter and then reads the bytes
+// with loads that bypass its L1; producer and consumer are on the same XCD by construction
+// (both read HW_REG_XCC_ID). The arithmetic is I1's and I2's, operation for operation: the
+// surface equals the two-kernel path's bit for bit (tests/test_gpu_acquisition.py).
+constexpr int kFuseX = 8;      // XCC_ID values
+constexpr int kFuseSlots = 4;  // ring slots per XCD, at most
+constexpr int kFuseLine = 32;  // counter stride (128 B: one counter per L2 line)
+constexpr int kFuseChunks = (kRow + kColThreads - 1) / kColThreads;  // column items per transform
+constexpr unsigned kFuseSpin = 1u << 22;  // polls (~1 us each, s_sleep'd) before giving up
+struct FuseSync {
+    unsigned arrive[kFuseX * kFuseLine];           // workgroups per XCC_ID
+    unsigned total[kFuseLine];                     // all workgroups
+    unsigned err[kFuseLine];                       // != 0: a wait timed out (the surface is void)
+    unsigned ready[kFuseX * kFuseSlots * kFuseLine];  // column items stored, per (XCD, slot)
+    unsigned freed[kFuseX * kFuseSlots * kFuseLine];  // row workers done copying, per (XCD, slot)
+};
+
+__device__ __forceinline__ unsigned ld_sc1(const unsigned* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned add_dev(unsigned* p, unsigned v)
+{
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// lane 0: poll until *p >= want (bounded); false on timeout (err set)
+__device__ __forceinline__ bool wait_ge(const unsigned* p, unsigned want, FuseSync* sy)
+{
+    for (unsigned n = 0; n < kFuseSpin; n++) {
+        if (ld_sc1(p) >= want) return true;
+        if (ld_sc1(sy->err)) return false;
+        __builtin_amdgcn_s_sleep(8);
+    }
+    add_dev(sy->err, 1u);
+    return false;
+}
+
+template <int P>
+__global__ __launch_bounds__(kRowThreads, 2) void inv_fused_kernel_f64(
+    const double2* __restrict__ C, const double2* __restrict__ X, int nbins, int nprn, int datalen,
+    int npairs, int nslot, double scale, const double2* __restrict__ tw_row, const double2* __restrict__ tw_col,
+    double2* __restrict__ ring, FuseSync* __restrict__ sy, double* __restrict__ corr)
+{
+    constexpr int Q = (kRow + kRowThreads - 1) / kRowThreads;
+    constexpr int64_t S = (int64_t)P * kRow;
+    __shared__ double2 s_a[kRowPad], s_tw[kRow];
+    __shared__ int s_role[6];  // xcc, rank, team size, XCD position, active XCDs, ok
+    const int tid = threadIdx.x;
+    // ---- census: this workgroup's XCD and rank in it, then wait for every workgroup
+    if (tid == 0) {
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+        xcc &= kFuseX - 1;
+        const unsigned rank = add_dev(&sy->arrive[xcc * kFuseLine], 1u);
+        add_dev(sy->total, 1u);
+        int ok = wait_ge(sy->total, gridDim.x, sy) ? 1 : 0;
+        // an XCD takes part when its team holds a row worker per row and at least 4
+        // column workers; pairs are dealt round-robin over those XCDs
+        int na = 0, xa = -1, nw = 0;
+        for (int x = 0; x < kFuseX; x++) {
+            const int w = (int)ld_sc1(&sy->arrive[x * kFuseLine]);
+            if (w >= P + 4) {
+                if (x == (int)xcc) { xa = na; nw = w; }
+                na++;
+            }
+        }
+        if (na == 0) ok = 0;
+        if (!ok && rank == 0 && xcc == 0) add_dev(sy->err, 1u);  // (no team: the surface is void)
+        s_role[0] = (int)xcc; s_role[1] = (int)rank; s_role[2] = nw; s_role[3] = xa; s_role[4] = na;
+        s_role[5] = ok;
+    }
+    __syncthreads();
+    const int xcc = s_role[0], rank = s_role[1], nw = s_role[2], xa = s_role[3], na = s_role[4];
+    if (!s_role[5] || xa < 0) return;
+    const int nr = P, nc = nw - P;                  // row workers (one per row), column workers
+    const int npx = (npairs - xa + na - 1) / na;    // this XCD's pairs: xa, xa + na, ...
+    const int ntr = npx * datalen;                  // ... and transforms (pair-major, ms minor)
+    unsigned* ready = &sy->ready[xcc * kFuseSlots * kFuseLine];
+    unsigned* freed = &sy->freed[xcc * kFuseSlots * kFuseLine];
+    double2* ring_x = ring + (int64_t)xcc * kFuseSlots * S;
+
+    if (rank >= nr) {
+        // ---- column worker (I1, inv_cols_kernel's arithmetic)
+        const int w = rank - nr;
+        for (int it = w; it < ntr * kFuseChunks; it += nc) {
+            const int j = it / kFuseChunks, ch = it - j * kFuseChunks, slot = j % nslot;
+            if (tid == 0) s_role[5] = wait_ge(&freed[slot * kFuseLine], (unsigned)(j / nslot * nr), sy);
+            __syncthreads();
+            if (!s_role[5]) return;
+            const int pi = j / datalen, ms = j - pi * datalen;
+            const int q = xa + pi * na, bin = q / nprn, p = q - bin * nprn;
+            const int k1 = ch * kColThreads + tid;
+            if (k1 < kRow) {
+                const double2* c = C + (int64_t)p * S + k1;
+                const double2* x = X + ((int64_t)ms * nbins + bin) * S + k1;
+                double2 v[P];
+#pragma unroll
+                for (int i = 0; i < P; i++) v[i] = cmulc(c[(int64_t)i * kRow], ld_nt(x + (int64_t)i * kRow));
+                double2* a = ring_x + (int64_t)slot * S + k1;
+                const double2* tw = tw_col + k1;
+                dft_prime<P, 1>(v, [&](int k, double2 y) { a[(int64_t)k * kRow] = cmulc(y, tw[(int64_t)k * kRow]); });
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's stores are in L2
+            __syncthreads();
+            if (tid == 0) add_dev(&ready[slot * kFuseLine], 1u);
+        }
+        return;
+    }
+    // ---- row worker: row tau2 = rank of every transform (I2's arithmetic)
+    const int tau2 = rank;
+    load_row_tw(s_tw, tw_row, tid);
+    double acc[Q];
+#pragma unroll
+    for (int i = 0; i < Q; i++) acc[i] = 0.0;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        ring_x, (short)0, (int)(kFuseSlots * S * sizeof(double2)), 0x00020000);
+    for (int j = 0; j < ntr; j++) {
+        const int slot = j % nslot;
+        if (tid == 0) s_role[5] = wait_ge(&ready[slot * kFuseLine], (unsigned)((j / nslot + 1) * kFuseChunks), sy);
+        __syncthreads();
+        if (!s_role[5]) return;
+        const int row0 = (int)(((int64_t)slot * S + (int64_t)tau2 * kRow) * 16);
+#pragma unroll
+        for (int i = 0; i < Q; i++) {
+            const int e = tid + i * kRowThreads;
+            if (e < kRow) {
+                typedef unsigned u4 __attribute__((ext_vector_type(4)));
+                const u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, row0 + e * 16, 0, 16 /* sc1 */);
+                s_a[e] = make_double2(__hiloint2double((int)v.y, (int)v.x), __hiloint2double((int)v.w, (int)v.z));
+            }
+        }
+        __syncthreads();  // the row is in LDS: the slot may be refilled
+        if (tid == 0) add_dev(&freed[slot * kFuseLine], 1u);
+        fft2000_batch_r20first<1, 1>(s_a, s_tw, tid);
+#pragma unroll
+        for (int i = 0; i < Q; i++) {  // the ms in order (acquisition.m:53-61)
+            const int t1 = tid + i * kRowThreads, t = t1 < kRow ? t1 : kRow - 1;
+            const double2 v = s_a[t];
+            acc[i] += (v.x * v.x + v.y * v.y) * scale;
+        }
+        const int pi = j / datalen, ms = j - pi * datalen;
+        if (ms == datalen - 1) {
+            const int q = xa + pi * na, bin = q / nprn, p = q - bin * nprn;
+            double* o = corr + (((int64_t)p * nbins + bin) * P + tau2) * kRow;
+#pragma unroll
+            for (int i = 0; i < Q; i++) {
+                const int t1 = tid + i * kRowThreads;
+                if (t1 < kRow) o[t1] = acc[i];
+                acc[i] = 0.0;
+            }
+        }
+        __syncthreads();  // (s_a is rewritten by the next transform's copy)
+    }
+}
+
 // ============================== fine frequency (fp64) =============================
 // x[n] = longrawsignal(S-cd + n) .* CA(rem(floor((n+1)/Fs*fc), 1023)+1), n < M = L*S
 // (acquisition.m:103-106); X[k] = DFT_N of x zero-padded to N = M*D (:108), D = datalen.
@@ -618,7 +808,7 @@ __global__ __launch_bounds__(kRowThreads) void fine_rows_kernel(
     constexpr int T = kFineT;
     // twiddles read from the (L2-resident) global table: 32 KB of LDS per block instead of
     // 64, five blocks per CU instead of two
-    __shared__ double2 s_a[kRow];
+    __shared__ double2 s_a[kRowPad];
     const int rho = blockIdx.x, r = blockIdx.y, tid = threadIdx.x;
     const int m2 = rho / P, n2 = rho - m2 * P;
     for (int m1 = tid; m1 < kRow; m1 += kRowThreads) {
@@ -818,6 +1008,41 @@ hipError_t launch_acq_fft_correlate(const double2* C, const double2* X, int64_t 
     }
     GNSS_INV(13) GNSS_INV(29)
 #undef GNSS_INV
+    return hipErrorInvalidValue;
+}
+
+size_t acq_fused_sync_bytes() { return sizeof(FuseSync); }
+size_t acq_fused_err_offset() { return offsetof(FuseSync, err); }
+size_t acq_fused_ring_bytes(int64_t S) { return sizeof(double2) * (size_t)kFuseX * kFuseSlots * (size_t)S; }
+
+// All (bin, PRN) pairs in one persistent launch (I1 + I2 fused, fp64). `sync` holds
+// acq_fused_sync_bytes() and `ring` acq_fused_ring_bytes(S); the launch zeroes `sync`.
+// Its err word is non-zero afterwards if a wait timed out (a grid that was not resident).
+hipError_t launch_acq_fft_correlate_fused(const double2* C, const double2* X, int64_t S, int datalen, int nbins,
+                                          int nprn, int nslot, const double2* tw_row, const double2* tw_col,
+                                          double2* ring, void* sync, double* corr, hipStream_t s)
+{
+    if (nslot < 2 || nslot > kFuseSlots) return hipErrorInvalidValue;
+    const double scale = 1.0 / ((double)S * (double)S);
+    int dev = 0, ncu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess) e = hipMemsetAsync(sync, 0, sizeof(FuseSync), s);
+    if (e != hipSuccess) return e;
+    FuseSync* sy = static_cast<FuseSync*>(sync);
+#define GNSS_FUSED(P_)                                                                          \
+    if (S == (int64_t)P_ * kRow) {                                                              \
+        int occ = 0;                                                                            \
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, inv_fused_kernel_f64<P_>, kRowThreads, 0); \
+        if (e != hipSuccess) return e;                                                          \
+        const int grid = ncu * std::min(occ, 2);                                                \
+        if (grid < 1) return hipErrorInvalidConfiguration;                                      \
+        hipLaunchKernelGGL(inv_fused_kernel_f64<P_>, dim3(grid), dim3(kRowThreads), 0, s, C, X, nbins, nprn, \
+                           datalen, nbins * nprn, nslot, scale, tw_row, tw_col, ring, sy, corr); \
+        return hipGetLastError();                                                               \
+    }
+    GNSS_FUSED(13) GNSS_FUSED(29)
+#undef GNSS_FUSED
     return hipErrorInvalidValue;
 }
 

@@ -391,7 +391,7 @@ template <> struct CplxReal<double2> { using T = double; };
 template <class V>
 int acq_search(gnss_ctx* ctx, const int8_t* blk, const double2* xa, int64_t S, int dl, int nb, int np,
                const gnss_signal* sg, const gnss_acq* acq, const float* ca, typename CplxReal<V>::T* corr,
-               Events& e_all, int* perm)
+               Events& e_all, int* perm, DevBuf& fsync)
 {
     const int dbl = sizeof(V) == sizeof(double2) ? 1 : 0;
     const size_t csz = sizeof(V);
@@ -429,6 +429,25 @@ int acq_search(gnss_ctx* ctx, const int8_t* blk, const double2* xa, int64_t S, i
         HIP_TRY(B.alloc(ctx, "acq.B", csz * ntr * S));
         HIP_TRY(X.alloc(ctx, "acq.X", csz * ntr * S));
         const int npairs = nb * np;
+        if (dbl && ctx->opt[GNSS_OPT_ACQ_FUSED]) {
+            // fp64: one persistent launch, the intermediate in each XCD's L2 (acq_fft.hip);
+            // the caller reads fsync's error word once the stream has drained
+            DevBuf ring;
+            const int nslot = ctx->opt[GNSS_OPT_ACQ_RING] ? (int)ctx->opt[GNSS_OPT_ACQ_RING] : 3;
+            HIP_TRY(ring.alloc(ctx, "acq.ring", acq_fused_ring_bytes(S)));
+            HIP_TRY(fsync.alloc(ctx, "acq.fsync", acq_fused_sync_bytes()));
+            HIP_TRY(hipStreamSynchronize(ctx->stream));
+            HIP_TRY(hipEventRecord(e_all.a, ctx->stream));
+            HIP_TRY(launch_acq_fft_forward<V>(blk, xa, S, dl, nb, sg->IF, acq->freqMin, acq->freqStep, sg->Fs, ca,
+                                              np, sg->codeFreqBasis, d_twr.as<V>(), d_twc.as<V>(), B.as<V>(),
+                                              X.as<V>(), ctx->stream));
+            const V* C = X.as<V>() + (size_t)nsig * S;
+            HIP_TRY(launch_acq_fft_correlate_fused(reinterpret_cast<const double2*>(C), X.as<double2>(), S, dl, nb,
+                                                   np, nslot, d_twr.as<double2>(), d_twc.as<double2>(),
+                                                   ring.as<double2>(), fsync.p, reinterpret_cast<double*>(corr),
+                                                   ctx->stream));
+            return GNSS_OK;
+        }
         // (bin, PRN) pairs per batch: the inverse intermediate round-trips through HBM
         // anyway (PMC, profiles/acq_traffic_r01.json), so batches of ~1 GiB, balanced (no
         // small tail batch that leaves the chip idle): config 2 (fp32) measured 7.94 ms of
@@ -680,12 +699,13 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     HIP_TRY(scratch.alloc(ctx, "acq.scratch", acq_scratch_bytes(np, np)));
     Events e_all, e_corr;  // e_corr.b marks the end of the PRN search
     int perm = 0;
+    DevBuf fsync;  // the fused correlator's counters (its error word is read below)
     if (dbl)
         st = acq_search<double2>(ctx, blk, xa, S, dl, nb, np, sg, acq, ca.as<float>(), corr.as<double>(), e_all,
-                                 &perm);
+                                 &perm, fsync);
     else
         st = acq_search<float2>(ctx, blk, xa, S, dl, nb, np, sg, acq, ca.as<float>(), corr.as<float>(), e_all,
-                                &perm);
+                                &perm, fsync);
     if (st) return st;
     const int cshift = (int)std::ceil(sg->Fs / sg->codeFreqBasis);  // :66
     if (dbl)
@@ -697,7 +717,13 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     HIP_TRY(hipEventRecord(e_corr.b, ctx->stream));
     std::vector<AcqPeak> ph((size_t)np);
     HIP_TRY(hipMemcpyAsync(ph.data(), peaks.p, sizeof(AcqPeak) * (size_t)np, hipMemcpyDeviceToHost, ctx->stream));
+    unsigned fused_err = 0;
+    if (fsync.p)
+        HIP_TRY(hipMemcpyAsync(&fused_err, static_cast<char*>(fsync.p) + acq_fused_err_offset(), sizeof(unsigned),
+                               hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (fused_err)
+        return fail(ctx, GNSS_EDEVICE, "fused correlator: a pipeline wait timed out (grid not resident)");
     ctx->timing.acq_hypothesis_samples = (int64_t)np * nb * dl * S;
 
     std::vector<int> acq_idx;

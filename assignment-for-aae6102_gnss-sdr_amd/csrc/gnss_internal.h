@@ -328,6 +328,14 @@ hipError_t launch_acq_fft_correlate(const double2* C, const double2* X, int64_t 
                                     int nbins, int nprn, int first_pair, int npair,
                                     const double2* tw_row, const double2* tw_col, double2* A,
                                     double* corr, hipStream_t s);
+// fp64, every (bin, PRN) pair in one persistent launch with the column/row intermediate
+// kept in each XCD's L2 (nslot ring slots per XCD, 2..4); see acq_fft.hip
+size_t acq_fused_sync_bytes();
+size_t acq_fused_err_offset();  // byte offset of the error word in the sync block
+size_t acq_fused_ring_bytes(int64_t S);
+hipError_t launch_acq_fft_correlate_fused(const double2* C, const double2* X, int64_t S, int datalen, int nbins,
+                                          int nprn, int nslot, const double2* tw_row, const double2* tw_col,
+                                          double2* ring, void* sync, double* corr, hipStream_t s);
 bool fine_fft_supported(int64_t S, int L);
 size_t fine_fft_scratch_bytes(int64_t S, int L, int datalen);
 hipError_t launch_fine_fft_tables(int64_t S, int L, int datalen, void* scratch, hipStream_t s);

@@ -237,8 +237,12 @@ int  gnss_ctx_set_window(gnss_ctx *ctx, uint64_t bytes);
 #define GNSS_OPT_FORCE_VPB    2  /* >= 2: virtual blocks per resident block of the loop     */
 #define GNSS_OPT_ACQ_ROCFFT   3  /* != 0: rocFFT instead of the own P x 2000 correlator     */
 #define GNSS_OPT_FINE_ROCFFT  4  /* != 0: rocFFT for the fine-frequency transform           */
-#define GNSS_OPT_ACQ_BATCH    5  /* > 0: (bin, PRN) pairs per correlator batch              */
-#define GNSS_OPT_COUNT        6
+#define GNSS_OPT_ACQ_BATCH    5  /* > 0: (bin, PRN) pairs per correlator batch (split path) */
+#define GNSS_OPT_ACQ_FUSED    6  /* != 0: fp64 correlator as one persistent launch with the
+                                    intermediate in each XCD's L2 (measured slower, kept
+                                    for the record; default: two launches per batch)      */
+#define GNSS_OPT_ACQ_RING     7  /* 2..4: ring slots per XCD of the fused correlator (3)    */
+#define GNSS_OPT_COUNT        8
 int  gnss_ctx_set_option(gnss_ctx *ctx, int key, int64_t value);
 
 /* Device memory owned by the ctx, for callers that keep an IF record resident

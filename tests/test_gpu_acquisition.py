@@ -175,3 +175,35 @@ def test_config4_all_32_prns_against_oracle(pkg, po, ctx):
           "min |SNR-12|", float(gate.min()))
     assert margin[acq_mask].min() > 1e-4
     assert gate.min() > 0.01
+
+
+@pytest.mark.parametrize("shape", ["cfg2", "cfg4"])
+def test_fused_correlator_equals_split_path(pkg, ctx, opts, shape):
+    """The fused fp64 correlator (GNSS_OPT_ACQ_FUSED: one persistent launch, the column/row
+    intermediate in each XCD's L2) against the default two-launch path (the intermediate
+    through HBM) at the benchmarked shapes, all 32 PRNs: every PRN's SNR,
+    peak, second peak, bin and code phase identical bit for bit, for ring depths 2, 3
+    and 4 (acquisition.m:47-61; the same arithmetic in the same order)."""
+    abi = pkg.abi
+    if shape == "cfg2":
+        skip, S, Fs, IF = 2, 58000, 58e6, 4.58e6
+        cfg = pkg.synth.opensky(skip_ms=skip)
+        acq = SimpleNamespace(freqNum=29, freqMin=-7000, freqStep=500, datalen=20, L=10)
+    else:
+        skip, S, Fs, IF = 1000, 26000, 26e6, 0.0
+        cfg = pkg.synth.urban(skip_ms=skip, Fs=Fs)
+        acq = SimpleNamespace(freqNum=81, freqMin=-10000, freqStep=250, datalen=10, L=10)
+    dev = pkg.DeviceRecord(ctx, (skip + 30) * S * 2)
+    pkg.synth.generate_device(ctx, cfg, dev)
+    file = SimpleNamespace(skip=skip, dataType=2, dataPrecision=1, data=None, fileRoute=None, dev=dev)
+    signal = SimpleNamespace(IF=IF, Fs=Fs, codeFreqBasis=1.023e6, ms=1e-3, Sample=S, codelength=1023.0)
+    g0, d0 = pkg.acquisition(file, signal, acq, ctx=ctx, diag=True)
+    opts(abi.OPT_ACQ_FUSED, 1)
+    for ring in (3, 2, 4):
+        opts(abi.OPT_ACQ_RING, ring)
+        g1, d1 = pkg.acquisition(file, signal, acq, ctx=ctx, diag=True)
+        for f in ("prn", "SNR", "peak", "peak2", "fbin", "codePhase"):
+            a, b = np.asarray(getattr(d0, f)), np.asarray(getattr(d1, f))
+            assert np.array_equal(a, b), (ring, f, a, b)
+        assert np.array_equal(g0.sv, g1.sv) and np.array_equal(g0.fineFreq, g1.fineFreq)
+    assert len(d0.prn) == 32

@@ -1,6 +1,6 @@
 """Acquisition-only driver for profiling: BASELINE config 2 (32 PRNs, +-7 kHz / 500 Hz,
 20 ms) on a device-resident synthetic Opensky record, fp64 correlation (ACQ_FP32=1: the
-fp32 fast mode). Args: [datalen] [freqNum]."""
+fp32 fast mode; ACQ_FUSED=<ring slots>: the fused correlator). Args: [datalen] [freqNum]."""
 import importlib, os, sys, time
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -10,6 +10,9 @@ dl = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 nb = int(sys.argv[2]) if len(sys.argv) > 2 else 29
 ctx = pkg.Context(0)
 ctx.set_acq_precision(os.environ.get("ACQ_FP32") is None)  # ACQ_FP32=1: the fp32 fast mode
+if os.environ.get("ACQ_FUSED"):
+    ctx.set_option(pkg.abi.OPT_ACQ_FUSED, 1)
+    ctx.set_option(pkg.abi.OPT_ACQ_RING, int(os.environ["ACQ_FUSED"]))
 file, signal, acq, track, _, _ = pkg.initParameters()
 skip = 5000
 cfg = pkg.synth.opensky(skip_ms=skip)

@@ -8,6 +8,8 @@
 #   tracksq      SQ counter passes (VALU / LDS / waits) of the tracking launches -> gpurun_out/track_sq.json
 #   acqpmc       FETCH / WRITE + SQ passes of the fp64 acquisition kernels -> gpurun_out/acq_counters.json
 #   probes       per timing-probe library (PROBES="0 1 2 8"): SQ fp64/VALU counts and GNSS_STAMPS
+#   acqab        rocprofv3 kernel stats of the config-2 acquisition: two-launch path, then the
+#                fused correlator at ring depths $RINGS (default "3"); + its FETCH/WRITE bytes
 #   cfg4         bench --workload cfg4 -> gpurun_out/bench_cfg4.json
 #   cfg5         bench --workload cfg5 + its PMC traffic + SQ passes -> gpurun_out/cfg5*.json
 set -o pipefail
@@ -51,6 +53,17 @@ for step in "$@"; do
       pmc acq_sq2 "$SQ2" python3 "$R/tools/acq_only.py" || exit 1
       python3 tools/pmc_sq.py gpurun_out/acq_counters.json gpurun_out/acq_fetch gpurun_out/acq_write gpurun_out/acq_sq1 gpurun_out/acq_sq2 -- "inv_cols_kernel<29, HIP_vector_type<double" "inv_rows_kernel_f64<29>" "fwd_rows_kernel<29" "fine_rows_kernel<29" "fine_cols_kernel<29>" || exit 1
       rm -f gpurun_out/acq_*/**/*kernel_trace.csv ;;
+    acqab)
+      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/acqab_split" -o run -- python3 "$R/tools/acq_only.py" ) > gpurun_out/acqab_split.log 2>&1 || { tail -20 gpurun_out/acqab_split.log; exit 1; }
+      python3 tools/prof_summary.py gpurun_out/acqab_split | head -6
+      for r in ${RINGS:-3}; do
+        ( cd /tmp && export TMPDIR=/tmp && ACQ_FUSED=$r timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/acqab_f$r" -o run -- python3 "$R/tools/acq_only.py" ) > gpurun_out/acqab_f$r.log 2>&1 || { tail -20 gpurun_out/acqab_f$r.log; exit 1; }
+        echo "ring $r:"; python3 tools/prof_summary.py gpurun_out/acqab_f$r | head -4
+      done
+      ACQ_FUSED=3 pmc acqf_fetch FETCH_SIZE python3 "$R/tools/acq_only.py" || exit 1
+      ACQ_FUSED=3 pmc acqf_write WRITE_SIZE python3 "$R/tools/acq_only.py" || exit 1
+      python3 tools/pmc_sq.py gpurun_out/acq_fused_bytes.json gpurun_out/acqf_fetch gpurun_out/acqf_write -- "inv_fused_kernel_f64<29>" || exit 1
+      rm -f gpurun_out/acq*/**/*kernel_trace.csv ;;
     cfg4)
       timeout -k 10 400 python3 bench.py --workload cfg4 $BENCH_ARGS > gpurun_out/bench_cfg4.json 2> gpurun_out/bench_cfg4.err \
         && tail -1 gpurun_out/bench_cfg4.json | cut -c1-500 || { tail -20 gpurun_out/bench_cfg4.err; exit 1; } ;;
