@@ -235,7 +235,7 @@ def run_cfg5(args, rank, world, local, dist, ctx):
         v = valu_roofline(sq, "track_run_kernel<11, 3", steps_per_dispatch=40)
         if v:
             v["source"] = sq_prov
-            v["counter_workload"] = "tools/track_only.py 100 400 11 32 (32 channels x 11 taps, 40 10-ms steps)"
+            v["counter_workload"] = "tools/track_only.py 1000 400 11 32 (32 channels x 11 taps, 40 10-ms steps)"
             roof["valu"] = v
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -445,7 +445,7 @@ def main():
         v = valu_roofline(sq, "track_run_kernel<3, 3", steps_per_dispatch=40)
         if v:
             v["source"] = sq_prov
-            v["counter_workload"] = "tools/track_only.py 100 400 (8 channels, 40 10-ms steps per dispatch)"
+            v["counter_workload"] = "tools/track_only.py 1000 400 (8 channels, 40 10-ms steps per dispatch)"
             roof["valu"] = v
 
     # the acquisition's fp32 fast mode (gnss_ctx_set_acq_precision(ctx, 0)) on the same
@@ -507,10 +507,13 @@ def main():
         "device_busy_frac": round((acq_ms + trk_ms) / args.steps / step_ms, 4),
         "roofline": roof,
         # the acquisition's own line (16 B per hypothesis-sample over the
-        # correlation time, the fine-frequency FFTs timed separately)
+        # correlation time, the fine-frequency FFTs timed separately); frac_fp64_model: the
+        # same model restated at the precision the path computes in (32 B: a complex-fp64
+        # spectrum read + an fp64 accumulator read and write)
         "acq_roofline": ({"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
                           "achieved": round(16.0 * acq_units / (acq_corr_ms * 1e-3) / 1e9, 2),
                           "frac": round(16.0 * acq_units / (acq_corr_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                          "frac_fp64_model": round(32.0 * acq_units / (acq_corr_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
                           "corr_ms": round(acq_corr_ms / args.steps, 3),
                           "fine_ms": round(acq_fine_ms / args.steps, 3)} if acq_corr_ms else None),
         # what bounds the acquisition kernels (PMC counters + rocprofv3 averages of this

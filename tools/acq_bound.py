@@ -1,13 +1,17 @@
-"""What bounds the fp64 acquisition kernels, from this round's PMC passes
-(profiles/r02_acq_counters.json: FETCH_SIZE / WRITE_SIZE / SQ counters, median per
-dispatch) and the rocprofv3 kernel-trace averages of the bench
-(profiles/r02_bench_kernel_summary.txt). HBM bytes = FETCH_SIZE x 2 + WRITE_SIZE (KB;
-MI355X_MICROARCH.md HBM section). Writes profiles/acq_bound_r02.json (read by bench.py)."""
+"""What bounds the fp64 acquisition kernels, from a round's PMC passes
+(profiles/rNN_acq_counters.json: FETCH_SIZE / WRITE_SIZE / SQ counters, median per
+dispatch; tools/gpu.sh acqpmc) and the rocprofv3 kernel-trace averages of the bench
+(profiles/rNN_bench_kernel_summary.txt; tools/gpu.sh prof). HBM bytes = FETCH_SIZE x 2 +
+WRITE_SIZE (KB; MI355X_MICROARCH.md HBM section). Writes profiles/acq_bound_rNN.json (read
+by bench.py), stamped with the source digest the counters were taken at.
+Usage: python3 tools/acq_bound.py [NN]   (default 03)"""
 import json, os, re, sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-cnt = json.load(open(os.path.join(ROOT, "profiles", "r02_acq_counters.json")))
-summ = open(os.path.join(ROOT, "profiles", "r02_bench_kernel_summary.txt")).read().splitlines()
+RN = sys.argv[1] if len(sys.argv) > 1 else "03"
+cnt = json.load(open(os.path.join(ROOT, "profiles", f"r{RN}_acq_counters.json")))
+summ = open(os.path.join(ROOT, "profiles", f"r{RN}_bench_kernel_summary.txt")).read().splitlines()
+meta = cnt.pop("_meta", {})
 
 
 def avg_us(sub):
@@ -22,7 +26,10 @@ for key, sub in (("inv_cols_kernel<29, double2>", "inv_cols_kernel<29, HIP_vecto
                  ("inv_rows_kernel_f64<29>", "inv_rows_kernel_f64<29>"),
                  ("fine_rows_kernel<29>", "fine_rows_kernel<29"),
                  ("fine_cols_kernel<29>", "fine_cols_kernel<29>")):
-    ck = next(k for k in cnt if k.startswith(key.split("<")[0]) and (("f64" in k) == ("f64" in key)))
+    ck = next((k for k in cnt if k.startswith(key.split("<")[0]) and (("f64" in k) == ("f64" in key))
+               and cnt[k]), None)
+    if ck is None:
+        continue
     c = {n: v["median_per_dispatch"] for n, v in cnt[ck].items()}
     us = avg_us(sub)
     hbm = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
@@ -39,5 +46,17 @@ for key, sub in (("inv_cols_kernel<29, double2>", "inv_cols_kernel<29, HIP_vecto
                   else "lds issue (fp64 2000-point Stockham passes in LDS)" if e["wait_inst_lds_frac"] > 0.2
                   else "latency (waves parked on loads / barriers)")
     out[key] = e
-json.dump(out, open(os.path.join(ROOT, "profiles", "acq_bound_r02.json"), "w"), indent=1)
+# the correlator's bytes per call against the models (config 2: 1.0764e9 hypothesis-samples
+# per call, 17 batches): SURVEY 8d's 16 B per hypothesis-sample (an fp32 product spectrum
+# read + an fp32 accumulator read and write) and its fp64 restatement, 32 B (the
+# reference's precision: a complex-fp64 spectrum read + an fp64 accumulator read and write)
+if "inv_cols_kernel<29, double2>" in out and "inv_rows_kernel_f64<29>" in out:
+    units, nbat = 1.0764e9, 17
+    per_call = nbat * (out["inv_cols_kernel<29, double2>"]["hbm_bytes_per_launch"]
+                       + out["inv_rows_kernel_f64<29>"]["hbm_bytes_per_launch"])
+    out["correlator_per_call"] = {"hbm_bytes": per_call, "batches": nbat,
+                                  "model_fp32_16B": 16 * units, "x_model_fp32": round(per_call / (16 * units), 3),
+                                  "model_fp64_32B": 32 * units, "x_model_fp64": round(per_call / (32 * units), 3)}
+out["_meta"] = meta
+json.dump(out, open(os.path.join(ROOT, "profiles", f"acq_bound_r{RN}.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))
