@@ -213,11 +213,23 @@ int stage_into(gnss_ctx* ctx, const gnss_file* f, int64_t lo, int64_t hi, int8_t
         hipEvent_t* e;
         ~EvGuard() { (void)hipEventDestroy(e[0]); (void)hipEventDestroy(e[1]); }
     } guard{done};
-    int fd = -1;
+    // the descriptor is closed on every return; an early return (a failed HIP call or a short
+    // read) first drains the stream, so no DMA still reads a pinned buffer the next call refills
+    struct FdGuard {
+        int fd;
+        hipStream_t s;
+        bool drained;
+        ~FdGuard()
+        {
+            if (fd >= 0) close(fd);
+            if (!drained) (void)hipStreamSynchronize(s);
+        }
+    } fg{-1, ctx->stream, false};
     if (!f->data) {
-        fd = open(f->path, O_RDONLY);
-        if (fd < 0) return fail(ctx, GNSS_EIO, "cannot open '%s'", f->path);
+        fg.fd = open(f->path, O_RDONLY);
+        if (fg.fd < 0) return fail(ctx, GNSS_EIO, "cannot open '%s'", f->path);
     }
+    const int fd = fg.fd;
     int64_t off = 0;
     for (int i = 0; off < n; i++, off += kStageChunk) {
         const int64_t len = std::min(kStageChunk, n - off);
@@ -232,19 +244,15 @@ int stage_into(gnss_ctx* ctx, const gnss_file* f, int64_t lo, int64_t hi, int8_t
                 if (r <= 0) break;
                 got += r;
             }
-            if (got != len) {
-                close(fd);
-                (void)hipStreamSynchronize(ctx->stream);
-                return fail(ctx, GNSS_EIO, "short read of '%s'", f->path);
-            }
+            if (got != len) return fail(ctx, GNSS_EIO, "short read of '%s'", f->path);
         }
         HIP_TRY(hipMemcpyAsync(dst + off, buf, (size_t)len, hipMemcpyHostToDevice, ctx->stream));
         HIP_TRY(hipEventRecord(done[i & 1], ctx->stream));
     }
-    if (fd >= 0) close(fd);
     ctx->timing.h2d_bytes += n;
     HIP_TRY(hipEventRecord(ev.b, ctx->stream));
     HIP_TRY(hipEventSynchronize(ev.b));
+    fg.drained = true;
     ctx->timing.h2d_ms += ev.ms();
     return GNSS_OK;
 }

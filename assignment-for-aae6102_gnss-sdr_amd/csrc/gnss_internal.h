@@ -116,12 +116,41 @@ constexpr double kTwoPi = 2.0 * 3.14159265358979323846;  // MATLAB 2*pi
 constexpr double kTwoPiLo = 2.4492935982947064e-16;      // 2*pi - kTwoPi
 constexpr double kInvTwoPi = 1.0 / kTwoPi;               // RN(1/kTwoPi)
 
-// x / b for a divisor known ahead (Fs, 2*pi) with rb = RN(1/b): Markstein's correction
-// q' = RN(q + r*rb), q = RN(x*rb), r = x - q*b (exact by FMA), is the IEEE quotient (rb
-// within half an ulp of 1/b, q within an ulp of x/b); three dependent FMA-class ops
-// instead of the ~10 of a general division on the tracking loop's critical path.
-// Checked against the IEEE division on 3.5e8 operands (tests/native/markstein.c).
+// x / b correctly rounded, for a divisor known ahead (Fs, 2*pi: b > 0) with rb = RN(1/b),
+// for every numerator whose quotient is a normal number above 2^-969 (all the tracking
+// tail's: codeFreq, 2*pi*f, phases, atan outputs, sample counts). q = RN(x*rb) is within
+// 2 ulps of x/b and q1 = RN(q + r*rb), r = x - q*b (by FMA), within half an ulp plus
+// ~2^-52 ulp of it (the exact q + r*rb differs from x/b by (x - q*b)(rb - 1/b)); q1 is
+// therefore RN(x/b) or its neighbour on x/b's side. The remainder r1 = x - q1*b is exact
+// (q1 within an ulp) and x/b - q1 = r1/b, so q1 is RN(x/b) iff |r1| < b*h, h half the
+// spacing from q1 to that neighbour (a quarter ulp below a power of two); b*h is exact and a
+// quotient of two doubles is never a midpoint, so the test decides, and a failed test means
+// the neighbour. (Markstein's correction alone is proven only for q within one ulp; this
+// needs no divisor-specific proof.) Checked against IEEE division: tests/native/markstein.cpp.
+// q1 within an ulp of x/b -> RN(x/b) (the rounding test above)
+GNSS_HD double div_round_fix(double x, double b, double q1)
+{
+    const double r1 = __builtin_fma(-q1, b, x);
+    int64_t bits = __builtin_bit_cast(int64_t, q1);
+    const int64_t mag = bits & 0x7fffffffffffffffLL;
+    const bool away = (r1 > 0) == (q1 > 0);  // |x/b| > |q1|
+    const double ulp = __builtin_bit_cast(double, (mag & 0x7ff0000000000000LL) - (52LL << 52));
+    const double h = ((mag & 0x000fffffffffffffLL) != 0 || away) ? 0.5 * ulp : 0.25 * ulp;
+    if (r1 != 0 && __builtin_fabs(r1) > h * b) bits += away ? 1 : -1;
+    return __builtin_bit_cast(double, bits);
+}
+
 GNSS_HD double div_const(double x, double b, double rb)
+{
+    const double q = x * rb;
+    const double r = __builtin_fma(-q, b, x);
+    return div_round_fix(x, b, __builtin_fma(r, rb, q));
+}
+
+// Markstein's correction alone (the first three steps above): the IEEE quotient k/Fs for the
+// integer sample counts k of CarrTime (trackingCT.m:104), verified exhaustively over the
+// step's k range for the run's Fs on the host (fast_div_exact); the per-sample path
+GNSS_HD double div_markstein(double x, double b, double rb)
 {
     const double q = x * rb;
     const double r = __builtin_fma(-q, b, x);

@@ -145,14 +145,12 @@ __device__ __forceinline__ TailK tail_k(const TrkParams& p)
 }
 
 // CarrTime = k/Fs (trackingCT.m:104) as the IEEE quotient: one FMA-corrected
-// reciprocal (host-verified exact for this Fs and k range) or a true division.
+// reciprocal (host-verified exact for this Fs and k range, fast_div_exact) or a true division.
 template <bool DIVIDE>
 __device__ __forceinline__ double carr_time(double kd, double Fs, double rFs)
 {
     if constexpr (DIVIDE) return kd / Fs;
-    const double q = kd * rFs;
-    const double e = __builtin_fma(-q, Fs, kd);
-    return __builtin_fma(e, rFs, q);
+    return div_markstein(kd, Fs, rFs);
 }
 
 // Wave(k) = (2*pi*(carrierFreq .* CarrTime)) + remPhase with the reference's roundings
@@ -213,12 +211,12 @@ struct StepSize {
     int64_t n, dv;
 };
 
-// codeFreq / Fs and k / Fs: the IEEE quotient by Markstein's correction, or a true division
-// where the host could not verify the correction for this Fs (TrkParams.exact_div)
+// codeFreq / Fs, (r + pe) / Fs, k / Fs: the IEEE quotient (div_const, correctly rounded for
+// every numerator)
 template <class P>
 __device__ __forceinline__ double over_fs(const P& p, double x)
 {
-    return p.exact_div ? x / p.Fs : div_const(x, p.Fs, p.inv_Fs);
+    return div_const(x, p.Fs, p.inv_Fs);
 }
 
 // 1/x to about 1 ulp: hardware reciprocal and two Newton steps (the lanes' boundary search
