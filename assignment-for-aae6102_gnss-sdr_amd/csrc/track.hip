@@ -394,16 +394,18 @@ __device__ __forceinline__ void prepare_desc_i(const P& p, const NcoState& c, in
 {
     if (role == 1) {
         // carrier increment delta = 2*pi*f/Fs as a double-double; dhi has 48 bits so
-        // m*dhi (m < 32) is exact
+        // m*dhi (m < 32) is exact. phi[m] is the rotation basis of lane_correlate, not a
+        // quantity of the reference (the per-sample Wave is formed exactly and eta takes up
+        // the difference), so its quotients need no correct rounding: Markstein's step alone
         const double f = c.carrierFreq;
         double dhi, dlo;
         {
             const double p0 = kTwoPi * f;
             double pe = __builtin_fma(kTwoPi, f, -p0);
             pe = pe + kTwoPiLo * f;
-            const double q = over_fs(p, p0);
+            const double q = div_markstein(p0, p.Fs, p.inv_Fs);
             const double r = __builtin_fma(-q, p.Fs, p0);
-            const double ql = over_fs(p, r + pe);
+            const double ql = div_markstein(r + pe, p.Fs, p.inv_Fs);
             dhi = __longlong_as_double(__double_as_longlong(q) & ~0x1FLL);
             dlo = (q - dhi) + ql;
         }
