@@ -11,7 +11,7 @@
 #   acqab        rocprofv3 kernel stats of the config-2 acquisition: two-launch path, then the
 #                fused correlator at ring depths $RINGS (default "3"); + its FETCH/WRITE bytes
 #   cfg4         bench --workload cfg4 -> gpurun_out/bench_cfg4.json
-#   cfg5         bench --workload cfg5 + its PMC traffic + SQ passes -> gpurun_out/cfg5*.json
+#   cfg5         bench --workload cfg5 + its PMC traffic + SQ passes -> gpurun_out/{bench_cfg5,traffic_cfg5,cfg5_sq}.json
 set -o pipefail
 mkdir -p gpurun_out
 R=$GRAFT_REPO_ROOT
@@ -70,6 +70,10 @@ for step in "$@"; do
     cfg5)
       timeout -k 10 500 python3 bench.py --workload cfg5 $BENCH_ARGS > gpurun_out/bench_cfg5.json 2> gpurun_out/bench_cfg5.err \
         && tail -1 gpurun_out/bench_cfg5.json | cut -c1-700 || { tail -20 gpurun_out/bench_cfg5.err; exit 1; }
+      pmc c5_fetch FETCH_SIZE python3 "$R/tools/track_only.py" 1000 90000 11 32 || exit 1
+      pmc c5_write WRITE_SIZE python3 "$R/tools/track_only.py" 1000 90000 11 32 || exit 1
+      python3 tools/pmc_traffic.py gpurun_out/c5_fetch gpurun_out/c5_write "track_run_kernel<11, 3" gpurun_out/traffic_cfg5.json \
+        "tools/track_only.py 1000 90000 11 32 (32 ch x 11 taps: one persistent launch = 9000 10-ms steps, virtual blocks). Below the algorithmic 2 B/channel-sample: the 32 channels read the same record region within ~1 ms of each other, so most IF lines are L2 / MALL hits" || exit 1
       pmc c5_sq1 "$SQ1" python3 "$R/tools/track_only.py" 1000 400 11 32 || exit 1
       pmc c5_sq3 "$SQ3" python3 "$R/tools/track_only.py" 1000 400 11 32 || exit 1
       python3 tools/pmc_sq.py gpurun_out/cfg5_sq.json gpurun_out/c5_sq1 gpurun_out/c5_sq3 -- "track_run_kernel<11, 3" || exit 1
