@@ -44,6 +44,7 @@ TRACK_SQ_FILES = ("r03_track_sq.json",)                            # SQ counters
 ACQ_BOUND_FILES = ("acq_bound_r03.json", "acq_bound_r02.json")     # fp64 acquisition kernels (tools/acq_bound.py)
 TRAFFIC_FILES_CFG5 = ("traffic_cfg5_r03.json", "traffic_cfg5_r02.json")  # the 11-tap 10-ms launch
 CFG5_SQ_FILES = ("r03_cfg5_sq.json",)
+TRAFFIC_FILES_CFG4 = ("traffic_cfg4_r03.json",)  # the config-4 correlator's kernels, bytes per call
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 import srcdigest  # noqa: E402
 
@@ -308,6 +309,11 @@ def run_cfg4(args, rank, world, local, dist, ctx):
                 "kernel": "acquisition correlator (fwd/inv P x 2000 FFT passes, fp64), rank 0",
                 "corr_ms_per_step": round(corr_ms / args.steps, 3),
                 "algorithmic_bytes_per_step": 16.0 * units / args.steps}
+        tj, prov = evidence(TRAFFIC_FILES_CFG4)
+        if tj and world == 1:  # (bytes of one full 32-PRN call: the N=1 step)
+            roof["traffic"] = tj.get("bytes_per_call")
+            roof["traffic_kernels"] = {k: v["bytes_per_call"] for k, v in tj.get("kernels", {}).items()}
+            roof["traffic_source"] = prov
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline_cfg4(file, signal, acq, dev, prns, S)

@@ -10,6 +10,7 @@
 #   probes       per timing-probe library (PROBES="0 1 2 8"): SQ fp64/VALU counts and GNSS_STAMPS
 #   acqab        rocprofv3 kernel stats of the config-2 acquisition: two-launch path, then the
 #                fused correlator at ring depths $RINGS (default "3"); + its FETCH/WRITE bytes
+#   acqpmc4      FETCH / WRITE passes of the config-4 acquisition's correlator kernels -> gpurun_out/traffic_cfg4.json
 #   cfg4         bench --workload cfg4 -> gpurun_out/bench_cfg4.json
 #   cfg5         bench --workload cfg5 + its PMC traffic + SQ passes -> gpurun_out/{bench_cfg5,traffic_cfg5,cfg5_sq}.json
 set -o pipefail
@@ -64,6 +65,13 @@ for step in "$@"; do
       ACQ_FUSED=3 pmc acqf_write WRITE_SIZE python3 "$R/tools/acq_only.py" || exit 1
       python3 tools/pmc_sq.py gpurun_out/acq_fused_bytes.json gpurun_out/acqf_fetch gpurun_out/acqf_write -- "inv_fused_kernel_f64<29>" || exit 1
       rm -f gpurun_out/acq*/**/*kernel_trace.csv ;;
+    acqpmc4)
+      ACQ_CFG=4 pmc a4_fetch FETCH_SIZE python3 "$R/tools/acq_only.py" || exit 1
+      ACQ_CFG=4 pmc a4_write WRITE_SIZE python3 "$R/tools/acq_only.py" || exit 1
+      python3 tools/pmc_call_bytes.py gpurun_out/a4_fetch gpurun_out/a4_write 3 gpurun_out/traffic_cfg4.json \
+        "tools/acq_only.py with ACQ_CFG=4 (the bench's config-4 record, 32 PRNs x 81 bins x 10 ms, fp64), the correlator's kernels (forward rows/cols, inverse cols/rows)" \
+        "fwd_rows_kernel<13" "fwd_cols_kernel<13" "inv_cols_kernel<13" "inv_rows_kernel_f64<13>" || exit 1
+      rm -f gpurun_out/a4_*/**/*kernel_trace.csv ;;
     cfg4)
       timeout -k 10 400 python3 bench.py --workload cfg4 $BENCH_ARGS > gpurun_out/bench_cfg4.json 2> gpurun_out/bench_cfg4.err \
         && tail -1 gpurun_out/bench_cfg4.json | cut -c1-500 || { tail -20 gpurun_out/bench_cfg4.err; exit 1; } ;;
