@@ -8,6 +8,7 @@
 #   tracksq      SQ counter passes (VALU / LDS / waits) of the tracking launches -> gpurun_out/track_sq.json
 #   acqpmc       FETCH / WRITE + SQ passes of the fp64 acquisition kernels -> gpurun_out/acq_counters.json
 #   probes       per timing-probe library (PROBES="0 1 2 8"): SQ fp64/VALU counts and GNSS_STAMPS
+#   probes1      the same libraries' GNSS_STAMPS of the 1-ms phase alone (tools/track_only.py 1000 0)
 #   acqab        rocprofv3 kernel stats of the config-2 acquisition: two-launch path, then the
 #                fused correlator at ring depths $RINGS (default "3"); + its FETCH/WRITE bytes
 #   acqpmc4      FETCH / WRITE passes of the config-4 acquisition's correlator kernels -> gpurun_out/traffic_cfg4.json
@@ -95,6 +96,12 @@ for step in "$@"; do
         rm -f gpurun_out/st_$n.bin  # (tens of MB: gpurun_out is copied back only below 64 MiB)
       done
       rm -f gpurun_out/pr*_sq/**/*kernel_trace.csv ;;
+    probes1)
+      for n in ${PROBES:-0}; do
+        GNSS_LIB=$R/tools/probe_lib/libgnss_probe$n.so GNSS_STAMPS=gpurun_out/st1_$n.bin TRK_ITERS=1 timeout -k 10 120 python3 tools/track_only.py 1000 0 > gpurun_out/st1_$n.log 2>&1 || { tail gpurun_out/st1_$n.log; exit 1; }
+        echo "== probe $n (1-ms phase)"; python3 tools/stamps_run.py gpurun_out/st1_$n.bin | grep -E "start ->|computed ->|partial out ->|all in ->|period \(|blk0 tail"
+        rm -f gpurun_out/st1_$n.bin
+      done ;;
     ab)  # A/B of library builds (tools/build_commit_lib.sh / build_probe.sh): AB="name ..." ->
          # tools/probe_lib/libgnss_<name>.so; 8-channel trackingCT (1000 ms + 4000 x 10 ms), per-launch
          # hipEvents and GNSS_STAMPS of the 10-ms launch (AB_TAPS=11 AB_NCH=32: the config-5 shape)
