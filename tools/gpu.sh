@@ -99,7 +99,7 @@ for step in "$@"; do
     probes1)
       for n in ${PROBES:-0}; do
         GNSS_LIB=$R/tools/probe_lib/libgnss_probe$n.so GNSS_STAMPS=gpurun_out/st1_$n.bin TRK_ITERS=1 timeout -k 10 120 python3 tools/track_only.py 1000 0 > gpurun_out/st1_$n.log 2>&1 || { tail gpurun_out/st1_$n.log; exit 1; }
-        echo "== probe $n (1-ms phase)"; python3 tools/stamps_run.py gpurun_out/st1_$n.bin | grep -E "start ->|computed ->|partial out ->|all in ->|period \(|blk0 tail"
+        echo "== probe $n (1-ms phase)"; python3 tools/stamps_run.py gpurun_out/st1_$n.bin | grep -E "start ->|computed ->|partial out ->|all in ->|period \(|blk0 tail|lane:"
         rm -f gpurun_out/st1_$n.bin
       done ;;
     ab)  # A/B of library builds (tools/build_commit_lib.sh / build_probe.sh): AB="name ..." ->

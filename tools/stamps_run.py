@@ -43,6 +43,12 @@ for path in sys.argv[1:]:
     spans = [(ch, (r0[21 + 3 * ch] - r0[20 + 3 * ch]) * 0.01, r0[22 + 3 * ch]) for ch in range(64) if r0[21 + 3 * ch]]
     if spans:
         print("  per-channel launch span (us) / steps:", ", ".join(f"ch{c} {t:.0f}/{n}" for c, t, n in spans))
+    e = np.fromfile(path, dtype=np.uint64)[:-1].reshape(-1, ROW)[:, :45].astype(np.int64)
+    e = e[(e[:, 40] != 0) & (e[:, 44] != 0)]
+    if len(e):  # probe bit 32: block 0 thread 0's lane phases
+        print(f"  lane: start->corr entry {us(e[:, 40] - e[:, 0]):6.2f}, boundary search {us(e[:, 41] - e[:, 40]):6.2f}, "
+              f"sincos {us(e[:, 42] - e[:, 41]):6.2f}, samples {us(e[:, 43] - e[:, 42]):6.2f}, "
+              f"epilogue {us(e[:, 44] - e[:, 43]):6.2f}, -> computed {us(e[:, 1] - e[:, 44]):6.2f}")
     d = np.fromfile(path, dtype=np.uint64)[:-1].reshape(-1, ROW)[:, :23].astype(np.int64)
     d = d[(d[:, 16] != 0) & (d[:, 21] != 0) & (d[:, 2] != 0)]
     if len(d):
