@@ -359,15 +359,44 @@ __device__ __forceinline__ void fft2000_batch(V* a, const TW& tw, int tid)
 }
 
 // 2000 = 20 x 10 x 10 with the radix-20 pass first (Ns = 1: no twiddles), so the widest
-// butterfly never holds twiddles in registers (the fp64 row kernel stays within 256 VGPRs);
-// one transform, its first stage's outputs padded (SW above): `a` holds kRowPad elements
-template <int DIR, int BATCH, class V, class TW>
-__device__ __forceinline__ void fft2000_batch_r20first(V* a, const TW& tw, int tid)
+// butterfly never holds twiddles in registers (the fp64 row kernels stay within 256 VGPRs);
+// one transform in `a` (kRowPad elements: its first stage's outputs padded, SW above). The
+// last stage's outputs go to put(i, t, value), not back to LDS: thread j < 200 computes
+// outputs t = j + 200*i (i < 10) and the caller consumes them from registers (one LDS
+// write and read of the row and a barrier less per transform). Ends with a barrier (the
+// caller may rewrite `a`).
+constexpr int kR20Out = 10;  // outputs per thread of the last radix-10 stage
+template <int DIR, class V, class TW, class Put>
+__device__ __forceinline__ void fft2000_r20first_put(V* a, const TW& tw, int tid, Put put)
 {
-    static_assert(BATCH == 1, "one transform (padded layout)");
-    stage_batch<DIR, 20, 1, BATCH, V, TW, 1>(a, tw, tid);
-    stage_batch<DIR, 10, 20, BATCH, V, TW, 2>(a, tw, tid);
-    stage_batch<DIR, 10, 200, BATCH>(a, tw, tid);
+    stage_batch<DIR, 20, 1, 1, V, TW, 1>(a, tw, tid);
+    stage_batch<DIR, 10, 20, 1, V, TW, 2>(a, tw, tid);
+    constexpr int R = 10, NB = kRow / R;  // NS = 200: k = j, outputs at j + 200*i
+    const bool on = tid < NB;
+    const int j = on ? tid : NB - 1;
+    V v[R];
+#pragma unroll
+    for (int i = 0; i < R; i++) v[i] = a[j + i * NB];
+#pragma unroll
+    for (int i = 1; i < R; i++) v[i] = twid<DIR>(v[i], tw[i * j]);
+    dft10<DIR>(v);
+    if (on) {
+#pragma unroll
+        for (int i = 0; i < R; i++) put(i, j + i * NB, v[i]);
+    }
+    __syncthreads();
+}
+
+// The fp64 correlator's inverse row transform with |.|^2 / S^2 accumulated per output in
+// registers: acc[i] of thread j < 200 is output j + 200*i, summed over the ms in order
+// (acquisition.m:53-61).
+constexpr int kInvOut = kR20Out;
+__device__ __forceinline__ void inv_row_power_f64(double2* a, const double2* s_tw, double scale,
+                                                  double (&acc)[kInvOut], int tid)
+{
+    fft2000_r20first_put<1>(a, s_tw, tid, [&](int i, int, double2 v) {
+        acc[i] = __builtin_fma(__builtin_fma(v.x, v.x, v.y * v.y), scale, acc[i]);
+    });
 }
 
 // a value read once (the column pass's intermediate): non-temporal load
@@ -431,10 +460,9 @@ __global__ __launch_bounds__(kRowThreads) void fwd_rows_kernel(
         }
     }
     __syncthreads();
-    fft2000_batch_r20first<-1, 1>(s_a, s_tw, tid);
     V* o = B + ((int64_t)s * P + n2) * kRow;
     const V* twc = tw_col + (int64_t)n2 * kRow;
-    for (int k1 = tid; k1 < kRow; k1 += kRowThreads) o[k1] = cmul(s_a[k1], twc[k1]);
+    fft2000_r20first_put<-1>(s_a, s_tw, tid, [&](int, int k1, V v) { o[k1] = cmul(v, twc[k1]); });
 }
 
 // ---- F2: forward columns: X[s][k1 + 2000*k2] = DFT_P over n2 of B[s][n2][k1]
@@ -564,9 +592,9 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel_f64(
     __shared__ double2 s_a[kRowPad], s_tw[kRow];
     const int tau2 = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
     load_row_tw(s_tw, tw_row, tid);
-    double acc[Q];
+    double acc[kInvOut];
 #pragma unroll
-    for (int i = 0; i < Q; i++) acc[i] = 0.0;
+    for (int i = 0; i < kInvOut; i++) acc[i] = 0.0;
     const double2* src = A + ((int64_t)g * datalen * P + tau2) * kRow;
     // the next ms's row in named registers (an indexed array here is kept in scratch)
     static_assert(Q == 8, "row prefetch is written for 8 values per lane");
@@ -588,22 +616,14 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel_f64(
         if (idx + 1 < datalen) GNSS_LD(idx + 1)
 #undef GNSS_LD
         __syncthreads();
-        fft2000_batch_r20first<1, 1>(s_a, s_tw, tid);
-#pragma unroll
-        for (int i = 0; i < Q; i++) {  // the ms in order (acquisition.m:53-61)
-            const int t1 = tid + i * kRowThreads, t = t1 < kRow ? t1 : kRow - 1;
-            const double2 v = s_a[t];
-            acc[i] += (v.x * v.x + v.y * v.y) * scale;
-        }
-        __syncthreads();
+        inv_row_power_f64(s_a, s_tw, scale, acc, tid);  // (ends with a barrier)
     }
     const int q = first_pair + g;
     const int bin = q / nprn, p = q - bin * nprn;
     double* o = corr + (((int64_t)p * nbins + bin) * P + tau2) * kRow;
+    if (tid < kRow / kInvOut) {
 #pragma unroll
-    for (int i = 0; i < Q; i++) {
-        const int t1 = tid + i * kRowThreads;
-        if (t1 < kRow) o[t1] = acc[i];
+        for (int i = 0; i < kInvOut; i++) o[tid + i * (kRow / kInvOut)] = acc[i];
     }
 }
 
@@ -730,9 +750,9 @@ __global__ __launch_bounds__(kRowThreads, 2) void inv_fused_kernel_f64(
     // ---- row worker: row tau2 = rank of every transform (I2's arithmetic)
     const int tau2 = rank;
     load_row_tw(s_tw, tw_row, tid);
-    double acc[Q];
+    double acc[kInvOut];
 #pragma unroll
-    for (int i = 0; i < Q; i++) acc[i] = 0.0;
+    for (int i = 0; i < kInvOut; i++) acc[i] = 0.0;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         ring_x, (short)0, (int)(kFuseSlots * S * sizeof(double2)), 0x00020000);
     for (int j = 0; j < ntr; j++) {
@@ -752,25 +772,17 @@ __global__ __launch_bounds__(kRowThreads, 2) void inv_fused_kernel_f64(
         }
         __syncthreads();  // the row is in LDS: the slot may be refilled
         if (tid == 0) add_dev(&freed[slot * kFuseLine], 1u);
-        fft2000_batch_r20first<1, 1>(s_a, s_tw, tid);
-#pragma unroll
-        for (int i = 0; i < Q; i++) {  // the ms in order (acquisition.m:53-61)
-            const int t1 = tid + i * kRowThreads, t = t1 < kRow ? t1 : kRow - 1;
-            const double2 v = s_a[t];
-            acc[i] += (v.x * v.x + v.y * v.y) * scale;
-        }
+        inv_row_power_f64(s_a, s_tw, scale, acc, tid);  // (ends with a barrier: s_a free)
         const int pi = j / datalen, ms = j - pi * datalen;
         if (ms == datalen - 1) {
             const int q = xa + pi * na, bin = q / nprn, p = q - bin * nprn;
             double* o = corr + (((int64_t)p * nbins + bin) * P + tau2) * kRow;
 #pragma unroll
-            for (int i = 0; i < Q; i++) {
-                const int t1 = tid + i * kRowThreads;
-                if (t1 < kRow) o[t1] = acc[i];
+            for (int i = 0; i < kInvOut; i++) {
+                if (tid < kRow / kInvOut) o[tid + i * (kRow / kInvOut)] = acc[i];
                 acc[i] = 0.0;
             }
         }
-        __syncthreads();  // (s_a is rewritten by the next transform's copy)
     }
 }
 
@@ -820,14 +832,13 @@ __global__ __launch_bounds__(kRowThreads) void fine_rows_kernel(
         s_a[m1] = cmul(x, tabA[(int64_t)r * kRow + m1]);  // w_RD^(-m1*r), [r][m1]: coalesced
     }
     __syncthreads();
-    fft2000_batch_r20first<-1, 1>(s_a, tw_row, tid);
     double sn, cs;
     const int64_t e = ((int64_t)(P * m2 + n2) * r) % N;
     sincospi(-2.0 * (double)e / (double)N, &sn, &cs);
     const double2 cb = make_double2(cs, sn);
     double2* o = E + (((int64_t)r * P + n2) * T + m2) * kRow;
-    for (int j1 = tid; j1 < kRow; j1 += kRowThreads)
-        o[j1] = cmul(cmul(s_a[j1], cb), tabB[m2 * kRow + j1]);  // w_{T*2000}^(-m2*j1), [m2][j1]
+    const double2* tb = tabB + m2 * kRow;  // w_{T*2000}^(-m2*j1), [m2][j1]
+    fft2000_r20first_put<-1>(s_a, tw_row, tid, [&](int, int j1, double2 v) { o[j1] = cmul(cmul(v, cb), tb[j1]); });
 }
 
 struct FineBest {
