@@ -295,6 +295,37 @@ template <int R, int DIR, class V> __device__ __forceinline__ void dft_r(V (&v)[
     else dft20<DIR>(v);
 }
 
+// Twiddles of the radix-20-first row transforms' two twiddled stages, laid out so a stage's
+// lanes read consecutive entries (a lane j of the Ns = 20 stage reads w^(10*i*(j mod 20)),
+// of the Ns = 200 stage w^(i*j): from the plain 2000-entry table that is a gather at a lane
+// stride of 10*i or i entries, up to 16-way LDS bank conflicts): t2[(i-1)*20 + k] =
+// w^(10*i*k), t3[(i-1)*200 + k] = w^(i*k), 1 980 entries, the same values. A plain pointer is
+// the 2000-entry table itself.
+template <class V> struct TwIK {
+    const V* t2;
+    const V* t3;
+};
+template <int NS, class V>
+__device__ __forceinline__ V tw_get(const V* tw, int, int, int m) { return tw[m]; }
+template <int NS, class V>
+__device__ __forceinline__ V tw_get(const TwIK<V>& tw, int i, int k, int m)
+{
+    static_assert(NS == 20 || NS == 200, "split twiddles: the radix-20-first stages");
+    return NS == 20 ? tw.t2[(i - 1) * 20 + k] : tw.t3[(i - 1) * 200 + k];
+}
+constexpr int kTwIK = 9 * 20 + 9 * 200;  // entries of the split layout
+template <class V>
+__device__ __forceinline__ TwIK<V> load_row_tw_ik(V* s_t, const V* tw_row, int tid)
+{
+    for (int e = tid; e < kTwIK; e += kRowThreads) {
+        const bool t2 = e < 9 * 20;
+        const int f = t2 ? e : e - 9 * 20;
+        const int i = t2 ? f / 20 + 1 : f / 200 + 1, k = t2 ? f % 20 : f % 200;
+        s_t[e] = tw_row[t2 ? 10 * i * k : i * k];
+    }
+    return TwIK<V>{s_t, s_t + 9 * 20};
+}
+
 // ---- BATCH 2000-point transforms side by side in LDS (transform b at a + b*2000), one
 // radix-R Stockham stage; every butterfly of the batch is spread over the block's threads.
 // SW = 1 (the Ns = 1 radix-20 stage of a single transform): outputs stored padded, element
@@ -324,9 +355,9 @@ __device__ __forceinline__ void stage_batch(V* a, const TW& tw, int tid)
 #pragma unroll
             for (int i = 0; i < R; i++) v[q][i] = src[j + i * NB];
         }
-        if (NS > 1) {
+        if constexpr (NS > 1) {
 #pragma unroll
-            for (int i = 1; i < R; i++) v[q][i] = twid<DIR>(v[q][i], tw[i * k * (kRow / (NS * R))]);
+            for (int i = 1; i < R; i++) v[q][i] = twid<DIR>(v[q][i], tw_get<NS>(tw, i, k, i * k * (kRow / (NS * R))));
         }
         dft_r<R, DIR>(v[q]);
     }
@@ -378,7 +409,7 @@ __device__ __forceinline__ void fft2000_r20first_put(V* a, const TW& tw, int tid
 #pragma unroll
     for (int i = 0; i < R; i++) v[i] = a[j + i * NB];
 #pragma unroll
-    for (int i = 1; i < R; i++) v[i] = twid<DIR>(v[i], tw[i * j]);
+    for (int i = 1; i < R; i++) v[i] = twid<DIR>(v[i], tw_get<NB>(tw, i, j, i * j));
     dft10<DIR>(v);
     if (on) {
 #pragma unroll
@@ -391,7 +422,8 @@ __device__ __forceinline__ void fft2000_r20first_put(V* a, const TW& tw, int tid
 // registers: acc[i] of thread j < 200 is output j + 200*i, summed over the ms in order
 // (acquisition.m:53-61).
 constexpr int kInvOut = kR20Out;
-__device__ __forceinline__ void inv_row_power_f64(double2* a, const double2* s_tw, double scale,
+template <class TW>
+__device__ __forceinline__ void inv_row_power_f64(double2* a, const TW& s_tw, double scale,
                                                   double (&acc)[kInvOut], int tid)
 {
     fft2000_r20first_put<1>(a, s_tw, tid, [&](int i, int, double2 v) {
@@ -429,9 +461,9 @@ __global__ __launch_bounds__(kRowThreads) void fwd_rows_kernel(
 {
     using R = Re<V>;
     constexpr int64_t S = (int64_t)P * kRow;
-    __shared__ V s_a[kRowPad], s_tw[kRow];
+    __shared__ V s_a[kRowPad], s_tw[kTwIK];
     const int n2 = blockIdx.x, s = blockIdx.y, tid = threadIdx.x;
-    load_row_tw(s_tw, tw_row, tid);
+    const TwIK<V> twk = load_row_tw_ik(s_tw, tw_row, tid);
     if (s < nsig) {
         const int idx = s / nbins, bin = s - idx * nbins;
         const double f = (IF + (freqMin + freqStep * (double)bin)) / Fs;  // cycles per sample
@@ -462,7 +494,7 @@ __global__ __launch_bounds__(kRowThreads) void fwd_rows_kernel(
     __syncthreads();
     V* o = B + ((int64_t)s * P + n2) * kRow;
     const V* twc = tw_col + (int64_t)n2 * kRow;
-    fft2000_r20first_put<-1>(s_a, s_tw, tid, [&](int, int k1, V v) { o[k1] = cmul(v, twc[k1]); });
+    fft2000_r20first_put<-1>(s_a, twk, tid, [&](int, int k1, V v) { o[k1] = cmul(v, twc[k1]); });
 }
 
 // ---- F2: forward columns: X[s][k1 + 2000*k2] = DFT_P over n2 of B[s][n2][k1]
@@ -589,9 +621,9 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel_f64(
     const double2* __restrict__ tw_row, double* __restrict__ corr, int nbins)
 {
     constexpr int Q = (kRow + kRowThreads - 1) / kRowThreads;
-    __shared__ double2 s_a[kRowPad], s_tw[kRow];
+    __shared__ double2 s_a[kRowPad], s_tw[kTwIK];
     const int tau2 = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
-    load_row_tw(s_tw, tw_row, tid);
+    const TwIK<double2> twk = load_row_tw_ik(s_tw, tw_row, tid);
     double acc[kInvOut];
 #pragma unroll
     for (int i = 0; i < kInvOut; i++) acc[i] = 0.0;
@@ -616,7 +648,7 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel_f64(
         if (idx + 1 < datalen) GNSS_LD(idx + 1)
 #undef GNSS_LD
         __syncthreads();
-        inv_row_power_f64(s_a, s_tw, scale, acc, tid);  // (ends with a barrier)
+        inv_row_power_f64(s_a, twk, scale, acc, tid);  // (ends with a barrier)
     }
     const int q = first_pair + g;
     const int bin = q / nprn, p = q - bin * nprn;
@@ -684,7 +716,7 @@ __global__ __launch_bounds__(kRowThreads, 2) void inv_fused_kernel_f64(
 {
     constexpr int Q = (kRow + kRowThreads - 1) / kRowThreads;
     constexpr int64_t S = (int64_t)P * kRow;
-    __shared__ double2 s_a[kRowPad], s_tw[kRow];
+    __shared__ double2 s_a[kRowPad], s_tw[kTwIK];
     __shared__ int s_role[6];  // xcc, rank, team size, XCD position, active XCDs, ok
     const int tid = threadIdx.x;
     // ---- census: this workgroup's XCD and rank in it, then wait for every workgroup
@@ -749,7 +781,7 @@ __global__ __launch_bounds__(kRowThreads, 2) void inv_fused_kernel_f64(
     }
     // ---- row worker: row tau2 = rank of every transform (I2's arithmetic)
     const int tau2 = rank;
-    load_row_tw(s_tw, tw_row, tid);
+    const TwIK<double2> twk = load_row_tw_ik(s_tw, tw_row, tid);
     double acc[kInvOut];
 #pragma unroll
     for (int i = 0; i < kInvOut; i++) acc[i] = 0.0;
@@ -772,7 +804,7 @@ __global__ __launch_bounds__(kRowThreads, 2) void inv_fused_kernel_f64(
         }
         __syncthreads();  // the row is in LDS: the slot may be refilled
         if (tid == 0) add_dev(&freed[slot * kFuseLine], 1u);
-        inv_row_power_f64(s_a, s_tw, scale, acc, tid);  // (ends with a barrier: s_a free)
+        inv_row_power_f64(s_a, twk, scale, acc, tid);  // (ends with a barrier: s_a free)
         const int pi = j / datalen, ms = j - pi * datalen;
         if (ms == datalen - 1) {
             const int q = xa + pi * na, bin = q / nprn, p = q - bin * nprn;
