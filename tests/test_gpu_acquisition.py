@@ -71,6 +71,27 @@ def test_no_satellites_acquired(pkg, po, ctx):
     assert len(g.sv) == 0 and len(g.fineFreq) == 0
 
 
+def test_argument_errors_raise(pkg, po, ctx):
+    """A PRN outside generateCAcode's shift table (g2s, 51 entries, generateCAcode.m:16-27:
+    MATLAB's g2s(PRN) is an index error) -> GNSS_EARG; a record shorter than the datalen ms
+    acquisition.m:34 reads -> GNSS_EIO (MATLAB's fread comes back short and
+    rawsignal(1+(idx-1)*Sample:idx*Sample) indexes past it, :57). The context stays usable."""
+    cfg = pkg.synth.scenario([], [], [], [], skip_ms=0)
+    data = po.synth_if(cfg, 0, 30 * 58000)
+    file, signal, acq, track = params(pkg, 0, data)
+    acq.freqMin, acq.freqNum, acq.datalen = -3000, 13, 20
+    for prns in ([0], [52], [3, -1]):
+        with pytest.raises(pkg.abi.GnssError) as e:
+            pkg.acquisition(file, signal, acq, ctx=ctx, prn_list=prns)
+        assert e.value.status == pkg.abi.EARG, prns
+    short, *_ = params(pkg, 0, data[: 2 * 58000 * 19])
+    with pytest.raises(pkg.abi.GnssError) as e:
+        pkg.acquisition(short, signal, acq, ctx=ctx, prn_list=[3])
+    assert e.value.status == pkg.abi.EIO
+    g = pkg.acquisition(file, signal, acq, ctx=ctx, prn_list=[1, 2])
+    assert len(g.sv) == 0
+
+
 def test_urban_parameters(pkg, po, ctx, precision):
     """BASELINE config 4 shape: IF = 0, Fs = 26 MHz (assumed), +-10 kHz / 250 Hz (81 bins),
     10 ms; PRN subset to bound the oracle's CPU time."""

@@ -237,6 +237,27 @@ def test_read_past_eof_in_10ms_phase_raises(pkg, ctx, opensky_short):
     assert e.value.status == pkg.abi.EIO
 
 
+def test_argument_errors_raise(pkg, ctx, opensky_short):
+    """Nothing acquired: trackingCT.m:20-22 tracks no channel and never assigns TckResultCT,
+    so MATLAB stops with an unassigned-output error -> GNSS_EARG. So do a channel index past
+    Acquired.sv (the shard list) and tap sets the loops cannot run on: a count other than
+    3 / 11 / 25, and three taps without -spacing, 0, +spacing (no E / P / L,
+    trackingCT.m:24)."""
+    skip, cfg, data = opensky_short
+    file, signal, acq, track = params(pkg, skip, data[: 2 * 58000 * 1400])
+    track.msToProcessCT_1ms, track.msToProcessCT_10ms = 700, 200
+    A = acquired_of([26], [57908], [4581800.0])
+    sp = float(track.CorrelatorSpacing)
+    for kw, Aq in [({}, acquired_of([], [], [])), (dict(channels=[1]), A), (dict(channels=[-1]), A),
+                   (dict(taps=[-sp, 0.0, sp, 2 * sp]), A), (dict(taps=[-sp / 2, 0.0, sp / 2]), A)]:
+        with pytest.raises(pkg.abi.GnssError) as e:
+            pkg.trackingCT(file, signal, track, Aq, ctx=ctx, **kw)
+        assert e.value.status == pkg.abi.EARG, kw
+    # and the context is still usable afterwards
+    T, cn0, cx = pkg.trackingCT(file, signal, track, A, ctx=ctx)
+    assert T.prns() == [26]
+
+
 def test_file_route_positioned_reads(pkg, ctx, opensky_short, tmp_path):
     """file.fileRoute path (positioned reads) == in-memory record."""
     skip, cfg, data = opensky_short
