@@ -2,12 +2,13 @@
 # N given, with GNSS_CORR_PROBE=N (track.hip: bits that drop parts of the correlator; 0 =
 # the full correlator) and GNSS_PROBE_BUILD=1 (gnss_api.cpp reads the GNSS_STAMPS /
 # GNSS_PROBE / GNSS_HOSTPROF / GNSS_FORCE_SUB10 environment hooks). Load one with
-# GNSS_LIB=<path>. Never used by the product, the tests or bench.py.
+# GNSS_LIB=<path>. Never used by the product, the tests or bench.py. EXTRA_FLAGS adds
+# compiler flags (e.g. -DGNSS_XCHG_LD_POL=17: the exchange's poll cache policy).
 set -e
 cd "$(dirname "$0")/../assignment-for-aae6102_gnss-sdr_amd/csrc"
 make -s
 mkdir -p ../../tools/probe_lib /tmp/gnss_probe_obj
-FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -pthread -DGNSS_PROBE_BUILD=1"
+FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -pthread -DGNSS_PROBE_BUILD=1 $EXTRA_FLAGS"
 /opt/rocm/bin/hipcc $FLAGS -c gnss_api.cpp -o /tmp/gnss_probe_obj/gnss_api.o &
 for n in "$@"; do
   /opt/rocm/bin/hipcc $FLAGS -DGNSS_CORR_PROBE=$n -c track.hip -o /tmp/gnss_probe_obj/track_$n.o &
