@@ -191,7 +191,7 @@ _torch_first = False
 
 # gnss_ctx_set_option keys (include/gnss_mi355x.h, ABI v9)
 (OPT_FORCE_SUB, OPT_NO_PERSIST, OPT_FORCE_VPB, OPT_ACQ_ROCFFT, OPT_FINE_ROCFFT, OPT_ACQ_BATCH, OPT_ACQ_FUSED,
- OPT_ACQ_RING) = range(8)
+ OPT_ACQ_RING, OPT_ACQ_PIPE) = range(9)
 
 
 def require_torch():

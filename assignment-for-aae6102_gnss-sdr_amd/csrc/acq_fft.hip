@@ -1015,15 +1015,17 @@ template hipError_t launch_acq_fft_forward<double2>(const int8_t*, const double2
 hipError_t launch_acq_fft_correlate(const float2* C, const float2* X, int64_t S, int datalen,
                                     int nbins, int nprn, int first_pair, int npair,
                                     const float2* tw_row, const float2* tw_col, float2* A,
-                                    float* corr, hipStream_t s)
+                                    float* corr, hipStream_t s, int parts)
 {
     const float scale = (float)(1.0 / ((double)S * (double)S));  // ifft's 1/N, squared
 #define GNSS_INV(P_)                                                                            \
     if (S == (int64_t)P_ * kRow) {                                                              \
+        if (parts & kAcqCols)                                                                   \
         hipLaunchKernelGGL((inv_cols_kernel<P_, float2>),                                       \
                            dim3((kRow + kColThreads - 1) / kColThreads, npair * datalen),       \
                            dim3(kColThreads), 0, s, C, X, nbins, nprn, datalen, first_pair,     \
                            tw_col, A);                                                          \
+        if (parts & kAcqRows)                                                                   \
         hipLaunchKernelGGL(inv_rows_kernel<P_>, dim3(P_, npair), dim3(kRowThreads), 0, s, A, nprn, \
                            datalen, first_pair, scale, tw_row, corr, nbins);                    \
         return hipGetLastError();                                                               \
@@ -1036,15 +1038,17 @@ hipError_t launch_acq_fft_correlate(const float2* C, const float2* X, int64_t S,
 hipError_t launch_acq_fft_correlate(const double2* C, const double2* X, int64_t S, int datalen,
                                     int nbins, int nprn, int first_pair, int npair,
                                     const double2* tw_row, const double2* tw_col, double2* A,
-                                    double* corr, hipStream_t s)
+                                    double* corr, hipStream_t s, int parts)
 {
     const double scale = 1.0 / ((double)S * (double)S);
 #define GNSS_INV(P_)                                                                            \
     if (S == (int64_t)P_ * kRow) {                                                              \
+        if (parts & kAcqCols)                                                                   \
         hipLaunchKernelGGL((inv_cols_kernel<P_, double2>),                                      \
                            dim3((kRow + kColThreads - 1) / kColThreads, npair * datalen),       \
                            dim3(kColThreads), 0, s, C, X, nbins, nprn, datalen, first_pair,     \
                            tw_col, A);                                                          \
+        if (parts & kAcqRows)                                                                   \
         hipLaunchKernelGGL(inv_rows_kernel_f64<P_>, dim3(P_, npair), dim3(kRowThreads), 0, s, A, nprn, \
                            datalen, first_pair, scale, tw_row, corr, nbins);                    \
         return hipGetLastError();                                                               \

@@ -34,6 +34,8 @@ using namespace gnss;
 struct gnss_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t stream2 = nullptr;       // the acquisition's row passes beside the column passes
+    hipEvent_t ev_cols[2] = {}, ev_rows[2] = {};  // their hand-offs, per intermediate buffer
     std::string err;
     gnss_timing timing{};
     int profiling = 0;
@@ -64,6 +66,11 @@ static const char* probe_env(const char* name)
 }
 
 namespace {
+// The acquisition's split correlator pipelines its batches over two streams by default
+// (GNSS_OPT_ACQ_PIPE; config-2 fp64 correlation 10.10-10.18 -> 9.75-9.88 ms on MI355X,
+// profiles/r03_ab_acq_pipe.txt).
+constexpr bool kAcqPipeDefault = true;
+
 // The context's pinned host buffer `key`, at least `bytes` (contents undefined).
 template <class T>
 T* pinned_buffer(gnss_ctx* ctx, const char* key, size_t count)
@@ -466,18 +473,47 @@ int acq_search(gnss_ctx* ctx, const int8_t* blk, const double2* xa, int64_t S, i
         int batch = (npairs + nbat - 1) / nbat;
         if (ctx->opt[GNSS_OPT_ACQ_BATCH] > 0) batch = (int)ctx->opt[GNSS_OPT_ACQ_BATCH];
         batch = std::min(batch, npairs);
-        HIP_TRY(A.alloc(ctx, "acq.A", csz * (size_t)batch * dl * S));
+        // Two streams: batch b's row pass (LDS-bound fp64 transforms, reading the intermediate)
+        // runs beside batch b+1's column pass (bound by the intermediate's writes), each batch
+        // in its own half of a double intermediate; the column pass of b+2 waits for the rows
+        // of b. Every pair is in one batch and its corr entries are written by its row pass
+        // alone, so the surface is bit-identical to the one-stream order.
+        const int64_t pipe = ctx->opt[GNSS_OPT_ACQ_PIPE];
+        const bool two = (pipe == 2 || (pipe == 0 && kAcqPipeDefault)) && npairs > batch;
+        hipStream_t s_cols = ctx->stream, s_rows = ctx->stream2;
+        const size_t abuf = (size_t)batch * dl * S;
+        HIP_TRY(A.alloc(ctx, "acq.A", csz * abuf * (two ? 2 : 1)));
         HIP_TRY(hipStreamSynchronize(ctx->stream));
         HIP_TRY(hipEventRecord(e_all.a, ctx->stream));
         HIP_TRY(launch_acq_fft_forward<V>(blk, xa, S, dl, nb, sg->IF, acq->freqMin, acq->freqStep, sg->Fs, ca, np,
                                           sg->codeFreqBasis, d_twr.as<V>(), d_twc.as<V>(), B.as<V>(), X.as<V>(),
                                           ctx->stream));
         const V* C = X.as<V>() + (size_t)nsig * S;
-        for (int q0 = 0; q0 < npairs; q0 += batch) {
-            const int nq = std::min(batch, npairs - q0);
-            HIP_TRY(launch_acq_fft_correlate(C, X.as<V>(), S, dl, nb, np, q0, nq, d_twr.as<V>(), d_twc.as<V>(),
-                                             A.as<V>(), corr, ctx->stream));
+        if (!two) {
+            for (int q0 = 0; q0 < npairs; q0 += batch) {
+                const int nq = std::min(batch, npairs - q0);
+                HIP_TRY(launch_acq_fft_correlate(C, X.as<V>(), S, dl, nb, np, q0, nq, d_twr.as<V>(),
+                                                 d_twc.as<V>(), A.as<V>(), corr, ctx->stream));
+            }
+            return GNSS_OK;
         }
+        int last = 0;
+        for (int q0 = 0, b = 0; q0 < npairs; q0 += batch, b++) {
+            const int nq = std::min(batch, npairs - q0);
+            const int h = b & 1;
+            V* Ah = A.as<V>() + (size_t)h * abuf;
+            if (b >= 2) HIP_TRY(hipStreamWaitEvent(s_cols, ctx->ev_rows[h], 0));  // rows of b-2 read Ah
+            HIP_TRY(launch_acq_fft_correlate(C, X.as<V>(), S, dl, nb, np, q0, nq, d_twr.as<V>(), d_twc.as<V>(), Ah,
+                                             corr, s_cols, kAcqCols));
+            HIP_TRY(hipEventRecord(ctx->ev_cols[h], s_cols));
+            HIP_TRY(hipStreamWaitEvent(s_rows, ctx->ev_cols[h], 0));
+            HIP_TRY(launch_acq_fft_correlate(C, X.as<V>(), S, dl, nb, np, q0, nq, d_twr.as<V>(), d_twc.as<V>(), Ah,
+                                             corr, s_rows, kAcqRows));
+            HIP_TRY(hipEventRecord(ctx->ev_rows[h], s_rows));
+            last = h;
+        }
+        // the caller's stream owns the result again (stream2 is in order: its last event covers all)
+        HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_rows[last], 0));
         return GNSS_OK;
     }
     // batched rocFFT (sample counts that are not P x 2000)
@@ -539,8 +575,13 @@ int gnss_ctx_create(int device, gnss_ctx** out)
     if (hipSetDevice(device) != hipSuccess) return GNSS_EDEVICE;
     gnss_ctx* ctx = new gnss_ctx();
     ctx->device = device;
-    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
-        delete ctx;
+    bool ok = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) == hipSuccess;
+    for (int i = 0; i < 2 && ok; i++)
+        ok = hipEventCreateWithFlags(&ctx->ev_cols[i], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&ctx->ev_rows[i], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        gnss_ctx_destroy(ctx);
         return GNSS_EDEVICE;
     }
     rocfft_setup();
@@ -552,14 +593,20 @@ void gnss_ctx_destroy(gnss_ctx* ctx)
 {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
     for (auto& kv : ctx->plans) rocfft_plan_destroy(kv.second);
     if (ctx->fft_work) (void)hipFree(ctx->fft_work);
     for (auto& kv : ctx->pool)
         if (kv.second.first) (void)hipFree(kv.second.first);
     for (auto& kv : ctx->pinned)
         if (kv.second.first) (void)hipHostFree(kv.second.first);
-    (void)hipStreamDestroy(ctx->stream);
+    for (int i = 0; i < 2; i++) {
+        if (ctx->ev_cols[i]) (void)hipEventDestroy(ctx->ev_cols[i]);
+        if (ctx->ev_rows[i]) (void)hipEventDestroy(ctx->ev_rows[i]);
+    }
+    if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
 

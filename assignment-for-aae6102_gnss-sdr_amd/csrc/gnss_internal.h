@@ -349,14 +349,16 @@ hipError_t launch_acq_fft_forward(const int8_t* iq, const double2* xs, int64_t S
                                   double freqMin, double freqStep, double Fs, const float* ca,
                                   int nprn, double codeFreqBasis, const V* tw_row,
                                   const V* tw_col, V* B, V* X, hipStream_t s);
+// parts: kAcqCols (the column pass into A), kAcqRows (the row pass out of A into corr), or both
+constexpr int kAcqCols = 1, kAcqRows = 2;
 hipError_t launch_acq_fft_correlate(const float2* C, const float2* X, int64_t S, int datalen,
                                     int nbins, int nprn, int first_pair, int npair,
                                     const float2* tw_row, const float2* tw_col, float2* A,
-                                    float* corr, hipStream_t s);
+                                    float* corr, hipStream_t s, int parts = kAcqCols | kAcqRows);
 hipError_t launch_acq_fft_correlate(const double2* C, const double2* X, int64_t S, int datalen,
                                     int nbins, int nprn, int first_pair, int npair,
                                     const double2* tw_row, const double2* tw_col, double2* A,
-                                    double* corr, hipStream_t s);
+                                    double* corr, hipStream_t s, int parts = kAcqCols | kAcqRows);
 // fp64, every (bin, PRN) pair in one persistent launch with the column/row intermediate
 // kept in each XCD's L2 (nslot ring slots per XCD, 2..4); see acq_fft.hip
 size_t acq_fused_sync_bytes();

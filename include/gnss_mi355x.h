@@ -242,7 +242,11 @@ int  gnss_ctx_set_window(gnss_ctx *ctx, uint64_t bytes);
                                     intermediate in each XCD's L2 (measured slower, kept
                                     for the record; default: two launches per batch)      */
 #define GNSS_OPT_ACQ_RING     7  /* 2..4: ring slots per XCD of the fused correlator (3)    */
-#define GNSS_OPT_COUNT        8
+#define GNSS_OPT_ACQ_PIPE     8  /* split path: 1 = column and row passes of every batch in
+                                    order on one stream, 2 = pipelined over two streams
+                                    (batch b's rows beside batch b+1's columns, two
+                                    intermediates); 0 = the engine's choice               */
+#define GNSS_OPT_COUNT        9
 int  gnss_ctx_set_option(gnss_ctx *ctx, int key, int64_t value);
 
 /* Device memory owned by the ctx, for callers that keep an IF record resident

@@ -228,3 +228,38 @@ def test_fused_correlator_equals_split_path(pkg, ctx, opts, shape):
             assert np.array_equal(a, b), (ring, f, a, b)
         assert np.array_equal(g0.sv, g1.sv) and np.array_equal(g0.fineFreq, g1.fineFreq)
     assert len(d0.prn) == 32
+
+
+@pytest.mark.parametrize("shape", ["cfg2", "cfg4"])
+def test_pipelined_batches_equal_one_stream(pkg, ctx, opts, shape, precision):
+    """The split correlator's batches pipelined over two streams (GNSS_OPT_ACQ_PIPE = 2:
+    batch b's row pass beside batch b+1's column pass, two intermediates) against the
+    same batches in order on one stream (= 1): every PRN's SNR, peak, second peak, bin and
+    code phase identical bit for bit at the benchmarked shapes, with the engine's batch
+    size and with 7 pairs per batch (an odd batch count and a short tail batch)
+    (acquisition.m:47-61; each pair's corr entries are written by its own row pass)."""
+    abi = pkg.abi
+    if shape == "cfg2":
+        skip, S, Fs, IF = 2, 58000, 58e6, 4.58e6
+        cfg = pkg.synth.opensky(skip_ms=skip)
+        acq = SimpleNamespace(freqNum=29, freqMin=-7000, freqStep=500, datalen=20, L=10)
+    else:
+        skip, S, Fs, IF = 1000, 26000, 26e6, 0.0
+        cfg = pkg.synth.urban(skip_ms=skip, Fs=Fs)
+        acq = SimpleNamespace(freqNum=81, freqMin=-10000, freqStep=250, datalen=10, L=10)
+    dev = pkg.DeviceRecord(ctx, (skip + 30) * S * 2)
+    pkg.synth.generate_device(ctx, cfg, dev)
+    file = SimpleNamespace(skip=skip, dataType=2, dataPrecision=1, data=None, fileRoute=None, dev=dev)
+    signal = SimpleNamespace(IF=IF, Fs=Fs, codeFreqBasis=1.023e6, ms=1e-3, Sample=S, codelength=1023.0)
+    for batch in (0, 7):
+        opts(abi.OPT_ACQ_BATCH, batch)
+        res = []
+        for pipe in (1, 2):
+            opts(abi.OPT_ACQ_PIPE, pipe)
+            res.append(pkg.acquisition(file, signal, acq, ctx=ctx, diag=True))
+        (g0, d0), (g1, d1) = res
+        for f in ("prn", "SNR", "peak", "peak2", "fbin", "codePhase"):
+            a, b = np.asarray(getattr(d0, f)), np.asarray(getattr(d1, f))
+            assert np.array_equal(a, b), (batch, f, a, b)
+        assert np.array_equal(g0.sv, g1.sv) and np.array_equal(g0.fineFreq, g1.fineFreq)
+        assert len(d0.prn) == 32

@@ -1,7 +1,8 @@
 """Acquisition-only driver for profiling: BASELINE config 2 (32 PRNs, +-7 kHz / 500 Hz,
 20 ms) on a device-resident synthetic Opensky record, fp64 correlation (ACQ_FP32=1: the
 fp32 fast mode; ACQ_FUSED=<ring slots>: the fused correlator; ACQ_CFG=4: BASELINE config 4
-instead, the bench's Urban record: Fs 26 MHz, IF 0, 32 PRNs, +-10 kHz / 250 Hz, 10 ms).
+instead, the bench's Urban record: Fs 26 MHz, IF 0, 32 PRNs, +-10 kHz / 250 Hz, 10 ms;
+ACQ_PIPE=1|2: the split correlator's batches on one stream / pipelined over two).
 Args: [datalen] [freqNum] (config 2 only). Three calls."""
 import importlib, os, sys, time
 import numpy as np
@@ -11,10 +12,12 @@ pkg = importlib.import_module("assignment-for-aae6102_gnss-sdr_amd")
 dl = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 nb = int(sys.argv[2]) if len(sys.argv) > 2 else 29
 ctx = pkg.Context(0)
-ctx.set_acq_precision(os.environ.get("ACQ_FP32") is None)  # ACQ_FP32=1: the fp32 fast mode
+ctx.set_acq_precision(not os.environ.get("ACQ_FP32"))  # ACQ_FP32=1: the fp32 fast mode
 if os.environ.get("ACQ_FUSED"):
     ctx.set_option(pkg.abi.OPT_ACQ_FUSED, 1)
     ctx.set_option(pkg.abi.OPT_ACQ_RING, int(os.environ["ACQ_FUSED"]))
+if os.environ.get("ACQ_PIPE"):
+    ctx.set_option(pkg.abi.OPT_ACQ_PIPE, int(os.environ["ACQ_PIPE"]))
 file, signal, acq, track, _, _ = pkg.initParameters()
 if os.environ.get("ACQ_CFG") == "4":  # bench.py run_cfg4's record and parameters
     skip, S = 1000, 26000

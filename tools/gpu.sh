@@ -12,8 +12,10 @@
 #   acqab        rocprofv3 kernel stats of the config-2 acquisition: two-launch path, then the
 #                fused correlator at ring depths $RINGS (default "3"); + its FETCH/WRITE bytes
 #   acqpmc4      FETCH / WRITE passes of the config-4 acquisition's correlator kernels -> gpurun_out/traffic_cfg4.json
+#   acqpipe      config-2 / config-4 acquisition timing, batches on one stream vs pipelined (tools/acq_only.py)
 #   cfg4         bench --workload cfg4 -> gpurun_out/bench_cfg4.json
-#   cfg5         bench --workload cfg5 + its PMC traffic + SQ passes -> gpurun_out/{bench_cfg5,traffic_cfg5,cfg5_sq}.json
+#   cfg5         bench --workload cfg5 -> gpurun_out/bench_cfg5.json
+#   cfg5pmc      the config-5 launch's PMC traffic + SQ passes -> gpurun_out/{traffic_cfg5,cfg5_sq}.json
 set -o pipefail
 mkdir -p gpurun_out
 R=$GRAFT_REPO_ROOT
@@ -78,7 +80,8 @@ for step in "$@"; do
         && tail -1 gpurun_out/bench_cfg4.json | cut -c1-500 || { tail -20 gpurun_out/bench_cfg4.err; exit 1; } ;;
     cfg5)
       timeout -k 10 500 python3 bench.py --workload cfg5 $BENCH_ARGS > gpurun_out/bench_cfg5.json 2> gpurun_out/bench_cfg5.err \
-        && tail -1 gpurun_out/bench_cfg5.json | cut -c1-700 || { tail -20 gpurun_out/bench_cfg5.err; exit 1; }
+        && tail -1 gpurun_out/bench_cfg5.json | cut -c1-700 || { tail -20 gpurun_out/bench_cfg5.err; exit 1; } ;;
+    cfg5pmc)
       pmc c5_fetch FETCH_SIZE python3 "$R/tools/track_only.py" 1000 90000 11 32 || exit 1
       pmc c5_write WRITE_SIZE python3 "$R/tools/track_only.py" 1000 90000 11 32 || exit 1
       python3 tools/pmc_traffic.py gpurun_out/c5_fetch gpurun_out/c5_write "track_run_kernel<11, 3" gpurun_out/traffic_cfg5.json \
@@ -87,6 +90,18 @@ for step in "$@"; do
       pmc c5_sq3 "$SQ3" python3 "$R/tools/track_only.py" 1000 400 11 32 || exit 1
       python3 tools/pmc_sq.py gpurun_out/cfg5_sq.json gpurun_out/c5_sq1 gpurun_out/c5_sq3 -- "track_run_kernel<11, 3" || exit 1
       rm -f gpurun_out/c5_*/**/*kernel_trace.csv ;;
+    acqpipe)  # split correlator: batches on one stream vs pipelined over two (ACQ_PIPE), cfg2 / cfg4, fp64 / fp32
+      for c in 2 4; do for f in "" 1; do for p in 1 2; do
+        echo "-- cfg$c fp32=${f:-0} pipe=$p"
+        ACQ_CFG=$c ACQ_FP32=$f ACQ_PIPE=$p timeout -k 10 200 python3 tools/acq_only.py > gpurun_out/acqpipe_${c}_${f:-0}_$p.txt 2>&1 \
+          && grep -E "acq wall|^sv" gpurun_out/acqpipe_${c}_${f:-0}_$p.txt | tail -2 | cut -c1-400 || { tail -20 gpurun_out/acqpipe_${c}_${f:-0}_$p.txt; exit 1; }
+      done; done; done ;;
+    acqmask)  # config-2 fp64 correlation vs GNSS_OPT_ACQ_PIPE (1 one stream, 2 two streams; PIPES="1 2")
+      for p in ${PIPES:-1 2 3 4 5 6}; do
+        ACQ_PIPE=$p timeout -k 10 200 python3 tools/acq_only.py > gpurun_out/acqmask_$p.txt 2>&1 \
+          && echo "pipe=$p corr_ms $(grep -o "'acq_corr_ms': [0-9.]*" gpurun_out/acqmask_$p.txt | cut -d' ' -f2 | tr '\n' ' ') $(grep -E '^(fbin|snr)' gpurun_out/acqmask_$p.txt | md5sum | cut -c1-8)" \
+          || { tail -20 gpurun_out/acqmask_$p.txt; exit 1; }
+      done ;;
     probes)  # timing-probe libraries (tools/build_probe.sh $PROBES): fp64 / VALU counts + stamps each
       for n in ${PROBES:-0}; do
         GNSS_LIB=$R/tools/probe_lib/libgnss_probe$n.so pmc pr${n}_sq "$SQ3" python3 "$R/tools/track_only.py" 1000 400 || exit 1
