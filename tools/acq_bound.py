@@ -10,7 +10,12 @@ import json, os, re, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 RN = sys.argv[1] if len(sys.argv) > 1 else "03"
 cnt = json.load(open(os.path.join(ROOT, "profiles", f"r{RN}_acq_counters.json")))
-summ = open(os.path.join(ROOT, "profiles", f"r{RN}_bench_kernel_summary.txt")).read().splitlines()
+# per-kernel durations: the one-stream order's kernel stats when present (tools/gpu.sh acqprof1;
+# the default pipelines batch b's row pass beside b+1's column pass, so the bench's kernel-trace
+# durations overlap and would understate each kernel's rate), else the bench's summary
+_one = os.path.join(ROOT, "profiles", f"r{RN}_acq_onestream_kernel_summary.txt")
+DUR_SRC = _one if os.path.exists(_one) else os.path.join(ROOT, "profiles", f"r{RN}_bench_kernel_summary.txt")
+summ = open(DUR_SRC).read().splitlines()
 meta = cnt.pop("_meta", {})
 
 
@@ -57,6 +62,7 @@ if "inv_cols_kernel<29, double2>" in out and "inv_rows_kernel_f64<29>" in out:
     out["correlator_per_call"] = {"hbm_bytes": per_call, "batches": nbat,
                                   "model_fp32_16B": 16 * units, "x_model_fp32": round(per_call / (16 * units), 3),
                                   "model_fp64_32B": 32 * units, "x_model_fp64": round(per_call / (32 * units), 3)}
+meta["durations_from"] = os.path.relpath(DUR_SRC, ROOT)
 out["_meta"] = meta
 json.dump(out, open(os.path.join(ROOT, "profiles", f"acq_bound_r{RN}.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))

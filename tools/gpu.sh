@@ -12,6 +12,7 @@
 #   acqab        rocprofv3 kernel stats of the config-2 acquisition: two-launch path, then the
 #                fused correlator at ring depths $RINGS (default "3"); + its FETCH/WRITE bytes
 #   acqpmc4      FETCH / WRITE passes of the config-4 acquisition's correlator kernels -> gpurun_out/traffic_cfg4.json
+#   acqprof1     kernel stats of the config-2 acquisition, passes on one stream -> gpurun_out/acq_onestream_summary.txt
 #   acqpipe      config-2 / config-4 acquisition timing, batches on one stream vs pipelined (tools/acq_only.py)
 #   cfg4         bench --workload cfg4 -> gpurun_out/bench_cfg4.json
 #   cfg5         bench --workload cfg5 -> gpurun_out/bench_cfg5.json
@@ -90,6 +91,11 @@ for step in "$@"; do
       pmc c5_sq3 "$SQ3" python3 "$R/tools/track_only.py" 1000 400 11 32 || exit 1
       python3 tools/pmc_sq.py gpurun_out/cfg5_sq.json gpurun_out/c5_sq1 gpurun_out/c5_sq3 -- "track_run_kernel<11, 3" || exit 1
       rm -f gpurun_out/c5_*/**/*kernel_trace.csv ;;
+    acqprof1)  # rocprofv3 kernel stats of the config-2 acquisition with its two passes in order on one
+      # stream (ACQ_PIPE=1): per-kernel durations free of the default pipeline's overlap (tools/acq_bound.py)
+      ( cd /tmp && export TMPDIR=/tmp && ACQ_PIPE=1 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/acq_onestream" -o run -- python3 "$R/tools/acq_only.py" ) > gpurun_out/acq_onestream.log 2>&1 || { tail -20 gpurun_out/acq_onestream.log; exit 1; }
+      python3 tools/prof_summary.py gpurun_out/acq_onestream > gpurun_out/acq_onestream_summary.txt && head -8 gpurun_out/acq_onestream_summary.txt
+      rm -f gpurun_out/acq_onestream/**/*kernel_trace.csv ;;
     acqpipe)  # split correlator: batches on one stream vs pipelined over two (ACQ_PIPE), cfg2 / cfg4, fp64 / fp32
       for c in 2 4; do for f in "" 1; do for p in 1 2; do
         echo "-- cfg$c fp32=${f:-0} pipe=$p"
