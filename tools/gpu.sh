@@ -105,7 +105,7 @@ for step in "$@"; do
     acqmask)  # config-2 fp64 correlation vs GNSS_OPT_ACQ_PIPE (1 one stream, 2 two streams; PIPES="1 2")
       for p in ${PIPES:-1 2 3 4 5 6}; do
         ACQ_PIPE=$p timeout -k 10 200 python3 tools/acq_only.py > gpurun_out/acqmask_$p.txt 2>&1 \
-          && echo "pipe=$p corr_ms $(grep -o "'acq_corr_ms': [0-9.]*" gpurun_out/acqmask_$p.txt | cut -d' ' -f2 | tr '\n' ' ') $(grep -E '^(fbin|snr)' gpurun_out/acqmask_$p.txt | md5sum | cut -c1-8)" \
+          && echo "pipe=$p corr_ms $(grep -o "'acq_corr_ms': [0-9.]*" gpurun_out/acqmask_$p.txt | cut -d' ' -f2 | tr '\n' ' ') fine_ms $(grep -o "'acq_fine_ms': [0-9.]*" gpurun_out/acqmask_$p.txt | cut -d' ' -f2 | tr '\n' ' ') $(grep -E '^(fbin|snr)' gpurun_out/acqmask_$p.txt | md5sum | cut -c1-8)" \
           || { tail -20 gpurun_out/acqmask_$p.txt; exit 1; }
       done ;;
     probes)  # timing-probe libraries (tools/build_probe.sh $PROBES): fp64 / VALU counts + stamps each
