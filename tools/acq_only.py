@@ -2,7 +2,8 @@
 20 ms) on a device-resident synthetic Opensky record, fp64 correlation (ACQ_FP32=1: the
 fp32 fast mode; ACQ_FUSED=<ring slots>: the fused correlator; ACQ_CFG=4: BASELINE config 4
 instead, the bench's Urban record: Fs 26 MHz, IF 0, 32 PRNs, +-10 kHz / 250 Hz, 10 ms;
-ACQ_PIPE=1|2: the split correlator's batches on one stream / pipelined over two).
+ACQ_PIPE=1|2: the split correlator's batches on one stream / pipelined over two; ACQ_BATCH=n:
+n (bin, PRN) pairs per batch).
 Args: [datalen] [freqNum] (config 2 only). Three calls."""
 import importlib, os, sys, time
 import numpy as np
@@ -16,6 +17,8 @@ ctx.set_acq_precision(not os.environ.get("ACQ_FP32"))  # ACQ_FP32=1: the fp32 fa
 if os.environ.get("ACQ_FUSED"):
     ctx.set_option(pkg.abi.OPT_ACQ_FUSED, 1)
     ctx.set_option(pkg.abi.OPT_ACQ_RING, int(os.environ["ACQ_FUSED"]))
+if os.environ.get("ACQ_BATCH"):  # (bin, PRN) pairs per correlator batch (GNSS_OPT_ACQ_BATCH)
+    ctx.set_option(pkg.abi.OPT_ACQ_BATCH, int(os.environ["ACQ_BATCH"]))
 if os.environ.get("ACQ_PIPE"):
     ctx.set_option(pkg.abi.OPT_ACQ_PIPE, int(os.environ["ACQ_PIPE"]))
 file, signal, acq, track, _, _ = pkg.initParameters()

@@ -91,6 +91,12 @@ for step in "$@"; do
       pmc c5_sq3 "$SQ3" python3 "$R/tools/track_only.py" 1000 400 11 32 || exit 1
       python3 tools/pmc_sq.py gpurun_out/cfg5_sq.json gpurun_out/c5_sq1 gpurun_out/c5_sq3 -- "track_run_kernel<11, 3" || exit 1
       rm -f gpurun_out/c5_*/**/*kernel_trace.csv ;;
+    acqbatch)  # config-2 fp64 correlation vs pairs per batch (BATCHES), pipelined default
+      for b in ${BATCHES:-28 40 55 75 116}; do
+        ACQ_BATCH=$b timeout -k 10 200 python3 tools/acq_only.py > gpurun_out/acqbatch_$b.txt 2>&1 \
+          && echo "batch=$b corr_ms $(grep -o "'acq_corr_ms': [0-9.]*" gpurun_out/acqbatch_$b.txt | cut -d' ' -f2 | tr '\n' ' ') $(grep -E '^(fbin|snr)' gpurun_out/acqbatch_$b.txt | md5sum | cut -c1-8)" \
+          || { tail -20 gpurun_out/acqbatch_$b.txt; exit 1; }
+      done ;;
     acqprof1)  # rocprofv3 kernel stats of the config-2 acquisition with its two passes in order on one
       # stream (ACQ_PIPE=1): per-kernel durations free of the default pipeline's overlap (tools/acq_bound.py)
       ( cd /tmp && export TMPDIR=/tmp && ACQ_PIPE=1 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/acq_onestream" -o run -- python3 "$R/tools/acq_only.py" ) > gpurun_out/acq_onestream.log 2>&1 || { tail -20 gpurun_out/acq_onestream.log; exit 1; }
