@@ -12,9 +12,10 @@ directory name is not a Python identifier).
 from . import abi, synth
 from .sdr import (Context, DeviceRecord, DeviceTrackOutBuffers, StructArray, TrackOutBuffers, acquisition, ca_code, colon,
                   default_context, initParameters, naviDecode_updated, trackingCT, trackingCT_multiCorr,
-                  trackingCT_POS, trackingCT_POS_updated_multicorrelator, trackingVT_run, trackingVT_step, vt_channel)
+                  trackingCT_POS, trackingCT_POS_updated_multicorrelator, trackingVT_POS_updated, trackingVT_run, trackingVT_step,
+                  vt_channel)
 
 __all__ = ["abi", "synth", "Context", "DeviceRecord", "DeviceTrackOutBuffers", "StructArray", "TrackOutBuffers",
            "acquisition", "ca_code", "colon", "default_context", "initParameters", "naviDecode_updated",
-           "trackingCT", "trackingCT_multiCorr", "trackingCT_POS", "trackingCT_POS_updated_multicorrelator", "trackingVT_run", "trackingVT_step",
+           "trackingCT", "trackingCT_multiCorr", "trackingCT_POS", "trackingCT_POS_updated_multicorrelator", "trackingVT_POS_updated", "trackingVT_run", "trackingVT_step",
            "vt_channel"]

@@ -117,7 +117,48 @@ class GnssVtOut(C.Structure):
     _fields_ = [(f, C.c_double) for f in ("E_i", "E_q", "P_i", "P_q", "L_i", "L_q", "carrError", "codeError",
                                           "carrNco", "remChip", "remCarrPhase", "codeFreq", "carrFreq")] + \
                [("numSample", C.c_int64), ("absoluteSample", C.c_int64), ("codedelay", C.c_double),
-                ("CN0", C.c_double), ("cn0_row", C.c_int32), ("status", C.c_int32)]
+                ("CN0", C.c_double), ("cn0_row", C.c_int32), ("status", C.c_int32),
+                ("deltaPr", C.c_double), ("prRate", C.c_double), ("sv_vel", C.c_double * 3)]
+
+
+# the vector half of trackingVT_POS_updated.m (ABI v10)
+VT_MAX_CH = 32
+EPH_SV_FIELDS = ["sqrta", "deltan", "toe", "M0", "ecc", "w", "Cus", "Cuc", "Crs", "Crc", "Cis", "Cic", "i0",
+                 "idot", "omegae", "omegadot", "toc", "af0", "af1", "af2", "TGD"]
+GEO_XYZ2LLH, GEO_LLH2XYZ, GEO_XYZ2ENU, GEO_EROTCORR, GEO_IONO, GEO_TROP = range(6)
+
+
+class GnssEphSv(C.Structure):
+    _fields_ = [(f, C.c_double) for f in EPH_SV_FIELDS]
+
+
+class GnssVtNavCfg(C.Structure):
+    _fields_ = [("cnslxyz", C.c_double * 3), ("ALPHA", C.c_double * 4), ("BETA", C.c_double * 4),
+                ("doy", C.c_double), ("cSpeed", C.c_double), ("Fc", C.c_double)]
+
+
+class GnssVtNav(C.Structure):
+    _fields_ = [("n", C.c_int32), ("pdi", C.c_int32), ("msIndex", C.c_int32), ("counterUptR", C.c_int32),
+                ("counter_r", C.c_int32), ("prn", C.c_int32 * VT_MAX_CH), ("cfg", GnssVtNavCfg),
+                ("Fs", C.c_double), ("IF", C.c_double), ("codeFreqBasis", C.c_double), ("ms", C.c_double),
+                ("cnslxyz", C.c_double * 3), ("total_state", C.c_double * 8), ("state_cov", C.c_double * 64),
+                ("R", C.c_double * (2 * VT_MAX_CH)), ("recordR2", C.c_double * (2 * VT_MAX_CH))] + \
+               [(f, C.c_double * VT_MAX_CH) for f in ("transmitTime", "tot_est_tck", "predictedPr_last",
+                                                     "counter_corr", "ionodel", "tropodel", "el", "az")] + \
+               [("numSample", C.c_int64 * VT_MAX_CH), ("eph", GnssEphSv * VT_MAX_CH)]
+
+
+class GnssVtNavSol(C.Structure):
+    _fields_ = [("localTime", C.c_double)] + \
+               [(f, C.c_double * 3) for f in ("usrPos", "usrVel", "usrPosENU", "usrVelENU", "usrPosLLH")] + \
+               [("clkBias", C.c_double), ("clkDrift", C.c_double), ("state", C.c_double * 8),
+                ("state_cov", C.c_double * 8), ("newZ", C.c_double * (2 * VT_MAX_CH)),
+                ("meas_inno", C.c_double * (2 * VT_MAX_CH)), ("satEA", C.c_double * VT_MAX_CH),
+                ("satAZ", C.c_double * VT_MAX_CH), ("predicted_z", C.c_double * (2 * VT_MAX_CH)),
+                ("satePos", C.c_double * 3), ("sateVel", C.c_double * 3),
+                ("svxyz_pos", (C.c_double * 3) * VT_MAX_CH), ("kalman_gain", (C.c_double * (2 * VT_MAX_CH)) * 8),
+                ("R", C.c_double * (2 * VT_MAX_CH)), ("r_row", C.c_int32),
+                ("reserved", C.c_int32)]
 
 
 class GnssSynthSv(C.Structure):
@@ -183,11 +224,27 @@ PROTOTYPES = {
                                    C.POINTER(GnssVtOut)]),
     "gnss_vt_prepare": (C.c_int, [C.POINTER(GnssSignal), C.c_int32, C.POINTER(GnssVtChan), C.c_double,
                                   C.POINTER(C.c_int32), C.POINTER(C.c_int64)]),
+    "gnss_sv_pos_vel": (C.c_int, [C.POINTER(GnssEphSv), C.c_double, C.POINTER(C.c_double),
+                                  C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                  C.POINTER(C.c_double)]),
+    "gnss_geo": (C.c_int, [C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "gnss_vt_nav_init": (C.c_int, [C.POINTER(GnssVtNavCfg), C.POINTER(GnssSignal), C.c_int32, C.c_int32,
+                                   C.POINTER(C.c_int32), C.POINTER(GnssEphSv), C.POINTER(C.c_double),
+                                   C.POINTER(C.c_double), C.c_double, C.c_double, C.POINTER(C.c_double),
+                                   C.POINTER(GnssVtNav)]),
+    "gnss_vt_nav_predict": (C.c_int, [C.POINTER(GnssVtNav), C.c_int32, C.c_int64, C.POINTER(C.c_double),
+                                      C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "gnss_vt_nav_update": (C.c_int, [C.POINTER(GnssVtNav), C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                     C.POINTER(C.c_double), C.POINTER(GnssVtNavSol)]),
+    "gnss_tracking_vt": (C.c_int, [C.c_void_p, C.POINTER(GnssFile), C.POINTER(GnssSignal), C.POINTER(GnssTrack),
+                                   C.c_int32, C.c_int32, C.POINTER(GnssVtChan), C.POINTER(GnssVtNav),
+                                   C.POINTER(GnssVtOut), C.POINTER(GnssVtNavSol)]),
 }
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libgnss_mi355x.so")
 _lib = None
 _torch_first = False
+LOADED_PATH = None  # the library file the process bound (bench.py digests it)
 
 # gnss_ctx_set_option keys (include/gnss_mi355x.h, ABI v9)
 (OPT_FORCE_SUB, OPT_NO_PERSIST, OPT_FORCE_VPB, OPT_ACQ_ROCFFT, OPT_FINE_ROCFFT, OPT_ACQ_BATCH, OPT_ACQ_FUSED,
@@ -221,11 +278,17 @@ def load(path: str | None = None):
         raise ImportError(f"{p} missing: the HIP extension is not built "
                           "(run `python -c 'import __graft_entry__ as g; g.build()'`)")
     # PyTorch-ROCm ships its own HIP / HSA runtime and finds no GPU if this library's runtime
-    # came up first: callers that hand torch tensors to the library (device-resident outputs,
-    # the RCCL gathers) import torch before the first load; require_torch() checks that.
-    # Everyone else never pays for torch.
+    # came up first, so it is imported here, before the library, whenever it is installed: a
+    # caller may create a Context first and hand tensors over later (device-resident outputs,
+    # the RCCL gathers). require_torch() still checks the order for a library loaded without
+    # torch installed at the time.
     global _torch_first
     if _lib is None:
+        if "torch" not in sys.modules:
+            try:  # PyTorch's runtime first: any later tensor exchange then works
+                import torch  # noqa: F401
+            except ImportError:
+                pass
         _torch_first = "torch" in sys.modules
     lib = C.CDLL(p)
     for name, (res, args) in PROTOTYPES.items():
@@ -235,5 +298,7 @@ def load(path: str | None = None):
         fn.restype = res
         fn.argtypes = args
     if path is None:
+        global LOADED_PATH
         _lib = lib
+        LOADED_PATH = os.path.abspath(p)
     return lib

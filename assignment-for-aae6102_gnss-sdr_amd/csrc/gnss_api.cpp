@@ -471,8 +471,10 @@ int acq_search(gnss_ctx* ctx, const int8_t* blk, const double2* xa, int64_t S, i
         const int target = (int)std::max<int64_t>(1, ((int64_t)1 << 30) / ((int64_t)dl * S * (int64_t)csz));
         const int nbat = (npairs + target - 1) / target;
         int batch = (npairs + nbat - 1) / nbat;
-        if (ctx->opt[GNSS_OPT_ACQ_BATCH] > 0) batch = (int)ctx->opt[GNSS_OPT_ACQ_BATCH];
-        batch = std::min(batch, npairs);
+        // the test hook, clamped before the narrowing (2^32 would become 0)
+        if (ctx->opt[GNSS_OPT_ACQ_BATCH] > 0)
+            batch = (int)std::min<int64_t>(ctx->opt[GNSS_OPT_ACQ_BATCH], (int64_t)npairs);
+        batch = std::max(1, std::min(batch, npairs));
         // Two streams: batch b's row pass (LDS-bound fp64 transforms, reading the intermediate)
         // runs beside batch b+1's column pass (bound by the intermediate's writes), each batch
         // in its own half of a double intermediate; the column pass of b+2 waits for the rows
@@ -497,24 +499,31 @@ int acq_search(gnss_ctx* ctx, const int8_t* blk, const double2* xa, int64_t S, i
             }
             return GNSS_OK;
         }
-        int last = 0;
-        for (int q0 = 0, b = 0; q0 < npairs; q0 += batch, b++) {
-            const int nq = std::min(batch, npairs - q0);
-            const int h = b & 1;
-            V* Ah = A.as<V>() + (size_t)h * abuf;
-            if (b >= 2) HIP_TRY(hipStreamWaitEvent(s_cols, ctx->ev_rows[h], 0));  // rows of b-2 read Ah
-            HIP_TRY(launch_acq_fft_correlate(C, X.as<V>(), S, dl, nb, np, q0, nq, d_twr.as<V>(), d_twc.as<V>(), Ah,
-                                             corr, s_cols, kAcqCols));
-            HIP_TRY(hipEventRecord(ctx->ev_cols[h], s_cols));
-            HIP_TRY(hipStreamWaitEvent(s_rows, ctx->ev_cols[h], 0));
-            HIP_TRY(launch_acq_fft_correlate(C, X.as<V>(), S, dl, nb, np, q0, nq, d_twr.as<V>(), d_twc.as<V>(), Ah,
-                                             corr, s_rows, kAcqRows));
-            HIP_TRY(hipEventRecord(ctx->ev_rows[h], s_rows));
-            last = h;
-        }
-        // the caller's stream owns the result again (stream2 is in order: its last event covers all)
-        HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_rows[last], 0));
-        return GNSS_OK;
+        // A launch error part way leaves row passes queued on stream2 that still write acq.A /
+        // corr: drain it before the error returns, so the next call's pooled buffers are free.
+        auto pipelined = [&]() -> int {
+            int last = 0;
+            for (int q0 = 0, b = 0; q0 < npairs; q0 += batch, b++) {
+                const int nq = std::min(batch, npairs - q0);
+                const int h = b & 1;
+                V* Ah = A.as<V>() + (size_t)h * abuf;
+                if (b >= 2) HIP_TRY(hipStreamWaitEvent(s_cols, ctx->ev_rows[h], 0));  // rows of b-2 read Ah
+                HIP_TRY(launch_acq_fft_correlate(C, X.as<V>(), S, dl, nb, np, q0, nq, d_twr.as<V>(), d_twc.as<V>(),
+                                                 Ah, corr, s_cols, kAcqCols));
+                HIP_TRY(hipEventRecord(ctx->ev_cols[h], s_cols));
+                HIP_TRY(hipStreamWaitEvent(s_rows, ctx->ev_cols[h], 0));
+                HIP_TRY(launch_acq_fft_correlate(C, X.as<V>(), S, dl, nb, np, q0, nq, d_twr.as<V>(), d_twc.as<V>(),
+                                                 Ah, corr, s_rows, kAcqRows));
+                HIP_TRY(hipEventRecord(ctx->ev_rows[h], s_rows));
+                last = h;
+            }
+            // the caller's stream owns the result again (stream2 is in order: its last event covers all)
+            HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_rows[last], 0));
+            return GNSS_OK;
+        };
+        const int pst = pipelined();
+        if (pst != GNSS_OK) (void)hipStreamSynchronize(s_rows);
+        return pst;
     }
     // batched rocFFT (sample counts that are not P x 2000)
     *perm = 0;
@@ -1825,6 +1834,163 @@ int gnss_tracking_vt_step(gnss_ctx* ctx, const gnss_file* file, const gnss_signa
                           gnss_vt_out* out)
 {
     return gnss_tracking_vt_run(ctx, file, sg, tr, pdi, n, 1, chans, codeFreq_new, out);
+}
+
+// trackingVT_POS_updated.m:157-476, the whole EKF-driven loop: per step, each channel's read
+// size (:164) and predicted code frequency (:180-227, gnss_vt_nav_predict, host), the
+// correlations and scalar ends of all channels in ONE launch of the VT kernel (the channel
+// states stay in HBM between steps), then the EKF (:357-467, gnss_vt_nav_update, host).
+int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg, const gnss_track* tr, int32_t n,
+                     int32_t nsteps, gnss_vt_chan* chans, gnss_vt_nav* nav, gnss_vt_out* out, gnss_vt_navsol* sol)
+{
+    if (!ctx || !file || !sg || !tr || !chans || !nav || !out || n < 1 || n != nav->n || nsteps < 0 ||
+        !(sg->Fs > 0) || !(sg->codeFreqBasis > 0) || sg->Fs != nav->Fs)
+        return fail(ctx, GNSS_EARG, "bad arguments (n must equal nav->n, signal as at gnss_vt_nav_init)");
+    ctx->err.clear();
+    ctx->timing = gnss_timing{};
+    if (nsteps == 0) return GNSS_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    const int pdi = nav->pdi;
+    const int prec = file->dataPrecision, dtyp = file->dataType;
+    if (!((prec == 1 && (dtyp == 1 || dtyp == 2)) || (prec == 2 && dtyp == 2)))
+        return fail(ctx, GNSS_EARG, "vector tracking: int8 I/Q, int8 real or int16 I/Q records");
+    const int bps = prec * dtyp;
+    const int64_t flen = file_length(file);
+    if (flen < 0) return fail(ctx, GNSS_EIO, "cannot open IF record");
+    for (int i = 0; i < n; i++) {
+        if (chans[i].prn != nav->prn[i]) return fail(ctx, GNSS_EARG, "chans[i].prn != nav->prn[i]");
+        if (chans[i].file_ptr < 0 || chans[i].file_ptr % bps) return fail(ctx, GNSS_EARG, "file_ptr");
+        if (chans[i].index_int < 0 || chans[i].index_int > 19 || chans[i].snrIndex < 1)
+            return fail(ctx, GNSS_EARG, "C/N0 state (index_int 0..19, snrIndex >= 1)");
+        if (!(chans[i].codeFreq > 0)) return fail(ctx, GNSS_EARG, "code frequency must be positive");
+    }
+    // The IF window: the steps' reads are sized by code frequencies the EKF has not predicted
+    // yet, so a window is staged for `span` steps at half the nominal code rate (twice the
+    // nominal read) and re-staged when a read would leave it. A resident record is used as is.
+    const int64_t nominal = (int64_t)std::ceil(sg->codelength * pdi / (sg->codeFreqBasis / sg->Fs));
+    const int64_t span = std::min<int64_t>(nsteps, 2000);
+    IfWindow w;
+    auto restage = [&](int64_t lo) -> int {
+        const int64_t hi = lo + (span * 2 * nominal + 64) * bps;
+        w.own.release();
+        w.ptr = nullptr;
+        w.base = w.len = 0;
+        return stage_window(ctx, file, lo, std::min(hi, flen), w);
+    };
+    int64_t lo0 = INT64_MAX;
+    for (int i = 0; i < n; i++) lo0 = std::min(lo0, chans[i].file_ptr);
+    int st = restage(lo0);
+    if (st) return st;
+    std::vector<unsigned> cab((size_t)n * 32);
+    for (int i = 0; i < n; i++) ca_bits(chans[i].prn, &cab[(size_t)i * 32]);
+    DevBuf d_chan, d_cf, d_out, d_ca;
+    HIP_TRY(d_chan.alloc(ctx, "vt.chan", sizeof(gnss_vt_chan) * (size_t)n));
+    HIP_TRY(d_cf.alloc(ctx, "vt.cf", sizeof(double) * (size_t)n));
+    HIP_TRY(d_out.alloc(ctx, "vt.out", sizeof(gnss_vt_out) * (size_t)n));
+    HIP_TRY(d_ca.alloc(ctx, "vt.ca", sizeof(unsigned) * cab.size()));
+    double* h_cf = pinned_buffer<double>(ctx, "vt.cf", (size_t)n);
+    gnss_vt_out* h_out = pinned_buffer<gnss_vt_out>(ctx, "vt.out", (size_t)n);
+    if (!h_cf || !h_out) return fail(ctx, GNSS_EDEVICE, "pinned VT step buffers");
+    HIP_TRY(hipMemcpyAsync(d_chan.p, chans, sizeof(gnss_vt_chan) * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(d_ca.p, cab.data(), sizeof(unsigned) * cab.size(), hipMemcpyHostToDevice, ctx->stream));
+    double t1, t2;
+    calc_loop_coef(tr->PLLBW, tr->PLLDamp, tr->PLLGain, t1, t2);
+    VtRunArgs A{};
+    A.file_len = flen;
+    A.chans = d_chan.as<gnss_vt_chan>();
+    A.codeFreq = d_cf.as<double>();
+    A.out = d_out.as<gnss_vt_out>();
+    A.ca_bits = d_ca.as<unsigned>();
+    A.Fs = sg->Fs;
+    A.ms = sg->ms;
+    A.codelength = sg->codelength;
+    A.tau1carr = t1;
+    A.tau2carr = t2;
+    A.n = n;
+    A.nsteps = 1;
+    A.pdi = pdi;
+    A.prec = prec;
+    A.dtype = dtyp;
+    // the host's view of what sizes the next read (:164): remChip / codeFreq / file_ptr of the
+    // last step, from the records the kernel returns
+    std::vector<double> remChip(n), cf_old(n), codeError(n), carrFreq(n), cf_new(n);
+    std::vector<int64_t> fptr(n);
+    for (int i = 0; i < n; i++) {
+        remChip[i] = chans[i].remChip;
+        cf_old[i] = chans[i].codeFreq;
+        fptr[i] = chans[i].file_ptr;
+    }
+    Events ev;
+    double kernel_ms = 0;
+    int result = GNSS_OK;
+    for (int s = 0; s < nsteps && result == GNSS_OK; s++) {
+        int64_t need_lo = INT64_MAX, need_hi = 0;
+        for (int i = 0; i < n; i++) {
+            const VtPrep p = vt_prepare(sg->Fs, sg->codelength, pdi, remChip[i], cf_old[i], cf_old[i]);
+            if (p.n < 1) {  // ceil(...) <= 0: an index MATLAB rejects
+                result = fail(ctx, GNSS_EINDEX, "step %d channel %d: read size %lld", s + 1, i, (long long)p.n);
+                break;
+            }
+            double cf = cf_old[i], dpr = 0, vel[3];
+            st = gnss_vt_nav_predict(nav, i, p.n, &cf, &dpr, vel);
+            if (st) {
+                result = fail(ctx, st, "step %d channel %d: svPosVel / trop_UNB3 failed", s + 1, i);
+                break;
+            }
+            cf_new[i] = cf;
+            h_cf[i] = cf;
+            gnss_vt_out& o = out[(size_t)s * n + i];
+            o.deltaPr = dpr;
+            o.prRate = 0;
+            for (int k = 0; k < 3; k++) o.sv_vel[k] = vel[k];
+            need_lo = std::min(need_lo, fptr[i]);
+            need_hi = std::max(need_hi, fptr[i] + p.n * bps);
+        }
+        if (result) break;
+        if (!file->dev_data && (need_lo < w.base || need_hi > w.base + w.len) && need_hi <= flen) {
+            HIP_TRY(hipStreamSynchronize(ctx->stream));
+            st = restage(need_lo);
+            if (st) return st;
+        }
+        A.rec = reinterpret_cast<const uint8_t*>(w.ptr);
+        A.base = w.base;
+        A.len = w.len;
+        HIP_TRY(hipMemcpyAsync(d_cf.p, h_cf, sizeof(double) * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipEventRecord(ev.a, ctx->stream));
+        HIP_TRY(launch_vt_run(A, ctx->stream));
+        HIP_TRY(hipEventRecord(ev.b, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(h_out, d_out.p, sizeof(gnss_vt_out) * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        kernel_ms += ev.ms();
+        for (int i = 0; i < n; i++) {
+            gnss_vt_out& o = out[(size_t)s * n + i];
+            const gnss_vt_out& h = h_out[i];
+            const double dpr = o.deltaPr, vel[3] = {o.sv_vel[0], o.sv_vel[1], o.sv_vel[2]};
+            o = h;
+            o.deltaPr = dpr;
+            o.prRate = 0;
+            for (int k = 0; k < 3; k++) o.sv_vel[k] = vel[k];
+            if (h.status) {
+                if (!result) result = fail(ctx, h.status, "step %d channel %d stopped (replica index / read past EOF)",
+                                           s + 1, i);
+                continue;
+            }
+            ctx->timing.track_channel_samples += h.numSample;
+            remChip[i] = h.remChip;
+            cf_old[i] = h.codeFreq;
+            fptr[i] = h.absoluteSample;
+            codeError[i] = h.codeError;
+            carrFreq[i] = h.carrFreq;
+        }
+        ctx->timing.track_launches += 1;
+        if (result) break;
+        st = gnss_vt_nav_update(nav, codeError.data(), cf_new.data(), carrFreq.data(), sol ? sol + s : nullptr);
+        if (st) result = fail(ctx, st, "step %d: navigation update failed (singular innovation covariance)", s + 1);
+    }
+    HIP_TRY(hipMemcpyAsync(chans, d_chan.p, sizeof(gnss_vt_chan) * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    ctx->timing.track_kernel_ms = kernel_ms;
+    return result;
 }
 
 int gnss_ca_code(int prn, int8_t* out1023)

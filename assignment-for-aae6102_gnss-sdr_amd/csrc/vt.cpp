@@ -44,6 +44,8 @@ int gnss_vt_nco_step(const gnss_signal* sg, const gnss_track* tr, int32_t pdi, g
                      double codeFreq_new, double sumI, double sumQ, gnss_vt_out* out)
 {
     if (!tr || !out || !c) return GNSS_EARG;
+    // the C/N0 window index vt_finish writes Zk[index_int] at (:294-295)
+    if (c->index_int < 0 || c->index_int > 19 || c->snrIndex < 1) return GNSS_EARG;
     int32_t code[3];
     int64_t n = 0;
     const int st = gnss_vt_prepare(sg, pdi, c, codeFreq_new, code, &n);

@@ -51,6 +51,8 @@ __global__ __launch_bounds__(kVtRun) void vt_run_kernel(VtRunArgs a)
     for (int s = 0; s < a.nsteps; s++) {
         gnss_vt_out* o = a.out + (int64_t)s * a.n + ch;
         const double cf = a.codeFreq[(int64_t)s * a.n + ch];
+        // every wave has read the last step's s_bad / s_p before lane 0 rewrites them
+        __syncthreads();
         if (tid == 0) {
             VtPrep p = vt_prepare(a.Fs, a.codelength, a.pdi, s_c.remChip, s_c.codeFreq, cf);
             int bad = !(cf > 0) ? GNSS_EARG : p.bad;

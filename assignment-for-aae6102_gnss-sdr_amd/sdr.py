@@ -686,3 +686,159 @@ def correlate_step(file, signal, prn, pdi, remChip, codeFreq, carrierFreq, remPh
         taps.ctypes.data_as(C.POINTER(C.c_double)), sums.ctypes.data_as(C.POINTER(C.c_double)),
         C.byref(ns)))
     return sums, ns.value
+
+
+# ---------------------------------------------------------------------------
+# trackingVT_POS_updated.m: the EKF-driven vector-tracking loop
+# ---------------------------------------------------------------------------
+# global ALPHA BETA of initParameters.m:29-31 (the broadcast iono model, "From RINEX file")
+ALPHA = [9.3132e-09, 1.4901e-08, -5.9605e-08, -1.1921e-07]
+BETA = [8.8064e+04, 4.9152e+04, -1.3107e+05, -3.2768e+05]
+
+VT_FIELDS = ["E_i", "E_q", "P_i", "P_q", "L_i", "L_q", "carrError", "codeError", "remChip", "remCarrPhase",
+             "codeFreq", "carrFreq", "carrNco", "absoluteSample", "codedelay", "deltaPr", "prRate"]
+
+
+def _struct_of(s, prn):
+    """eph(prn) / TckResultCT(prn): a StructArray (or any callable), a dict keyed by PRN, or a
+    sequence indexed like the MATLAB struct array (prn - 1)."""
+    if callable(s):
+        return s(prn)
+    if isinstance(s, dict):
+        return s[int(prn)]
+    return s[int(prn) - 1]
+
+
+def _first(x):
+    return float(np.atleast_1d(np.asarray(x, dtype=np.float64)).ravel()[0])
+
+
+def _vec1(v, prn):
+    """sbf.nav1(prn): MATLAB 1-based vector indexing."""
+    return _first(np.asarray(v).ravel()[int(prn) - 1])
+
+
+def eph_sv(eph, prn, eph_idx=1):
+    """The gnss_eph_sv of ephemeris(prn).*(eph_idx) (svPosVel.m:23-44; the VT loop passes
+    eph_idx = 1, trackingVT_POS_updated.m:36)."""
+    e = _struct_of(eph, prn)
+    out = abi.GnssEphSv()
+    for f in abi.EPH_SV_FIELDS:
+        setattr(out, f, float(np.atleast_1d(np.asarray(getattr(e, f), dtype=np.float64)).ravel()[eph_idx - 1]))
+    return out
+
+
+def trackingVT_POS_updated(file, signal, track, cmn, solu, Acquired, cnslxyz, eph, sbf, TckResult_Eph,
+                           TckResultCT, navSolutionsCT, *, ctx: Context | None = None, ALPHA_=None,
+                           BETA_=None, nsteps: int | None = None, return_cn0: bool = False):
+    """trackingVT_POS_updated.m:1-476 -> (TckResultVT, navSolutionsVT[, CN0_VT]).
+
+    The loop of track.msToProcessVT / track.pdi steps: per step and channel the read size (:164)
+    and the code frequency predicted from the EKF's receiver state (:180-227; host,
+    gnss_vt_nav_predict), the E/P/L correlations, NCO, PLL and C/N0 of every channel in one
+    GPU launch (:229-352), then the 8-state EKF on the code and carrier measurements
+    (:357-467; host, gnss_vt_nav_update) -- all inside gnss_tracking_vt.
+
+    Initialisation as the reference: the EKF state from navSolutionsCT row
+    file.skiptimeVT / solu.navSolPeriod (:66-70), the channels from TckResultCT(prn) at
+    msStartTckVT (:100-124: built from the LAST channel's sbf.nav1 / eph.sfb(1) and capped at
+    that channel's record length, as the reference's loop variable leaves them),
+    transmitTimeVT = navSolutionsCT.timeTransmit(1, :) (:131). TckResult_Eph only feeds
+    sampleStart (:89-99), which no output reads; it is index-checked like MATLAB when given
+    (the reference ships none: None skips the check). ALPHA_ / BETA_ default to
+    initParameters.m's globals. nsteps overrides datalength / pdi (a shorter run).
+
+    TckResultVT(prn) carries the fields of :324-352 (sv_vel as nsteps x 3; amplitude,
+    navi_data, navi_dataL035 are the constant 0 the reference records); navSolutionsVT the
+    rows of :418-436 (svxyz_pos n x 3 x nsteps, kalman_gain 8 x 2n x nsteps as the
+    reference's 3-D arrays) and R (:466). A channel error MATLAB raises on (a replica index
+    out of range, a read past the end of the record) raises GnssError.
+    """
+    ctx = ctx or default_context()
+    sv = [int(p) for p in np.atleast_1d(Acquired.sv)]
+    n = len(sv)
+    if not 1 <= n <= abi.VT_MAX_CH:
+        raise ValueError(f"vector tracking takes 1..{abi.VT_MAX_CH} channels")
+    pdi = int(track.pdi)
+    if nsteps is None:
+        nsteps = int(track.msToProcessVT) // pdi
+    row = file.skiptimeVT / solu.navSolPeriod
+    if row != int(row) or row < 1:
+        raise IndexError("file.skiptimeVT / solu.navSolPeriod must be a positive integer row (:66)")
+    row = int(row)
+    # :89-107
+    if TckResult_Eph is not None:
+        for p in sv:
+            k = int(_vec1(sbf.nav1, p) + _first(_struct_of(eph, p).sfb) * 20)
+            np.asarray(_struct_of(TckResult_Eph, p).absoluteSample).ravel()[k - 1]  # MATLAB's index check
+    last = sv[-1]
+    ms = int(_vec1(sbf.nav1, last) + _first(_struct_of(eph, last).sfb) * 20 + row)
+    ms = min(ms, np.asarray(_struct_of(TckResultCT, last).codeFreq).size)
+    chans = []
+    for p in sv:  # :109-132
+        t = _struct_of(TckResultCT, p)
+        g = lambda f: float(np.asarray(getattr(t, f), dtype=np.float64).ravel()[ms - 1])
+        c = vt_channel(p, int(g("absoluteSample")), g("remChip"), g("remCarrPhase"), g("codeFreq"),
+                       g("carrFreq"), g("carrFreq"), g("carrFreq") - g("carrFreq"), g("carrError"))
+        chans.append(c)
+    arr = (abi.GnssVtChan * n)(*chans)
+    cfg = abi.GnssVtNavCfg()
+    cfg.cnslxyz[:] = [float(x) for x in np.asarray(cnslxyz, dtype=np.float64).ravel()[:3]]
+    cfg.ALPHA[:] = [float(x) for x in (ALPHA_ if ALPHA_ is not None else ALPHA)]
+    cfg.BETA[:] = [float(x) for x in (BETA_ if BETA_ is not None else BETA)]
+    cfg.doy, cfg.cSpeed, cfg.Fc = float(cmn.doy), float(cmn.cSpeed), float(signal.Fc)
+    ephs = (abi.GnssEphSv * n)(*[eph_sv(eph, p) for p in sv])
+    ns = navSolutionsCT
+    pos = (C.c_double * 3)(*np.asarray(ns.usrPos, dtype=np.float64)[row - 1, :3])
+    vel = (C.c_double * 3)(*np.asarray(ns.usrVel, dtype=np.float64)[row - 1, :3])
+    tt = (C.c_double * n)(*np.asarray(ns.timeTransmit, dtype=np.float64).reshape(-1, n)[0])
+    s = to_c_signal(signal)
+    nav = abi.GnssVtNav()
+    st = ctx.lib.gnss_vt_nav_init(C.byref(cfg), C.byref(s), pdi, n, (C.c_int32 * n)(*sv), ephs, pos, vel,
+                                  _vec1(ns.clkBias, row), _vec1(ns.clkDrift, row), tt, C.byref(nav))
+    if st != abi.OK:
+        raise abi.GnssError(st, "gnss_vt_nav_init")
+    outs = (abi.GnssVtOut * (nsteps * n))()
+    sols = (abi.GnssVtNavSol * nsteps)()
+    f, keep = to_c_file(file)
+    t, keep2 = to_c_track(track)
+    st = ctx.lib.gnss_tracking_vt(ctx.h, C.byref(f), C.byref(s), C.byref(t), n, nsteps, arr, C.byref(nav), outs,
+                                  sols)
+    ctx.check(st)
+    R = np.ctypeslib.as_array(outs).reshape(nsteps, n)  # a structured view of the records
+    entries = {}
+    for i, p in enumerate(sv):
+        e = SimpleNamespace(**{k: R[k][:, i].astype(np.float64) for k in VT_FIELDS})
+        e.sv_vel = R["sv_vel"][:, i].copy()
+        for k in ("amplitude", "navi_data", "navi_dataL035"):
+            setattr(e, k, np.zeros(nsteps))
+        entries[p] = e
+    nsol = _navsol_arrays(sols, nsteps, n)
+    TckResultVT = StructArray(entries)
+    if return_cn0:
+        rows = int(R["cn0_row"].max()) if nsteps else 0
+        cn0 = np.zeros((rows, n))
+        for i in range(n):
+            m = R["cn0_row"][:, i] > 0
+            cn0[R["cn0_row"][:, i][m] - 1, i] = R["CN0"][:, i][m]
+        return TckResultVT, nsol, cn0
+    return TckResultVT, nsol
+
+
+def _navsol_arrays(sols, nsteps, n):
+    """navSolutionsVT (:418-436, :466) from the gnss_vt_navsol rows."""
+    N = 2 * n
+    S = np.ctypeslib.as_array(sols).reshape(nsteps)
+    out = SimpleNamespace(**{k: S[k].copy() for k in ("localTime", "clkBias", "clkDrift")})
+    for k in ("usrPos", "usrVel", "usrPosENU", "usrVelENU", "usrPosLLH", "satePos", "sateVel", "state",
+              "state_cov"):
+        setattr(out, k, S[k].copy())
+    for k in ("meas_inno", "newZ", "predicted_z"):
+        setattr(out, k, S[k][:, :N].copy())
+    for k in ("satEA", "satAZ"):
+        setattr(out, k, S[k][:, :n].copy())
+    out.svxyz_pos = np.moveaxis(S["svxyz_pos"][:, :n], 0, -1).copy()          # n x 3 x nsteps
+    out.kalman_gain = np.moveaxis(S["kalman_gain"][:, :, :N], 0, -1).copy()   # 8 x 2n x nsteps
+    out.R = S["R"][S["r_row"] > 0][:, :N].copy()
+    out.record_correction = np.zeros((nsteps, n))  # correction(svindex) = 0 (:128, :469)
+    return out

@@ -249,7 +249,7 @@ def run_cfg5(args, rank, world, local, dist, ctx):
             "config": {"workload": f"trackingCT cfg5 (32 ch, 11 taps -0.5:0.1:0.5, 1000 ms @1ms + "
                                    f"{args.n10_cfg5} ms @10ms)", "parallelism": f"channels x{world}",
                        "channels_per_rank": len(mine)},
-            "code": {"src_digest": SRC_DIGEST, "git_commit": srcdigest.head_commit()},
+            "code": code_stamp(),
             "roofline": roof, "cpu_baseline": cpu}
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -326,7 +326,7 @@ def run_cfg4(args, rank, world, local, dist, ctx):
             "config": {"workload": "acquisition cfg4 (32 PRN, +-10kHz/250Hz, 10 ms, L 10)",
                        "parallelism": f"PRNs x{world}", "prns_per_rank": len(mine)},
             "acquired": [int(x) for x in A.sv], "acq_ms_rank0": round(ta["acq_ms"], 3),
-            "code": {"src_digest": SRC_DIGEST, "git_commit": srcdigest.head_commit()},
+            "code": code_stamp(),
             "roofline": roof, "cpu_baseline": cpu}
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -526,7 +526,7 @@ def main():
         # round's separate passes, tools/acq_bound.py; a PMC pass cannot run in this process)
         "acq_kernel_bounds": acq_bounds(),
         "acq_fp32_fast_mode": fast,
-        "code": {"src_digest": SRC_DIGEST, "git_commit": srcdigest.head_commit()},
+        "code": code_stamp(),
         "cpu_baseline": cpu,
     }
     if rank == 0:
@@ -585,10 +585,11 @@ def cpu_baseline_cfg4(file, signal, acq, dev, prns, S):
         return float(np.median(r))
 
     one = leg([prns[0]], 1)
-    many = leg(list(prns), len(prns))
+    nt = quota_threads(len(prns))
+    many = leg(list(prns), nt)
     model, ncpu = host_cpu()
-    return {"value": round(many / 1e6, 4), "unit": "Msamples/s", "cores": len(prns), "kind": "port",
-            "sample": f"oracle/ C fp64 restatement, acquisition of the {len(prns)} PRNs (one thread each) over "
+    return {"value": round(many / 1e6, 4), "unit": "Msamples/s", "cores": nt, "kind": "port",
+            "sample": f"oracle/ C fp64 restatement, acquisition of the {len(prns)} PRNs on {nt} threads over "
                       f"{a1.freqNum} bins x {a1.datalen} ms + fine FFT (median of 3)",
             "one_thread": {"value": round(one / 1e6, 4), "sample": "1 PRN, same grid"},
             "cpu_quota": cpu_quota(), "host_cpu": model, "nproc": ncpu}
@@ -620,11 +621,12 @@ def cpu_baseline_cfg5(file, signal, track, A, taps, dev):
 
     one = leg(1, 1)
     nall = len(A.sv)
-    many = leg(nall, nall)
+    nt = quota_threads(nall)
+    many = leg(nall, nt)
     model, ncpu = host_cpu()
-    return {"value": round(many / 1e6, 4), "unit": "Msamples/s", "cores": nall, "kind": "port",
+    return {"value": round(many / 1e6, 4), "unit": "Msamples/s", "cores": nt, "kind": "port",
             "sample": f"oracle/ C fp64 restatement, trackingCT with 11 taps, {nall} channels x (1000 ms @1ms "
-                      f"+ {n10s} ms @10ms) on {nall} threads (median of 3)",
+                      f"+ {n10s} ms @10ms) on {nt} threads (median of 3)",
             "one_thread": {"value": round(one / 1e6, 4), "sample": "1 channel, same length"},
             "cpu_quota": cpu_quota(), "host_cpu": model, "nproc": ncpu}
 
@@ -661,10 +663,10 @@ def cpu_baseline(file, signal, acq, track, A, dev, args, ta, tt):
         ra, rt = [], []
         for _ in range(reps):
             t = time.perf_counter()
-            po.acquisition(f2, signal, a1, prn_list=prn_list, nthreads=nprn)
+            po.acquisition(f2, signal, a1, prn_list=prn_list, nthreads=quota_threads(nprn))
             ra.append(len(prn_list) * a1.freqNum * a1.datalen * S / (time.perf_counter() - t))
             t = time.perf_counter()
-            po.trackingCT(f2, signal, tr, A1, nthreads=nch)
+            po.trackingCT(f2, signal, tr, A1, nthreads=quota_threads(nch))
             rt.append(nch * (1000 + n10s) * S / (time.perf_counter() - t))
         r_acq, r_trk = float(np.median(ra)), float(np.median(rt))
         return r_acq, r_trk, (U_acq + U_trk) / (U_acq / r_acq + U_trk / r_trk)
@@ -690,12 +692,13 @@ def cpu_baseline(file, signal, acq, track, A, dev, args, ta, tt):
     except Exception:
         pass
     model, ncpu = host_cpu()
-    return {"value": round(v_n / 1e6, 4), "unit": "Msamples/s", "cores": n_prn, "kind": "port",
-            "sample": f"oracle/ C fp64 restatement (median of 3): acquisition of the {n_prn} PRNs (one thread "
-                      f"each) over {a1.freqNum} bins x {a1.datalen} ms + fine FFT, trackingCT of the {n_ch} "
-                      f"channels (one thread each) 1000 ms @1ms (+phase-B rerun) + {n10s} ms @10ms; per-unit "
+    th_a, th_t = quota_threads(n_prn), quota_threads(n_ch)
+    return {"value": round(v_n / 1e6, 4), "unit": "Msamples/s", "cores": max(th_a, th_t), "kind": "port",
+            "sample": f"oracle/ C fp64 restatement (median of 3): acquisition of the {n_prn} PRNs ({th_a} "
+                      f"threads) over {a1.freqNum} bins x {a1.datalen} ms + fine FFT, trackingCT of the {n_ch} "
+                      f"channels ({th_t} threads) 1000 ms @1ms (+phase-B rerun) + {n10s} ms @10ms; per-unit "
                       "rates extrapolated to the GPU step's unit mix",
-            "threads": {"acquisition": n_prn, "tracking": n_ch}, "cpu_quota": cpu_quota(),
+            "threads": {"acquisition": th_a, "tracking": th_t}, "cpu_quota": cpu_quota(),
             "one_thread": {"value": round(v_1 / 1e6, 4), "acq_Msamples_s": round(a_1 / 1e6, 4),
                            "track_Msamples_s": round(t_1 / 1e6, 4), "sample": "1 PRN, 1 channel, same lengths"},
             "all_units": {"value": round(v_n / 1e6, 4), "acq_Msamples_s": round(a_n / 1e6, 4),
@@ -705,6 +708,23 @@ def cpu_baseline(file, signal, acq, track, A, dev, args, ta, tt):
                                   "threads": 1},
             "host_cpu": model, "nproc": ncpu,
             "label": "CPU restatement of acquisition.m / trackingCT.m (MATLAB itself is absent)"}
+
+
+def code_stamp():
+    """What the line was measured with: the sources' digest, the commit (git where the tree has
+    .git, else .head_sha; its source named), and the sha256 of the library file this process
+    actually loaded."""
+    lib = pkg.abi.LOADED_PATH
+    return {"src_digest": SRC_DIGEST, "git_commit": srcdigest.head_commit(),
+            "git_commit_source": srcdigest.head_commit_source(),
+            "lib": os.path.relpath(lib, ROOT) if lib else None,
+            "lib_sha256": srcdigest.file_digest(lib) if lib else None}
+
+
+def quota_threads(units):
+    """Threads for a CPU leg of `units` independent units: one per unit, capped at the CPU
+    quota (32 threads on a 16-CPU share ran oversubscribed under a 32-core label)."""
+    return max(1, min(int(units), int(cpu_quota())))
 
 
 def cpu_quota():

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define GNSS_ABI_VERSION 9
+#define GNSS_ABI_VERSION 10
 
 /* ---- status codes (SURVEY §8b "Error conventions") --------------------- */
 #define GNSS_OK         0
@@ -406,6 +406,10 @@ typedef struct gnss_vt_out {
     double  CN0;            /* CN0_VT(cn0_row, svindex) when cn0_row > 0 (:301)           */
     int32_t cn0_row;        /* 1-based row written by this step, 0: none                  */
     int32_t status;         /* GNSS_OK, or the channel's error at this step (vt_run)      */
+    /* ABI v10, written by gnss_tracking_vt (the vector half; 0 from vt_run / vt_step):     */
+    double  deltaPr;        /* TckResultVT(prn).deltaPr(msIndex) (:221,351), m/s          */
+    double  prRate;         /* TckResultVT(prn).prRate: never assigned in the loop, 0 (:142) */
+    double  sv_vel[3];      /* TckResultVT(prn).sv_vel(msIndex,:) (:185,346), m/s ECEF     */
 } gnss_vt_out;
 
 /* nsteps steps of the n channels in ONE launch (one workgroup per channel loops over the
@@ -436,6 +440,146 @@ int gnss_vt_nco_step(const gnss_signal *signal, const gnss_track *track, int32_t
  * chip values (+-1) the quirk multiplies the sums by, *numSample = ceil(...) (:161). */
 int gnss_vt_prepare(const gnss_signal *signal, int32_t pdi, const gnss_vt_chan *chan,
                     double codeFreq_new, int32_t code_out[3], int64_t *numSample);
+
+/* ---- trackingVT_POS_updated.m, the vector half (ABI v10) -------------
+ * The EKF that drives the VT loop's code NCOs: per step and channel, the satellite position
+ * at the block's transmit time (svPosVel.m), the iono / tropo corrections every 0.1 s
+ * (ionocorr.m, trop_UNB3.m), the predicted pseudorange with the earth-rotation correction
+ * (erotcorr.m) and from it the code frequency (:180-227); after the step's correlations the
+ * 8-state EKF (position, velocity, clock bias, clock drift) on the 2n code and carrier
+ * measurements (:357-442) and the adaptive measurement noise (:444-467). Host C++ (fp64 with
+ * MATLAB's operation order, -ffp-contract=off); libm's sin / cos / atan2 / pow and MATLAB's
+ * BLAS-backed matrix products and inv() round differently in the last place, so the values
+ * match the reference within the ulp bounds stated in tests/test_vt_nav_kat.py. */
+#define GNSS_VT_MAX_CH 32
+
+/* ephemeris(prn).*(eph_idx) -- the fields svPosVel.m:23-44 reads (eph_idx = 1, :36). */
+typedef struct gnss_eph_sv {
+    double sqrta, deltan, toe, M0, ecc, w, Cus, Cuc, Crs, Crc, Cis, Cic, i0, idot, omegae, omegadot;
+    double toc, af0, af1, af2, TGD;
+} gnss_eph_sv;
+
+/* The inputs of the vector half beyond the tracking structs: cnslxyz, the iono model
+ * (initParameters.m:29-31), cmn.doy / cmn.cSpeed, signal.Fc. */
+typedef struct gnss_vt_nav_cfg {
+    double cnslxyz[3]; /* the cnslxyz argument (SDR_main.m:66: llh2xyz(solu.iniPos)), ECEF m:
+                          the ionocorr user position (:200) and the navSolutionsVT ENU
+                          origin (:407-415)                                                  */
+    double ALPHA[4];   /* global ALPHA, BETA: broadcast iono model (initParameters.m:29-30)  */
+    double BETA[4];
+    double doy;        /* cmn.doy (trop_UNB3, :201)                                          */
+    double cSpeed;     /* cmn.cSpeed, m/s                                                    */
+    double Fc;         /* signal.Fc, Hz (the carrier's pseudorange rate, :380)               */
+} gnss_vt_nav_cfg;
+
+/* The loop's navigation state (all of trackingVT_POS_updated.m's cross-step variables other
+ * than the channels' NCO state, which is gnss_vt_chan). Caller-allocated POD: init fills it,
+ * predict / update advance it; it may be copied (a checkpoint) between steps. */
+typedef struct gnss_vt_nav {
+    int32_t n, pdi;
+    int32_t msIndex;            /* the step being run: 1-based, advanced by update        */
+    int32_t counterUptR, counter_r;
+    int32_t prn[GNSS_VT_MAX_CH];
+    gnss_vt_nav_cfg cfg;
+    double  Fs, IF, codeFreqBasis, ms;
+    double  cnslxyz[3];
+    double  total_state[8];     /* [estPos estVel clkBias clkDrift] (:70, :400, :440)     */
+    double  state_cov[64];      /* row-major 8 x 8 (:49, :391, :398)                      */
+    double  R[2 * GNSS_VT_MAX_CH];     /* diag(mesurement_noise) (:55-56, :447-462)      */
+    double  recordR2[2 * GNSS_VT_MAX_CH]; /* sum(recordR.^2) over the rows since the last
+                                             noise update (:395, :446)                    */
+    double  transmitTime[GNSS_VT_MAX_CH];  /* transmitTimeVT (:131, :181)                 */
+    double  tot_est_tck[GNSS_VT_MAX_CH];   /* this step's (:182)                          */
+    double  predictedPr_last[GNSS_VT_MAX_CH];
+    double  counter_corr[GNSS_VT_MAX_CH];  /* (:86, :189-204)                             */
+    double  ionodel[GNSS_VT_MAX_CH], tropodel[GNSS_VT_MAX_CH];
+    double  el[GNSS_VT_MAX_CH], az[GNSS_VT_MAX_CH];   /* degrees (:195-196)               */
+    int64_t numSample[GNSS_VT_MAX_CH];     /* this step's reads (:164)                    */
+    gnss_eph_sv eph[GNSS_VT_MAX_CH];
+} gnss_vt_nav;
+
+/* navSolutionsVT.*(msIndex,:) of one step (:418-436). The 2n-long rows hold the code
+ * measurements (channels 0..n-1) then the carrier ones (n..2n-1). */
+typedef struct gnss_vt_navsol {
+    double localTime;
+    double usrPos[3], usrVel[3];
+    double usrPosENU[3], usrVelENU[3], usrPosLLH[3];   /* LLH: degrees, degrees, m       */
+    double clkBias, clkDrift;
+    double state[8];              /* error_state after the update (:428)                  */
+    double state_cov[8];          /* diag(state_cov) (:431)                               */
+    double newZ[2 * GNSS_VT_MAX_CH];
+    double meas_inno[2 * GNSS_VT_MAX_CH];
+    double satEA[GNSS_VT_MAX_CH], satAZ[GNSS_VT_MAX_CH];  /* el / az, degrees             */
+    double predicted_z[2 * GNSS_VT_MAX_CH];  /* H_pos * error_state (:434)               */
+    double satePos[3], sateVel[3]; /* svxyzr_pos / sv_vel_pos of the LAST channel (:426-427:
+                                      svindex is the loop's last value there)             */
+    double svxyz_pos[GNSS_VT_MAX_CH][3];  /* navSolutionsVT.svxyz_pos(:,:,msIndex) (:429)  */
+    double kalman_gain[8][2 * GNSS_VT_MAX_CH]; /* (:430), columns 0..2n-1 used           */
+    double R[2 * GNSS_VT_MAX_CH]; /* navSolutionsVT.R(counter_r,:) when r_row > 0 (:466) */
+    int32_t r_row;                /* 1-based row of navSolutionsVT.R written, 0: none     */
+    int32_t reserved;
+} gnss_vt_navsol;
+
+/* svPosVel.m: SV position / velocity (ECEF), clock correction (m, m/s) and group delay (s)
+ * at transmit time t (GPS seconds of week). Any output pointer may be NULL. */
+int gnss_sv_pos_vel(const gnss_eph_sv *eph, double t, double pos[3], double vel[3],
+                    double *clkcorr_m, double *clkcorr_m_vel, double *grpdel);
+/* The SDR_MATLAB-main/geo helpers the loop uses, exported for their known-answer tests:
+ *   GNSS_GEO_XYZ2LLH  in xyz[3]            -> out llh[3] (rad, rad, m)   xyz2llh.m
+ *   GNSS_GEO_LLH2XYZ  in llh[3]            -> out xyz[3]                 llh2xyz.m
+ *   GNSS_GEO_XYZ2ENU  in xyz[3], org[3]    -> out enu[3]                 xyz2enu.m
+ *   GNSS_GEO_EROTCORR in svxyz[3], pr      -> out svxyzr[3]              erotcorr.m
+ *   GNSS_GEO_IONO     in t, svxyz[3], usrxyz[3], ALPHA[4], BETA[4] -> out[0] m  ionocorr.m
+ *   GNSS_GEO_TROP     in doy, lat (deg), alt (m), el (deg)   -> out[0] m  trop_UNB3.m  */
+#define GNSS_GEO_XYZ2LLH  0
+#define GNSS_GEO_LLH2XYZ  1
+#define GNSS_GEO_XYZ2ENU  2
+#define GNSS_GEO_EROTCORR 3
+#define GNSS_GEO_IONO     4
+#define GNSS_GEO_TROP     5
+int gnss_geo(int fn, const double *in, double *out);
+
+/* The loop's initialisation (:39-86, :109-155): the EKF (Transistion_Matrix with pdi * ms,
+ * state_cov, process / measurement noise), total_state from the navigation solution of the
+ * scalar loop at row skiptimeVT/navSolPeriod (usrPos, usrVel, clkBias, clkDrift, :66-70),
+ * transmitTimeVT = navSolutionsCT.timeTransmit(1, :) (:131), counters. prn[n], eph[n] per
+ * channel in Acquired.sv order. The channels' NCO state (gnss_vt_chan) comes from
+ * TckResultCT at msStartTckVT (:114-124); the caller builds it (sdr.trackingVT_POS_updated).
+ * pdi = track.pdi. GNSS_EARG for n outside 1..GNSS_VT_MAX_CH. */
+int gnss_vt_nav_init(const gnss_vt_nav_cfg *cfg, const gnss_signal *signal, int32_t pdi, int32_t n,
+                     const int32_t *prn, const gnss_eph_sv *eph, const double usrPos[3],
+                     const double usrVel[3], double clkBias, double clkDrift,
+                     const double *timeTransmit, gnss_vt_nav *nav);
+
+/* The tracking-side prediction for channel i of step nav->msIndex (:180-227): advance the
+ * transmit time by numSample / Fs (the step's read, sized with the LAST code frequency, :164),
+ * svPosVel at it, the iono / tropo update every corrUpt steps, the predicted pseudorange
+ * and, from step 2 on, codeFreq = codeFreqBasis * (1 - deltaPr / c); at step 1 *codeFreq is
+ * left as passed (TckResultCT's codeFreq(msStartTckVT), :218-219). Outputs the step's
+ * deltaPr and sv_vel. */
+int gnss_vt_nav_predict(gnss_vt_nav *nav, int32_t i, int64_t numSample, double *codeFreq,
+                        double *deltaPr, double sv_vel[3]);
+
+/* The navigation update after every channel's correlation of step nav->msIndex (:357-467):
+ * measurements Z = [codeError * c / codeFreq ; prr_predicted - prr_measured - clkDrift +
+ * sv_clk_vel] from each channel's codeError, codeFreq and carrFreq (TckResultVT of this
+ * step), the Kalman update, the state prediction for the next step and, every
+ * 200 / pdi steps, the measurement-noise update. sol (may be NULL) receives the
+ * navSolutionsVT row. Advances nav->msIndex. */
+int gnss_vt_nav_update(gnss_vt_nav *nav, const double *codeError, const double *codeFreq,
+                       const double *carrFreq, gnss_vt_navsol *sol);
+
+/* The whole loop (trackingVT_POS_updated.m:157-476) for nsteps = msToProcessVT / pdi steps:
+ * per step, every channel's read size and predicted code frequency on the host, the
+ * correlations and NCO / PLL / DLL / C/N0 of all channels in one launch of the VT kernel
+ * (vt.hip; chans stay resident in HBM), then the EKF on the host. chans[n] and *nav advance
+ * in place; out[s * n + i] = TckResultVT(Acquired.sv(i)).*(s + 1) incl. deltaPr / prRate /
+ * sv_vel; sol[s] (may be NULL) = navSolutionsVT row s + 1. A channel error (a replica index
+ * MATLAB rejects, a read past EOF) stops the loop at that step (MATLAB raises): the step's
+ * records hold the status, the call returns it. */
+int gnss_tracking_vt(gnss_ctx *ctx, const gnss_file *file, const gnss_signal *signal,
+                     const gnss_track *track, int32_t n, int32_t nsteps, gnss_vt_chan *chans,
+                     gnss_vt_nav *nav, gnss_vt_out *out, gnss_vt_navsol *sol);
 
 /* generateCAcode.m:16-64: the 1023 +-1 chips of PRN 1..51 used by the kernels. */
 int gnss_ca_code(int prn, int8_t *out1023);

@@ -1437,3 +1437,578 @@ void or_synth_if(const gnss_synth *cfg, uint64_t sample0, uint64_t nsamples, int
         dst[2 * i + 1] = (int8_t)vq;
     }
 }
+
+/* ===========================================================================================
+ * trackingVT_POS_updated.m, the vector half: the geo helpers of
+ * SDR_MATLAB-main/geo, the code-frequency prediction (:180-227) and the 8-state EKF
+ * (:357-467), restated line by line; the closed loop with or_vt_step's correlator.
+ * =========================================================================================== */
+
+/* sin / cos as separate libm calls: MATLAB evaluates sin() and cos() element by element, and
+ * gcc would otherwise fuse a sin / cos pair of one argument into glibc's sincos(), which
+ * rounds differently in the last place (the product's host code, built by clang, calls sin
+ * and cos; oracle and product then agree bit for bit on the navigation half). */
+__attribute__((noinline)) static double or_nsin(double x) { return sin(x); }
+__attribute__((noinline)) static double or_ncos(double x) { return cos(x); }
+
+/* xyz2llh.m:25-69 */
+void or_xyz2llh(const double *xyz, double *llh)
+{
+    double x = xyz[0], y = xyz[1], z = xyz[2];
+    double x2 = x * x, y2 = y * y, z2 = z * z;                 /* x^2 */
+    double a = 6378137.0000, b = 6356752.3142;
+    double e = sqrt(1 - (b / a) * (b / a));                    /* (b/a).^2 */
+    double b2 = b * b, e2 = e * e, ep = e * (a / b);
+    double r = sqrt(x2 + y2), r2 = r * r;
+    double E2 = a * a - b * b;
+    double F = 54 * b2 * z2;
+    double G = r2 + (1 - e2) * z2 - e2 * E2;
+    double c = (e2 * e2 * F * r2) / (G * G * G);
+    double s = pow(1 + c + sqrt(c * c + 2 * c), 1.0 / 3.0);
+    double q = s + 1 / s + 1;
+    double P = F / (3 * (q * q) * G * G);
+    double Q = sqrt(1 + 2 * e2 * e2 * P);
+    double ro = -(P * e2 * r) / (1 + Q) + sqrt((a * a / 2) * (1 + 1 / Q) - (P * (1 - e2) * z2) / (Q * (1 + Q)) -
+                                               P * r2 / 2);
+    double t0 = r - e2 * ro;
+    double tmp = t0 * t0;
+    double U = sqrt(tmp + z2), V = sqrt(tmp + (1 - e2) * z2);
+    double zo = (b2 * z) / (a * V);
+    double height = U * (1 - b2 / (a * V));
+    double lat = atan((z + ep * ep * zo) / r);
+    double temp = atan(y / x), lon;
+    if (x >= 0) lon = temp;
+    else if (x < 0 && y >= 0) lon = M_PI + temp;
+    else lon = temp - M_PI;
+    llh[0] = lat;
+    llh[1] = lon;
+    llh[2] = height;
+}
+
+/* llh2xyz.m:20-34 */
+void or_llh2xyz(const double *llh, double *xyz)
+{
+    double re = 6378137.0, eflat = (1.0 / 298.257223563);
+    double e2 = (2 - eflat) * eflat;
+    double slat = or_nsin(llh[0]), clat = or_ncos(llh[0]);
+    double r_N = re / sqrt(1 - e2 * slat * slat);
+    xyz[0] = (r_N + llh[2]) * clat * or_ncos(llh[1]);
+    xyz[1] = (r_N + llh[2]) * clat * or_nsin(llh[1]);
+    xyz[2] = (r_N * (1 - e2) + llh[2]) * slat;
+}
+
+/* R * d for a 3x3 R, each row's sum left to right */
+static void or_mv3(double R[3][3], const double *d, double *out)
+{
+    for (int i = 0; i < 3; i++) {
+        double s = 0;
+        for (int j = 0; j < 3; j++) s = s + R[i][j] * d[j];
+        out[i] = s;
+    }
+}
+
+/* xyz2enu.m:32-47 */
+void or_xyz2enu(const double *xyz, const double *orgxyz, double *enu)
+{
+    double difxyz[3] = {xyz[0] - orgxyz[0], xyz[1] - orgxyz[1], xyz[2] - orgxyz[2]};
+    double orgllh[3];
+    or_xyz2llh(orgxyz, orgllh);
+    double phi = orgllh[0], lam = orgllh[1];
+    double sinphi = or_nsin(phi), cosphi = or_ncos(phi), sinlam = or_nsin(lam), coslam = or_ncos(lam);
+    double R[3][3] = {{-sinlam, coslam, 0},
+                      {-sinphi * coslam, -sinphi * sinlam, cosphi},
+                      {cosphi * coslam, cosphi * sinlam, sinphi}};
+    or_mv3(R, difxyz, enu);
+}
+
+/* erotcorr.m:21-35 */
+void or_erotcorr(const double *svxyz, double pr, double *svxyzr)
+{
+    double omega = 7.2921151467e-5;
+    double deltat = pr / 299792458;
+    double theta = omega * deltat;
+    double rotmat[3][3] = {{or_ncos(theta), or_nsin(theta), 0}, {-or_nsin(theta), or_ncos(theta), 0}, {0, 0, 1}};
+    or_mv3(rotmat, svxyz, svxyzr);
+}
+
+/* ionocorr.m:21-61 (phiu / lambdau are the SATELLITE's latitude / longitude, :23,33,38) */
+double or_ionocorr(double systime, const double *svxyz, const double *usrxyz, const double *ALPHA,
+                   const double *BETA)
+{
+    double svllh[3], svenu[3];
+    or_xyz2llh(svxyz, svllh);
+    or_xyz2enu(svxyz, usrxyz, svenu);
+    double el = atan2(svenu[2], sqrt(svenu[0] * svenu[0] + svenu[1] * svenu[1]));
+    double az = atan2(svenu[0], svenu[1]);
+    double E = el / M_PI;
+    double F = 1 + 16 * ((0.53 - E) * (0.53 - E) * (0.53 - E));
+    double psi = 0.00137 / (E + 0.11) - 0.022;
+    double phiu = svllh[0] / M_PI;
+    double phii = phiu + psi * or_ncos(az);
+    if (phii > 0.416) phii = 0.416;
+    if (phii < -0.416) phii = -0.416;
+    double lambdau = svllh[1] / M_PI;
+    double lambdai = lambdau + psi * or_nsin(az) / or_ncos(phii * M_PI);
+    double phim = phii + 0.064 * or_ncos((lambdai - 1.616) * M_PI);
+    double t = 4.32e4 * lambdai + systime;
+    while ((t < 0) | (t >= 86400)) {
+        if (t >= 86400) t = t - 86400;
+        if (t < 0) t = t + 86400;
+    }
+    double PER = BETA[0] + BETA[1] * phim + BETA[2] * (phim * phim) + BETA[3] * (phim * phim * phim);
+    if (PER < 72000) PER = 72000;
+    double x = 2 * M_PI * (t - 50400) / PER;
+    double AMP = ALPHA[0] + ALPHA[1] * phim + ALPHA[2] * (phim * phim) + ALPHA[3] * (phim * phim * phim);
+    if (AMP < 0) AMP = 0;
+    double Tiono;
+    if (fabs(x) < 1.57) Tiono = F * (5e-9 + AMP * (1 - (x * x) / 2 + ((x * x) * (x * x)) / 24));
+    else Tiono = F * 5e-9;
+    return Tiono * 299792458;
+}
+
+/* trop_UNB3.m (Get_UNB3_Model.m, Trop_Saastamoinen_UNB3_Components.m, Trop_Black_Eisner_Map.m;
+ * MATLAB's cosd reduces by quadrants first). Returns GNSS_EINDEX for |lat| <= 15 (avg(0,:)). */
+int or_trop_unb3(double doy, double lat, double alt, double el, double *out)
+{
+    static const double avg[5][6] = {{15.0, 1013.25, 299.65, 26.31, 0.00630, 2.77},
+                                     {30.0, 1017.25, 294.15, 21.79, 0.00605, 3.15},
+                                     {45.0, 1015.75, 283.15, 11.66, 0.00558, 2.57},
+                                     {60.0, 1011.75, 272.15, 6.78, 0.00539, 1.81},
+                                     {75.0, 1013.00, 263.65, 4.11, 0.00453, 1.55}};
+    static const double amp[5][6] = {{15.0, 0.00, 0.00, 0.00, 0.00, 0.00},
+                                     {30.0, -3.75, 7.00, 8.85, 0.00025, 0.33},
+                                     {45.0, -2.25, 11.00, 7.24, 0.00032, 0.46},
+                                     {60.0, -1.75, 15.00, 5.36, 0.00081, 0.74},
+                                     {75.0, -0.50, 14.50, 3.39, 0.00062, 0.30}};
+    double UNB3_GM = 9.80665, UNB3_RD = 287.054, UNB3_K1 = 0.000077604, UNB3_K2 = 0.382;
+    double doy2rad = 2 * M_PI / 365.25, ep = UNB3_GM / UNB3_RD;
+    if (lat < 0.0) doy = doy - 211.0;
+    else doy = doy - 28.0;
+    double cosphs = or_ncos(doy * doy2rad);
+    lat = fabs(lat);
+    int p1, p2;
+    double m;
+    if (lat >= 75.0) { p1 = 4; p2 = 4; m = 0; }
+    else if (lat <= 15.0) return GNSS_EINDEX;
+    else {
+        p1 = (int)floor((lat - 15) / 15) + 1;
+        p2 = p1 + 1;
+        m = (lat - avg[p1 - 1][0]) / (avg[p2 - 1][0] - avg[p1 - 1][0]);
+    }
+#define OR_LI(tb, c) (m * (tb[p2 - 1][c] - tb[p1 - 1][c]) + tb[p1 - 1][c])
+    double Pavg = OR_LI(avg, 1), Tavg = OR_LI(avg, 2), WVPavg = OR_LI(avg, 3), Bavg = OR_LI(avg, 4);
+    double Lavg = OR_LI(avg, 5);
+    double Pamp = OR_LI(amp, 1), Tamp = OR_LI(amp, 2), WVPamp = OR_LI(amp, 3), Bamp = OR_LI(amp, 4);
+    double Lamp = OR_LI(amp, 5);
+#undef OR_LI
+    double T0 = Tavg - Tamp * cosphs, P0 = Pavg - Pamp * cosphs, WVP0 = WVPavg - WVPamp * cosphs;
+    double beta = Bavg - Bamp * cosphs, lambda = Lavg - Lamp * cosphs;
+    double T = T0 - beta * alt;
+    double P = P0 * pow((T / T0), ep / (beta));
+    double WVP = WVP0 * pow((T / T0), (ep * ((lambda) + 1) / (beta)) - 1);
+    double K_dry = P * UNB3_K1 * UNB3_RD / UNB3_GM;
+    double K_wet = WVP * UNB3_K2 * UNB3_RD / ((UNB3_GM * (lambda + 1) - beta * UNB3_RD) * T0);
+    /* cosd(el) */
+    double nq = round(el / 90), rr = (M_PI / 180) * (el - nq * 90);
+    long mq = ((long)nq % 4 + 4) % 4;
+    double ce = mq == 0 ? or_ncos(rr) : mq == 1 ? -or_nsin(rr) : mq == 2 ? -or_ncos(rr) : or_nsin(rr);
+    double m_dry = 1.0 / sqrt(1.0 - ce * ce / 1.002001);
+    double m_wet = m_dry;
+    *out = K_dry * m_dry + K_wet * m_wet;
+    return GNSS_OK;
+}
+
+/* svPosVel.m:21-177; eph[21] in gnss_eph_sv order */
+int or_svposvel(const double *eph, double t, double *sv_xyz, double *sv_vel, double *clkcorr_m,
+                double *clkcorr_m_vel, double *grpdel)
+{
+    double SQRTSMA = eph[0], DELTAN = eph[1], TOE = eph[2], MZERO = eph[3], ECCEN = eph[4], ARGPERI = eph[5];
+    double CUS = eph[6], CUC = eph[7], CRS = eph[8], CRC = eph[9], CIS = eph[10], CIC = eph[11];
+    double IZERO = eph[12], IDOT = eph[13], OMEGAZERO = eph[14], OMEGADOT = eph[15];
+    double toc = eph[16], AF0 = eph[17], AF1 = eph[18], AF2 = eph[19], TGD = eph[20];
+    double tkc = t - toc;
+    int iter = 0;
+    while (tkc > 302400) { tkc = tkc - 604800; if (++iter > 3) return GNSS_EARG; }
+    iter = 0;
+    while (tkc < -302400) { tkc = tkc + 604800; if (++iter > 3) return GNSS_EARG; }
+    double F = -4.442807633e-10;
+    double clkcorr = (AF0 + AF1 * tkc + AF2 * tkc * tkc) - TGD;
+    double gpsPi = 3.1415926535898, mu = 3986005e8, OMGedot = 7.2921151467e-5;
+    double tk = (t - clkcorr) - TOE;
+    iter = 0;
+    while (tk > 302400) { tk = tk - 604800; if (++iter > 3) return GNSS_EARG; }
+    iter = 0;
+    while (tk < -302400) { tk = tk + 604800; if (++iter > 3) return GNSS_EARG; }
+    double A = (SQRTSMA) * (SQRTSMA);
+    double n_o = sqrt(mu / (A * A * A));
+    double n = n_o + DELTAN;
+    double Mk = MZERO + n * tk;
+    Mk = fmod(Mk + 2 * gpsPi, 2 * gpsPi);
+    double Ek = Mk, sep = 1, oldEk = Ek;
+    iter = 0;
+    while (sep > 1e-13) {
+        Ek = Mk + ECCEN * or_nsin(Ek);
+        sep = fabs(Ek - oldEk);
+        oldEk = Ek;
+        iter = iter + 1;
+        if (iter > 10) break;
+    }
+    Ek = fmod(Ek + 2 * gpsPi, 2 * gpsPi);
+    double cos_Ek = or_ncos(Ek), sin_Ek = or_nsin(Ek);
+    double c1 = 1 - ECCEN * cos_Ek;
+    double Ek_dot = n / c1;
+    double c2 = sqrt(1 - ECCEN * ECCEN);
+    double sin_vk = (c2 * sin_Ek) / (1 - ECCEN * cos_Ek);
+    double cos_vk = (cos_Ek - ECCEN) / (1 - ECCEN * cos_Ek);
+    double vk = atan2(sin_vk, cos_vk);
+    double vk_dot = Ek_dot * c2 / c1;
+    double PHIk = vk + ARGPERI;
+    PHIk = fmod(PHIk, 2 * gpsPi);
+    double c2phik = or_ncos(2 * PHIk), s2phik = or_nsin(2 * PHIk);
+    double delta_uk = CUS * s2phik + CUC * c2phik;
+    double delta_rk = CRS * s2phik + CRC * c2phik;
+    double delta_ik = CIS * s2phik + CIC * c2phik;
+    double uk = PHIk + delta_uk;
+    double uk_dot = vk_dot * (1 + 2 * ((CUS * c2phik - CUC * s2phik)));
+    double rk = A * (1 - ECCEN * cos_Ek) + delta_rk;
+    double rk_dot = A * ECCEN * Ek_dot * sin_Ek + 2 * vk_dot * (CRS * c2phik - CRC * s2phik);
+    double ik = IZERO + delta_ik + IDOT * tk;
+    double ik_dot = IDOT + vk_dot * 2 * (CIS * c2phik - CIC * s2phik);
+    double cos_uk = or_ncos(uk), sin_uk = or_nsin(uk);
+    double xxk = rk * cos_uk, yyk = rk * sin_uk;
+    double xxk_dot = rk_dot * cos_uk - uk_dot * rk * sin_uk;
+    double yyk_dot = rk_dot * sin_uk + uk_dot * rk * cos_uk;
+    double OMGk = OMEGAZERO + (OMEGADOT - OMGedot) * (tk) - OMGedot * TOE;
+    OMEGADOT = OMEGADOT - OMGedot;
+    OMGk = fmod(OMGk + 2 * gpsPi, 2 * gpsPi);
+    double cosO = or_ncos(OMGk), sinO = or_nsin(OMGk), cosi = or_ncos(ik), sini = or_nsin(ik);
+    sv_xyz[0] = xxk * cosO - yyk * cosi * sinO;
+    sv_xyz[1] = xxk * sinO + yyk * cosi * cosO;
+    sv_xyz[2] = yyk * sini;
+    sv_vel[0] = xxk_dot * cosO - OMEGADOT * xxk * sinO - yyk_dot * cosi * sinO + ik_dot * yyk * sini * sinO -
+                OMEGADOT * yyk * cosi * cosO;
+    sv_vel[1] = xxk_dot * sinO + OMEGADOT * xxk * cosO + yyk_dot * cosi * cosO - ik_dot * yyk * sini * cosO -
+                OMEGADOT * yyk * cosi * sinO;
+    sv_vel[2] = yyk_dot * sini + ik_dot * yyk * cosi;
+    double c3 = F * ECCEN * SQRTSMA;
+    *clkcorr_m = 299792458 * (AF0 + AF1 * tkc + AF2 * tkc * tkc + c3 * sin_Ek);
+    *grpdel = TGD;
+    *clkcorr_m_vel = 299792458 * (AF1 + 2 * AF2 * tkc + c3 * cos_Ek * Ek_dot);
+    return GNSS_OK;
+}
+
+/* C(m x n) = A(m x k) * B(k x n), row-major, k summed left to right from 0 */
+static void or_mm(const double *A, const double *B, double *Cm, int m, int k, int n)
+{
+    for (int i = 0; i < m; i++)
+        for (int j = 0; j < n; j++) {
+            double s = 0;
+            for (int q = 0; q < k; q++) s = s + A[i * k + q] * B[q * n + j];
+            Cm[i * n + j] = s;
+        }
+}
+
+/* inv(A) (N x N, row-major, overwritten): Gaussian elimination with partial pivoting (first
+ * largest |pivot|), multipliers stored in place, then each column of the identity solved
+ * forward and back. The reference's inv() is LAPACK's getrf + getri; this fixed order is the
+ * restatement's (and the product's, vtnav.cpp inv_lu). Returns 0 if singular. */
+static int or_inv(double *A, int N, double *X)
+{
+    int perm[2 * OR_VT_MAXCH];
+    for (int i = 0; i < N; i++) perm[i] = i;
+    for (int j = 0; j < N; j++) {
+        int p = j;
+        for (int i = j + 1; i < N; i++)
+            if (fabs(A[i * N + j]) > fabs(A[p * N + j])) p = i;
+        if (A[p * N + j] == 0) return 0;
+        if (p != j) {
+            for (int k = 0; k < N; k++) {
+                double t = A[j * N + k];
+                A[j * N + k] = A[p * N + k];
+                A[p * N + k] = t;
+            }
+            int t = perm[j];
+            perm[j] = perm[p];
+            perm[p] = t;
+        }
+        for (int i = j + 1; i < N; i++) {
+            A[i * N + j] = A[i * N + j] / A[j * N + j];
+            for (int k = j + 1; k < N; k++) A[i * N + k] = A[i * N + k] - A[i * N + j] * A[j * N + k];
+        }
+    }
+    double y[2 * OR_VT_MAXCH];
+    for (int c = 0; c < N; c++) {
+        for (int i = 0; i < N; i++) {
+            y[i] = (perm[i] == c) ? 1.0 : 0.0;
+            for (int k = 0; k < i; k++) y[i] = y[i] - A[i * N + k] * y[k];
+        }
+        for (int i = N - 1; i >= 0; i--) {
+            double s = y[i];
+            for (int k = i + 1; k < N; k++) s = s - A[i * N + k] * X[k * N + c];
+            X[i * N + c] = s / A[i * N + i];
+        }
+    }
+    return 1;
+}
+
+/* :39-86, :131-155 */
+int or_vtnav_init(or_vtnav *v, int n, int pdi, const int *prn, const double *eph21, const double *cnslxyz,
+                  const double *ALPHA, const double *BETA, double doy, double cSpeed, double Fc, double Fs,
+                  double IF, double codeFreqBasis, double ms, const double *usrPos, const double *usrVel,
+                  double clkBias, double clkDrift, const double *timeTransmit)
+{
+    if (n < 1 || n > OR_VT_MAXCH || pdi < 1) return GNSS_EARG;
+    memset(v, 0, sizeof *v);
+    v->n = n;
+    v->pdi = pdi;
+    v->msIndex = 1;
+    for (int i = 0; i < n; i++) {
+        v->prn[i] = prn[i];
+        memcpy(v->eph[i], eph21 + 21 * i, 21 * sizeof(double));
+        v->transmitTimeVT[i] = timeTransmit[i];             /* :131 */
+    }
+    memcpy(v->ALPHA, ALPHA, sizeof v->ALPHA);
+    memcpy(v->BETA, BETA, sizeof v->BETA);
+    v->doy = doy;
+    v->cSpeed = cSpeed;
+    v->Fc = Fc;
+    v->Fs = Fs;
+    v->IF = IF;
+    v->codeFreqBasis = codeFreqBasis;
+    v->ms = ms;
+    memcpy(v->cnslxyz, cnslxyz, sizeof v->cnslxyz);            /* the argument (SDR_main.m:66) */
+    for (int i = 0; i < 8; i++) v->Tm[i][i] = 1;              /* :40-47 */
+    v->Tm[0][3] = v->Tm[1][4] = v->Tm[2][5] = v->Tm[6][7] = pdi * ms;
+    const double sc[8] = {1e-1, 1e-1, 1e-1, 1e-1, 1e-1, 1e-1, 1e0, 1e0};
+    for (int i = 0; i < 8; i++) v->state_cov[i][i] = 1e5 * sc[i]; /* :49 */
+    const double pn[8] = {1e0, 1e0, 1e0, 1e-1, 1e-1, 1e-1, 1e-1, 1e-2};
+    for (int i = 0; i < 8; i++) v->process_noise[i][i] = pn[i];   /* :51-54 */
+    for (int i = 0; i < n; i++) {                                  /* :55-56 */
+        v->mesurement_noise[i][i] = 3e-1;
+        v->mesurement_noise[n + i][n + i] = 1e-1;
+    }
+    v->thresUptR = 200 / pdi;                                      /* :63 */
+    for (int k = 0; k < 3; k++) {
+        v->estPos[k] = usrPos[k];
+        v->estVel[k] = usrVel[k];
+    }
+    v->clkBias = clkBias;
+    v->clkDrift = clkDrift;
+    for (int k = 0; k < 3; k++) {                                  /* :70 */
+        v->total_state[k] = usrPos[k];
+        v->total_state[3 + k] = usrVel[k];
+    }
+    v->total_state[6] = clkBias;
+    v->total_state[7] = clkDrift;
+    v->corrUpt = 0.1 / (pdi * ms);                                 /* :84-86 */
+    for (int i = 0; i < n; i++) v->counter_corr[i] = v->corrUpt - 1 * 1.0;
+    return GNSS_OK;
+}
+
+/* :181-224 for channel i (numSample already sized, :164); *codeFreq left as passed at msIndex 1 */
+int or_vtnav_predict(or_vtnav *v, int i, int64_t numSample, double *codeFreq, double *deltaPr, double *sv_vel)
+{
+    v->numSample[i] = (double)numSample;
+    v->transmitTimeVT[i] = v->transmitTimeVT[i] + (double)numSample / v->Fs;
+    v->tot_est_tck[i] = v->transmitTimeVT[i];
+    double svxyz[3], vel[3], sv_clk, sv_clk_vel, grpdel;
+    int st = or_svposvel(v->eph[i], v->tot_est_tck[i], svxyz, vel, &sv_clk, &sv_clk_vel, &grpdel);
+    if (st) return st;
+    v->counter_corr[i] = v->counter_corr[i] + 1;
+    if (v->counter_corr[i] == v->corrUpt) {
+        double svenu[3], temp[3];
+        or_xyz2enu(svxyz, v->estPos, svenu);
+        double el_rad = atan(svenu[2] / sqrt(svenu[0] * svenu[0] + svenu[1] * svenu[1]));
+        double az_rad = atan2(svenu[0], svenu[1]);
+        v->az[i] = az_rad * 180 / M_PI;
+        v->el[i] = el_rad * 180 / M_PI;
+        or_xyz2llh(v->estPos, temp);
+        double user_ll[3] = {temp[0] * 180 / M_PI, temp[1] * 180 / M_PI, temp[2]};
+        v->ionodel[i] = or_ionocorr(v->tot_est_tck[i], svxyz, v->cnslxyz, v->ALPHA, v->BETA);
+        double tr;
+        st = or_trop_unb3(v->doy, user_ll[0], user_ll[2], v->el[i], &tr);
+        if (st) return st;
+        v->tropodel_unb3[i] = fabs(tr);
+        v->counter_corr[i] = 0;
+    }
+    double r = sqrt((svxyz[0] - v->estPos[0]) * (svxyz[0] - v->estPos[0]) +
+                    (svxyz[1] - v->estPos[1]) * (svxyz[1] - v->estPos[1]) +
+                    (svxyz[2] - v->estPos[2]) * (svxyz[2] - v->estPos[2]));
+    double pr = r + v->clkBias + sv_clk - grpdel * v->cSpeed - v->tropodel_unb3[i] - v->ionodel[i];
+    double svr[3];
+    or_erotcorr(svxyz, pr, svr);
+    r = sqrt((svr[0] - v->estPos[0]) * (svr[0] - v->estPos[0]) + (svr[1] - v->estPos[1]) * (svr[1] - v->estPos[1]) +
+             (svr[2] - v->estPos[2]) * (svr[2] - v->estPos[2]));
+    pr = r + v->clkBias + sv_clk - grpdel * v->cSpeed - v->tropodel_unb3[i] - v->ionodel[i];
+    if (v->msIndex != 1) {
+        v->deltaPr[i] = (pr - v->predictedPr_last[i]) / (v->pdi * v->ms);
+        *codeFreq = v->codeFreqBasis * (1 - v->deltaPr[i] / v->cSpeed);
+    }
+    v->predictedPr_last[i] = pr;
+    *deltaPr = v->deltaPr[i];
+    memcpy(sv_vel, vel, sizeof vel);
+    return GNSS_OK;
+}
+
+/* :321 and :357-467; state_out[8] = estPos, estVel, clkBias, clkDrift after the update (may be
+ * NULL), es_out[8] = error_state (may be NULL) */
+int or_vtnav_update(or_vtnav *v, const double *codeError, const double *codeFreq, const double *carrFreq,
+                    double *state_out, double *es_out)
+{
+    const int n = v->n, N = 2 * n;
+    double Z[2 * OR_VT_MAXCH], H[2 * OR_VT_MAXCH][8];
+    memset(H, 0, sizeof H);
+    for (int i = 0; i < n; i++) Z[i] = codeError[i] * v->cSpeed / codeFreq[i];        /* :321 */
+    double numSample_min = v->numSample[0];
+    for (int i = 1; i < n; i++)
+        if (v->numSample[i] < numSample_min) numSample_min = v->numSample[i];
+    numSample_min = numSample_min - 1;                                                 /* :357 */
+    for (int i = 0; i < n; i++) {
+        double tot_est_pos = v->tot_est_tck[i] - (v->numSample[i] - numSample_min) / v->Fs;
+        v->tot_est_pos[i] = tot_est_pos;
+        double svxyz_pos[3], sv_vel_pos[3], sv_clk_pos, sv_clk_vel, grpdel;
+        int st = or_svposvel(v->eph[i], tot_est_pos, svxyz_pos, sv_vel_pos, &sv_clk_pos, &sv_clk_vel, &grpdel);
+        if (st) return st;
+        double d0 = svxyz_pos[0] - v->estPos[0], d1 = svxyz_pos[1] - v->estPos[1], d2 = svxyz_pos[2] - v->estPos[2];
+        double r = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+        double ppr = r + v->clkBias + sv_clk_pos - grpdel * v->cSpeed - v->tropodel_unb3[i] - v->ionodel[i];
+        double svr[3];
+        or_erotcorr(svxyz_pos, ppr, svr);
+        d0 = svr[0] - v->estPos[0];
+        d1 = svr[1] - v->estPos[1];
+        d2 = svr[2] - v->estPos[2];
+        r = sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+        double a[3] = {(svr[0] - v->estPos[0]) / r, (svr[1] - v->estPos[1]) / r, (svr[2] - v->estPos[2]) / r};
+        for (int k = 0; k < 3; k++) {
+            H[i][k] = -a[k];
+            H[n + i][3 + k] = -a[k];
+        }
+        H[i][6] = 1;
+        H[n + i][7] = 1;
+        double prr_measured = (carrFreq[i] + v->IF) * v->cSpeed / v->Fc;
+        double prr_predicted = 0;
+        for (int k = 0; k < 3; k++) prr_predicted = prr_predicted + (v->estVel[k] - sv_vel_pos[k]) * a[k];
+        Z[n + i] = prr_predicted - prr_measured - v->clkDrift + sv_clk_vel;
+    }
+    /* :387-404 */
+    double es[8] = {0}, Tt[8][8], TP[8][8], TPT[8][8], Ht[8][2 * OR_VT_MAXCH];
+    for (int r = 0; r < 8; r++)
+        for (int c = 0; c < 8; c++) Tt[r][c] = v->Tm[c][r];
+    or_mm(&v->Tm[0][0], &v->state_cov[0][0], &TP[0][0], 8, 8, 8);
+    or_mm(&TP[0][0], &Tt[0][0], &TPT[0][0], 8, 8, 8);
+    for (int r = 0; r < 8; r++)
+        for (int c = 0; c < 8; c++) v->state_cov[r][c] = TPT[r][c] + v->process_noise[r][c];
+    double Hc[2 * OR_VT_MAXCH * 8];
+    for (int r = 0; r < N; r++)
+        for (int c = 0; c < 8; c++) {
+            Hc[r * 8 + c] = H[r][c];
+            Ht[c][r] = H[r][c];
+        }
+    double Htc[8 * 2 * OR_VT_MAXCH];
+    for (int r = 0; r < 8; r++)
+        for (int c = 0; c < N; c++) Htc[r * N + c] = Ht[r][c];
+    double PHt[8 * 2 * OR_VT_MAXCH], HP[2 * OR_VT_MAXCH * 8], S[4 * OR_VT_MAXCH * OR_VT_MAXCH];
+    double Si[4 * OR_VT_MAXCH * OR_VT_MAXCH], K[8 * 2 * OR_VT_MAXCH];
+    or_mm(&v->state_cov[0][0], Htc, PHt, 8, 8, N);
+    or_mm(Hc, &v->state_cov[0][0], HP, N, 8, 8);
+    or_mm(HP, Htc, S, N, 8, N);
+    for (int r = 0; r < N; r++)
+        for (int c = 0; c < N; c++) S[r * N + c] = S[r * N + c] + v->mesurement_noise[r][c];
+    if (!or_inv(S, N, Si)) return GNSS_EINDEX;
+    or_mm(PHt, Si, K, 8, N, N);
+    v->counterUptR = v->counterUptR + 1;
+    for (int k = 0; k < N; k++) v->recordR[v->counterUptR - 1][k] = Z[k] - 0.0; /* newZ' - H*0 (:395) */
+    double inno[2 * OR_VT_MAXCH];
+    for (int k = 0; k < N; k++) inno[k] = Z[k];
+    double Kz[8];
+    or_mm(K, inno, Kz, 8, N, 1);
+    for (int k = 0; k < 8; k++) es[k] = es[k] + Kz[k];
+    double KH[64], IKH[64], Pn[64];
+    or_mm(K, Hc, KH, 8, N, 8);
+    for (int r = 0; r < 8; r++)
+        for (int c = 0; c < 8; c++) IKH[r * 8 + c] = (r == c ? 1.0 : 0.0) - KH[r * 8 + c];
+    or_mm(IKH, &v->state_cov[0][0], Pn, 8, 8, 8);
+    memcpy(&v->state_cov[0][0], Pn, sizeof Pn);
+    for (int k = 0; k < 8; k++) v->total_state[k] = v->total_state[k] + es[k];
+    for (int k = 0; k < 3; k++) {
+        v->estPos[k] = v->total_state[k];
+        v->estVel[k] = v->total_state[3 + k];
+    }
+    v->clkBias = v->total_state[6];
+    v->clkDrift = v->total_state[7];
+    if (state_out) {
+        for (int k = 0; k < 3; k++) {
+            state_out[k] = v->estPos[k];
+            state_out[3 + k] = v->estVel[k];
+        }
+        state_out[6] = v->clkBias;
+        state_out[7] = v->clkDrift;
+    }
+    if (es_out) memcpy(es_out, es, sizeof es);
+    /* :440-442 */
+    double xn[8];
+    or_mm(&v->Tm[0][0], v->total_state, xn, 8, 8, 1);
+    memcpy(v->total_state, xn, sizeof xn);
+    for (int k = 0; k < 3; k++) v->estPos[k] = v->total_state[k];
+    v->clkBias = v->total_state[6];
+    /* :445-467 */
+    if (v->counterUptR == v->thresUptR) {
+        double tmpR[2 * OR_VT_MAXCH];
+        for (int k = 0; k < N; k++) {
+            double s = 0;
+            for (int r = 0; r < v->thresUptR; r++) s = s + v->recordR[r][k] * v->recordR[r][k];
+            tmpR[k] = 1.0 / v->counterUptR * s;
+        }
+        for (int i = 0; i < n; i++) {
+            v->mesurement_noise[i][i] = tmpR[i] * 10;
+            v->mesurement_noise[n + i][n + i] = tmpR[n + i] * 1;
+        }
+        for (int idx = 0; idx < n; idx++) {
+            if (v->mesurement_noise[idx][idx] >= 12000) v->mesurement_noise[idx][idx] = 12000;
+            else if (v->mesurement_noise[idx][idx] <= 0.01) v->mesurement_noise[idx][idx] = 0.01;
+            if (v->mesurement_noise[idx + n][idx + n] >= 400) v->mesurement_noise[idx + n][idx + n] = 400;
+            else if (v->mesurement_noise[idx + n][idx + n] <= 0.01) v->mesurement_noise[idx + n][idx + n] = 0.01;
+        }
+        v->counterUptR = 0;
+        v->counter_r = v->counter_r + 1;
+    }
+    v->msIndex = v->msIndex + 1;
+    return GNSS_OK;
+}
+
+size_t or_vtnav_size(void) { return sizeof(or_vtnav); }
+
+/* The closed loop (:160-476): nsteps steps of n channels on an IF record, or_vt_step's
+ * correlator (its sums in long double) with the EKF closing the loop. chan_st[n][30] (VT_STATE,
+ * advanced), ca[n][1023]. rec[nsteps][n][23] = the VT_REC fields + deltaPr, prRate, sv_vel[3];
+ * nav_out[nsteps][8] = estPos, estVel, clkBias, clkDrift after each update. */
+int or_tracking_vt(const uint8_t *raw, int64_t nbytes, int prec, int dtype, or_vtnav *v, double *chan_st,
+                   const int8_t *ca, double codelength, double tau1carr, double tau2carr, int nsteps, double *rec,
+                   double *nav_out)
+{
+    const int n = v->n;
+    for (int s = 0; s < nsteps; s++) {
+        double codeError[OR_VT_MAXCH], cfk[OR_VT_MAXCH], carrFreq[OR_VT_MAXCH];
+        for (int i = 0; i < n; i++) {
+            double *st = chan_st + 30 * i;
+            double *r = rec + ((int64_t)s * n + i) * 23;
+            int64_t numSample = (int64_t)ceil((codelength * v->pdi - st[1]) / (st[3] / v->Fs)); /* :164 */
+            if (numSample < 1) return GNSS_EINDEX;
+            double cf = st[3], dpr, vel[3];
+            int e = or_vtnav_predict(v, i, numSample, &cf, &dpr, vel);
+            if (e) return e;
+            e = or_vt_step(raw, nbytes, prec, dtype, st, cf, ca + 1023 * i, v->Fs, codelength, v->ms, v->pdi,
+                           tau1carr, tau2carr, NULL, r);
+            if (e) return e;
+            r[18] = dpr;
+            r[19] = 0; /* prRate: never assigned (:142) */
+            memcpy(r + 20, vel, sizeof vel);
+            codeError[i] = r[7];
+            cfk[i] = cf;
+            carrFreq[i] = r[12];
+        }
+        int e = or_vtnav_update(v, codeError, cfk, carrFreq, nav_out ? nav_out + 8 * s : NULL, NULL);
+        if (e) return e;
+    }
+    return GNSS_OK;
+}

@@ -92,6 +92,45 @@ int or_vt_step(const uint8_t *raw, int64_t nbytes, int prec, int dtype, double *
 double or_loop_filter(double outLast, double discri, double discriLast, double tau1, double tau2,
                       double T);
 
+/* trackingVT_POS_updated.m, the vector half: SDR_MATLAB-main/geo helpers,
+ * the code-frequency prediction (:180-227), the EKF (:357-467) and the closed loop. */
+#define OR_VT_MAXCH 32
+typedef struct or_vtnav {
+    int n, pdi, msIndex, counterUptR, counter_r, thresUptR;
+    int prn[OR_VT_MAXCH];
+    double eph[OR_VT_MAXCH][21];  /* gnss_eph_sv order */
+    double ALPHA[4], BETA[4], doy, cSpeed, Fc, Fs, IF, codeFreqBasis, ms, corrUpt;
+    double cnslxyz[3];
+    double estPos[3], estVel[3], clkBias, clkDrift, total_state[8];
+    double Tm[8][8], state_cov[8][8], process_noise[8][8];
+    double mesurement_noise[2 * OR_VT_MAXCH][2 * OR_VT_MAXCH];
+    double recordR[200][2 * OR_VT_MAXCH];
+    double transmitTimeVT[OR_VT_MAXCH], tot_est_tck[OR_VT_MAXCH], tot_est_pos[OR_VT_MAXCH];
+    double predictedPr_last[OR_VT_MAXCH], deltaPr[OR_VT_MAXCH], counter_corr[OR_VT_MAXCH];
+    double ionodel[OR_VT_MAXCH], tropodel_unb3[OR_VT_MAXCH], el[OR_VT_MAXCH], az[OR_VT_MAXCH];
+    double numSample[OR_VT_MAXCH];
+} or_vtnav;
+void or_xyz2llh(const double *xyz, double *llh);
+void or_llh2xyz(const double *llh, double *xyz);
+void or_xyz2enu(const double *xyz, const double *orgxyz, double *enu);
+void or_erotcorr(const double *svxyz, double pr, double *svxyzr);
+double or_ionocorr(double systime, const double *svxyz, const double *usrxyz, const double *ALPHA,
+                   const double *BETA);
+int or_trop_unb3(double doy, double lat, double alt, double el, double *out);
+int or_svposvel(const double *eph, double t, double *sv_xyz, double *sv_vel, double *clkcorr_m,
+                double *clkcorr_m_vel, double *grpdel);
+size_t or_vtnav_size(void);
+int or_vtnav_init(or_vtnav *v, int n, int pdi, const int *prn, const double *eph21, const double *cnslxyz,
+                  const double *ALPHA, const double *BETA, double doy, double cSpeed, double Fc, double Fs,
+                  double IF, double codeFreqBasis, double ms, const double *usrPos, const double *usrVel,
+                  double clkBias, double clkDrift, const double *timeTransmit);
+int or_vtnav_predict(or_vtnav *v, int i, int64_t numSample, double *codeFreq, double *deltaPr, double *sv_vel);
+int or_vtnav_update(or_vtnav *v, const double *codeError, const double *codeFreq, const double *carrFreq,
+                    double *state_out, double *es_out);
+int or_tracking_vt(const uint8_t *raw, int64_t nbytes, int prec, int dtype, or_vtnav *v, double *chan_st,
+                   const int8_t *ca, double codelength, double tau1carr, double tau2carr, int nsteps, double *rec,
+                   double *nav_out);
+
 /* Synthetic IF — CPU twin of the HIP generator. */
 void or_synth_if(const gnss_synth *cfg, uint64_t sample0, uint64_t nsamples, int8_t *dst,
                  int nthreads);

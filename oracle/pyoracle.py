@@ -256,3 +256,127 @@ def bit_edge(P_i):
     st = C.c_int()
     cx = load().or_bit_edge(P.ctypes.data, len(P), C.byref(st))
     return cx, st.value
+
+
+# ---- trackingVT_POS_updated.m, the vector half ------------------------------
+def _vtnav_protos(lib):
+    if getattr(lib, "_vtnav_ready", False):
+        return lib
+    D, P = C.c_double, C.c_void_p
+    for f in ("or_xyz2llh", "or_llh2xyz"):
+        getattr(lib, f).argtypes = [P, P]
+    lib.or_xyz2enu.argtypes = [P, P, P]
+    lib.or_erotcorr.argtypes = [P, D, P]
+    lib.or_ionocorr.argtypes = [D, P, P, P, P]
+    lib.or_ionocorr.restype = D
+    lib.or_trop_unb3.argtypes = [D, D, D, D, P]
+    lib.or_svposvel.argtypes = [P, D, P, P, P, P, P]
+    lib.or_vtnav_size.restype = C.c_size_t
+    lib.or_vtnav_init.argtypes = [P, C.c_int, C.c_int, P, P, P, P, P, D, D, D, D, D, D, D, P, P, D, D, P]
+    lib.or_vtnav_predict.argtypes = [P, C.c_int, C.c_int64, P, P, P]
+    lib.or_vtnav_update.argtypes = [P, P, P, P, P, P]
+    lib.or_tracking_vt.argtypes = [P, C.c_int64, C.c_int, C.c_int, P, P, P, D, D, D, C.c_int, P, P]
+    lib._vtnav_ready = True
+    return lib
+
+
+def _d(x, n=None):
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.float64).ravel())
+    assert n is None or a.size == n
+    return a
+
+
+def geo(fn, *args):
+    """The SDR_MATLAB-main/geo helpers of the oracle: fn in xyz2llh, llh2xyz, xyz2enu (xyz, org),
+    erotcorr (svxyz, pr), ionocorr (t, svxyz, usrxyz, ALPHA, BETA), trop_UNB3 (doy, lat, alt,
+    el) -> float64 array (or float)."""
+    lib = _vtnav_protos(load())
+    out = np.zeros(3)
+    if fn in ("xyz2llh", "llh2xyz"):
+        x = _d(args[0], 3)
+        getattr(lib, "or_" + fn)(x.ctypes.data, out.ctypes.data)
+    elif fn == "xyz2enu":
+        a, b = _d(args[0], 3), _d(args[1], 3)
+        lib.or_xyz2enu(a.ctypes.data, b.ctypes.data, out.ctypes.data)
+    elif fn == "erotcorr":
+        a = _d(args[0], 3)
+        lib.or_erotcorr(a.ctypes.data, float(args[1]), out.ctypes.data)
+    elif fn == "ionocorr":
+        sv, us, al, be = _d(args[1], 3), _d(args[2], 3), _d(args[3], 4), _d(args[4], 4)
+        return lib.or_ionocorr(float(args[0]), sv.ctypes.data, us.ctypes.data, al.ctypes.data, be.ctypes.data)
+    elif fn == "trop_UNB3":
+        o = C.c_double()
+        st = lib.or_trop_unb3(*[float(a) for a in args], C.byref(o))
+        if st:
+            raise abi.GnssError(st, "trop_UNB3")
+        return o.value
+    else:
+        raise ValueError(fn)
+    return out
+
+
+def svposvel(eph21, t):
+    """svPosVel.m -> (pos[3], vel[3], clkcorr_m, clkcorr_m_vel, grpdel)."""
+    lib = _vtnav_protos(load())
+    e = _d(eph21, 21)
+    pos, vel = np.zeros(3), np.zeros(3)
+    c1, c2, g = C.c_double(), C.c_double(), C.c_double()
+    st = lib.or_svposvel(e.ctypes.data, float(t), pos.ctypes.data, vel.ctypes.data, C.byref(c1), C.byref(c2),
+                         C.byref(g))
+    if st:
+        raise abi.GnssError(st, "svPosVel")
+    return pos, vel, c1.value, c2.value, g.value
+
+
+class VtNav:
+    """The oracle's navigation state of the VT loop (or_vtnav): init (:39-155), predict
+    (:180-227), update (:357-467)."""
+
+    def __init__(self, prns, eph21, cnslxyz, ALPHA, BETA, doy, cSpeed, Fc, signal, usrPos, usrVel, clkBias,
+                 clkDrift, timeTransmit, pdi=1):
+        self.lib = _vtnav_protos(load())
+        self.n = n = len(prns)
+        self.buf = np.zeros(self.lib.or_vtnav_size(), dtype=np.uint8)
+        pr = np.ascontiguousarray(prns, dtype=np.int32)
+        self._keep = [_d(eph21, 21 * n), _d(cnslxyz, 3), _d(ALPHA, 4), _d(BETA, 4), _d(usrPos, 3), _d(usrVel, 3),
+                      _d(timeTransmit, n)]
+        e, ip, al, be, up, uv, tt = self._keep
+        st = self.lib.or_vtnav_init(self.buf.ctypes.data, n, int(pdi), pr.ctypes.data, e.ctypes.data,
+                                    ip.ctypes.data, al.ctypes.data, be.ctypes.data, float(doy), float(cSpeed),
+                                    float(Fc), float(signal.Fs), float(signal.IF), float(signal.codeFreqBasis),
+                                    float(signal.ms), up.ctypes.data, uv.ctypes.data, float(clkBias),
+                                    float(clkDrift), tt.ctypes.data)
+        assert st == 0, st
+
+    def predict(self, i, numSample, codeFreq):
+        cf, dpr, vel = C.c_double(codeFreq), C.c_double(), np.zeros(3)
+        st = self.lib.or_vtnav_predict(self.buf.ctypes.data, int(i), int(numSample), C.byref(cf), C.byref(dpr),
+                                       vel.ctypes.data)
+        if st:
+            raise abi.GnssError(st, "or_vtnav_predict")
+        return cf.value, dpr.value, vel
+
+    def update(self, codeError, codeFreq, carrFreq):
+        """-> (state[8] = estPos, estVel, clkBias, clkDrift after the update, error_state[8])."""
+        a, b, c = _d(codeError, self.n), _d(codeFreq, self.n), _d(carrFreq, self.n)
+        x, es = np.zeros(8), np.zeros(8)
+        st = self.lib.or_vtnav_update(self.buf.ctypes.data, a.ctypes.data, b.ctypes.data, c.ctypes.data,
+                                      x.ctypes.data, es.ctypes.data)
+        if st:
+            raise abi.GnssError(st, "or_vtnav_update")
+        return x, es
+
+    def tracking(self, iq, chan_st, prns, nsteps, codelength=1023.0, pll=(15, 0.707, 0.25), prec=1, dtype=2):
+        """The closed loop (or_tracking_vt): chan_st [n][30] VT_STATE rows, advanced in place.
+        Returns (status, rec [nsteps][n][23]: VT_REC + deltaPr, prRate, sv_vel[3],
+        nav [nsteps][8]: estPos, estVel, clkBias, clkDrift after each update)."""
+        t1, t2 = calc_loop_coef(*pll)
+        raw = np.ascontiguousarray(iq).view(np.uint8).reshape(-1)
+        ca = np.ascontiguousarray(np.stack([generate_ca(p) for p in prns]), dtype=np.int8)
+        assert chan_st.dtype == np.float64 and chan_st.flags.c_contiguous and chan_st.shape == (self.n, 30)
+        rec = np.zeros((nsteps, self.n, 23))
+        nav = np.zeros((nsteps, 8))
+        st = self.lib.or_tracking_vt(raw.ctypes.data, raw.size, int(prec), int(dtype), self.buf.ctypes.data,
+                                     chan_st.ctypes.data, ca.ctypes.data, float(codelength), t1, t2, int(nsteps),
+                                     rec.ctypes.data, nav.ctypes.data)
+        return st, rec, nav

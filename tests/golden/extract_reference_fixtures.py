@@ -20,6 +20,10 @@ are data (inputs + expected outputs), committed under tests/golden/:
                                trackingVT_POS_updated.m on the real Opensky IF, 5 PRNs x 5000
                                1-ms steps): the correlator outputs and the NCO / loop state of
                                steps 1..1200 (the vector-tracking NCO replay, tests/test_vt_kat.py).
+  ref_vt_nav_Opensky.npz       (--vtnav) the vector half of trackingVT_POS_updated.m: its inputs
+                               (nAcquired sv, eph_Opensky_40 / sbf_Opensky_40, navSolCT_10ms_Opensky,
+                               the TckResultCT_pos state at msStartTckVT) and its outputs over all
+                               5000 steps (codeFreq, deltaPr, prRate, sv_vel; tests/test_vt_nav_kat.py).
 
 Only scipy.io.loadmat (a MAT-v5 parser that executes nothing) is used.
 """
@@ -83,6 +87,45 @@ def vt_fixture(nsteps=1200):
     arrs["CN0_VT"] = np.asarray(d["CN0_VT"], dtype=np.float64)[: nsteps // 20]
     np.savez_compressed(os.path.join(HERE, "ref_tckRstVT_Opensky.npz"), **arrs)
     print("VT prns", prns)
+
+
+EPH_SV_FIELDS = ["sqrta", "deltan", "toe", "M0", "ecc", "w", "Cus", "Cuc", "Crs", "Crc", "Cis", "Cic", "i0",
+                 "idot", "omegae", "omegadot", "toc", "af0", "af1", "af2", "TGD"]
+
+
+def vt_nav_fixture():
+    """ref_vt_nav_Opensky.npz: the INPUTS SDR_main.m:69-93 hands trackingVT_POS_updated.m
+    (nAcquired_Opensky_5000.mat's sv; eph_Opensky_40.mat, loaded for msToProcessCT_10ms = 40000,
+    at eph_idx 1; sbf_Opensky_40.mat's nav1; navSolCT_10ms_Opensky.mat; the TckResultCT_pos
+    state of tckRstCT_10ms_Opensky.mat at msStartTckVT) and its OUTPUT for all 5000 steps
+    (tckRstVT_Opensky_updated.mat: codeFreq, deltaPr, prRate, sv_vel, and the correlator side's
+    codeError / carrFreq / remChip / absoluteSample the EKF consumes)."""
+    ld = lambda f, k: sio.loadmat(os.path.join(REF, f), squeeze_me=True, struct_as_record=False)[k]
+    na = ld("nAcquired_Opensky_5000.mat", "nAcquired")
+    sv = [int(p) for p in np.atleast_1d(na.sv)]
+    eph = ld("eph_Opensky_40.mat", "eph")
+    sbf = ld("sbf_Opensky_40.mat", "sbf")
+    ns = ld("navSolCT_10ms_Opensky.mat", "navSolutionsCT")
+    ct = ld("tckRstCT_10ms_Opensky.mat", "TckResultCT_pos")
+    vt = ld("tckRstVT_Opensky_updated.mat", "TckResultVT")
+    out = {"prns": np.array(sv)}
+    out["eph"] = np.array([[float(np.atleast_1d(getattr(eph[p - 1], f))[0]) for f in EPH_SV_FIELDS] for p in sv])
+    out["eph_sfb1"] = np.array([float(np.atleast_1d(eph[p - 1].sfb)[0]) for p in sv])  # eph(prn).sfb(1)
+    out["nav1"] = np.array([float(np.atleast_1d(sbf.nav1)[p - 1]) for p in sv])
+    for f in ("usrPos", "usrVel"):
+        out["navSolCT_" + f] = np.asarray(getattr(ns, f), dtype=np.float64)[:10]
+    for f in ("clkBias", "clkDrift"):
+        out["navSolCT_" + f] = np.asarray(getattr(ns, f), dtype=np.float64).ravel()[:10]
+    out["navSolCT_timeTransmit"] = np.asarray(ns.timeTransmit, dtype=np.float64)[:2]
+    # TckResultCT_pos fields around msStartTckVT (min(.., 3000) = 3000 here): the last 3 steps
+    out["ct_len"] = np.array([np.asarray(ct[p - 1].codeFreq).size for p in sv])
+    for f in ("codeFreq", "remChip", "carrFreq", "remCarrPhase", "absoluteSample", "codedelay", "carrError"):
+        out["ct_" + f] = np.stack([np.asarray(getattr(ct[p - 1], f), dtype=np.float64)[-3:] for p in sv])
+    for f in ("codeFreq", "deltaPr", "prRate", "codeError", "carrFreq", "remChip", "absoluteSample"):
+        out["vt_" + f] = np.stack([np.asarray(getattr(vt[p - 1], f), dtype=np.float64).ravel() for p in sv])
+    out["vt_sv_vel"] = np.stack([np.asarray(vt[p - 1].sv_vel, dtype=np.float64) for p in sv])
+    np.savez_compressed(os.path.join(HERE, "ref_vt_nav_Opensky.npz"), **out)
+    print("VT nav fixture", sv, out["vt_codeFreq"].shape)
 
 
 def fig_series(path):
@@ -164,5 +207,8 @@ def navdecode_fixture():
 if __name__ == "__main__":
     if "--navdecode" in sys.argv:
         navdecode_fixture()
+        sys.exit(0)
+    if "--vtnav" in sys.argv:
+        vt_nav_fixture()
         sys.exit(0)
     sys.exit(main())

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol(pkg):
 
 def test_abi_version_and_strerror(pkg):
     lib = pkg.abi.load()
-    assert lib.gnss_abi_version() == 9
+    assert lib.gnss_abi_version() == 10
     for code in range(6):
         assert lib.gnss_strerror(code)
 
@@ -40,6 +40,8 @@ STRUCTS = {
     "gnss_acquired": "GnssAcquired", "gnss_acq_diag": "GnssAcqDiag", "gnss_track": "GnssTrack",
     "gnss_track_out": "GnssTrackOut", "gnss_timing": "GnssTiming", "gnss_synth_sv": "GnssSynthSv",
     "gnss_synth": "GnssSynth", "gnss_vt_chan": "GnssVtChan", "gnss_vt_out": "GnssVtOut",
+    "gnss_eph_sv": "GnssEphSv", "gnss_vt_nav_cfg": "GnssVtNavCfg", "gnss_vt_nav": "GnssVtNav",
+    "gnss_vt_navsol": "GnssVtNavSol",
 }
 
 

@@ -1,0 +1,146 @@
+"""GPU closed loop of vector tracking (trackingVT_POS_updated.m:157-476 through
+sdr.trackingVT_POS_updated -> gnss_tracking_vt): the EKF-predicted code frequencies drive the VT
+correlator kernel step by step and the correlator outputs drive the EKF, against the oracle's
+closed loop (or_tracking_vt: or_vt_step's correlator, long-double sums, and the or_vtnav EKF,
+itself pinned by the reference's recorded run in tests/test_vt_nav_kat.py).
+
+Inputs: the reference's own VT inputs (tests/vt_nav_common.py: 5 PRNs, eph_Opensky_40,
+navSolCT_10ms_Opensky row 5, TckResultCT at msStartTckVT) on the synthetic Opensky record (the
+reference ships no IF), the channels' file pointers placed on the synthetic scene's code phases.
+
+Tolerances: read sizes, file offsets, codedelay, sv_vel and the C/N0 row positions bit-exact; the
+carrier-wiped sums within 1e-9 of |P| (fp64 fixed-order workgroup sums against long double, as
+tests/test_gpu_vt.py); what the sums feed (carrier NCO, the EKF's Doppler measurements, its state
+and the next code frequency) within the bounds written at each assert.
+"""
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+
+import vt_nav_common as V
+from conftest import params
+
+pytestmark = pytest.mark.gpu
+
+S = 58000
+
+
+def _inputs(pkg, z, skip):
+    """The reference-shaped arguments of trackingVT_POS_updated (SDR_main.m:99) for the
+    synthetic record: Acquired, eph, sbf, TckResultCT (3000 rows; row msStartTckVT = 3000 holds
+    the reference's state, absoluteSample moved onto the scene), navSolutionsCT."""
+    prns = [int(p) for p in z["prns"]]
+    scene = dict(zip(pkg.synth.OPENSKY_SV, pkg.synth.OPENSKY_CODEDELAY))
+    Acquired = SimpleNamespace(sv=np.array(prns))
+    eph = {}
+    for i, p in enumerate(prns):
+        e = SimpleNamespace(**{f: np.array([z["eph"][i, j]]) for j, f in enumerate(pkg.abi.EPH_SV_FIELDS)})
+        e.sfb = np.array([z["eph_sfb1"][i]])
+        eph[p] = e
+    nav1 = np.zeros(32)
+    for i, p in enumerate(prns):
+        nav1[p - 1] = z["nav1"][i]
+    sbf = SimpleNamespace(nav1=nav1)
+    ct = {}
+    for i, p in enumerate(prns):
+        e = SimpleNamespace()
+        for f in ("codeFreq", "remChip", "carrFreq", "remCarrPhase", "codedelay", "carrError"):
+            a = np.zeros(3000)
+            a[-3:] = z["ct_" + f][i]
+            setattr(e, f, a)
+        e.absoluteSample = np.zeros(3000)
+        e.absoluteSample[-1] = (S - scene[p] + 1 + skip * S) * 2
+        ct[p] = e
+    ns = SimpleNamespace(**{k: z["navSolCT_" + k] for k in ("usrPos", "usrVel", "clkBias", "clkDrift",
+                                                          "timeTransmit")})
+    return Acquired, eph, sbf, ct, ns
+
+
+def _oracle_loop(pkg, po, z, ct, data, nsteps):
+    prns = [int(p) for p in z["prns"]]
+    st = np.stack([po.vt_state(ct[p].absoluteSample[-1], ct[p].remChip[-1], ct[p].remCarrPhase[-1],
+                               ct[p].codeFreq[-1], ct[p].carrFreq[-1], ct[p].carrFreq[-1], 0.0,
+                               ct[p].carrError[-1]) for p in prns])
+    onav = V.oracle_nav(pkg, po, z)
+    status, rec, nav = onav.tracking(np.ascontiguousarray(data, dtype=np.int8), st, prns, nsteps)
+    return status, rec, nav
+
+
+def test_vector_tracking_closed_loop_against_oracle(pkg, po, ctx, opensky_short):
+    skip, cfg, data = opensky_short
+    file, signal, acq, track = params(pkg, skip, data)
+    _, _, _, _, solu, cmn = pkg.initParameters()
+    z = V.fixture()
+    Acquired, eph, sbf, ct, ns = _inputs(pkg, z, skip)
+    nsteps = 1200
+    tck, nsol, cn0 = pkg.trackingVT_POS_updated(file, signal, track, cmn, solu, Acquired, V.cnslxyz(pkg), eph,
+                                                sbf, None, ct, ns, ctx=ctx, nsteps=nsteps, return_cn0=True)
+    t = ctx.timing()
+    assert t["track_launches"] == nsteps
+    print(f"gnss_tracking_vt: {nsteps} steps x 5 channels, kernel {t['track_kernel_ms']:.1f} ms")
+    status, rec, onav = _oracle_loop(pkg, po, z, ct, data, nsteps)
+    assert status == 0
+    R = {k: rec[:, :, j] for j, k in enumerate(po.VT_REC + ["deltaPr", "prRate"])}
+    prns = [int(p) for p in z["prns"]]
+    worst = dict(sum=0.0, cf=0.0, dpr=0.0, carr=0.0)
+    for i, p in enumerate(prns):
+        g = tck(p)
+        # integer / exact: the read sizes and offsets the code frequencies produced
+        assert np.array_equal(g.absoluteSample, R["absoluteSample"][:, i]), p
+        assert np.array_equal(g.codedelay, R["codedelay"][:, i]), p
+        assert np.array_equal(g.sv_vel, rec[:, i, 20:23]), p  # svPosVel at the (exact) transmit time
+        assert np.all(g.prRate == 0) and np.all(g.amplitude == 0)
+        scale = np.maximum(np.maximum(np.abs(R["P_i"][:, i]), np.abs(R["P_q"][:, i])), 1.0)
+        for f in ("E_i", "E_q", "P_i", "P_q", "L_i", "L_q"):
+            worst["sum"] = max(worst["sum"], float(np.max(np.abs(getattr(g, f) - R[f][:, i]) / scale)))
+        worst["cf"] = max(worst["cf"], float(np.max(np.abs(g.codeFreq - R["codeFreq"][:, i]) / g.codeFreq)))
+        worst["dpr"] = max(worst["dpr"], float(np.max(np.abs(g.deltaPr - R["deltaPr"][:, i]))))
+        worst["carr"] = max(worst["carr"], float(np.max(np.abs(g.carrFreq - R["carrFreq"][:, i]))))
+        for f in ("remChip", "remCarrPhase", "carrNco", "carrError"):
+            assert np.allclose(getattr(g, f), R[f][:, i], rtol=1e-9, atol=1e-9), (p, f)
+        assert g.codeFreq[0] == ct[p].codeFreq[-1]  # msIndex 1 keeps TckResultCT's (:218-219)
+    print({k: f"{v:.3g}" for k, v in worst.items()})
+    assert worst["sum"] < 1e-9
+    assert worst["carr"] < 1e-6          # Hz: the PLL's carrError differs by the sums' rounding
+    assert worst["cf"] < 1e-12           # relative: the Doppler measurements move the state by < 1 um
+    assert worst["dpr"] < 1e-4           # m/s: a few ulps of a 2e7-m range over 1 ms
+    # the EKF state after each update (navSolutionsVT.usrPos / usrVel / clkBias / clkDrift)
+    assert np.allclose(nsol.usrPos, onav[:, :3], rtol=0, atol=1e-5)
+    assert np.allclose(nsol.usrVel, onav[:, 3:6], rtol=0, atol=1e-5)
+    assert np.allclose(nsol.clkBias, onav[:, 6], rtol=0, atol=1e-5)
+    assert np.allclose(nsol.clkDrift, onav[:, 7], rtol=0, atol=1e-6)
+    # navSolutionsVT's shapes (:418-436, :466) and the R updates every 200 steps
+    n = len(prns)
+    assert nsol.usrPosENU.shape == (nsteps, 3) and nsol.state.shape == (nsteps, 8)
+    assert nsol.newZ.shape == (nsteps, 2 * n) and nsol.satEA.shape == (nsteps, n)
+    assert nsol.svxyz_pos.shape == (n, 3, nsteps) and nsol.kalman_gain.shape == (8, 2 * n, nsteps)
+    assert nsol.R.shape == (nsteps // 200, 2 * n)
+    assert np.all(nsol.R[:, :n] >= 0.01) and np.all(nsol.R[:, :n] <= 12000)
+    assert np.all(nsol.R[:, n:] >= 0.01) and np.all(nsol.R[:, n:] <= 400)
+    # CN0_VT: one row per 20 steps and channel (:296-304)
+    assert cn0.shape == (nsteps // 20, n)
+    c_ref = np.zeros_like(cn0)
+    for i in range(n):
+        m = R["cn0_row"][:, i] > 0
+        c_ref[R["cn0_row"][:, i][m].astype(int) - 1, i] = R["CN0"][:, i][m]
+    assert np.allclose(cn0, c_ref, rtol=1e-9, atol=0)
+
+
+def test_vector_tracking_stops_past_eof(pkg, ctx, opensky_short):
+    """A read past the end of the record stops the loop with EIO, as MATLAB's fread of a short
+    block feeds a size-mismatched product and raises (:165-181)."""
+    skip, cfg, data = opensky_short
+    file, signal, acq, track = params(pkg, skip, data)
+    _, _, _, _, solu, cmn = pkg.initParameters()
+    z = V.fixture()
+    Acquired, eph, sbf, ct, ns = _inputs(pkg, z, skip)
+    steps_left = (len(data) - int(max(ct[p].absoluteSample[-1] for p in ct))) // (2 * S)
+    with pytest.raises(pkg.abi.GnssError) as ei:
+        pkg.trackingVT_POS_updated(file, signal, track, cmn, solu, Acquired, V.cnslxyz(pkg), eph, sbf, None, ct,
+                                   ns, ctx=ctx, nsteps=steps_left + 20)
+    assert ei.value.status == pkg.abi.EIO
+    # the context stays usable
+    tck, nsol = pkg.trackingVT_POS_updated(file, signal, track, cmn, solu, Acquired, V.cnslxyz(pkg), eph, sbf,
+                                           None, ct, ns, ctx=ctx, nsteps=10)
+    assert nsol.usrPos.shape == (10, 3)
