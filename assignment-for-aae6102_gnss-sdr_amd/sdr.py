@@ -639,7 +639,8 @@ def trackingVT_step(file, signal, track, chans, codeFreq_new, pdi=1, *, ctx: Con
                                             cf.ctypes.data_as(C.POINTER(C.c_double)), outs))
     for i in range(n):
         C.memmove(C.byref(chans[i]), C.byref(arr[i]), C.sizeof(abi.GnssVtChan))
-    return [{k: getattr(o, k) for k, _ in abi.GnssVtOut._fields_} for o in outs]
+    return [{k: (getattr(o, k)[:] if k == "sv_vel" else getattr(o, k)) for k, _ in abi.GnssVtOut._fields_}
+            for o in outs]
 
 
 def trackingVT_run(file, signal, track, chans, codeFreq_series, pdi=1, *, ctx: Context | None = None):
@@ -663,8 +664,7 @@ def trackingVT_run(file, signal, track, chans, codeFreq_series, pdi=1, *, ctx: C
                                       cf.ctypes.data_as(C.POINTER(C.c_double)), outs)
     for i in range(n):
         C.memmove(C.byref(chans[i]), C.byref(arr[i]), C.sizeof(abi.GnssVtChan))
-    rec = np.frombuffer(outs, dtype=np.dtype([(k, {C.c_double: "f8", C.c_int64: "i8", C.c_int32: "i4"}[t_])
-                                              for k, t_ in abi.GnssVtOut._fields_])).reshape(nsteps, n)
+    rec = np.ctypeslib.as_array(outs).reshape(nsteps, n)  # a structured view of the records
     ctx.check(st)
     return {k: rec[k].copy() for k in rec.dtype.names}
 

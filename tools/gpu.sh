@@ -32,7 +32,7 @@ for step in "$@"; do
   echo "== $step $(date +%T)"
   case $step in
     tests)
-      timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu.log 2>&1 \
+      timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS} ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu.log 2>&1 \
         && echo "TESTS_OK $(tail -1 gpurun_out/pytest_gpu.log)" || { grep -E "FAIL|Error" gpurun_out/pytest_gpu.log | tail -30; tail -40 gpurun_out/pytest_gpu.log; exit 1; } ;;
     bench)
       timeout -k 10 400 python3 bench.py $BENCH_ARGS > gpurun_out/bench.json 2> gpurun_out/bench.err \
