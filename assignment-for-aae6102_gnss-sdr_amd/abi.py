@@ -246,9 +246,9 @@ _lib = None
 _torch_first = False
 LOADED_PATH = None  # the library file the process bound (bench.py digests it)
 
-# gnss_ctx_set_option keys (include/gnss_mi355x.h, ABI v9)
+# gnss_ctx_set_option keys (include/gnss_mi355x.h, ABI v10)
 (OPT_FORCE_SUB, OPT_NO_PERSIST, OPT_FORCE_VPB, OPT_ACQ_ROCFFT, OPT_FINE_ROCFFT, OPT_ACQ_BATCH, OPT_ACQ_FUSED,
- OPT_ACQ_RING, OPT_ACQ_PIPE) = range(9)
+ OPT_ACQ_RING, OPT_ACQ_PIPE, OPT_VT_BLOCKS) = range(10)
 
 
 def require_torch():

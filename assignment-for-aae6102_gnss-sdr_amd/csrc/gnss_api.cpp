@@ -11,6 +11,7 @@
 #include <rocfft/rocfft.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cmath>
 #include <cstdio>
@@ -18,7 +19,6 @@
 #include <cstdlib>
 #include <functional>
 #include <thread>
-#include <chrono>
 #include <vector>
 #include <fcntl.h>
 #include <map>
@@ -1911,6 +1911,22 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     A.pdi = pdi;
     A.prec = prec;
     A.dtype = dtyp;
+    // int8 records: each step over nb blocks per channel (vt_step_kernel), the step's code
+    // frequencies in the kernel arguments and its records written to pinned host memory (no
+    // copy commands per step); int16 (per-read means first): one block per channel
+    // (vt_run_kernel)
+    const bool multi = prec == 1;
+    DevBuf d_part, d_ticket;
+    if (multi) {
+        A.nb = (int)std::max<int64_t>(1, (nominal + kVtStepSamples - 1) / kVtStepSamples);
+        if (ctx->opt[GNSS_OPT_VT_BLOCKS] > 0) A.nb = (int)std::min<int64_t>(ctx->opt[GNSS_OPT_VT_BLOCKS], 1024);
+        HIP_TRY(d_part.alloc(ctx, "vt.part", sizeof(double) * 2 * (size_t)n * A.nb));
+        HIP_TRY(d_ticket.alloc(ctx, "vt.ticket", sizeof(unsigned) * (size_t)n));
+        HIP_TRY(hipMemsetAsync(d_ticket.p, 0, sizeof(unsigned) * (size_t)n, ctx->stream));
+        A.part = d_part.as<double>();
+        A.ticket = d_ticket.as<unsigned>();
+        A.out = h_out;
+    }
     // the host's view of what sizes the next read (:164): remChip / codeFreq / file_ptr of the
     // last step, from the records the kernel returns
     std::vector<double> remChip(n), cf_old(n), codeError(n), carrFreq(n), cf_new(n);
@@ -1923,6 +1939,7 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     Events ev;
     double kernel_ms = 0;
     int result = GNSS_OK;
+    const auto t_loop = std::chrono::steady_clock::now();
     for (int s = 0; s < nsteps && result == GNSS_OK; s++) {
         int64_t need_lo = INT64_MAX, need_hi = 0;
         for (int i = 0; i < n; i++) {
@@ -1955,13 +1972,21 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         A.rec = reinterpret_cast<const uint8_t*>(w.ptr);
         A.base = w.base;
         A.len = w.len;
-        HIP_TRY(hipMemcpyAsync(d_cf.p, h_cf, sizeof(double) * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
-        HIP_TRY(hipEventRecord(ev.a, ctx->stream));
-        HIP_TRY(launch_vt_run(A, ctx->stream));
-        HIP_TRY(hipEventRecord(ev.b, ctx->stream));
-        HIP_TRY(hipMemcpyAsync(h_out, d_out.p, sizeof(gnss_vt_out) * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+        if (multi) {  // (per-step events only in profiling mode: each is a queue command)
+            for (int i = 0; i < n; i++) A.cf_arg[i] = h_cf[i];
+            if (ctx->profiling) HIP_TRY(hipEventRecord(ev.a, ctx->stream));
+            HIP_TRY(launch_vt_step(A, ctx->stream));
+            if (ctx->profiling) HIP_TRY(hipEventRecord(ev.b, ctx->stream));
+        } else {
+            HIP_TRY(hipMemcpyAsync(d_cf.p, h_cf, sizeof(double) * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+            HIP_TRY(hipEventRecord(ev.a, ctx->stream));
+            HIP_TRY(launch_vt_run(A, ctx->stream));
+            HIP_TRY(hipEventRecord(ev.b, ctx->stream));
+            HIP_TRY(hipMemcpyAsync(h_out, d_out.p, sizeof(gnss_vt_out) * (size_t)n, hipMemcpyDeviceToHost,
+                                   ctx->stream));
+        }
         HIP_TRY(hipStreamSynchronize(ctx->stream));
-        kernel_ms += ev.ms();
+        if (ctx->profiling || !multi) kernel_ms += ev.ms();
         for (int i = 0; i < n; i++) {
             gnss_vt_out& o = out[(size_t)s * n + i];
             const gnss_vt_out& h = h_out[i];
@@ -1989,7 +2014,8 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     }
     HIP_TRY(hipMemcpyAsync(chans, d_chan.p, sizeof(gnss_vt_chan) * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
-    ctx->timing.track_kernel_ms = kernel_ms;
+    ctx->timing.track_kernel_ms = kernel_ms;  // (int8 records: summed in profiling mode only)
+    ctx->timing.track_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_loop).count();
     return result;
 }
 

@@ -299,6 +299,22 @@ hipError_t launch_track_expand(const double* src, int64_t rec_cap, int stride, i
                                const int64_t* job, double* dst, int64_t ML, int64_t n10, int ntaps,
                                hipStream_t s);
 
+// Timing probes (per-step wall-clock stamps, the GNSS_PROBE bits) exist only in the probe
+// builds (tools/build_probe.sh, tools/build_commit_lib.sh: -DGNSS_PROBE_BUILD=1): in the
+// product library every stamp / probe branch of the kernels folds away at compile time.
+#ifndef GNSS_PROBE_BUILD
+#define GNSS_PROBE_BUILD 0
+#endif
+constexpr bool kProbe = GNSS_PROBE_BUILD != 0;
+// A/B knobs of the tracking exchange (tools/build_variant.sh; product: 0): s_sleep between
+// the sweep's poll rounds, and a channel's blocks on one XCD (8 channels).
+#ifndef GNSS_XCHG_SLEEP
+#define GNSS_XCHG_SLEEP 0
+#endif
+#ifndef GNSS_XCD_LOCAL
+#define GNSS_XCD_LOCAL 0
+#endif
+
 constexpr int kTrkThreads = 256;
 constexpr int kArriveStride = 64;   // words: one 256-B line per counter
 constexpr int kArrivePerChan = 9;   // 8 XCD-group counters + the channel counter
@@ -577,8 +593,21 @@ struct VtRunArgs {
     const unsigned* ca_bits;  // [n][32] C/A chips as sign bits (bit set: -1)
     double Fs, ms, codelength, tau1carr, tau2carr;
     int n, nsteps, pdi, prec, dtype;
+    // launch_vt_step only: [n][nb][2] block partials, [n] arrival tickets (zero between
+    // launches: the last block of a channel resets its own), nb blocks per channel
+    double* part;
+    unsigned* ticket;
+    int nb;
+    double cf_arg[GNSS_VT_MAX_CH];  // launch_vt_step: the step's code frequencies (kernel args)
 };
 hipError_t launch_vt_run(const VtRunArgs& a, hipStream_t s);
+// One step of the n channels over n x nb blocks (int8 records; nsteps must be 1): each block
+// sums a contiguous 1/nb of the channel's read, the channel's last block to arrive adds
+// the nb partials in block order and runs the scalar end. The EKF loop's step (one launch
+// per step: the next code frequencies come from the host between steps).
+hipError_t launch_vt_step(const VtRunArgs& a, hipStream_t s);
+constexpr int kVtStepThreads = 256;
+constexpr int kVtStepSamples = 8 * kVtStepThreads;  // samples per block at the nominal read
 // generateCAcode.m's 1023 +-1 chips of `prn` (host)
 void ca_chips(int prn, float* out);
 

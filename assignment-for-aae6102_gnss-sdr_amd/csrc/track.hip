@@ -1064,7 +1064,7 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(const TrkParams
 
     g_desc* dp = (g_desc*)(b.desc + ch);  // global views: scalar loads, no flat waits
     g_chan* cp = (g_chan*)(b.chan + ch);
-    unsigned long long* srow = b.stamps && ch == 0 ? stamp_row(b) : nullptr;
+    unsigned long long* srow = kProbe && b.stamps && ch == 0 ? stamp_row(b) : nullptr;
     if (srow && tid == 0) stamp_max(srow, 8 + blk, wall_clock64());  // block start
     const int64_t g_first = dp->g_first, g_last = dp->g_last;
     const int64_t g0 = g_first + ((int64_t)blk * T + tid) * SUB;  // first group of the lane
@@ -1093,7 +1093,7 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(const TrkParams
         return;
     }
     double oI[NT], oQ[NT];
-    if (p.probe & 2) {  // timing probe: no correlation (loads, reduction and hand-off only)
+    if (kProbe && (p.probe & 2)) {  // timing probe: no correlation (loads, reduction and hand-off only)
 #pragma unroll
         for (int s = 0; s < NT; s++) { oI[s] = (double)raw[0].x; oQ[s] = 0.0; }
     } else {
@@ -1162,7 +1162,7 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(const TrkParams
     o.remPhase = dp->remPhase_next;
     o.pdi = dp->pdi;
     o.phaseC = dp->phaseC;
-    const bool dbg = b.dbg_sums || (p.probe & 1);
+    const bool dbg = b.dbg_sums || (kProbe && (p.probe & 1));
     if (tid < CL * NV && tid % CL == 0) {
         const int v = tid / CL;
         if (dbg) {
@@ -1189,7 +1189,7 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(const TrkParams
     nx.pos = s_c.pos + p.bps * o.n;
     nx.Index = s_c.Index + (o.phaseC ? 10 : 1);
     if (wv == 0 || wv == 3) {
-        if (p.probe & 8) return;
+        if (kProbe && (p.probe & 8)) return;
         if (srow && wv == 0 && lane == 0) stamp_max(srow, 5, wall_clock64());  // loop updated
         prepare_desc_i(p, nx, o.pdi, o.phaseC, wv == 0 ? 0 : 1, lane, b.desc + ch);
         if (srow && wv == 0 && lane == 0) {
@@ -1210,7 +1210,7 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(const TrkParams
                 stamp_max(srow, 2, wall_clock64());
             }
         }
-    } else if (p.probe & 4) {
+    } else if (kProbe && (p.probe & 4)) {
         return;
     } else if (wv == 1) {
         if (lane == 0) write_record_i(p, b, ch, s_c, o, u, s_fin);
@@ -1319,6 +1319,7 @@ __device__ bool sweep16(__amdgpu_buffer_rsrc_t r, int n, unsigned tag, unsigned*
             }
         }
         if (!todo) break;
+        if constexpr (GNSS_XCHG_SLEEP > 0) __builtin_amdgcn_s_sleep(GNSS_XCHG_SLEEP);  // (A/B knob)
         if (++late >= 64) {
             const unsigned long long t = wall_clock64();
             if (!t0) t0 = t;
@@ -1396,8 +1397,11 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
     // one-block-per-block form, the loop compiled away -- the headline's 8 channels.)
     const int vpb_ = VB ? vpb : 1;
     const int pbpc = (bpc + vpb_ - 1) / vpb_;
-    const int ch = blockIdx.x / pbpc;
-    const int pblk = blockIdx.x - ch * pbpc;
+    // (A/B knob GNSS_XCD_LOCAL: with 8 channels, channel = the block's XCD (blocks are dealt
+    // round-robin over the 8 XCDs), so a channel's exchange stays in one L2)
+    const bool xl = GNSS_XCD_LOCAL && !VB && p.nch == 8;
+    const int ch = xl ? (int)(blockIdx.x & 7) : (int)(blockIdx.x / pbpc);
+    const int pblk = xl ? (int)(blockIdx.x >> 3) : (int)(blockIdx.x - ch * pbpc);
     const int blk = pblk * vpb_;
     const int nvb = VB ? (bpc - blk < vpb_ ? bpc - blk : vpb_) : 1;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1463,7 +1467,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         pre_ok = false;
     };
     // timing probe: per-channel launch span in row 0, words 20 + 3 ch .. (block 0)
-    const unsigned long long t_start = wall_clock64();
+    const unsigned long long t_start = kProbe ? wall_clock64() : 0ull;
     for (int s = 0; s < nsteps; s++) {
         const StepDesc& D = s_d[cur];
         const int bad = D.bad ? D.bad : D.bad_tap;
@@ -1493,7 +1497,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         // timing probe (GNSS_STAMPS), channel 0, row s: [0] step start, [1] computed,
         // [2] partial out, [3] all partials in, [4] next descriptor ready (block 0);
         // [5..9] the same for the channel's last block
-        unsigned long long* srow = b.stamps && ch == 0 && (io || pblk == pbpc - 1)
+        unsigned long long* srow = kProbe && b.stamps && ch == 0 && (io || pblk == pbpc - 1)
                                        ? b.stamps + (size_t)(s % kStampSlots) * kStampRow + (io ? 0 : 5) : nullptr;
         if (srow && tid == 0) srow[0] = wall_clock64();
 
@@ -1505,7 +1509,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         // the launch's length).
         for (int jv = 0; jv < nvb; jv++) {
             const int vb = blk + jv;
-            switch ((p.probe & 64) ? ch % 3 : (p.probe & 128) ? 0 : (s + ch) % 3) {
+            switch ((kProbe && (p.probe & 64)) ? ch % 3 : (kProbe && (p.probe & 128)) ? 0 : (s + ch) % 3) {
             case 0: __builtin_amdgcn_s_setprio(0); break;
             case 1: __builtin_amdgcn_s_setprio(1); break;
             default: __builtin_amdgcn_s_setprio(2); break;
@@ -1528,7 +1532,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
                 if (tid < NV * 4 && (tid & 3) == 0)
                     publish16(pg, ((s & 1) * kMaxBpcRun + vb) * NV + (tid >> 2), bsum, tag0 + s + 1);
                 if (srow && tid == 0) srow[2] = wall_clock64();
-                if (b.stamps && ch == 0 && tid == 0) {  // latest partial of the channel (all blocks)
+                if (kProbe && b.stamps && ch == 0 && tid == 0) {  // latest partial of the channel (all blocks)
                     unsigned long long* r = b.stamps + (size_t)(s % kStampSlots) * kStampRow;
                     atomicMax(r + 23, wall_clock64());
                     atomicMax(r + 24, ~wall_clock64());  // (earliest, complemented)
@@ -1641,7 +1645,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         if (srow && tid == 0) srow[4] = wall_clock64();
         cur ^= 1;
     }
-    if (b.stamps && io && tid == 0 && ch < 64) {
+    if (kProbe && b.stamps && io && tid == 0 && ch < 64) {
         b.stamps[20 + 3 * ch] = t_start;
         b.stamps[21 + 3 * ch] = wall_clock64();
         b.stamps[22 + 3 * ch] = (unsigned long long)nsteps;

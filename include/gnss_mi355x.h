@@ -246,7 +246,8 @@ int  gnss_ctx_set_window(gnss_ctx *ctx, uint64_t bytes);
                                     order on one stream, 2 = pipelined over two streams
                                     (batch b's rows beside batch b+1's columns, two
                                     intermediates); 0 = the engine's choice               */
-#define GNSS_OPT_COUNT        9
+#define GNSS_OPT_VT_BLOCKS    9  /* > 0: blocks per channel of gnss_tracking_vt's step      */
+#define GNSS_OPT_COUNT        10
 int  gnss_ctx_set_option(gnss_ctx *ctx, int key, int64_t value);
 
 /* Device memory owned by the ctx, for callers that keep an IF record resident

@@ -74,11 +74,14 @@ def test_vector_tracking_closed_loop_against_oracle(pkg, po, ctx, opensky_short)
     z = V.fixture()
     Acquired, eph, sbf, ct, ns = _inputs(pkg, z, skip)
     nsteps = 1200
+    ctx.set_profiling(True)
     tck, nsol, cn0 = pkg.trackingVT_POS_updated(file, signal, track, cmn, solu, Acquired, V.cnslxyz(pkg), eph,
                                                 sbf, None, ct, ns, ctx=ctx, nsteps=nsteps, return_cn0=True)
     t = ctx.timing()
+    ctx.set_profiling(False)
     assert t["track_launches"] == nsteps
-    print(f"gnss_tracking_vt: {nsteps} steps x 5 channels, kernel {t['track_kernel_ms']:.1f} ms")
+    print(f"gnss_tracking_vt: {nsteps} steps x 5 channels, loop {t['track_ms']:.1f} ms, kernel "
+          f"{t['track_kernel_ms']:.1f} ms")
     status, rec, onav = _oracle_loop(pkg, po, z, ct, data, nsteps)
     assert status == 0
     R = {k: rec[:, :, j] for j, k in enumerate(po.VT_REC + ["deltaPr", "prRate"])}

@@ -16,6 +16,7 @@
 #   acqpipe      config-2 / config-4 acquisition timing, batches on one stream vs pipelined (tools/acq_only.py)
 #   cfg4         bench --workload cfg4 -> gpurun_out/bench_cfg4.json
 #   cfg5         bench --workload cfg5 -> gpurun_out/bench_cfg5.json
+#   vt           tools/vt_only.py: the VT loop's wall / kernel time per step -> gpurun_out/vt_only.txt
 #   cfg5pmc      the config-5 launch's PMC traffic + SQ passes -> gpurun_out/{traffic_cfg5,cfg5_sq}.json
 set -o pipefail
 mkdir -p gpurun_out
@@ -133,12 +134,26 @@ for step in "$@"; do
          # tools/probe_lib/libgnss_<name>.so; 8-channel trackingCT (1000 ms + 4000 x 10 ms), per-launch
          # hipEvents and GNSS_STAMPS of the 10-ms launch (AB_TAPS=11 AB_NCH=32: the config-5 shape)
       for v in $AB; do
-        GNSS_LIB=$R/tools/probe_lib/libgnss_$v.so TRK_PROFILE=1 TRK_ITERS=3 timeout -k 10 120 python3 tools/track_only.py 1000 40000 ${AB_TAPS:-3} ${AB_NCH:-8} > gpurun_out/ab_$v.log 2>&1 || { tail -5 gpurun_out/ab_$v.log; exit 1; }
+        GNSS_LIB=$R/tools/probe_lib/libgnss_$v.so TRK_HASH=1 TRK_PROFILE=1 TRK_ITERS=3 timeout -k 10 120 python3 tools/track_only.py 1000 40000 ${AB_TAPS:-3} ${AB_NCH:-8} > gpurun_out/ab_$v.log 2>&1 || { tail -5 gpurun_out/ab_$v.log; exit 1; }
+        echo "ab $v: $(grep -E 'track10|sha256' gpurun_out/ab_$v.log | tail -3 | tr '\n' ' ')"
+        [ -n "$AB_NOSTAMPS" ] && continue
         GNSS_LIB=$R/tools/probe_lib/libgnss_$v.so GNSS_STAMPS=gpurun_out/abst_$v.bin TRK_ITERS=1 timeout -k 10 120 python3 tools/track_only.py 1000 2000 ${AB_TAPS:-3} ${AB_NCH:-8} > /dev/null 2>&1 || exit 1
-        echo "ab $v: $(grep track10 gpurun_out/ab_$v.log | tail -2 | tr '\n' ' ')"
         python3 tools/stamps_run.py gpurun_out/abst_$v.bin | grep -E "period|computed|all partials|next desc|tail" | sed "s/^/   /"
         rm -f gpurun_out/abst_$v.bin
       done ;;
+    vt)  # vector tracking, 5 000 EKF-driven 1-ms steps of the reference's 5 channels (tools/vt_only.py)
+      timeout -k 10 300 python3 tools/vt_only.py ${VT_ARGS} > gpurun_out/vt_only.txt 2>&1 && cat gpurun_out/vt_only.txt || { tail -20 gpurun_out/vt_only.txt; exit 1; } ;;
+    vtab)  # tools/vt_only.py under each library of VTLIBS (tools/probe_lib/libgnss_<name>.so; "prod" = the
+           # product) and each VT_NB of VTNBS (blocks per channel)
+      for v in ${VTLIBS:-prod}; do for nb in ${VTNBS:-0}; do
+        L=$R/assignment-for-aae6102_gnss-sdr_amd/lib/libgnss_mi355x.so; [ "$v" != prod ] && L=$R/tools/probe_lib/libgnss_$v.so
+        GNSS_LIB=$L VT_NB=$( [ "$nb" != 0 ] && echo $nb ) timeout -k 10 120 python3 tools/vt_only.py 2000 2 > gpurun_out/vtab_${v}_$nb.txt 2>&1 \
+          && echo "vtab $v nb=$nb: $(grep '^vt ' gpurun_out/vtab_${v}_$nb.txt | tail -1 | cut -c1-110)" || { tail -5 gpurun_out/vtab_${v}_$nb.txt; exit 1; }
+      done; done ;;
+    vtprof)  # rocprofv3 kernel stats of tools/vt_only.py (1 000 steps, one iteration)
+      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/vtprof" -o run -- python3 "$R/tools/vt_only.py" 1000 1 ) > gpurun_out/vtprof.log 2>&1 || { tail -20 gpurun_out/vtprof.log; exit 1; }
+      python3 tools/prof_summary.py gpurun_out/vtprof > gpurun_out/vtprof_summary.txt && head -8 gpurun_out/vtprof_summary.txt
+      rm -f gpurun_out/vtprof/**/*kernel_trace.csv ;;
     lat)  # fp64 / fp32 dependent-latency micro-benchmark (tools/micro/lat2, built in-tree)
       timeout -k 10 60 ./tools/micro/lat2 > gpurun_out/lat2.txt 2>&1 && cat gpurun_out/lat2.txt || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;

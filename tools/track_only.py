@@ -31,3 +31,9 @@ for it in range(int(os.environ.get('TRK_ITERS', '2'))):
     tm = ctx.timing()
     print("track wall", round(time.perf_counter() - t, 4), "track10_kernel_ms", round(tm["track10_kernel_ms"], 3),
           "track_kernel_ms", round(tm["track_kernel_ms"], 3), "launches", tm["track_launches"], flush=True)
+if os.environ.get("TRK_HASH"):  # a digest of every record / tap value of the last call (A/B bit-identity)
+    import hashlib
+    h = hashlib.sha256(np.ascontiguousarray(buf.rec).tobytes())
+    if getattr(buf, "taps", None) is not None:
+        h.update(np.ascontiguousarray(buf.taps).tobytes())
+    print("records sha256", h.hexdigest()[:16], flush=True)
