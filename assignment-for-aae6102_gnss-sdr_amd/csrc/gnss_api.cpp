@@ -463,8 +463,9 @@ int acq_search(gnss_ctx* ctx, const int8_t* blk, const double2* xa, int64_t S, i
                                                    ctx->stream));
             return GNSS_OK;
         }
-        // (bin, PRN) pairs per batch: the inverse intermediate round-trips through HBM
-        // anyway (PMC, profiles/acq_traffic_r01.json), so batches of ~1 GiB, balanced (no
+        // (bin, PRN) pairs per batch: the inverse intermediate leaves the L2 either way (PMC
+        // FETCH / WRITE, which count Infinity-Cache hits too, profiles/acq_traffic_r01.json),
+        // and smaller batches measured slower, so batches of ~1 GiB, balanced (no
         // small tail batch that leaves the chip idle): config 2 (fp32) measured 7.94 ms of
         // correlation at 28 pairs per batch (256 MB), 7.09-7.29 at 112, 7.15-7.30 at 232
         // (tools/gpu_acq_batch.sh). Pairs are independent: the bits do not depend on it.

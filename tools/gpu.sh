@@ -143,6 +143,12 @@ for step in "$@"; do
       done ;;
     vt)  # vector tracking, 5 000 EKF-driven 1-ms steps of the reference's 5 channels (tools/vt_only.py)
       timeout -k 10 300 python3 tools/vt_only.py ${VT_ARGS} > gpurun_out/vt_only.txt 2>&1 && cat gpurun_out/vt_only.txt || { tail -20 gpurun_out/vt_only.txt; exit 1; } ;;
+    geom)  # the 10-ms launch by channels x lane span: GEOM="nch:sub ..." (sub 0 = the engine's), 1000 ms + 4000 x 10 ms
+      for g in ${GEOM:-1:0 1:2 1:1 8:0}; do
+        n=${g%%:*}; u=${g##*:}
+        TRK_SUB=$( [ "$u" != 0 ] && echo $u ) TRK_HASH=1 TRK_PROFILE=1 TRK_ITERS=2 timeout -k 10 120 python3 tools/track_only.py 1000 40000 3 $n > gpurun_out/geom_${n}_$u.log 2>&1 \
+          && echo "geom nch=$n sub=$u: $(grep -E 'track10|sha256' gpurun_out/geom_${n}_$u.log | tail -2 | tr '\n' ' ')" || { tail -5 gpurun_out/geom_${n}_$u.log; exit 1; }
+      done ;;
     vtab)  # tools/vt_only.py under each library of VTLIBS (tools/probe_lib/libgnss_<name>.so; "prod" = the
            # product) and each VT_NB of VTNBS (blocks per channel)
       for v in ${VTLIBS:-prod}; do for nb in ${VTNBS:-0}; do

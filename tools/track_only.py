@@ -23,6 +23,8 @@ A = SimpleNamespace(sv=np.array([cfg.sv[i].prn for i in range(nch)]), SNR=np.zer
                     codedelay=np.array(cds[:nch]), fineFreq=np.array([4.58e6 + cfg.sv[i].doppler_hz for i in range(nch)]))
 track.msToProcessCT_1ms, track.msToProcessCT_10ms = N1, N10
 taps = None if ntaps == 3 else np.array([-0.5, -0.4, -0.3, -0.2, -0.1, 0.0, 0.1, 0.2, 0.3, 0.4, 0.5])
+if os.environ.get("TRK_SUB"):  # lane span 8 * v samples (GNSS_OPT_FORCE_SUB; A/B of the lane geometry)
+    ctx.set_option(pkg.abi.OPT_FORCE_SUB, int(os.environ["TRK_SUB"]))
 if os.environ.get("TRK_PROFILE"):
     ctx.set_profiling(True)  # per-launch hipEvents: track10_kernel_ms = the 10-ms launch(es)
 for it in range(int(os.environ.get('TRK_ITERS', '2'))):
