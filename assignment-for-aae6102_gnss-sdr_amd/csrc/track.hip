@@ -760,6 +760,9 @@ struct LdsRaw {
 #ifndef GNSS_CORR_PROBE
 #define GNSS_CORR_PROBE 0
 #endif
+#ifndef GNSS_FLUSH_PROBE
+#define GNSS_FLUSH_PROBE 0  // (A/B probe: 1 = block 0 writes no record)
+#endif
 
 template <int NT, int SUB, bool DIVIDE, bool RELOAD, int FMT, class Desc, class Raw>
 __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* dp, const Raw& raw,
@@ -1327,7 +1330,19 @@ __device__ bool sweep16(__amdgpu_buffer_rsrc_t r, int n, unsigned tag, unsigned*
             late = 0;
         }
     }
-    return !__syncthreads_or(todo != 0);
+    // The closing barrier must not wait for this block's outstanding global STORES (block 0's
+    // wave 1 has just written the previous step's record there: __syncthreads' fence would
+    // hold the whole block for their completion, ~1.9 us, and block 0 would start every step
+    // last). The polls' own loads have completed (their tags were compared), the gathered
+    // words are in LDS: a wave vote through LDS and an LDS-only barrier suffice.
+    __shared__ unsigned s_vote[kTrkThreads / 64];
+    const unsigned any_left = __ballot(todo != 0) != 0ull ? 1u : 0u;
+    if ((threadIdx.x & 63) == 0) s_vote[threadIdx.x >> 6] = any_left;
+    lds_barrier();
+    unsigned v = 0;
+#pragma unroll
+    for (int w = 0; w < kTrkThreads / 64; w++) v |= s_vote[w];
+    return v == 0;
 }
 
 // Grid census (guide G16: residency is a precondition, not a given): every block
@@ -1457,7 +1472,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
     auto flush = [&]() {
         if (wv == 1) {
             if (io) {
-                if (lane == 0) write_record_i(p, b, ch, s_c, s_o, s_u, s_fin, pre_ok ? pre : nullptr);
+                if (lane == 0 && !(GNSS_FLUSH_PROBE & 1)) write_record_i(p, b, ch, s_c, s_o, s_u, s_fin, pre_ok ? pre : nullptr);
                 if (b.taps_rec && lane < NV && s_c.slot < p.rec_cap)
                     b.taps_rec[((int64_t)ch * p.rec_cap + s_c.slot) * NV + lane] = s_fin[lane];
             }
@@ -1488,6 +1503,9 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         }
         const int64_t A = uni(D.A), n = uni(D.n);
         if (pend && io && wv == 1 && lane == 0) {  // (used by the flush below, after the compute)
+            // the previous flush's dvpre store has landed before its entry is read back (the
+            // sweep's barrier no longer waits for it; a step later this wait costs nothing)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const int64_t* dvp = b.dvpre + (int64_t)ch * (p.rec_cap + 1);
             const int64_t cols = record_cols(p, s_c, s_o.phaseC);
             pre[0] = dvp[s_c.nstep];
@@ -1500,6 +1518,10 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         unsigned long long* srow = kProbe && b.stamps && ch == 0 && (io || pblk == pbpc - 1)
                                        ? b.stamps + (size_t)(s % kStampSlots) * kStampRow + (io ? 0 : 5) : nullptr;
         if (srow && tid == 0) srow[0] = wall_clock64();
+        // (probe: every block of channel 0, its step start at [40 + blk] and its correlate's end
+        // at [40 + 256 + blk] of the step's row)
+        unsigned long long* brow = kProbe && b.stamps && ch == 0 ? b.stamps + (size_t)(s % kStampSlots) * kStampRow : nullptr;
+        if (brow && tid == 0) brow[40 + blk] = wall_clock64();
 
         // ---- correlate this block's lanes (IF prefetched into s_raw). The CU's other
         // blocks (other channels) may be in their latency-bound scalar end meanwhile: the
@@ -1527,6 +1549,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
                     prefetch_raw<SUB>(iq, uni(D.g_first) + ((int64_t)(vb + 1) * T + tid) * SUB, gmax, s_raw, tid);
                 __builtin_amdgcn_s_setprio(3);
                 if (srow && tid == 0) srow[1] = wall_clock64();
+                if (brow && tid == 0) brow[40 + 256 + vb] = wall_clock64();
                 // block sum in a fixed order, published as granules
                 const double bsum = block_partial<NT>(s_mem, oI, oQ, tid);
                 if (tid < NV * 4 && (tid & 3) == 0)
@@ -1558,6 +1581,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
                      io ? 3 * 64 : 4 * 64, b.run_err, (s & 1) * kMaxBpcRun * NV))
             return;
         if (srow && tid == 0) srow[3] = wall_clock64();
+        if (brow && tid == 0) brow[40 + 512 + blk] = wall_clock64();  // (probe: this block's all-in)
         // wave 2 issues the whole block's next IF (it starts at A + n, ftell after this
         // read; the polls above would have queued behind it) and waits for it at the end
         // of the tail: the correlator waves never stall on it
@@ -1643,6 +1667,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         pend = true;
         lds_barrier();
         if (srow && tid == 0) srow[4] = wall_clock64();
+        if (brow && tid == 0) brow[40 + 768 + blk] = wall_clock64();  // (probe: this block's next step ready)
         cur ^= 1;
     }
     if (kProbe && b.stamps && io && tid == 0 && ch < 64) {

@@ -11,6 +11,11 @@ SRC=${SRC:-track}
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -pthread -Wall -Wno-unused-function "$@" \
   -c $SRC.hip -o /tmp/gnss_variant_obj/${SRC}_$NAME.o
 OBJS=$(ls ../build/*.o | grep -v "/$SRC.o$")
+if [ -n "$PROBE" ]; then  # PROBE=1: the host side's probe hooks too (GNSS_STAMPS, GNSS_PROBE environment)
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -pthread -DGNSS_PROBE_BUILD=1 \
+    -c gnss_api.cpp -o /tmp/gnss_variant_obj/gnss_api_$NAME.o
+  OBJS="$(echo $OBJS | tr ' ' '\n' | grep -v '/gnss_api.o$' | tr '\n' ' ') /tmp/gnss_variant_obj/gnss_api_$NAME.o"
+fi
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../tools/probe_lib/libgnss_$NAME.so \
   /tmp/gnss_variant_obj/${SRC}_$NAME.o $OBJS -L/opt/rocm/lib -lrocfft -pthread -Wl,-rpath,/opt/rocm/lib
 echo "built tools/probe_lib/libgnss_$NAME.so"

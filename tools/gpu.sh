@@ -149,6 +149,19 @@ for step in "$@"; do
         TRK_SUB=$( [ "$u" != 0 ] && echo $u ) TRK_HASH=1 TRK_PROFILE=1 TRK_ITERS=2 timeout -k 10 120 python3 tools/track_only.py 1000 40000 3 $n > gpurun_out/geom_${n}_$u.log 2>&1 \
           && echo "geom nch=$n sub=$u: $(grep -E 'track10|sha256' gpurun_out/geom_${n}_$u.log | tail -2 | tr '\n' ' ')" || { tail -5 gpurun_out/geom_${n}_$u.log; exit 1; }
       done ;;
+    xstamps)  # per-block stamps + SQ counters of probe-build variants (AB="pspread pxl"): tools/stamps_blocks.py
+      for v in $AB; do
+        L=$R/tools/probe_lib/libgnss_$v.so
+        GNSS_LIB=$L GNSS_STAMPS=gpurun_out/xst_$v.bin TRK_ITERS=1 timeout -k 10 120 python3 tools/track_only.py 1000 2000 > gpurun_out/xst_$v.log 2>&1 || { tail -5 gpurun_out/xst_$v.log; exit 1; }
+        echo "== $v"; python3 tools/stamps_run.py gpurun_out/xst_$v.bin | grep -E "period|computed|all partials|next desc|tail:" | sed "s/^/   /"
+        python3 tools/stamps_blocks.py gpurun_out/xst_$v.bin 96 | sed "s/^/   /"
+        rm -f gpurun_out/xst_$v.bin
+        GNSS_LIB=$L pmc xsq1_$v "$SQ1" python3 "$R/tools/track_only.py" 1000 400 || exit 1
+        GNSS_LIB=$L pmc xsq2_$v "$SQ2" python3 "$R/tools/track_only.py" 1000 400 || exit 1
+        python3 tools/pmc_sq.py gpurun_out/xsq_$v.json gpurun_out/xsq1_$v gpurun_out/xsq2_$v -- "track_run_kernel<3, 3, false, false>" > /dev/null || exit 1
+        python3 -c "import json; d=json.load(open('gpurun_out/xsq_$v.json')); k=[x for x in d if not x.startswith('_')][0]; print('   SQ', {c: round(w['median_per_dispatch']) for c, w in d[k].items() if isinstance(w, dict) and 'median_per_dispatch' in w})" | cut -c1-1200
+        rm -f gpurun_out/xsq*_$v/**/*kernel_trace.csv
+      done ;;
     vtab)  # tools/vt_only.py under each library of VTLIBS (tools/probe_lib/libgnss_<name>.so; "prod" = the
            # product) and each VT_NB of VTNBS (blocks per channel)
       for v in ${VTLIBS:-prod}; do for nb in ${VTNBS:-0}; do
