@@ -54,6 +54,7 @@ __device__ __forceinline__ double uni(double v) { return __longlong_as_double(un
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const i32x4 g_i32x4;
 typedef __attribute__((address_space(1))) double g_dbl;
+typedef __attribute__((address_space(1))) long long g_i64;
 typedef __attribute__((address_space(1))) unsigned g_u32;
 typedef __attribute__((address_space(1))) unsigned long long g_u64;
 typedef __attribute__((address_space(1))) const StepDesc g_desc;
@@ -579,38 +580,51 @@ __device__ __forceinline__ int64_t record_cols(const TrkParams& p, const TrkChan
 }
 
 // `pre`, when given, holds dvpre[nstep] and dvpre[cols] loaded ahead by the caller.
+// part (the persistent loop splits a step's record over two blocks, each writing its half
+// while the exchange is in flight, so neither becomes the step's last block; every block holds
+// the same state): 1 = the sums and the codedelay bookkeeping (delayValue prefix sums, `pre`),
+// 2 = the loop / NCO fields, the mod() fields and the 1-ms P_i series; 3 = all.
 __device__ __forceinline__ void write_record_i(const TrkParams& p, const TrkBuffers& b, int ch, const TrkChan& c,
                              const StepOut& o, const LoopUpd& u, const double* s,
-                             const int64_t* pre = nullptr)
+                             const int64_t* pre = nullptr, int part = 3)
 {
     const double P_i = s[2 * p.iP], P_q = s[2 * p.iP + 1];
-    const int64_t pos = c.pos + p.bps * o.n;  // ftell after fread
-    const int64_t col = c.nstep;          // 0-based IndexSmall - 1
-    int64_t* dvpre = b.dvpre + (int64_t)ch * (p.rec_cap + 1);
-    const int64_t dvsum = (pre ? pre[0] : dvpre[col]) + o.delayValue;
-    dvpre[col + 1] = dvsum;
-    const int64_t nstep = col + 1;
-    // sum(delayValue(1:Index)) over an nsv x N matrix (column-major, quirk A.11)
-    const int64_t cols = record_cols(p, c, o.phaseC);
-    const double codedelay =
-        (double)c.codedelay0 + (double)(cols == nstep ? dvsum : (pre ? pre[1] : dvpre[cols]));
-    const double absS = (double)pos;
-    const double m = fmod_pos(absS / p.dataBytesPerSample, p.Fs * p.ms);  // mod() of positives
     const int64_t slot = c.slot;
-    if (slot < p.rec_cap) {
-        double* r = b.rec + ((int64_t)ch * p.rec_cap + slot) * GNSS_NFIELDS;
-        r[GNSS_F_P_i] = P_i;                     r[GNSS_F_P_q] = P_q;
-        r[GNSS_F_E_i] = s[2 * p.iE];             r[GNSS_F_E_q] = s[2 * p.iE + 1];
-        r[GNSS_F_L_i] = s[2 * p.iL];             r[GNSS_F_L_q] = s[2 * p.iL + 1];
-        r[GNSS_F_PLLdiscri] = u.PLLdiscri;       r[GNSS_F_DLLdiscri] = u.DLLdiscri;
-        r[GNSS_F_codedelay] = codedelay;         r[GNSS_F_remChip] = o.remChip;
-        r[GNSS_F_codeFreq] = u.codeFreq;         r[GNSS_F_carrierFreq] = u.carrierFreq;
-        // (trackingCT_POS_updated.m:289 has no remSample: the slot holds absoluteSampleCodedelay)
-        r[GNSS_F_remPhase] = o.remPhase;         r[GNSS_F_remSample] = p.conv ? m : o.remSample;
-        r[GNSS_F_numSample] = (double)o.n;       r[GNSS_F_delayValue] = (double)o.delayValue;
-        r[GNSS_F_absoluteSample] = absS;         r[GNSS_F_codedelay2] = m;
+    // global-address-space views: flat stores count on lgkmcnt too, so every LDS wait after
+    // one (s_fin, the state) would wait for the store's completion
+    g_dbl* r = (g_dbl*)(b.rec + ((int64_t)ch * p.rec_cap + slot) * GNSS_NFIELDS);
+    if (part & 1) {
+        const int64_t col = c.nstep;          // 0-based IndexSmall - 1
+        g_i64* dvpre = (g_i64*)(b.dvpre + (int64_t)ch * (p.rec_cap + 1));
+        const int64_t dvsum = (pre ? pre[0] : dvpre[col]) + o.delayValue;
+        dvpre[col + 1] = dvsum;
+        const int64_t nstep = col + 1;
+        // sum(delayValue(1:Index)) over an nsv x N matrix (column-major, quirk A.11)
+        const int64_t cols = record_cols(p, c, o.phaseC);
+        const double codedelay =
+            (double)c.codedelay0 + (double)(cols == nstep ? dvsum : (pre ? pre[1] : dvpre[cols]));
+        if (slot < p.rec_cap) {
+            r[GNSS_F_P_i] = P_i;                     r[GNSS_F_P_q] = P_q;
+            r[GNSS_F_E_i] = s[2 * p.iE];             r[GNSS_F_E_q] = s[2 * p.iE + 1];
+            r[GNSS_F_L_i] = s[2 * p.iL];             r[GNSS_F_L_q] = s[2 * p.iL + 1];
+            r[GNSS_F_codedelay] = codedelay;
+        }
     }
-    if (!o.phaseC && slot < b.n1) b.p_i_1ms[(int64_t)ch * b.n1 + slot] = P_i;
+    if (part & 2) {
+        const int64_t pos = c.pos + p.bps * o.n;  // ftell after fread
+        const double absS = (double)pos;
+        const double m = fmod_pos(absS / p.dataBytesPerSample, p.Fs * p.ms);  // mod() of positives
+        if (slot < p.rec_cap) {
+            r[GNSS_F_PLLdiscri] = u.PLLdiscri;       r[GNSS_F_DLLdiscri] = u.DLLdiscri;
+            r[GNSS_F_remChip] = o.remChip;
+            r[GNSS_F_codeFreq] = u.codeFreq;         r[GNSS_F_carrierFreq] = u.carrierFreq;
+            // (trackingCT_POS_updated.m:289 has no remSample: the slot holds absoluteSampleCodedelay)
+            r[GNSS_F_remPhase] = o.remPhase;         r[GNSS_F_remSample] = p.conv ? m : o.remSample;
+            r[GNSS_F_numSample] = (double)o.n;       r[GNSS_F_delayValue] = (double)o.delayValue;
+            r[GNSS_F_absoluteSample] = absS;         r[GNSS_F_codedelay2] = m;
+        }
+        if (!o.phaseC && slot < b.n1) ((g_dbl*)b.p_i_1ms)[(int64_t)ch * b.n1 + slot] = P_i;
+    }
 }
 // out-of-line copy for the persistent kernel (keeps its register budget)
 __device__ __noinline__ void write_record(const TrkParams& p, const TrkBuffers& b, int ch, const TrkChan& c, const StepOut& o, const LoopUpd& u, const double* s)
@@ -691,7 +705,7 @@ __device__ __forceinline__ void update_state_inplace(const TrkParams& p, const T
 #pragma unroll
             for (int k = 0; k < 20; k++) Z[k] = c.Zk[k];
             const double cn = cn0_estimate(Z, 1 * p.ms * o.pdi);
-            double* cn0 = o.phaseC ? b.cn0_10 : b.cn0_1;
+            g_dbl* cn0 = (g_dbl*)(o.phaseC ? b.cn0_10 : b.cn0_1);
             if (snrIndex <= p.cn0_cap) cn0[(int64_t)ch * p.cn0_cap + snrIndex - 1] = cn;
         }
         index_int = 0;
@@ -1469,14 +1483,31 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
     // The pending step's side effects, by wave 1 while the next step's partials are in
     // flight (off the critical path): the state replica (every block, in place) and, in
     // block 0, the record, C/N0 and taps.
+    // The record's halves, the taps and the C/N0 value go to three different blocks (one when
+    // the channel has one), so that no block's flush outlasts the exchange it overlaps: one
+    // block doing all of it measured ~1.7 us, and that block then started every step last
+    // (profiles/r04_block0_lateness.txt).
+    const int duty_b = pbpc > 1 ? 1 : 0, duty_c = pbpc > 2 ? 2 : duty_b;
+    int s_now = 0;  // (probe stamps of the flush)
     auto flush = [&]() {
         if (wv == 1) {
-            if (io) {
-                if (lane == 0 && !(GNSS_FLUSH_PROBE & 1)) write_record_i(p, b, ch, s_c, s_o, s_u, s_fin, pre_ok ? pre : nullptr);
-                if (b.taps_rec && lane < NV && s_c.slot < p.rec_cap)
-                    b.taps_rec[((int64_t)ch * p.rec_cap + s_c.slot) * NV + lane] = s_fin[lane];
+            // (probe GNSS_FLUSH_PROBE & 2: block 0's record part twice, stamped at [2000..2002]
+            // of the step's row: cold, then warm)
+            unsigned long long* fr = kProbe && (GNSS_FLUSH_PROBE & 2) && b.stamps && ch == 0 && io && lane == 0
+                                         ? b.stamps + (size_t)(s_now % kStampSlots) * kStampRow : nullptr;
+            if (fr) fr[2000] = wall_clock64();
+            if (lane == 0 && !(GNSS_FLUSH_PROBE & 1)) {
+                if (io) write_record_i(p, b, ch, s_c, s_o, s_u, s_fin, pre_ok ? pre : nullptr, duty_b == 0 ? 3 : 1);
+                else if (pblk == duty_b) write_record_i(p, b, ch, s_c, s_o, s_u, s_fin, nullptr, 2);
             }
-            if (lane == 0) update_state_inplace(p, b, ch, s_c, s_o, s_u, s_fin, io);
+            if (fr) {
+                fr[2001] = wall_clock64();
+                write_record_i(p, b, ch, s_c, s_o, s_u, s_fin, pre_ok ? pre : nullptr, 3);
+                fr[2002] = wall_clock64();
+            }
+            if (pblk == duty_b && b.taps_rec && lane < NV && s_c.slot < p.rec_cap)
+                ((g_dbl*)b.taps_rec)[((int64_t)ch * p.rec_cap + s_c.slot) * NV + lane] = s_fin[lane];
+            if (lane == 0) update_state_inplace(p, b, ch, s_c, s_o, s_u, s_fin, pblk == duty_c);
         }
         pend = false;
         pre_ok = false;
@@ -1484,6 +1515,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
     // timing probe: per-channel launch span in row 0, words 20 + 3 ch .. (block 0)
     const unsigned long long t_start = kProbe ? wall_clock64() : 0ull;
     for (int s = 0; s < nsteps; s++) {
+        s_now = s;
         const StepDesc& D = s_d[cur];
         const int bad = D.bad ? D.bad : D.bad_tap;
         const bool stop = !D.phaseC && D.Index + 1 > n1_target;  // 1-ms run of this channel done
@@ -1506,7 +1538,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
             // the previous flush's dvpre store has landed before its entry is read back (the
             // sweep's barrier no longer waits for it; a step later this wait costs nothing)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const int64_t* dvp = b.dvpre + (int64_t)ch * (p.rec_cap + 1);
+            const g_i64* dvp = (const g_i64*)(b.dvpre + (int64_t)ch * (p.rec_cap + 1));  // (global loads: see write_record_i)
             const int64_t cols = record_cols(p, s_c, s_o.phaseC);
             pre[0] = dvp[s_c.nstep];
             pre[1] = cols < s_c.nstep + 1 ? dvp[cols] : 0;

@@ -53,3 +53,9 @@ if m.any():
     print(f"  tail (all-in -> ready): blk0 {np.median(rd[:, 0] - ai[:, 0]) * us:.2f}, others {np.median(rd[:, 1:] - ai[:, 1:]) * us:.2f}")
     ai_late = np.argsort(np.median(ai - ai.min(1, keepdims=True), axis=0))[::-1][:6]
     print("  latest all-in: " + ", ".join(f"blk {b} +{np.median(ai[:, b] - ai.min(1)) * us:.2f}" for b in ai_late))
+# (GNSS_FLUSH_PROBE & 2 builds) block 0's record part cold, then the whole record again warm
+f0, f1, f2 = a[:, 2000], a[:, 2001], a[:, 2002]
+m = (f0 > 0) & (f1 > 0) & (f2 > 0)
+if m.any():
+    print(f"  blk0 record: first (cold) {np.median((f1 - f0)[m]) * us:.2f} us, again (warm, all fields) "
+          f"{np.median((f2 - f1)[m]) * us:.2f} us")
