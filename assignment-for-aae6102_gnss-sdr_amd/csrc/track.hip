@@ -1597,7 +1597,8 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
 
         // the step's remPhase / remSample (role 2 of the descriptor, off the tail: the
         // next tail reads them after the sweep's closing barrier)
-        if (wv == 1 && lane == 0) desc_rem(tk, &s_d[cur]);
+        // (by wave 2, a poller, so that wave 1's flush of the previous step starts at once)
+        if (wv == 2 && lane == 0) desc_rem(tk, &s_d[cur]);
         if (pend) {
             if (srow && tid == 64) srow[16] = wall_clock64();
             flush();  // (the sweep's closing barrier publishes it)
