@@ -774,6 +774,9 @@ struct LdsRaw {
 #ifndef GNSS_CORR_PROBE
 #define GNSS_CORR_PROBE 0
 #endif
+#ifndef GNSS_SWEEP_IO_ALL
+#define GNSS_SWEEP_IO_ALL 0  // (A/B: block 0's wave 1 polls after its flush, as the other blocks' do)
+#endif
 #ifndef GNSS_FLUSH_PROBE
 #define GNSS_FLUSH_PROBE 0  // (A/B probe: 1 = block 0 writes no record)
 #endif
@@ -1610,8 +1613,8 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         // (waves 0, 2, 3 poll; wave 1 is flushing the previous step meanwhile)
         // (block 0: waves 0, 2, 3 poll while wave 1 writes the record; the other blocks'
         // wave 1 flush is short and it joins the polling after it)
-        if (!sweep16(pg, bpc * NV, tag0 + s + 1, pw, io ? (wv == 1 ? -1 : tid - (wv > 1 ? 64 : 0)) : tid,
-                     io ? 3 * 64 : 4 * 64, b.run_err, (s & 1) * kMaxBpcRun * NV))
+        if (!sweep16(pg, bpc * NV, tag0 + s + 1, pw, GNSS_SWEEP_IO_ALL || !io ? tid : (wv == 1 ? -1 : tid - (wv > 1 ? 64 : 0)),
+                     GNSS_SWEEP_IO_ALL || !io ? 4 * 64 : 3 * 64, b.run_err, (s & 1) * kMaxBpcRun * NV))
             return;
         if (srow && tid == 0) srow[3] = wall_clock64();
         if (brow && tid == 0) brow[40 + 512 + blk] = wall_clock64();  // (probe: this block's all-in)
