@@ -1476,6 +1476,10 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         s_post[tid] = p.tap_post[tid];
     }
     __syncthreads();
+    // block 0, wave 1, lane 0: dvpre[s_c.nstep], the running delayValue prefix its flushes
+    // extend (no read-back of its own stores)
+    int64_t dvrun = 0;
+    if (io && wv == 1 && lane == 0) dvrun = ((const g_i64*)(b.dvpre + (int64_t)ch * (p.rec_cap + 1)))[s_c.nstep];
     if (!s_d[0].bad && !s_d[0].bad_tap)
         prefetch_raw<SUB>(iq, s_d[0].g_first + ((int64_t)blk * T + tid) * SUB, gmax, s_raw, tid);
 
@@ -1500,12 +1504,22 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
                                          ? b.stamps + (size_t)(s_now % kStampSlots) * kStampRow : nullptr;
             if (fr) fr[2000] = wall_clock64();
             if (lane == 0 && !(GNSS_FLUSH_PROBE & 1)) {
-                if (io) write_record_i(p, b, ch, s_c, s_o, s_u, s_fin, pre_ok ? pre : nullptr, duty_b == 0 ? 3 : 1);
+                if (io) {
+                    if (!pre_ok) {  // (a launch's last flush: the column's prefix read here)
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        const g_i64* dvp = (const g_i64*)(b.dvpre + (int64_t)ch * (p.rec_cap + 1));
+                        const int64_t cols = record_cols(p, s_c, s_o.phaseC);
+                        pre[1] = cols < s_c.nstep + 1 ? dvp[cols] : 0;
+                    }
+                    pre[0] = dvrun;
+                    write_record_i(p, b, ch, s_c, s_o, s_u, s_fin, pre, duty_b == 0 ? 3 : 1);
+                    dvrun += s_o.delayValue;  // = dvpre[nstep + 1], the value just stored
+                }
                 else if (pblk == duty_b) write_record_i(p, b, ch, s_c, s_o, s_u, s_fin, nullptr, 2);
             }
             if (fr) {
                 fr[2001] = wall_clock64();
-                write_record_i(p, b, ch, s_c, s_o, s_u, s_fin, pre_ok ? pre : nullptr, 3);
+                write_record_i(p, b, ch, s_c, s_o, s_u, s_fin, pre, 3);
                 fr[2002] = wall_clock64();
             }
             if (pblk == duty_b && b.taps_rec && lane < NV && s_c.slot < p.rec_cap)
@@ -1537,16 +1551,6 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
             return;
         }
         const int64_t A = uni(D.A), n = uni(D.n);
-        if (pend && io && wv == 1 && lane == 0) {  // (used by the flush below, after the compute)
-            // the previous flush's dvpre store has landed before its entry is read back (the
-            // sweep's barrier no longer waits for it; a step later this wait costs nothing)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const g_i64* dvp = (const g_i64*)(b.dvpre + (int64_t)ch * (p.rec_cap + 1));  // (global loads: see write_record_i)
-            const int64_t cols = record_cols(p, s_c, s_o.phaseC);
-            pre[0] = dvp[s_c.nstep];
-            pre[1] = cols < s_c.nstep + 1 ? dvp[cols] : 0;
-            pre_ok = true;
-        }
         // timing probe (GNSS_STAMPS), channel 0, row s: [0] step start, [1] computed,
         // [2] partial out, [3] all partials in, [4] next descriptor ready (block 0);
         // [5..9] the same for the channel's last block
@@ -1578,6 +1582,16 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
                 lane_correlate<NT, SUB, DIVIDE, true, 0>(p, &D, LdsRaw{s_raw + tid}, 8 * g0 - A, cabits,
                                                       reinterpret_cast<double2*>(s_mem) + tid, &s_zero, oI, oQ);
                 __syncthreads();  // slots and s_raw free
+                if (pend && io && wv == 1 && lane == 0 && jv == 0) {
+                    // the pending record's older delayValue prefix (quirk A.11's column), loaded
+                    // here and not at the step's start: an outstanding load there held this
+                    // wave at the correlate's vmcnt(0) wait (its IF landed long before)
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the last flush's stores)
+                    const g_i64* dvp = (const g_i64*)(b.dvpre + (int64_t)ch * (p.rec_cap + 1));
+                    const int64_t cols = record_cols(p, s_c, s_o.phaseC);
+                    pre[1] = cols < s_c.nstep + 1 ? dvp[cols] : 0;
+                    pre_ok = true;
+                }
                 // the next virtual block's IF, every lane its own groups (waited for at the
                 // top of its iteration), in flight during this block's reduction
                 if (VB && jv + 1 < nvb)
