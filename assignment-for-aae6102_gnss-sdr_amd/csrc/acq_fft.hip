@@ -514,7 +514,14 @@ __global__ __launch_bounds__(kColThreads) void fwd_cols_kernel(const V* __restri
 // ---- I1: inverse columns of Z = C_p .* conj(X_{ms,bin}) for transform t = (pair, ms)
 // of this batch; pair q = first_pair + t / datalen -> bin = q / nprn, p = q % nprn.
 template <int P, class V>
-__global__ __launch_bounds__(kColThreads) void inv_cols_kernel(
+#ifndef GNSS_INVCOLS_WPE
+#define GNSS_INVCOLS_WPE 0  // (A/B: waves per EU asked of inv_cols; 0 = the compiler's choice)
+#endif
+__global__ __launch_bounds__(kColThreads)
+#if GNSS_INVCOLS_WPE > 0
+__attribute__((amdgpu_waves_per_eu(GNSS_INVCOLS_WPE, GNSS_INVCOLS_WPE)))
+#endif
+void inv_cols_kernel(
     const V* __restrict__ C, const V* __restrict__ X, int nbins, int nprn, int datalen,
     int first_pair, const V* __restrict__ tw_col, V* __restrict__ A)
 {

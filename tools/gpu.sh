@@ -162,6 +162,14 @@ for step in "$@"; do
         python3 -c "import json; d=json.load(open('gpurun_out/xsq_$v.json')); k=[x for x in d if not x.startswith('_')][0]; print('   SQ', {c: round(w['median_per_dispatch']) for c, w in d[k].items() if isinstance(w, dict) and 'median_per_dispatch' in w})" | cut -c1-1200
         rm -f gpurun_out/xsq*_$v/**/*kernel_trace.csv
       done ;;
+    acqlib)  # config-2 acquisition (tools/acq_only.py, fp64) under each library of ACQLIBS (tools/probe_lib/libgnss_<name>.so,
+             # "prod" = the product): correlation ms of the three calls and a digest of the decisions
+      for v in ${ACQLIBS:-prod}; do
+        L=$R/assignment-for-aae6102_gnss-sdr_amd/lib/libgnss_mi355x.so; [ "$v" != prod ] && L=$R/tools/probe_lib/libgnss_$v.so
+        GNSS_LIB=$L timeout -k 10 200 python3 tools/acq_only.py > gpurun_out/acqlib_$v.txt 2>&1 \
+          && echo "acqlib $v: corr_ms $(grep -o "'acq_corr_ms': [0-9.]*" gpurun_out/acqlib_$v.txt | cut -d' ' -f2 | tr '\n' ' ') acq_ms $(grep -o "'acq_ms': [0-9.]*" gpurun_out/acqlib_$v.txt | cut -d' ' -f2 | tr '\n' ' ') $(grep -E '^(fbin|snr|sv)' gpurun_out/acqlib_$v.txt | md5sum | cut -c1-8)" \
+          || { tail -20 gpurun_out/acqlib_$v.txt; exit 1; }
+      done ;;
     vtab)  # tools/vt_only.py under each library of VTLIBS (tools/probe_lib/libgnss_<name>.so; "prod" = the
            # product) and each VT_NB of VTNBS (blocks per channel)
       for v in ${VTLIBS:-prod}; do for nb in ${VTNBS:-0}; do
