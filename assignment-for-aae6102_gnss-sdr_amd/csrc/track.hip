@@ -774,6 +774,9 @@ struct LdsRaw {
 #ifndef GNSS_CORR_PROBE
 #define GNSS_CORR_PROBE 0
 #endif
+#ifndef GNSS_IO_DR_WAVE
+#define GNSS_IO_DR_WAVE 2  // (A/B: the wave of block 0 that runs the remPhase role)
+#endif
 #ifndef GNSS_SWEEP_IO_ALL
 #define GNSS_SWEEP_IO_ALL 0  // (A/B: block 0's wave 1 polls after its flush, as the other blocks' do)
 #endif
@@ -1615,7 +1618,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         // the step's remPhase / remSample (role 2 of the descriptor, off the tail: the
         // next tail reads them after the sweep's closing barrier)
         // (by wave 2, a poller, so that wave 1's flush of the previous step starts at once)
-        if (wv == 2 && lane == 0) desc_rem(tk, &s_d[cur]);
+        if (wv == (io ? GNSS_IO_DR_WAVE : 2) && lane == 0) desc_rem(tk, &s_d[cur]);
         if (pend) {
             if (srow && tid == 64) srow[16] = wall_clock64();
             flush();  // (the sweep's closing barrier publishes it)

@@ -26,7 +26,7 @@ pytestmark = pytest.mark.gpu
 S = 58000
 
 
-def _inputs(pkg, z, skip):
+def _inputs(pkg, z, skip, bps=2):
     """The reference-shaped arguments of trackingVT_POS_updated (SDR_main.m:99) for the
     synthetic record: Acquired, eph, sbf, TckResultCT (3000 rows; row msStartTckVT = 3000 holds
     the reference's state, absoluteSample moved onto the scene), navSolutionsCT."""
@@ -50,21 +50,43 @@ def _inputs(pkg, z, skip):
             a[-3:] = z["ct_" + f][i]
             setattr(e, f, a)
         e.absoluteSample = np.zeros(3000)
-        e.absoluteSample[-1] = (S - scene[p] + 1 + skip * S) * 2
+        e.absoluteSample[-1] = (S - scene[p] + 1 + skip * S) * bps
         ct[p] = e
     ns = SimpleNamespace(**{k: z["navSolCT_" + k] for k in ("usrPos", "usrVel", "clkBias", "clkDrift",
                                                           "timeTransmit")})
     return Acquired, eph, sbf, ct, ns
 
 
-def _oracle_loop(pkg, po, z, ct, data, nsteps):
+def _oracle_loop(pkg, po, z, ct, data, nsteps, prec=1, dtype=2):
     prns = [int(p) for p in z["prns"]]
     st = np.stack([po.vt_state(ct[p].absoluteSample[-1], ct[p].remChip[-1], ct[p].remCarrPhase[-1],
                                ct[p].codeFreq[-1], ct[p].carrFreq[-1], ct[p].carrFreq[-1], 0.0,
                                ct[p].carrError[-1]) for p in prns])
     onav = V.oracle_nav(pkg, po, z)
-    status, rec, nav = onav.tracking(np.ascontiguousarray(data, dtype=np.int8), st, prns, nsteps)
+    status, rec, nav = onav.tracking(np.ascontiguousarray(data).view(np.int8), st, prns, nsteps, prec=prec,
+                                     dtype=dtype)
     return status, rec, nav
+
+
+def _compare(pkg, po, z, tck, nsol, rec, onav, tol_sum=1e-9):
+    """The closed loops side by side: read sizes / offsets / codedelay / sv_vel exact, sums within
+    tol_sum of |P|, code frequency within 1e-12 relative, the EKF state within 10 um."""
+    R = {k: rec[:, :, j] for j, k in enumerate(po.VT_REC + ["deltaPr", "prRate"])}
+    worst = 0.0
+    for i, p in enumerate(int(x) for x in z["prns"]):
+        g = tck(p)
+        assert np.array_equal(g.absoluteSample, R["absoluteSample"][:, i]), p
+        assert np.array_equal(g.codedelay, R["codedelay"][:, i]), p
+        assert np.array_equal(g.sv_vel, rec[:, i, 20:23]), p
+        scale = np.maximum(np.maximum(np.abs(R["P_i"][:, i]), np.abs(R["P_q"][:, i])), 1.0)
+        for f in ("P_i", "P_q"):
+            worst = max(worst, float(np.max(np.abs(getattr(g, f) - R[f][:, i]) / scale)))
+        assert np.allclose(g.codeFreq, R["codeFreq"][:, i], rtol=1e-12, atol=0), p
+        assert np.allclose(g.deltaPr, R["deltaPr"][:, i], rtol=0, atol=1e-4), p
+    assert worst < tol_sum, worst
+    assert np.allclose(nsol.usrPos, onav[:, :3], rtol=0, atol=1e-5)
+    assert np.allclose(nsol.clkBias, onav[:, 6], rtol=0, atol=1e-5)
+    return worst
 
 
 def test_vector_tracking_closed_loop_against_oracle(pkg, po, ctx, opensky_short):
@@ -147,3 +169,42 @@ def test_vector_tracking_stops_past_eof(pkg, ctx, opensky_short):
     tck, nsol = pkg.trackingVT_POS_updated(file, signal, track, cmn, solu, Acquired, V.cnslxyz(pkg), eph, sbf,
                                            None, ct, ns, ctx=ctx, nsteps=10)
     assert nsol.usrPos.shape == (10, 3)
+
+
+@pytest.mark.parametrize("prec,dtyp", [(2, 2), (1, 1)], ids=["int16-iq", "int8-real"])
+def test_vector_tracking_formats(pkg, po, ctx, opensky_short, prec, dtyp):
+    """The EKF-driven loop on the other record formats of :163-176 (int16 I/Q with each read's
+    means removed: the one-block-per-channel step; int8 real: the multi-block step), 300 steps
+    against the oracle's closed loop on the same bytes."""
+    skip, cfg, data = opensky_short
+    rec8 = pkg.synth.convert_record(data, prec, dtyp)
+    file = SimpleNamespace(skip=skip, dataType=dtyp, dataPrecision=prec, data=rec8, fileRoute=None, dev=None,
+                           skiptimeVT=100)
+    _, signal, _, track, solu, cmn = pkg.initParameters()
+    z = V.fixture()
+    Acquired, eph, sbf, ct, ns = _inputs(pkg, z, skip, bps=prec * dtyp)
+    nsteps = 300
+    tck, nsol = pkg.trackingVT_POS_updated(file, signal, track, cmn, solu, Acquired, V.cnslxyz(pkg), eph, sbf,
+                                           None, ct, ns, ctx=ctx, nsteps=nsteps)
+    status, rec, onav = _oracle_loop(pkg, po, z, ct, rec8, nsteps, prec=prec, dtype=dtyp)
+    assert status == 0
+    print(prec, dtyp, "worst sum / |P|", _compare(pkg, po, z, tck, nsol, rec, onav))
+
+
+@pytest.mark.parametrize("nb", [1, 7, 64])
+def test_vector_tracking_step_blocks(pkg, po, ctx, opensky_short, opts, nb):
+    """The multi-block step (vt_step_kernel) at other block counts per channel
+    (GNSS_OPT_VT_BLOCKS; the engine's is 29): another fixed association of the same per-sample
+    terms, the same loop against the oracle."""
+    skip, cfg, data = opensky_short
+    file, signal, acq, track = params(pkg, skip, data)
+    _, _, _, _, solu, cmn = pkg.initParameters()
+    z = V.fixture()
+    Acquired, eph, sbf, ct, ns = _inputs(pkg, z, skip)
+    opts(pkg.abi.OPT_VT_BLOCKS, nb)
+    nsteps = 300
+    tck, nsol = pkg.trackingVT_POS_updated(file, signal, track, cmn, solu, Acquired, V.cnslxyz(pkg), eph, sbf,
+                                           None, ct, ns, ctx=ctx, nsteps=nsteps)
+    status, rec, onav = _oracle_loop(pkg, po, z, ct, data, nsteps)
+    assert status == 0
+    print(nb, "worst sum / |P|", _compare(pkg, po, z, tck, nsol, rec, onav))
