@@ -2,7 +2,7 @@
 its record (HIP generator, skip 5000 ms), the config-2 acquisition of it and the config-3
 trackingCT of all 8 acquired channels (1000 ms @1 ms + countinx + 40 000 ms @10 ms: the
 persistent 10-ms loop's 4 000 closed-loop steps) -- against the oracle's run of the same
-record for two channels (tests/golden/golden_track_long.npz, made on the GPU box by
+record for every channel in the golden (all 8 from round 4; two before) (tests/golden/golden_track_long.npz, made on the GPU box by
 tests/golden/make_golden_long.py; the record's xxh64 digest proves the bytes are the same).
 Integer fields bit-exact over all ~5 000 distinct steps, P/E/L within 1e-8 of the series
 RMS (north-star 1e-5), NCO state 1e-7 relative, C/N0 1e-6 dB."""
