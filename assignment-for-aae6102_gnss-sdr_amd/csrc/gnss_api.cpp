@@ -1185,7 +1185,7 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
     // blocks in turn -- the lane geometry and so the bits stay those of bpc blocks.
     // GNSS_OPT_FORCE_VPB (test hook) asks for at least that many.
     auto vpb_for = [&](int pdi, int sub) {
-        if (ctx->opt[GNSS_OPT_NO_PERSIST] || P.fmt != 0 || bpc_for(pdi, sub) > kMaxBpcRun) return 0;
+        if (ctx->opt[GNSS_OPT_NO_PERSIST] || P.fmt != 0 || bpc_for(pdi, sub) > run_bpc_cap(P.ntaps)) return 0;
         const int bpc = bpc_for(pdi, sub);
         int v0 = 1;
         if (ctx->opt[GNSS_OPT_FORCE_VPB] > 0) v0 = (int)std::min<int64_t>(ctx->opt[GNSS_OPT_FORCE_VPB], kMaxVpb);

@@ -321,6 +321,9 @@ constexpr int kArrivePerChan = 9;   // 8 XCD-group counters + the channel counte
 constexpr int kStampSlots = 2200;
 constexpr int kMaxBpc = 1024; // blocks per channel per step (partial buffer)
 constexpr int kMaxBpcRun = 256;  // blocks per channel of the persistent kernel
+// ... as its LDS holds them: above 3 taps 192 (the partials' LDS then leaves room for three
+// blocks per CU; 192 blocks of 24-sample lanes = 1.18 M samples per step)
+constexpr int run_bpc_cap(int ntaps) { return ntaps > 3 ? 192 : kMaxBpcRun; }
 constexpr int kMaxVpb = 16;      // virtual blocks per resident block of the persistent kernel
 constexpr int kDescWords = (int)(sizeof(StepDesc) / 4);
 

@@ -996,37 +996,54 @@ __device__ __forceinline__ void lds_barrier()
 // Block: the NV tap sums of the block's 256 lanes: 8-lane runs, then four runs per lane,
 // then a DPP quad butterfly. Slots are free on entry (caller's barrier); the value is in
 // lanes tid = 4v (v < NV); LDS barriers only (global loads in flight stay so).
+// Taps per pass of the block reduction: all of them at 3 taps; above, two passes of half the
+// taps each, so the reduction's LDS (2 * taps * (T + 32) doubles) fits three 11-tap blocks per
+// CU. Every value is reduced by the same lanes in the same order either way (same bits).
+template <int NT> constexpr int red_taps() { return NT > 3 ? (NT + 1) / 2 : NT; }
+template <int NT> constexpr int red_words() { return 2 * red_taps<NT>() * (kTrkThreads + 32); }
+
 template <int NT>
 __device__ __forceinline__ double block_partial(double* s_mem, const double (&oI)[NT],
                                                 const double (&oQ)[NT], int tid)
 {
-    constexpr int NV = 2 * NT, T = kTrkThreads;
-    double* red = s_mem;            // [NV][T]
-    double* red2 = s_mem + NV * T;  // [NV][32]
-#pragma unroll
-    for (int q = 0; q < NT; q++) {
-        red[(2 * q) * T + tid] = oI[q];
-        red[(2 * q + 1) * T + tid] = oQ[q];
-    }
-    lds_barrier();
-    for (int e = tid; e < NV * 32; e += T) {
-        const double* r = red + (e >> 5) * T + (e & 31) * 8;
-        double a = r[0];
-#pragma unroll
-        for (int k = 1; k < 8; k++) a += r[k];
-        red2[e] = a;
-    }
-    lds_barrier();
+    constexpr int NV = 2 * NT, T = kTrkThreads, HT = red_taps<NT>();
+    double* red = s_mem;                 // [2 HT][T]
+    double* red2 = s_mem + 2 * HT * T;   // [2 HT][32]
     double a = 0.0;
-    if (tid < NV * 4) {  // 4 lanes per value (waves 0, and 1 for 11 taps)
-        const double* r = red2 + (tid >> 2) * 32 + (tid & 3) * 8;
-        a = r[0];
 #pragma unroll
-        for (int k = 1; k < 8; k++) a += r[k];
-        a += dpp_f64<0xB1>(a);  // quad_perm [1,0,3,2]
-        a += dpp_f64<0x4E>(a);  // quad_perm [2,3,0,1] (IEEE addition commutes: lanes agree)
+    for (int q0 = 0; q0 < NT; q0 += HT) {  // taps q0 .. q0 + HT - 1 (values 2 q0 ..)
+        const int nv = (NT - q0 < HT ? NT - q0 : HT) * 2;
+#pragma unroll
+        for (int q = 0; q < HT; q++) {
+            if (q0 + q < NT) {
+                red[(2 * q) * T + tid] = oI[q0 + q];
+                red[(2 * q + 1) * T + tid] = oQ[q0 + q];
+            }
+        }
+        lds_barrier();
+        for (int e = tid; e < nv * 32; e += T) {
+            const double* r = red + (e >> 5) * T + (e & 31) * 8;
+            double x = r[0];
+#pragma unroll
+            for (int k = 1; k < 8; k++) x += r[k];
+            red2[e] = x;
+        }
+        lds_barrier();
+        // 4 lanes per value: value v = 2 q0 + (tid - 8 q0) / 4 in lanes 4v .. 4v + 3
+        const int t = tid - 8 * q0;
+        if (t >= 0 && t < nv * 4) {
+            const double* r = red2 + (t >> 2) * 32 + (t & 3) * 8;
+            a = r[0];
+#pragma unroll
+            for (int k = 1; k < 8; k++) a += r[k];
+        }
+        // (the butterfly on every lane: DPP reads its quad, whose lanes are all this pass's or none)
+        if (t >= 0 && t < nv * 4) {
+            a += dpp_f64<0xB1>(a);  // quad_perm [1,0,3,2]
+            a += dpp_f64<0x4E>(a);  // quad_perm [2,3,0,1] (IEEE addition commutes: lanes agree)
+        }
+        lds_barrier();  // red / red2 read before the next pass or the caller reuses the slots
     }
-    lds_barrier();  // red2 read before the caller reuses the slots
     return a;
 }
 
@@ -1078,7 +1095,7 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(const TrkParams
 
     // LDS: running sums slot[8][T], then the block reduction
     constexpr int kSlot = 8 * T * 2;
-    constexpr int kRed = NV * (T + 32);
+    constexpr int kRed = red_words<NT>();
     __shared__ __attribute__((aligned(16))) double s_mem[kSlot > kRed ? kSlot : kRed];
     __shared__ double s_fin[NV];
     __shared__ int s_last;
@@ -1413,8 +1430,11 @@ __device__ __forceinline__ void prefetch_raw(const int8_t* iq, int64_t g0, int64
 // (the same fp64 code on the same sums: bit-identical copies), so a step needs one
 // exchange only: each block publishes its partial sums and reads everyone's. Block 0
 // of the channel writes the records, C/N0 and, at the end, the state.
+#ifndef GNSS_WPE_TAPS
+#define GNSS_WPE_TAPS 2  // (A/B: waves per EU of the > 3-tap persistent forms; 3 = three blocks per CU)
+#endif
 template <int NT, int SUB, bool DIVIDE, bool VB = false>
-__global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT > 3 ? 2 : 3, NT > 3 ? 2 : 3))) void track_run_kernel(const TrkParams* __restrict__ pp,
+__global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT > 3 ? GNSS_WPE_TAPS : 3, NT > 3 ? GNSS_WPE_TAPS : 3))) void track_run_kernel(const TrkParams* __restrict__ pp,
                                                                const TrkBuffers* __restrict__ bp, int bpc,
                                                                int vpb, int nsteps, unsigned tag0)
 {
@@ -1443,8 +1463,8 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
     const bool io = pblk == 0;
 
     constexpr int kSlot = 8 * T * 2;                  // running sums [8][T] double2
-    constexpr int kRed = NV * (T + 32);               // block reduction
-    constexpr int kPart = kMaxBpcRun * NV;            // everyone's partials (as words)
+    constexpr int kRed = red_words<NT>();             // block reduction
+    constexpr int kPart = run_bpc_cap(NT) * NV;       // everyone's partials (as words)
     constexpr int kMem0 = kSlot > kRed ? kSlot : kRed;
     constexpr int kMem = kMem0 > kPart + 16 * NV ? kMem0 : kPart + 16 * NV;
     __shared__ __attribute__((aligned(16))) double s_mem[kMem];
