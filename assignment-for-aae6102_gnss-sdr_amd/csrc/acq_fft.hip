@@ -513,6 +513,26 @@ __global__ __launch_bounds__(kColThreads) void fwd_cols_kernel(const V* __restri
 
 // ---- I1: inverse columns of Z = C_p .* conj(X_{ms,bin}) for transform t = (pair, ms)
 // of this batch; pair q = first_pair + t / datalen -> bin = q / nprn, p = q % nprn.
+// one V (complex fp64 / fp32) by a raw buffer load
+template <class V> __device__ __forceinline__ V buf_ld(__amdgpu_buffer_rsrc_t r, int voff, int soff);
+template <> __device__ __forceinline__ double2 buf_ld<double2>(__amdgpu_buffer_rsrc_t r, int voff, int soff)
+{
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    const u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+    return make_double2(__hiloint2double((int)v.y, (int)v.x), __hiloint2double((int)v.w, (int)v.z));
+}
+template <> __device__ __forceinline__ float2 buf_ld<float2>(__amdgpu_buffer_rsrc_t r, int voff, int soff)
+{
+    typedef unsigned u2 __attribute__((ext_vector_type(2)));
+    const u2 v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+    return make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
+}
+#ifndef GNSS_COLS_BUF
+#define GNSS_COLS_BUF 1  // (A/B: 0 = the column pass's plain loads)
+#endif
+#ifndef GNSS_TW_ROWS
+#define GNSS_TW_ROWS 1  // (A/B: 0 = the column pass multiplies by the four-step twiddle)
+#endif
 template <int P, class V>
 #ifndef GNSS_INVCOLS_WPE
 #define GNSS_INVCOLS_WPE 0  // (A/B: waves per EU asked of inv_cols; 0 = the compiler's choice)
@@ -529,16 +549,51 @@ void inv_cols_kernel(
     if (k1 >= kRow) return;
     const int q = first_pair + t / datalen, idx = t % datalen;
     const int bin = q / nprn, p = q - bin * nprn;
-    const V* c = C + (int64_t)p * P * kRow + k1;
-    const V* x = X + ((int64_t)idx * nbins + bin) * P * kRow + k1;
     V v[P];
+    if (GNSS_COLS_BUF) {
+        // buffer loads (row offsets in SGPRs: no per-load 64-bit address arithmetic), every
+        // code-spectrum value first, then the signal spectrum 8 rows at a time with the next 8
+        // in flight: the lane waits for L2 about 4 times, not once per row as the compiler's
+        // interleaved schedule did
+        constexpr int kB = P * kRow * (int)sizeof(V), G = 8;
+        const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(C + (int64_t)p * P * kRow), (short)0, kB, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(X + ((int64_t)idx * nbins + bin) * P * kRow), (short)0, kB, 0x00020000);
+        const int vo = k1 * (int)sizeof(V);
 #pragma unroll
-    for (int i = 0; i < P; i++) v[i] = cmulc(c[(int64_t)i * kRow], x[(int64_t)i * kRow]);
+        for (int i = 0; i < P; i++) v[i] = buf_ld<V>(rc, vo, i * kRow * (int)sizeof(V));
+        V xa[G];
+#pragma unroll
+        for (int i = 0; i < G; i++) xa[i] = buf_ld<V>(rx, vo, (i < P ? i : P - 1) * kRow * (int)sizeof(V));
+#pragma unroll
+        for (int g = 0; g < P; g += G) {
+            V xb[G];
+#pragma unroll
+            for (int i = 0; i < G; i++)
+                if (g + G + i < P) xb[i] = buf_ld<V>(rx, vo, (g + G + i) * kRow * (int)sizeof(V));
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < G; i++)
+                if (g + i < P) v[g + i] = cmulc(v[g + i], xa[i]);
+#pragma unroll
+            for (int i = 0; i < G; i++) xa[i] = xb[i];
+        }
+    } else {
+        const V* c = C + (int64_t)p * P * kRow + k1;
+        const V* x = X + ((int64_t)idx * nbins + bin) * P * kRow + k1;
+#pragma unroll
+        for (int i = 0; i < P; i++) v[i] = cmulc(c[(int64_t)i * kRow], x[(int64_t)i * kRow]);
+    }
     V* a = A + (int64_t)t * P * kRow + k1;
     const V* tw = tw_col + k1;
-    // A is streamed once (to the row pass): non-temporal stores keep C and X in the caches
+    // A is streamed once (to the row pass): non-temporal stores keep C and X in the caches.
+    // GNSS_TW_ROWS: the four-step twiddle w^(k1 k2) is applied by the row pass as it loads
+    // the row (the same product of the same operands: same bits), so this pass issues no
+    // load after its first store -- on gfx9 a load's vmcnt wait also waits for every store
+    // issued before it, and the twiddle reads between the stores serialised them.
     dft_prime<P, 1>(v, [&](int k, V y) {
-        const V z = cmulc(y, tw[(int64_t)k * kRow]);
+        const V z = GNSS_TW_ROWS ? y : cmulc(y, tw[(int64_t)k * kRow]);
         __builtin_nontemporal_store(z.x, &a[(int64_t)k * kRow].x);
         __builtin_nontemporal_store(z.y, &a[(int64_t)k * kRow].y);
     });
@@ -550,7 +605,7 @@ void inv_cols_kernel(
 template <int P>
 __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel(
     const float2* __restrict__ A, int nprn, int datalen, int first_pair, float scale,
-    const float2* __restrict__ tw_row, float* __restrict__ corr, int nbins)
+    const float2* __restrict__ tw_row, const float2* __restrict__ tw_col, float* __restrict__ corr, int nbins)
 {
     constexpr int Q = (kRow + kRowThreads - 1) / kRowThreads;
     constexpr int V4 = kRow / 2;  // float4 = two complex
@@ -578,8 +633,20 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel(
         v.w = __builtin_nontemporal_load(&q->w);
         return v;
     };
+    // (GNSS_TW_ROWS) this row's four-step twiddles w^(tau2 k1), k1 = 2e, 2e + 1, held for every ms
+    float4 tw4[QV];
+#pragma unroll
+    for (int i = 0; i < QV; i++) {
+        const int e = tid + i * kRowThreads;
+        tw4[i] = reinterpret_cast<const float4*>(tw_col + (int64_t)tau2 * kRow)[e < V4 ? e : V4 - 1];
+    }
     auto st = [&](int h, int i, float4 v) {
         const int e = tid + i * kRowThreads;
+        if (GNSS_TW_ROWS) {
+            const float2 lo = cmulc(make_float2(v.x, v.y), make_float2(tw4[i].x, tw4[i].y));
+            const float2 hi = cmulc(make_float2(v.z, v.w), make_float2(tw4[i].z, tw4[i].w));
+            v = make_float4(lo.x, lo.y, hi.x, hi.y);
+        }
         if (e < V4) s_a4[h * V4 + e] = v;
     };
     float4 a0 = ld(0, 0), a1 = ld(0, 1), a2 = ld(0, 2), a3 = ld(0, 3);
@@ -625,7 +692,7 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel(
 template <int P>
 __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel_f64(
     const double2* __restrict__ A, int nprn, int datalen, int first_pair, double scale,
-    const double2* __restrict__ tw_row, double* __restrict__ corr, int nbins)
+    const double2* __restrict__ tw_row, const double2* __restrict__ tw_col, double* __restrict__ corr, int nbins)
 {
     constexpr int Q = (kRow + kRowThreads - 1) / kRowThreads;
     __shared__ double2 s_a[kRowPad], s_tw[kTwIK];
@@ -646,8 +713,20 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel_f64(
         n3 = ld_nt(r + 3 * kRowThreads); n4 = ld_nt(r + 4 * kRowThreads);                      \
         n5 = ld_nt(r + 5 * kRowThreads); n6 = ld_nt(r + 6 * kRowThreads); n7 = ld_nt(r + e7 - tid); \
     }
+    // (GNSS_TW_ROWS) this row's four-step twiddles w^(tau2 k1) for the lane's 8 elements, held
+    // for every ms: the column pass's product cmulc(y, w), moved here
+    double2 w0, w1, w2, w3, w4, w5, w6, w7;
+    if (GNSS_TW_ROWS) {
+        const double2* t = tw_col + (int64_t)tau2 * kRow + tid;
+        w0 = t[0]; w1 = t[kRowThreads]; w2 = t[2 * kRowThreads]; w3 = t[3 * kRowThreads];
+        w4 = t[4 * kRowThreads]; w5 = t[5 * kRowThreads]; w6 = t[6 * kRowThreads]; w7 = t[e7 - tid];
+    }
     GNSS_LD(0)
     for (int idx = 0; idx < datalen; idx++) {
+        if (GNSS_TW_ROWS) {
+            n0 = cmulc(n0, w0); n1 = cmulc(n1, w1); n2 = cmulc(n2, w2); n3 = cmulc(n3, w3);
+            n4 = cmulc(n4, w4); n5 = cmulc(n5, w5); n6 = cmulc(n6, w6); n7 = cmulc(n7, w7);
+        }
         s_a[tid] = n0; s_a[tid + kRowThreads] = n1; s_a[tid + 2 * kRowThreads] = n2;
         s_a[tid + 3 * kRowThreads] = n3; s_a[tid + 4 * kRowThreads] = n4;
         s_a[tid + 5 * kRowThreads] = n5; s_a[tid + 6 * kRowThreads] = n6;
@@ -778,7 +857,9 @@ __global__ __launch_bounds__(kRowThreads, 2) void inv_fused_kernel_f64(
                 for (int i = 0; i < P; i++) v[i] = cmulc(c[(int64_t)i * kRow], ld_nt(x + (int64_t)i * kRow));
                 double2* a = ring_x + (int64_t)slot * S + k1;
                 const double2* tw = tw_col + k1;
-                dft_prime<P, 1>(v, [&](int k, double2 y) { a[(int64_t)k * kRow] = cmulc(y, tw[(int64_t)k * kRow]); });
+                dft_prime<P, 1>(v, [&](int k, double2 y) {
+                    a[(int64_t)k * kRow] = GNSS_TW_ROWS ? y : cmulc(y, tw[(int64_t)k * kRow]);
+                });
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's stores are in L2
             __syncthreads();
@@ -806,7 +887,8 @@ __global__ __launch_bounds__(kRowThreads, 2) void inv_fused_kernel_f64(
             if (e < kRow) {
                 typedef unsigned u4 __attribute__((ext_vector_type(4)));
                 const u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, row0 + e * 16, 0, 16 /* sc1 */);
-                s_a[e] = make_double2(__hiloint2double((int)v.y, (int)v.x), __hiloint2double((int)v.w, (int)v.z));
+                const double2 y = make_double2(__hiloint2double((int)v.y, (int)v.x), __hiloint2double((int)v.w, (int)v.z));
+                s_a[e] = GNSS_TW_ROWS ? cmulc(y, tw_col[(int64_t)tau2 * kRow + e]) : y;
             }
         }
         __syncthreads();  // the row is in LDS: the slot may be refilled
@@ -1034,7 +1116,7 @@ hipError_t launch_acq_fft_correlate(const float2* C, const float2* X, int64_t S,
                            tw_col, A);                                                          \
         if (parts & kAcqRows)                                                                   \
         hipLaunchKernelGGL(inv_rows_kernel<P_>, dim3(P_, npair), dim3(kRowThreads), 0, s, A, nprn, \
-                           datalen, first_pair, scale, tw_row, corr, nbins);                    \
+                           datalen, first_pair, scale, tw_row, tw_col, corr, nbins);            \
         return hipGetLastError();                                                               \
     }
     GNSS_INV(13) GNSS_INV(29)
@@ -1057,7 +1139,7 @@ hipError_t launch_acq_fft_correlate(const double2* C, const double2* X, int64_t 
                            tw_col, A);                                                          \
         if (parts & kAcqRows)                                                                   \
         hipLaunchKernelGGL(inv_rows_kernel_f64<P_>, dim3(P_, npair), dim3(kRowThreads), 0, s, A, nprn, \
-                           datalen, first_pair, scale, tw_row, corr, nbins);                    \
+                           datalen, first_pair, scale, tw_row, tw_col, corr, nbins);            \
         return hipGetLastError();                                                               \
     }
     GNSS_INV(13) GNSS_INV(29)

@@ -41,3 +41,4 @@ for it in range(3):
 print("sv", list(A.sv), "cd", list(A.codedelay), "ff", list(A.fineFreq))
 print("fbin", list(d.fbin), "cp", list(d.codePhase))
 print("snr", [round(x, 4) for x in d.SNR])
+print("snrhex", [float(x).hex() for x in d.SNR])  # (bit-identity across library builds)
