@@ -530,6 +530,9 @@ template <> __device__ __forceinline__ float2 buf_ld<float2>(__amdgpu_buffer_rsr
 #ifndef GNSS_COLS_BUF
 #define GNSS_COLS_BUF 1  // (A/B: 0 = the column pass's plain loads)
 #endif
+#ifndef GNSS_COLS_GROUP
+#define GNSS_COLS_GROUP 8  // (A/B: signal-spectrum rows per load group of the column pass)
+#endif
 #ifndef GNSS_TW_ROWS
 #define GNSS_TW_ROWS 1  // (A/B: 0 = the column pass multiplies by the four-step twiddle)
 #endif
@@ -550,12 +553,44 @@ void inv_cols_kernel(
     const int q = first_pair + t / datalen, idx = t % datalen;
     const int bin = q / nprn, p = q - bin * nprn;
     V v[P];
-    if (GNSS_COLS_BUF) {
+    if (GNSS_COLS_BUF == 2) {
+        // (A/B) code and signal rows loaded together, G rows at a time with the next G in
+        // flight: fewer registers held than all code rows first
+        constexpr int kB = P * kRow * (int)sizeof(V), G = GNSS_COLS_GROUP;
+        const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(C + (int64_t)p * P * kRow), (short)0, kB, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(X + ((int64_t)idx * nbins + bin) * P * kRow), (short)0, kB, 0x00020000);
+        const int vo = k1 * (int)sizeof(V);
+        V ca[G], xa[G];
+#pragma unroll
+        for (int i = 0; i < G; i++) {
+            const int r = (i < P ? i : P - 1) * kRow * (int)sizeof(V);
+            ca[i] = buf_ld<V>(rc, vo, r);
+            xa[i] = buf_ld<V>(rx, vo, r);
+        }
+#pragma unroll
+        for (int g = 0; g < P; g += G) {
+            V cb[G], xb[G];
+#pragma unroll
+            for (int i = 0; i < G; i++)
+                if (g + G + i < P) {
+                    cb[i] = buf_ld<V>(rc, vo, (g + G + i) * kRow * (int)sizeof(V));
+                    xb[i] = buf_ld<V>(rx, vo, (g + G + i) * kRow * (int)sizeof(V));
+                }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < G; i++)
+                if (g + i < P) v[g + i] = cmulc(ca[i], xa[i]);
+#pragma unroll
+            for (int i = 0; i < G; i++) { ca[i] = cb[i]; xa[i] = xb[i]; }
+        }
+    } else if (GNSS_COLS_BUF) {
         // buffer loads (row offsets in SGPRs: no per-load 64-bit address arithmetic), every
         // code-spectrum value first, then the signal spectrum 8 rows at a time with the next 8
         // in flight: the lane waits for L2 about 4 times, not once per row as the compiler's
         // interleaved schedule did
-        constexpr int kB = P * kRow * (int)sizeof(V), G = 8;
+        constexpr int kB = P * kRow * (int)sizeof(V), G = GNSS_COLS_GROUP;
         const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
             (void*)(C + (int64_t)p * P * kRow), (short)0, kB, 0x00020000);
         const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
@@ -689,13 +724,28 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel(
 // a padded layout x -> x + x/20 against the radix-20 pass's 2-way store conflicts (28 %
 // of the LDS cycles by SQ_LDS_BANK_CONFLICT): 350 -> 481 us per launch (index divisions);
 // radix 10-10-20 (conflict-free first pass, twiddles in the radix-20 pass): 350 -> 367 us.
+#ifndef GNSS_INVROWS_WPE
+#define GNSS_INVROWS_WPE 0  // (A/B: waves per EU of the fp64 row pass -- its LDS then dynamic, so the
+                            // compiler takes the register limit -- for a column-pass wave to fit beside
+                            // its two blocks per CU; 0 = static LDS, the compiler's choice)
+#endif
 template <int P>
-__global__ __launch_bounds__(kRowThreads) void inv_rows_kernel_f64(
+__global__ __launch_bounds__(kRowThreads)
+#if GNSS_INVROWS_WPE > 0
+__attribute__((amdgpu_waves_per_eu(GNSS_INVROWS_WPE, GNSS_INVROWS_WPE)))
+#endif
+void inv_rows_kernel_f64(
     const double2* __restrict__ A, int nprn, int datalen, int first_pair, double scale,
     const double2* __restrict__ tw_row, const double2* __restrict__ tw_col, double* __restrict__ corr, int nbins)
 {
     constexpr int Q = (kRow + kRowThreads - 1) / kRowThreads;
+#if GNSS_INVROWS_WPE > 0
+    extern __shared__ double2 s_dyn[];  // (kRowPad + kTwIK) elements, given at the launch
+    double2* s_a = s_dyn;
+    double2* s_tw = s_dyn + kRowPad;
+#else
     __shared__ double2 s_a[kRowPad], s_tw[kTwIK];
+#endif
     const int tau2 = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
     const TwIK<double2> twk = load_row_tw_ik(s_tw, tw_row, tid);
     double acc[kInvOut];
@@ -1138,7 +1188,8 @@ hipError_t launch_acq_fft_correlate(const double2* C, const double2* X, int64_t 
                            dim3(kColThreads), 0, s, C, X, nbins, nprn, datalen, first_pair,     \
                            tw_col, A);                                                          \
         if (parts & kAcqRows)                                                                   \
-        hipLaunchKernelGGL(inv_rows_kernel_f64<P_>, dim3(P_, npair), dim3(kRowThreads), 0, s, A, nprn, \
+        hipLaunchKernelGGL(inv_rows_kernel_f64<P_>, dim3(P_, npair), dim3(kRowThreads),          \
+                           GNSS_INVROWS_WPE > 0 ? (kRowPad + kTwIK) * sizeof(double2) : 0, s, A, nprn, \
                            datalen, first_pair, scale, tw_row, tw_col, corr, nbins);            \
         return hipGetLastError();                                                               \
     }

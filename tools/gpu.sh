@@ -149,6 +149,11 @@ for step in "$@"; do
         TRK_SUB=$( [ "$u" != 0 ] && echo $u ) TRK_HASH=1 TRK_PROFILE=1 TRK_ITERS=2 timeout -k 10 120 python3 tools/track_only.py 1000 40000 3 $n > gpurun_out/geom_${n}_$u.log 2>&1 \
           && echo "geom nch=$n sub=$u: $(grep -E 'track10|sha256' gpurun_out/geom_${n}_$u.log | tail -2 | tr '\n' ' ')" || { tail -5 gpurun_out/geom_${n}_$u.log; exit 1; }
       done ;;
+    c5geom)  # config-5 shape by channel count: 11 taps, 1000 ms + 9000 x 10 ms, C5NCH="1 4 8 32" channels
+      for n in ${C5NCH:-1 4 8 32}; do
+        TRK_HASH=1 TRK_PROFILE=1 TRK_ITERS=2 timeout -k 10 150 python3 tools/track_only.py 1000 90000 11 $n > gpurun_out/c5geom_$n.log 2>&1 \
+          && echo "c5geom nch=$n: $(grep -E 'track10|sha256' gpurun_out/c5geom_$n.log | tail -2 | tr '\n' ' ')" || { tail -5 gpurun_out/c5geom_$n.log; exit 1; }
+      done ;;
     xstamps)  # per-block stamps + SQ counters of probe-build variants (AB="pspread pxl"): tools/stamps_blocks.py
       for v in $AB; do
         L=$R/tools/probe_lib/libgnss_$v.so
