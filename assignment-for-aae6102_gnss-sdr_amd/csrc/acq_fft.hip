@@ -724,28 +724,13 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel(
 // a padded layout x -> x + x/20 against the radix-20 pass's 2-way store conflicts (28 %
 // of the LDS cycles by SQ_LDS_BANK_CONFLICT): 350 -> 481 us per launch (index divisions);
 // radix 10-10-20 (conflict-free first pass, twiddles in the radix-20 pass): 350 -> 367 us.
-#ifndef GNSS_INVROWS_WPE
-#define GNSS_INVROWS_WPE 0  // (A/B: waves per EU of the fp64 row pass -- its LDS then dynamic, so the
-                            // compiler takes the register limit -- for a column-pass wave to fit beside
-                            // its two blocks per CU; 0 = static LDS, the compiler's choice)
-#endif
 template <int P>
-__global__ __launch_bounds__(kRowThreads)
-#if GNSS_INVROWS_WPE > 0
-__attribute__((amdgpu_waves_per_eu(GNSS_INVROWS_WPE, GNSS_INVROWS_WPE)))
-#endif
-void inv_rows_kernel_f64(
+__global__ __launch_bounds__(kRowThreads) void inv_rows_kernel_f64(
     const double2* __restrict__ A, int nprn, int datalen, int first_pair, double scale,
     const double2* __restrict__ tw_row, const double2* __restrict__ tw_col, double* __restrict__ corr, int nbins)
 {
     constexpr int Q = (kRow + kRowThreads - 1) / kRowThreads;
-#if GNSS_INVROWS_WPE > 0
-    extern __shared__ double2 s_dyn[];  // (kRowPad + kTwIK) elements, given at the launch
-    double2* s_a = s_dyn;
-    double2* s_tw = s_dyn + kRowPad;
-#else
     __shared__ double2 s_a[kRowPad], s_tw[kTwIK];
-#endif
     const int tau2 = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
     const TwIK<double2> twk = load_row_tw_ik(s_tw, tw_row, tid);
     double acc[kInvOut];
@@ -1188,8 +1173,7 @@ hipError_t launch_acq_fft_correlate(const double2* C, const double2* X, int64_t 
                            dim3(kColThreads), 0, s, C, X, nbins, nprn, datalen, first_pair,     \
                            tw_col, A);                                                          \
         if (parts & kAcqRows)                                                                   \
-        hipLaunchKernelGGL(inv_rows_kernel_f64<P_>, dim3(P_, npair), dim3(kRowThreads),          \
-                           GNSS_INVROWS_WPE > 0 ? (kRowPad + kTwIK) * sizeof(double2) : 0, s, A, nprn, \
+        hipLaunchKernelGGL(inv_rows_kernel_f64<P_>, dim3(P_, npair), dim3(kRowThreads), 0, s, A, nprn, \
                            datalen, first_pair, scale, tw_row, tw_col, corr, nbins);            \
         return hipGetLastError();                                                               \
     }
