@@ -527,24 +527,6 @@ template <> __device__ __forceinline__ float2 buf_ld<float2>(__amdgpu_buffer_rsr
     const u2 v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
     return make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
 }
-// one V by a raw buffer store, non-temporal (cache policy nt)
-template <class V> __device__ __forceinline__ void buf_st_nt(V v, __amdgpu_buffer_rsrc_t r, int voff, int soff);
-template <> __device__ __forceinline__ void buf_st_nt<double2>(double2 v, __amdgpu_buffer_rsrc_t r, int voff, int soff)
-{
-    typedef unsigned u4 __attribute__((ext_vector_type(4)));
-    const long long a = __double_as_longlong(v.x), b = __double_as_longlong(v.y);
-    const u4 w = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
-    __builtin_amdgcn_raw_buffer_store_b128(w, r, voff, soff, 2 /* nt */);
-}
-template <> __device__ __forceinline__ void buf_st_nt<float2>(float2 v, __amdgpu_buffer_rsrc_t r, int voff, int soff)
-{
-    typedef unsigned u2 __attribute__((ext_vector_type(2)));
-    const u2 w = {__float_as_uint(v.x), __float_as_uint(v.y)};
-    __builtin_amdgcn_raw_buffer_store_b64(w, r, voff, soff, 2 /* nt */);
-}
-#ifndef GNSS_COLS_BUFST
-#define GNSS_COLS_BUFST 0  // (A/B: the column pass's stores as buffer stores)
-#endif
 #ifndef GNSS_COLS_BUF
 #define GNSS_COLS_BUF 1  // (A/B: 0 = the column pass's plain loads)
 #endif
@@ -645,14 +627,6 @@ void inv_cols_kernel(
     // the row (the same product of the same operands: same bits), so this pass issues no
     // load after its first store -- on gfx9 a load's vmcnt wait also waits for every store
     // issued before it, and the twiddle reads between the stores serialised them.
-    if (GNSS_COLS_BUFST && GNSS_TW_ROWS) {
-        // (A/B) buffer stores, nt: row offsets in SGPRs as for the loads
-        const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(A + (int64_t)t * P * kRow), (short)0, P * kRow * (int)sizeof(V), 0x00020000);
-        const int vo = k1 * (int)sizeof(V);
-        dft_prime<P, 1>(v, [&](int k, V y) { buf_st_nt<V>(y, ra, vo, k * kRow * (int)sizeof(V)); });
-        return;
-    }
     dft_prime<P, 1>(v, [&](int k, V y) {
         const V z = GNSS_TW_ROWS ? y : cmulc(y, tw[(int64_t)k * kRow]);
         __builtin_nontemporal_store(z.x, &a[(int64_t)k * kRow].x);
