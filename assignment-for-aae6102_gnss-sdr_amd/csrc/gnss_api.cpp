@@ -1844,9 +1844,9 @@ int gnss_tracking_vt_step(gnss_ctx* ctx, const gnss_file* file, const gnss_signa
 int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg, const gnss_track* tr, int32_t n,
                      int32_t nsteps, gnss_vt_chan* chans, gnss_vt_nav* nav, gnss_vt_out* out, gnss_vt_navsol* sol)
 {
-    if (!ctx || !file || !sg || !tr || !chans || !nav || !out || n < 1 || n != nav->n || nsteps < 0 ||
-        !(sg->Fs > 0) || !(sg->codeFreqBasis > 0) || sg->Fs != nav->Fs)
-        return fail(ctx, GNSS_EARG, "bad arguments (n must equal nav->n, signal as at gnss_vt_nav_init)");
+    if (!ctx || !file || !sg || !tr || !chans || !nav || !out || n < 1 || n > GNSS_VT_MAX_CH || n != nav->n ||
+        nsteps < 0 || !(sg->Fs > 0) || !(sg->codeFreqBasis > 0) || sg->Fs != nav->Fs)
+        return fail(ctx, GNSS_EARG, "bad arguments (n in 1..GNSS_VT_MAX_CH and equal to nav->n, signal as at gnss_vt_nav_init)");
     ctx->err.clear();
     ctx->timing = gnss_timing{};
     if (nsteps == 0) return GNSS_OK;

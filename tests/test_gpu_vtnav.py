@@ -208,3 +208,24 @@ def test_vector_tracking_step_blocks(pkg, po, ctx, opensky_short, opts, nb):
     status, rec, onav = _oracle_loop(pkg, po, z, ct, data, nsteps)
     assert status == 0
     print(nb, "worst sum / |P|", _compare(pkg, po, z, tck, nsol, rec, onav))
+
+
+def test_vector_tracking_channel_bound(pkg, ctx):
+    """gnss_tracking_vt refuses more than GNSS_VT_MAX_CH channels (its per-step kernel arguments
+    hold that many code frequencies) before touching anything, and the context stays usable."""
+    import ctypes as C
+    abi = pkg.abi
+    file, signal, _, track, _, _ = pkg.initParameters()
+    f, keep = pkg.sdr.to_c_file(file)
+    s = pkg.sdr.to_c_signal(signal)
+    t, keep2 = pkg.sdr.to_c_track(track)
+    n = 33
+    chans = (abi.GnssVtChan * n)()
+    nav = abi.GnssVtNav()
+    nav.n = n
+    outs = (abi.GnssVtOut * n)()
+    st = ctx.lib.gnss_tracking_vt(ctx.h, C.byref(f), C.byref(s), C.byref(t), n, 1, chans, C.byref(nav), outs, None)
+    assert st == abi.EARG
+    assert ctx.lib.gnss_tracking_vt(ctx.h, C.byref(f), C.byref(s), C.byref(t), 0, 1, chans, C.byref(nav), outs,
+                                    None) == abi.EARG
+    ctx.timing()  # (the context still answers)
