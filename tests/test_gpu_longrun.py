@@ -73,7 +73,7 @@ def test_config5_full_length_against_oracle(pkg, ctx):
     """BASELINE config 5 at its benchmarked length: the bench's 32-SV
     record, all 32 channels x 11 taps (-0.5:0.1:0.5) tracked on one GPU exactly as the bench
     runs them (the virtual-block persistent launch, one launch per phase: 1000 ms @1 ms +
-    countinx + 90 000 ms @10 ms), against the oracle's run of three of the channels
+    countinx + 90 000 ms @10 ms), against the oracle's run of eight of the channels (three before round 4)
     (tests/golden/golden_cfg5_long.npz, tests/golden/make_golden_cfg5.py). Integer fields
     bit-exact over every step, E/P/L and all 22 tap sums within 1e-8 of the series RMS,
     NCO state 1e-7 relative, C/N0 1e-6 dB. Reference: trackingCT.m:73-171,:178-213,:377-525;
