@@ -47,7 +47,10 @@ for key, sub in (("inv_cols_kernel<29, double2>", "inv_cols_kernel<29, HIP_vecto
          "wait_inst_lds_frac": round(c["SQ_WAIT_INST_LDS"] / wave, 3),
          "valu_active_frac": round(c["SQ_ACTIVE_INST_VALU"] / wave, 3),
          "lds_bank_conflict_frac": round(c["SQ_LDS_BANK_CONFLICT"] / lds, 3) if lds else 0.0}
-    e["bound"] = ("hbm (streaming writes of the batch intermediate)" if e["hbm_frac"] and e["hbm_frac"] > 0.4
+    writes = c.get("WRITE_SIZE", 0.0) * 1024.0 > 0.5 * hbm  # (mostly a write stream)
+    e["bound"] = ("hbm (streaming writes of the batch intermediate)" if e["hbm_frac"] and e["hbm_frac"] > 0.5 and writes
+                  else "hbm read + fp64 Stockham passes in LDS" if e["hbm_frac"] and e["hbm_frac"] > 0.4
+                  and e["wait_inst_lds_frac"] > 0.1
                   else "lds issue (fp64 2000-point Stockham passes in LDS)" if e["wait_inst_lds_frac"] > 0.2
                   else "latency (waves parked on loads / barriers)")
     out[key] = e
