@@ -146,7 +146,8 @@ def test_config5_full_length_against_oracle(pkg, ctx):
         print(f"channel {int(c)}: E/P/L max err / rms {e_epl:.2e}, taps {e_taps:.2e} (quantum 2e-9), "
               f"{int(tap_off[:, :end].any(axis=0).sum())} tie-flip steps, strict over {end} of {got.shape[1]} steps")
         assert e_taps < 1e-8 and e_epl < 1e-8, (int(c), e_epl, e_taps)
-        assert np.allclose(got[nco][:, :end], rnco[:, :end], rtol=1e-7, atol=1e-9), int(c)
+        assert np.allclose(got[nco][:, :ee], rnco[:, :ee], rtol=1e-7, atol=1e-9), int(c)  # (the loop
+        # update of a tie-flip step in E / P / L already runs on the flipped sums)
         ref_cn0 = z[f"CN0_{j}"]
         rows = len(ref_cn0) if end == got.shape[1] else max(0, (end - n1) // 20 - 1)
         assert np.allclose(b.CN0[:rows, c], ref_cn0[:rows], rtol=0, atol=1e-6)
