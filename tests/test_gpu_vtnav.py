@@ -216,6 +216,7 @@ def test_vector_tracking_channel_bound(pkg, ctx):
     import ctypes as C
     abi = pkg.abi
     file, signal, _, track, _, _ = pkg.initParameters()
+    file.data = np.zeros(4096, dtype=np.int8)  # (never read: the call fails on n first)
     f, keep = pkg.sdr.to_c_file(file)
     s = pkg.sdr.to_c_signal(signal)
     t, keep2 = pkg.sdr.to_c_track(track)
