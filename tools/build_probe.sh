@@ -16,8 +16,8 @@ done
 wait
 for n in "$@"; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../tools/probe_lib/libgnss_probe$n.so \
-    /tmp/gnss_probe_obj/track_$n.o /tmp/gnss_probe_obj/gnss_api.o ../build/acq.o ../build/acq_fft.o \
-    ../build/synth.o ../build/ifmt.o ../build/vt.o ../build/navdecode.o ../build/lnav.o ../build/vt_host.o \
+    /tmp/gnss_probe_obj/track_$n.o /tmp/gnss_probe_obj/gnss_api.o \
+    $(ls ../build/*.o | grep -v -e '/track.o$' -e '/gnss_api.o$') \
     -L/opt/rocm/lib -lrocfft -pthread -Wl,-rpath,/opt/rocm/lib
 done
 ls -la ../../tools/probe_lib
