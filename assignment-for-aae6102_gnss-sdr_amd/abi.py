@@ -177,6 +177,9 @@ PROTOTYPES = {
     "gnss_abi_version": (C.c_int, []),
     "gnss_strerror": (C.c_char_p, [C.c_int]),
     "gnss_ctx_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    "gnss_ctx_create_multi": (C.c_int, [C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_void_p)]),
+    "gnss_ctx_members": (C.c_int, [C.c_void_p]),
+    "gnss_device_count": (C.c_int, []),
     "gnss_ctx_destroy": (None, [C.c_void_p]),
     "gnss_last_error": (C.c_char_p, [C.c_void_p]),
     "gnss_last_timing": (C.c_int, [C.c_void_p, C.POINTER(GnssTiming)]),
@@ -246,9 +249,10 @@ _lib = None
 _torch_first = False
 LOADED_PATH = None  # the library file the process bound (bench.py digests it)
 
-# gnss_ctx_set_option keys (include/gnss_mi355x.h, ABI v10)
+# gnss_ctx_set_option keys (include/gnss_mi355x.h, ABI v11)
 (OPT_FORCE_SUB, OPT_NO_PERSIST, OPT_FORCE_VPB, OPT_ACQ_ROCFFT, OPT_FINE_ROCFFT, OPT_ACQ_BATCH, OPT_ACQ_FUSED,
- OPT_ACQ_RING, OPT_ACQ_PIPE, OPT_VT_BLOCKS) = range(10)
+ OPT_ACQ_RING, OPT_ACQ_PIPE, OPT_VT_BLOCKS, OPT_FORCE_PEER) = range(11)
+MAX_DEVICES = 16
 
 
 def require_torch():
@@ -284,11 +288,11 @@ def load(path: str | None = None):
     # torch installed at the time.
     global _torch_first
     if _lib is None:
-        if "torch" not in sys.modules:
+        if "torch" not in sys.modules and os.environ.get("GNSS_NO_TORCH", "0") != "1":
             try:  # PyTorch's runtime first: any later tensor exchange then works
                 import torch  # noqa: F401
-            except ImportError:
-                pass
+            except Exception:  # (a torch that fails to import, e.g. an OSError from its ROCm
+                pass  # libraries, must not stop the GNSS library from loading; require_torch() checks)
         _torch_first = "torch" in sys.modules
     lib = C.CDLL(p)
     for name, (res, args) in PROTOTYPES.items():

@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "gnss_internal.h"
+#include "group.h"
 
 using namespace gnss;
 
@@ -53,6 +54,11 @@ struct gnss_ctx {
     int acq_fp64 = 1;      // acquisition correlation precision: 1 = fp64 (reference), 0 = fp32
     uint64_t window = 0;   // trackingCT: max IF bytes resident in HBM (0: the whole read range)
     int64_t opt[GNSS_OPT_COUNT] = {};  // gnss_ctx_set_option (test hooks; all 0 by default)
+    // multi-device context (gnss_ctx_create_multi): the member contexts (empty: a plain one);
+    // the group itself is also a context on devices[0], for the entry points that do not shard
+    std::vector<gnss_ctx*> members;
+    bool member = false;  // a group's member: dev_data on another device is copied in (xGMI)
+    int fail_chan = -1;   // tracking: the channel whose status the last call returned (group.h)
 };
 
 // Timing-probe hooks read from the environment in probe builds only (tools/build_probe.sh
@@ -264,6 +270,17 @@ int stage_into(gnss_ctx* ctx, const gnss_file* f, int64_t lo, int64_t hi, int8_t
     return GNSS_OK;
 }
 
+// The HIP device a device pointer belongs to (-1 if HIP does not know it).
+int pointer_device(const void* p)
+{
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    return a.device;
+}
+
 int stage_window(gnss_ctx* ctx, const gnss_file* f, int64_t lo, int64_t hi, IfWindow& w)
 {
     const int64_t flen = file_length(f);
@@ -272,11 +289,31 @@ int stage_window(gnss_ctx* ctx, const gnss_file* f, int64_t lo, int64_t hi, IfWi
     hi = std::min<int64_t>(hi, flen);
     if (hi <= lo) { hi = lo; }
     if (f->dev_data) {
-        w.ptr = static_cast<const int8_t*>(f->dev_data);
-        w.base = 0;
-        w.len = flen;
-        if ((reinterpret_cast<uintptr_t>(w.ptr) & 15) != 0)
+        if ((reinterpret_cast<uintptr_t>(f->dev_data) & 15) != 0)
             return fail(ctx, GNSS_EARG, "dev_data must be 16-byte aligned");
+        const int pd = ctx->member ? pointer_device(f->dev_data) : ctx->device;
+        if (pd == ctx->device && !(ctx->member && ctx->opt[GNSS_OPT_FORCE_PEER])) {
+            w.ptr = static_cast<const int8_t*>(f->dev_data);
+            w.base = 0;
+            w.len = flen;
+            return GNSS_OK;
+        }
+        // a group member whose record lives on another device of the node (devices[0]): the
+        // range [lo, hi) into this device's HBM by one peer copy over xGMI
+        const int64_t n = hi - lo;
+        HIP_TRY(w.own.alloc((size_t)n + 64));
+        Events ev;
+        HIP_TRY(hipEventRecord(ev.a, ctx->stream));
+        if (n > 0)
+            HIP_TRY(hipMemcpyPeerAsync(w.own.p, ctx->device, static_cast<const int8_t*>(f->dev_data) + lo,
+                                       pd < 0 ? ctx->device : pd, (size_t)n, ctx->stream));
+        HIP_TRY(hipEventRecord(ev.b, ctx->stream));
+        HIP_TRY(hipEventSynchronize(ev.b));
+        ctx->timing.h2d_bytes += n;
+        ctx->timing.h2d_ms += ev.ms();
+        w.ptr = w.own.as<int8_t>();
+        w.base = lo;
+        w.len = n;
         return GNSS_OK;
     }
     const int64_t n = hi - lo;
@@ -558,6 +595,190 @@ int acq_search(gnss_ctx* ctx, const int8_t* blk, const double2* xa, int64_t S, i
 }
 }  // namespace
 
+// The sibling loop of trackingCT_POS_updated.m (its tracking half): steps and countinx.
+struct PosCfg {
+    int32_t ctPOS;            // track.ctPOS (datalength, trackingCT_POS_updated.m:50)
+    const int32_t* countinx;  // countinx(svIndex) of countinx.mat (:29), by channel position
+    // 0: trackingCT_POS_updated.m. 1 or 10: trackingCT_POS_updated_multicorrelator.m, every
+    // step at this pdi (track.pdi, :46), 25 taps, ctPOS = datalength/pdi steps (:170)
+    int32_t mc_pdi;
+};
+
+// trackingCT_multiCorr-GIVEN.m (function trackingCT_multiCorr): `datalength` 1-ms steps
+// per channel (:27, hard-coded 50000 there), trackingCT conventions otherwise
+struct GivenCfg {
+    int32_t datalength;
+};
+
+// ---------------------------------------------------------------------------
+// Multi-device contexts (gnss_ctx_create_multi): the group's member contexts run their
+// shards side by side, one host thread per device (group.h has the dealing and merging).
+// ---------------------------------------------------------------------------
+namespace {
+
+template <class F>
+void for_members(gnss_ctx* g, F fn)
+{
+    std::vector<int> devs;
+    for (gnss_ctx* m : g->members) devs.push_back(m->device);
+    std::vector<std::thread> th;
+    for (const std::vector<int>& ks : group::by_device(devs))
+        th.emplace_back([&fn, ks]() {
+            for (int k : ks) fn(k);
+        });
+    for (auto& t : th) t.join();
+}
+
+}  // namespace
+
+extern "C" int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg,
+                                const gnss_acq* acq, gnss_acquired* out, gnss_acq_diag* diag);
+
+// acquisition.m's PRN loop (:47-80) dealt over the members; Acquired / diag merged in list order
+static int group_acquisition(gnss_ctx* g, const gnss_file* file, const gnss_signal* sg, const gnss_acq* acq,
+                             gnss_acquired* out, gnss_acq_diag* diag)
+{
+    if (!file || !sg || !acq || !out) return GNSS_EARG;
+    memset(out, 0, sizeof(*out));
+    if (diag) memset(diag, 0, sizeof(*diag));
+    g->timing = gnss_timing{};
+    std::vector<int32_t> prns;
+    if (acq->n_prn > 0 && acq->prn_list) prns.assign(acq->prn_list, acq->prn_list + acq->n_prn);
+    else for (int i = 1; i <= 32; i++) prns.push_back(i);  // acquisition.m:47
+    if (prns.size() > GNSS_MAX_SV) return fail(g, GNSS_EARG, "too many PRNs");
+    const int M = (int)g->members.size();
+    const auto shards = group::deal((int)prns.size(), M);
+    std::vector<std::vector<int32_t>> plist((size_t)M);
+    for (int k = 0; k < M; k++)
+        for (int i : shards[(size_t)k]) plist[(size_t)k].push_back(prns[(size_t)i]);
+    std::vector<gnss_acquired> outs((size_t)M);
+    std::vector<gnss_acq_diag> diags((size_t)M);
+    std::vector<int> st((size_t)M, GNSS_ENODATA);
+    std::vector<char> ran((size_t)M, 0);
+    for_members(g, [&](int k) {
+        memset(&outs[(size_t)k], 0, sizeof(gnss_acquired));
+        memset(&diags[(size_t)k], 0, sizeof(gnss_acq_diag));
+        if (plist[(size_t)k].empty()) return;  // (more members than PRNs)
+        gnss_acq a = *acq;
+        a.n_prn = (int32_t)plist[(size_t)k].size();
+        a.prn_list = plist[(size_t)k].data();
+        st[(size_t)k] = gnss_acquisition(g->members[(size_t)k], file, sg, &a, &outs[(size_t)k],
+                                         diag ? &diags[(size_t)k] : nullptr);
+        ran[(size_t)k] = 1;
+    });
+    std::vector<gnss_timing> tm;
+    for (int k = 0; k < M; k++)
+        if (ran[(size_t)k]) tm.push_back(g->members[(size_t)k]->timing);
+    g->timing = group::combine_timing(tm);
+    for (int k = 0; k < M; k++)
+        if (st[(size_t)k] != GNSS_OK && st[(size_t)k] != GNSS_ENODATA)
+            return fail(g, st[(size_t)k], "member %d (device %d): %s", k, g->members[(size_t)k]->device,
+                        g->members[(size_t)k]->err.c_str());
+    if (!group::merge_acquired(prns, shards, outs, diag ? &diags : nullptr, out, diag))
+        return fail(g, GNSS_EDEVICE, "multi-device acquisition: member results do not match their PRN shards");
+    const int status = group::acquisition_status(st, out->n);
+    if (status == GNSS_ENODATA) return fail(g, GNSS_ENODATA, "No satellites acquired");  // :84-85
+    return status;
+}
+
+static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg, const gnss_track* tr,
+                         const gnss_acquired* acq, gnss_track_out* out, const PosCfg* pos,
+                         const GivenCfg* gv, const int32_t* dev_slot);
+
+// trackingCT.m's channel loop (:22-528) dealt over the members. Host outputs: every member
+// writes its channels' rows of the caller's arrays (disjoint). GNSS_OUT_DEVICE: a member on
+// the output's device expands into it directly; another expands into a buffer of its own HBM
+// and copies each channel's contiguous row block over xGMI.
+static int group_tracking(gnss_ctx* g, const gnss_file* file, const gnss_signal* sg, const gnss_track* tr,
+                          const gnss_acquired* acq, gnss_track_out* out, const PosCfg* pos)
+{
+    if (!file || !sg || !tr || !acq || !out) return GNSS_EARG;
+    g->timing = gnss_timing{};
+    const int nsv = acq->n;
+    std::vector<int32_t> chans;
+    if (tr->chan && tr->n_chan > 0) chans.assign(tr->chan, tr->chan + tr->n_chan);
+    else for (int i = 0; i < nsv; i++) chans.push_back(i);
+    bool ok = nsv > 0 && nsv <= GNSS_MAX_SV;
+    for (int c : chans) ok = ok && c >= 0 && c < nsv;
+    if (!ok) return tracking_impl(g, file, sg, tr, acq, out, pos, nullptr, nullptr);  // (its own error)
+    const int M = (int)g->members.size();
+    const auto shards = group::deal((int)chans.size(), M);
+    const bool odev = (out->flags & GNSS_OUT_DEVICE) != 0;
+    int outdev = g->device;
+    if (odev && (out->rec || out->taps)) {
+        const int d = pointer_device(out->rec ? (const void*)out->rec : (const void*)out->taps);
+        if (d >= 0) outdev = d;
+    }
+    const int ntaps = pos ? (pos->mc_pdi ? GNSS_MC_TAPS : 3) : (tr->n_taps > 0 ? tr->n_taps : 3);
+    const int64_t ML = out->max_len;
+    const size_t rec_blk = (size_t)GNSS_NFIELDS * (size_t)ML, tap_blk = (size_t)2 * ntaps * (size_t)ML;
+    std::vector<group::TrackStatus> ts((size_t)M, group::TrackStatus{GNSS_OK, 0});
+    std::vector<int32_t> rows((size_t)M, 0);
+    std::vector<char> ran((size_t)M, 0);
+    for_members(g, [&](int k) {
+        gnss_ctx* m = g->members[(size_t)k];
+        std::vector<int32_t> mine;
+        for (int i : shards[(size_t)k]) mine.push_back(chans[(size_t)i]);
+        if (mine.empty()) return;
+        ran[(size_t)k] = 1;
+        gnss_track t = *tr;
+        t.chan = mine.data();
+        t.n_chan = (int32_t)mine.size();
+        gnss_track_out o = *out;
+        const bool remote = odev && (m->device != outdev || m->opt[GNSS_OPT_FORCE_PEER] != 0);
+        DevBuf lrec, ltap;
+        std::vector<int32_t> slot(mine.size());
+        auto set_err = [&](int st, const char* what) {
+            ts[(size_t)k] = group::TrackStatus{st, -1};
+            m->err = what;
+        };
+        if (remote) {
+            for (size_t i = 0; i < mine.size(); i++) slot[i] = (int32_t)i;
+            if (hipSetDevice(m->device) != hipSuccess ||
+                (out->rec && lrec.alloc(m, "grp.rec", sizeof(double) * rec_blk * mine.size()) != hipSuccess) ||
+                (out->taps && ltap.alloc(m, "grp.taps", sizeof(double) * tap_blk * mine.size()) != hipSuccess)) {
+                set_err(GNSS_EDEVICE, "multi-device tracking: member output buffers");
+                return;
+            }
+            o.rec = out->rec ? lrec.as<double>() : nullptr;
+            o.taps = out->taps ? ltap.as<double>() : nullptr;
+        }
+        const int st = tracking_impl(m, file, sg, &t, acq, &o, pos, nullptr, remote ? slot.data() : nullptr);
+        ts[(size_t)k] = group::TrackStatus{st, m->fail_chan};
+        rows[(size_t)k] = o.cn0_rows;
+        if (st != GNSS_OK || !remote) return;
+        bool copied = true;
+        for (size_t i = 0; i < mine.size() && copied; i++) {
+            const int64_t c = mine[i];
+            if (out->rec)
+                copied = hipMemcpyPeerAsync(out->rec + c * (int64_t)rec_blk, outdev, lrec.as<double>() + i * rec_blk,
+                                            m->device, sizeof(double) * rec_blk, m->stream) == hipSuccess;
+            if (copied && out->taps)
+                copied = hipMemcpyPeerAsync(out->taps + c * (int64_t)tap_blk, outdev, ltap.as<double>() + i * tap_blk,
+                                            m->device, sizeof(double) * tap_blk, m->stream) == hipSuccess;
+        }
+        if (!copied || hipStreamSynchronize(m->stream) != hipSuccess) set_err(GNSS_EDEVICE, "multi-device tracking: peer copy of the rows");
+    });
+    std::vector<gnss_timing> tm;
+    for (int k = 0; k < M; k++)
+        if (ran[(size_t)k]) tm.push_back(g->members[(size_t)k]->timing);
+    g->timing = group::combine_timing(tm);
+    const int status = group::tracking_status(ts);
+    if (status != GNSS_OK) {
+        if (out->len) for (int c : chans) out->len[c] = 0;
+        for (int k = 0; k < M; k++)
+            if (ts[(size_t)k].status == status)
+                return fail(g, status, "member %d (device %d): %s", k, g->members[(size_t)k]->device,
+                            g->members[(size_t)k]->err.c_str());
+        return fail(g, status, "multi-device tracking failed");
+    }
+    int32_t r = 0;
+    for (int k = 0; k < M; k++)
+        if (ran[(size_t)k]) r = std::max(r, rows[(size_t)k]);
+    out->cn0_rows = r;
+    return GNSS_OK;
+}
+
 extern "C" {
 
 int gnss_abi_version(void) { return GNSS_ABI_VERSION; }
@@ -599,9 +820,58 @@ int gnss_ctx_create(int device, gnss_ctx** out)
     return GNSS_OK;
 }
 
+int gnss_ctx_create_multi(const int* devices, int n, gnss_ctx** out)
+{
+    if (!out) return GNSS_EARG;
+    *out = nullptr;
+    if (!devices || n < 1 || n > GNSS_MAX_DEVICES) return GNSS_EARG;
+    gnss_ctx* g = nullptr;
+    int st = gnss_ctx_create(devices[0], &g);
+    if (st) return st;
+    for (int k = 0; k < n; k++) {
+        gnss_ctx* m = nullptr;
+        if ((st = gnss_ctx_create(devices[k], &m))) {
+            gnss_ctx_destroy(g);
+            return st;
+        }
+        m->member = true;
+        g->members.push_back(m);
+    }
+    // peer access between the distinct devices (the xGMI copies of records and rows; a pair
+    // without it still copies, staged by the runtime)
+    std::vector<int> ds(devices, devices + n);
+    std::sort(ds.begin(), ds.end());
+    ds.erase(std::unique(ds.begin(), ds.end()), ds.end());
+    for (int a : ds)
+        for (int b : ds) {
+            int can = 0;
+            if (a == b || hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can) continue;
+            if (hipSetDevice(a) == hipSuccess) (void)hipDeviceEnablePeerAccess(b, 0);
+            (void)hipGetLastError();  // (hipErrorPeerAccessAlreadyEnabled is fine)
+        }
+    (void)hipSetDevice(devices[0]);
+    *out = g;
+    return GNSS_OK;
+}
+
+int gnss_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int gnss_ctx_members(const gnss_ctx* ctx)
+{
+    if (!ctx) return 0;
+    return ctx->members.empty() ? 1 : (int)ctx->members.size();
+}
+
 void gnss_ctx_destroy(gnss_ctx* ctx)
 {
     if (!ctx) return;
+    for (gnss_ctx* m : ctx->members) gnss_ctx_destroy(m);
+    ctx->members.clear();
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
@@ -633,6 +903,7 @@ int gnss_ctx_set_profiling(gnss_ctx* ctx, int enable)
 {
     if (!ctx) return GNSS_EARG;
     ctx->profiling = enable;
+    for (gnss_ctx* m : ctx->members) m->profiling = enable;
     return GNSS_OK;
 }
 
@@ -640,13 +911,17 @@ int gnss_ctx_set_window(gnss_ctx* ctx, uint64_t bytes)
 {
     if (!ctx) return GNSS_EARG;
     ctx->window = bytes;
+    for (gnss_ctx* m : ctx->members) m->window = bytes;
     return GNSS_OK;
 }
 
 int gnss_ctx_set_option(gnss_ctx* ctx, int key, int64_t value)
 {
     if (!ctx || key < 0 || key >= GNSS_OPT_COUNT) return GNSS_EARG;
+    if (key == GNSS_OPT_VT_BLOCKS && (value < 0 || value > GNSS_VT_MAX_BLOCKS))
+        return fail(ctx, GNSS_EARG, "GNSS_OPT_VT_BLOCKS outside 0..%d", GNSS_VT_MAX_BLOCKS);
     ctx->opt[key] = value;
+    for (gnss_ctx* m : ctx->members) m->opt[key] = value;
     return GNSS_OK;
 }
 
@@ -654,6 +929,7 @@ int gnss_ctx_set_acq_precision(gnss_ctx* ctx, int fp64)
 {
     if (!ctx || (fp64 != 0 && fp64 != 1)) return GNSS_EARG;
     ctx->acq_fp64 = fp64;
+    for (gnss_ctx* m : ctx->members) m->acq_fp64 = fp64;
     return GNSS_OK;
 }
 
@@ -698,6 +974,7 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
                      const gnss_acq* acq, gnss_acquired* out, gnss_acq_diag* diag)
 {
     if (!ctx || !file || !sg || !acq || !out) return GNSS_EARG;
+    if (!ctx->members.empty()) return group_acquisition(ctx, file, sg, acq, out, diag);
     memset(out, 0, sizeof(*out));
     if (diag) memset(diag, 0, sizeof(*diag));
     ctx->timing = gnss_timing{};
@@ -899,27 +1176,15 @@ struct StepGraph {
 
 }  // namespace
 
-// The sibling loop of trackingCT_POS_updated.m (its tracking half): steps and countinx.
-struct PosCfg {
-    int32_t ctPOS;            // track.ctPOS (datalength, trackingCT_POS_updated.m:50)
-    const int32_t* countinx;  // countinx(svIndex) of countinx.mat (:29), by channel position
-    // 0: trackingCT_POS_updated.m. 1 or 10: trackingCT_POS_updated_multicorrelator.m, every
-    // step at this pdi (track.pdi, :46), 25 taps, ctPOS = datalength/pdi steps (:170)
-    int32_t mc_pdi;
-};
-
-// trackingCT_multiCorr-GIVEN.m (function trackingCT_multiCorr): `datalength` 1-ms steps
-// per channel (:27, hard-coded 50000 there), trackingCT conventions otherwise
-struct GivenCfg {
-    int32_t datalength;
-};
-
 // trackingCT.m (pos == gv == nullptr), the tracking loop of trackingCT_POS_updated.m (pos)
 // or of trackingCT_multiCorr-GIVEN.m (gv)
+// dev_slot (a group member whose GNSS_OUT_DEVICE rows go through a buffer of its own): channel
+// i of the call expands into row block dev_slot[i] of out->rec / out->taps instead of chans[i].
 static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg, const gnss_track* tr,
                          const gnss_acquired* acq, gnss_track_out* out, const PosCfg* pos,
-                         const GivenCfg* gv = nullptr)
+                         const GivenCfg* gv = nullptr, const int32_t* dev_slot = nullptr)
 {
+    if (ctx) ctx->fail_chan = -1;
     // GNSS_HOSTPROF: host-side phases of this call on stderr
     const bool hp = probe_env("GNSS_HOSTPROF") != nullptr;
     const auto h0 = std::chrono::steady_clock::now();
@@ -1278,7 +1543,7 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
 
     DevBuf d_pgran, d_err;
     if (persist1 || persist10) {
-        HIP_TRY(d_pgran.alloc(ctx, "trk.d_pgran", sizeof(unsigned long long) * (size_t)nch * 2 * kMaxBpcRun * 4 * ntaps));
+        HIP_TRY(d_pgran.alloc(ctx, "trk.d_pgran", sizeof(unsigned long long) * 2 * (size_t)nch * gran_per_chan(ntaps)));
         HIP_TRY(d_err.alloc(ctx, "trk.d_err", 16));
         HIP_TRY(hipMemsetAsync(d_pgran.p, 0, d_pgran.n, ctx->stream));
         HIP_TRY(hipMemsetAsync(d_err.p, 0, 16, ctx->stream));
@@ -1509,8 +1774,11 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
 
     if (hp) fprintf(stderr, "hostprof d2h done %.3f ms\n", hms());
     int status = GNSS_OK;
-    for (auto& t : chh)
+    for (int i = 0; i < nch; i++) {
+        const TrkChan& t = chh[i];
+        if (t.status && ctx->fail_chan < 0) ctx->fail_chan = chans[i];  // (the first failing channel)
         if (t.status && (status == GNSS_OK || t.status == GNSS_ENODATA)) status = t.status;
+    }
     if (status != GNSS_OK) {
         if (out->len) for (int c : chans) out->len[c] = 0;
         return fail(ctx, status, status == GNSS_ENODATA ? "Not enough raw data" : "tracking failed: %s",
@@ -1536,7 +1804,7 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
         std::vector<int64_t> job(2 * (size_t)nch);
         for (int i = 0; i < nch; i++) {
             job[2 * i] = n1_of(i);
-            job[2 * i + 1] = chans[i];
+            job[2 * i + 1] = dev_slot ? dev_slot[i] : chans[i];
         }
         DevBuf d_job;
         HIP_TRY(d_job.alloc(ctx, "trk.d_job", sizeof(int64_t) * job.size()));
@@ -1609,6 +1877,7 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
 int gnss_tracking_ct(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg, const gnss_track* tr,
                      const gnss_acquired* acq, gnss_track_out* out)
 {
+    if (ctx && !ctx->members.empty()) return group_tracking(ctx, file, sg, tr, acq, out, nullptr);
     return tracking_impl(ctx, file, sg, tr, acq, out, nullptr);
 }
 
@@ -1616,6 +1885,7 @@ int gnss_tracking_ct_pos(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
                          const gnss_acquired* acq, int32_t ctPOS, const int32_t* countinx, gnss_track_out* out)
 {
     const PosCfg pc{ctPOS, countinx, 0};
+    if (ctx && !ctx->members.empty()) return group_tracking(ctx, file, sg, tr, acq, out, &pc);
     return tracking_impl(ctx, file, sg, tr, acq, out, &pc);
 }
 
@@ -1634,6 +1904,7 @@ int gnss_tracking_ct_mc(gnss_ctx* ctx, const gnss_file* file, const gnss_signal*
     if (pdi != 1 && pdi != 10) return fail(ctx, GNSS_EARG, "multicorrelator: pdi must be 1 or 10");
     if (msPosCT < pdi) return fail(ctx, GNSS_EARG, "multicorrelator: msPosCT/pdi must be >= 1");
     const PosCfg pc{msPosCT / pdi, nullptr, pdi};  // msIndex = 1:datalength/pdi (:170)
+    if (!ctx->members.empty()) return group_tracking(ctx, file, sg, tr, acq, out, &pc);
     return tracking_impl(ctx, file, sg, tr, acq, out, &pc);
 }
 
@@ -1919,8 +2190,9 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     const bool multi = prec == 1;
     DevBuf d_part, d_ticket;
     if (multi) {
-        A.nb = (int)std::max<int64_t>(1, (nominal + kVtStepSamples - 1) / kVtStepSamples);
-        if (ctx->opt[GNSS_OPT_VT_BLOCKS] > 0) A.nb = (int)std::min<int64_t>(ctx->opt[GNSS_OPT_VT_BLOCKS], 1024);
+        A.nb = (int)std::min<int64_t>(std::max<int64_t>(1, (nominal + kVtStepSamples - 1) / kVtStepSamples),
+                                      GNSS_VT_MAX_BLOCKS);
+        if (ctx->opt[GNSS_OPT_VT_BLOCKS] > 0) A.nb = (int)ctx->opt[GNSS_OPT_VT_BLOCKS];
         HIP_TRY(d_part.alloc(ctx, "vt.part", sizeof(double) * 2 * (size_t)n * A.nb));
         HIP_TRY(d_ticket.alloc(ctx, "vt.ticket", sizeof(unsigned) * (size_t)n));
         HIP_TRY(hipMemsetAsync(d_ticket.p, 0, sizeof(unsigned) * (size_t)n, ctx->stream));
@@ -1969,6 +2241,9 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
             HIP_TRY(hipStreamSynchronize(ctx->stream));
             st = restage(need_lo);
             if (st) return st;
+            if (need_lo < w.base || need_hi > w.base + w.len)
+                return fail(ctx, GNSS_EDEVICE, "step %d: the restaged IF window [%lld, %lld) does not cover the reads [%lld, %lld)",
+                            s + 1, (long long)w.base, (long long)(w.base + w.len), (long long)need_lo, (long long)need_hi);
         }
         A.rec = reinterpret_cast<const uint8_t*>(w.ptr);
         A.base = w.base;

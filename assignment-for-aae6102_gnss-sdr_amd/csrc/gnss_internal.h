@@ -262,7 +262,7 @@ struct TrkBuffers {
     double* dbg_sums;         // if set: last arriver stores the raw sums [nch][2*ntaps], no finalize
     unsigned long long* stamps;  // timing probe (GNSS_STAMPS): [kStampSlots][8] wall clock + counter
     // persistent step loop (track_run_kernel): R2 hand-off granules {tag:32 | word:32}
-    unsigned long long* pgran;   // [nch][2 (step parity)][kMaxBpcRun][4*ntaps] block partials
+    unsigned long long* pgran;   // [nch][gran_per_chan(ntaps)][2] block partials (16-B granules)
     unsigned* run_err;           // set when a hand-off wait times out
     int32_t n1;               // msToProcessCT_1ms
 };
@@ -325,6 +325,19 @@ constexpr int kMaxBpcRun = 256;  // blocks per channel of the persistent kernel
 // blocks per CU; 192 blocks of 24-sample lanes = 1.18 M samples per step)
 constexpr int run_bpc_cap(int ntaps) { return ntaps > 3 ? 192 : kMaxBpcRun; }
 constexpr int kMaxVpb = 16;      // virtual blocks per resident block of the persistent kernel
+// The persistent kernel's 16-B hand-off granules per channel. 3 taps: [2 (step parity)]
+// [kMaxBpcRun][6]. Above 3 taps only the loop's E/P/L go through the step's exchange
+// ([2][kMaxBpcRun][<= 6], region A); the other taps' partials (region B) are published after
+// them and summed one step later by their owner blocks: [kDeferSlots (step mod 4)]
+// [value < 2 ntaps][kMaxBpcRun]. Four slots: a block can run at most two steps ahead of the
+// owner that still reads a slot.
+constexpr int kDeferSlots = 4;
+constexpr int gran_region_b(int ntaps) { return ntaps > 3 ? 2 * kMaxBpcRun * 6 : 0; }
+constexpr int gran_slot_b(int ntaps) { return 2 * ntaps * kMaxBpcRun; }
+constexpr int gran_per_chan(int ntaps)
+{
+    return ntaps > 3 ? gran_region_b(ntaps) + kDeferSlots * gran_slot_b(ntaps) : 2 * kMaxBpcRun * 2 * ntaps;
+}
 constexpr int kDescWords = (int)(sizeof(StepDesc) / 4);
 
 // ----------------------------------------------------------------------------

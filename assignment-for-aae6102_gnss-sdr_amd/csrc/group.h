@@ -1,0 +1,157 @@
+// group.h — the bookkeeping of a multi-device context (gnss_ctx_create_multi), host C++ only
+// (no HIP: tests/native/group_test.cpp compiles it on the CPU).
+//
+// The reference runs the PRN loop of acquisition.m:47-80 and the channel loop of
+// trackingCT.m:22-528 one item after the other; items share no state (quirk A.11's global
+// svindex / nsv aside, which every shard keeps), so a multi-device context deals them
+// round-robin over its member contexts and merges the members' results back into the
+// caller's arrays in the reference's order. Everything here is that dealing and merging.
+#ifndef GNSS_GROUP_H
+#define GNSS_GROUP_H
+
+#include <algorithm>
+#include <cstdint>
+#include <vector>
+
+#include "../../include/gnss_mi355x.h"
+
+namespace gnss {
+namespace group {
+
+// items 0..n-1 dealt round-robin over m members: member k gets k, k + m, k + 2m, ...
+inline std::vector<std::vector<int>> deal(int n, int m)
+{
+    std::vector<std::vector<int>> s((size_t)(m > 0 ? m : 0));
+    for (int i = 0; i < n && m > 0; i++) s[(size_t)(i % m)].push_back(i);
+    return s;
+}
+
+// Member results of one acquisition call merged into the reference's output: `prns` is the
+// call's PRN list (acquisition.m:47 order), shards[k] the list positions member k searched,
+// outs[k] / diags[k] its results (its own PRNs, in its list order). Acquired rows and diag
+// rows come out in PRN-list order, as the serial loop appends them (:70-74). Returns false
+// if a member's output names a PRN it was not given (a bookkeeping error).
+inline bool merge_acquired(const std::vector<int32_t>& prns, const std::vector<std::vector<int>>& shards,
+                           const std::vector<gnss_acquired>& outs, const std::vector<gnss_acq_diag>* diags,
+                           gnss_acquired* out, gnss_acq_diag* diag)
+{
+    const size_t m = shards.size();
+    std::vector<int> owner(prns.size(), -1);
+    for (size_t k = 0; k < m; k++)
+        for (int i : shards[k]) owner[(size_t)i] = (int)k;
+    std::vector<int> ia(m, 0), id(m, 0);  // next unread row of each member's out / diag
+    out->n = 0;
+    if (diag) diag->n = 0;
+    for (size_t i = 0; i < prns.size(); i++) {
+        const int k = owner[i];
+        if (k < 0) return false;
+        const gnss_acquired& o = outs[(size_t)k];
+        if (ia[(size_t)k] < o.n && o.sv[ia[(size_t)k]] == prns[i]) {
+            const int r = ia[(size_t)k]++, w = out->n++;
+            out->sv[w] = o.sv[r];
+            out->SNR[w] = o.SNR[r];
+            out->Doppler[w] = o.Doppler[r];
+            out->codedelay[w] = o.codedelay[r];
+            out->fineFreq[w] = o.fineFreq[r];
+        }
+        if (diag && diags) {
+            const gnss_acq_diag& d = (*diags)[(size_t)k];
+            if (id[(size_t)k] >= d.n || d.prn[id[(size_t)k]] != prns[i]) return false;
+            const int r = id[(size_t)k]++, w = diag->n++;
+            diag->prn[w] = d.prn[r];
+            diag->SNR[w] = d.SNR[r];
+            diag->fbin[w] = d.fbin[r];
+            diag->codePhase[w] = d.codePhase[r];
+            diag->peak[w] = d.peak[r];
+            diag->peak2[w] = d.peak2[r];
+        }
+    }
+    for (size_t k = 0; k < m; k++)
+        if (ia[k] != outs[k].n) return false;  // a row of a PRN the member was not given
+    return true;
+}
+
+// The status of a sharded acquisition: a member whose PRNs yield nothing returns
+// GNSS_ENODATA ("No satellites acquired", acquisition.m:84-85), which holds for the call
+// only when the merged result is empty; any other failure is the first member's in order.
+inline int acquisition_status(const std::vector<int>& st, int merged_n)
+{
+    for (int s : st)
+        if (s != GNSS_OK && s != GNSS_ENODATA) return s;
+    return merged_n > 0 ? GNSS_OK : GNSS_ENODATA;
+}
+
+// The status of a sharded tracking call. One context decides it over its channels in
+// order (gnss_api.cpp, tracking_impl): GNSS_ENODATA ("Not enough raw data") if any channel
+// ran short, else the status of the first failing channel. Member k reports its status and
+// the global index of the channel that set it (-1: failed before any channel ran, i.e. an
+// argument error that every member shares). The same rule over the members' reports gives
+// the one-context answer.
+struct TrackStatus {
+    int status;
+    int chan;
+};
+inline int tracking_status(const std::vector<TrackStatus>& st)
+{
+    int best = GNSS_OK, best_chan = 0;
+    for (const TrackStatus& t : st) {
+        if (t.status == GNSS_OK) continue;
+        if (t.status == GNSS_ENODATA) return GNSS_ENODATA;
+    }
+    for (const TrackStatus& t : st) {
+        if (t.status == GNSS_OK) continue;
+        if (best == GNSS_OK || t.chan < best_chan) {
+            best = t.status;
+            best_chan = t.chan;
+        }
+    }
+    return best;
+}
+
+// Timing of a group call: the members ran side by side, so durations are the slowest
+// member's and counts are summed.
+inline gnss_timing combine_timing(const std::vector<gnss_timing>& t)
+{
+    gnss_timing r{};
+    for (const gnss_timing& x : t) {
+        r.acq_ms = std::max(r.acq_ms, x.acq_ms);
+        r.acq_corr_ms = std::max(r.acq_corr_ms, x.acq_corr_ms);
+        r.acq_fine_ms = std::max(r.acq_fine_ms, x.acq_fine_ms);
+        r.track_ms = std::max(r.track_ms, x.track_ms);
+        r.track_kernel_ms = std::max(r.track_kernel_ms, x.track_kernel_ms);
+        r.track_launches += x.track_launches;
+        r.track_channel_samples += x.track_channel_samples;
+        r.acq_hypothesis_samples += x.acq_hypothesis_samples;
+        r.h2d_ms = std::max(r.h2d_ms, x.h2d_ms);
+        r.track10_kernel_ms = std::max(r.track10_kernel_ms, x.track10_kernel_ms);
+        r.track10_launches += x.track10_launches;
+        r.track10_channel_samples += x.track10_channel_samples;
+        r.h2d_bytes += x.h2d_bytes;
+        r.track_segments += x.track_segments;
+    }
+    return r;
+}
+
+// Members grouped by device: members on one device run one after the other (two persistent
+// tracking grids on one GPU would not both be resident), devices side by side. Returns, per
+// distinct device in first-appearance order, the member indices on it.
+inline std::vector<std::vector<int>> by_device(const std::vector<int>& devices)
+{
+    std::vector<int> seen;
+    std::vector<std::vector<int>> g;
+    for (size_t k = 0; k < devices.size(); k++) {
+        auto it = std::find(seen.begin(), seen.end(), devices[k]);
+        if (it == seen.end()) {
+            seen.push_back(devices[k]);
+            g.push_back({(int)k});
+        } else {
+            g[(size_t)(it - seen.begin())].push_back((int)k);
+        }
+    }
+    return g;
+}
+
+}  // namespace group
+}  // namespace gnss
+
+#endif

@@ -1047,6 +1047,51 @@ __device__ __forceinline__ double block_partial(double* s_mem, const double (&oI
     return a;
 }
 
+// One pass of block_partial over a chosen set of taps (the persistent loop's split of the
+// > 3-tap reduction: the loop's E/P/L first, the other taps after their publication). The
+// taps of bit mask `sel` (at most red_taps<NT>() of them) take part in tap order: the q-th
+// one's I / Q are the pass's values 2q / 2q + 1, reduced by exactly block_partial's lanes and
+// order (8-lane runs, four runs per lane, the DPP quad butterfly), so every value has the bits
+// block_partial gives it. Value w of the pass ends in lanes 4w .. 4w + 3.
+template <int NT>
+__device__ __forceinline__ double block_pass(double* s_mem, const double (&oI)[NT], const double (&oQ)[NT],
+                                             int tid, unsigned sel)
+{
+    constexpr int T = kTrkThreads;
+    constexpr int HT = red_taps<NT>();
+    double* red = s_mem;                 // [2 HT][T]
+    double* red2 = s_mem + 2 * HT * T;   // [2 HT][32]
+#pragma unroll
+    for (int s = 0; s < NT; s++) {
+        if ((sel >> s) & 1u) {  // (sel wave-uniform: scalar branches)
+            const int q = __builtin_popcount(sel & ((1u << s) - 1u));
+            red[(2 * q) * T + tid] = oI[s];
+            red[(2 * q + 1) * T + tid] = oQ[s];
+        }
+    }
+    lds_barrier();
+    const int nv = 2 * __builtin_popcount(sel);
+    for (int e = tid; e < nv * 32; e += T) {
+        const double* r = red + (e >> 5) * T + (e & 31) * 8;
+        double x = r[0];
+#pragma unroll
+        for (int k = 1; k < 8; k++) x += r[k];
+        red2[e] = x;
+    }
+    lds_barrier();
+    double a = 0.0;
+    if (tid < nv * 4) {
+        const double* r = red2 + (tid >> 2) * 32 + (tid & 3) * 8;
+        a = r[0];
+#pragma unroll
+        for (int k = 1; k < 8; k++) a += r[k];
+        a += dpp_f64<0xB1>(a);  // quad_perm [1,0,3,2]
+        a += dpp_f64<0x4E>(a);  // quad_perm [2,3,0,1]
+    }
+    lds_barrier();  // red / red2 read before the next pass or the caller reuses the slots
+    return a;
+}
+
 // Channel: the sum over the bpc block partials of value v = tid / L (tid < L*NV, L = 16
 // lanes per value where 16*NV fits the block, else 8): lane q = tid % L adds blocks q,
 // q+L, ... in order, then a DPP butterfly over the L lanes. Every lane of the L returns the
@@ -1054,6 +1099,22 @@ __device__ __forceinline__ double block_partial(double* s_mem, const double (&oI
 template <int NV> constexpr int chan_lanes()
 {
     return 16 * NV <= kTrkThreads ? 16 : 8 * NV <= kTrkThreads ? 8 : 4;  // (25 taps: 4)
+}
+
+// The same sum with the lane count L given (the persistent loop's deferred taps keep the L
+// of the whole tap set, chan_lanes<2 NT>(), whatever subset of values it sums at once).
+template <int L, class Load>
+__device__ __forceinline__ double channel_sum_l(int bpc, int tid, Load load)
+{
+    const int v = tid / L, q = tid % L;
+    double a = 0.0;
+#pragma unroll 4
+    for (int k = q; k < bpc; k += L) a += load(k, v);
+    a += dpp_f64<0xB1>(a);   // quad_perm [1,0,3,2]
+    a += dpp_f64<0x4E>(a);   // quad_perm [2,3,0,1]
+    if constexpr (L >= 8) a += dpp_f64<0x141>(a);   // row_half_mirror: the other quad of the 8
+    if constexpr (L == 16) a += dpp_f64<0x140>(a);  // row_mirror: the other 8 of the 16
+    return a;
 }
 
 template <int NV, class Load>
@@ -1382,6 +1443,52 @@ __device__ bool sweep16(__amdgpu_buffer_rsrc_t r, int n, unsigned tag, unsigned*
     return v == 0;
 }
 
+// sweep16 over two granule ranges at once (the persistent loop's > 3-tap form: this step's
+// E/P/L partials, plus in the blocks that own deferred taps the previous step's partials of
+// those taps). Logical granule e < n1 is base1 + e (tag1, words to dst1[2e]); e >= n1 is
+// base2 + e - n1 (tag2, dst2). Same pollers, bound and closing vote as sweep16.
+__device__ bool sweep16x2(__amdgpu_buffer_rsrc_t r, int n1, int base1, unsigned tag1, unsigned* dst1, int n2,
+                          int base2, unsigned tag2, unsigned* dst2, int pid, int np, unsigned* err)
+{
+    const int n = n1 + n2;
+    unsigned long long todo = 0;
+    if (pid >= 0)
+        for (int k = 0, e = pid; e < n; k++, e += np) todo |= 1ull << k;
+    unsigned long long t0 = 0;
+    int late = 0;
+    while (todo) {
+        for (int k = 0; (todo >> k) != 0; k++) {
+            if (!((todo >> k) & 1ull)) continue;
+            const int e = pid + k * np;
+            const bool first = e < n1;
+            const int e2 = first ? e : e - n1;
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, ((first ? base1 : base2) + e2) * 16, 0, kPolSc1);
+            const unsigned tg = first ? tag1 : tag2;
+            if (v.y == tg && v.w == tg) {
+                unsigned* d = first ? dst1 : dst2;
+                d[2 * e2] = v.x;
+                d[2 * e2 + 1] = v.z;
+                todo &= ~(1ull << k);
+            }
+        }
+        if (!todo) break;
+        if (++late >= 64) {
+            const unsigned long long t = wall_clock64();
+            if (!t0) t0 = t;
+            else if (t - t0 > 200000000ull) { atomicExch(err, 1u); break; }
+            late = 0;
+        }
+    }
+    __shared__ unsigned s_vote2[kTrkThreads / 64];
+    const unsigned any_left = __ballot(todo != 0) != 0ull ? 1u : 0u;
+    if ((threadIdx.x & 63) == 0) s_vote2[threadIdx.x >> 6] = any_left;
+    lds_barrier();
+    unsigned v = 0;
+#pragma unroll
+    for (int w = 0; w < kTrkThreads / 64; w++) v |= s_vote2[w];
+    return v == 0;
+}
+
 // Grid census (guide G16: residency is a precondition, not a given): every block
 // arrives on one counter; the last arrival starts the launch, a block that waits ~20 ms
 // aborts it instead (one CAS decides). On abort every block leaves before touching any
@@ -1484,10 +1591,91 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
     const int8_t* iq = b.iq - p.buf_base;  // absolute-byte addressing
     const int64_t gmax = (p.buf_base + p.buf_len) / 16 - 1;  // last resident 16-B group
     const unsigned cabits = lane < 32 ? ((g_cu32*)b.ca_bits)[ch * 32 + lane] : 0u;
-    // this channel's granules: [parity][block][value] x 16 B
+    // this channel's granules (gran_per_chan): 3 taps [parity][block][value] x 16 B; above,
+    // region A [parity][block][E/P/L value] and region B [step mod 4][value][block]
     const __amdgpu_buffer_rsrc_t pg = __builtin_amdgcn_make_buffer_rsrc(
-        b.pgran + (int64_t)ch * 2 * kMaxBpcRun * 2 * NV, (short)0, 2 * kMaxBpcRun * NV * 16, kBufRsrcWord3);
+        b.pgran + (int64_t)ch * 2 * gran_per_chan(NT), (short)0, gran_per_chan(NT) * 16, kBufRsrcWord3);
     constexpr int kChanWords = (int)(sizeof(TrkChan) / 8);
+
+    // Above 3 taps (config 5's 11-tap ACF) only E / P / L feed the loop (trackingCT.m:470-483):
+    // they are reduced, published and swept first (region A); the other taps' values (B,
+    // only when the caller asked for the taps) are reduced after that publication, overlapping
+    // the exchange, and the previous step's are swept beside this step's E/P/L by the blocks
+    // that own them (a run of B values per block, blocks 3, 4, ...), whose idle tail wave
+    // sums them and writes the taps one step late. Every value keeps its reduction lanes and
+    // order (block_pass, channel_sum_l with the whole tap set's lane count), so the records
+    // and taps are the bits of the one-exchange form and of the per-step kernel.
+    constexpr bool kDefer = NT > 3;
+    constexpr int CL = chan_lanes<NV>();
+    constexpr int HT = red_taps<NT>();
+    // The configuration lives in LDS and is read where it is used (volatile LDS loads, never
+    // hoisted into registers that would live across the step loop: this kernel is at its
+    // register budget). selA / selB: the loop's taps / the others; NA: E/P/L values; nBv: B
+    // values; hb: B taps per reduction pass; [own_lo, own_lo + own_n): this block's B values;
+    // bslot / bneg (wave 1): the slot and phase-C sign of the step whose B values are due.
+    struct DeferCfg {
+        unsigned selA, selB;
+        int NA, nBv, hb, own_lo, own_n, bneg;
+        int64_t bslot;
+        int vmap[kDefer ? NV : 1];  // A values, then B values -> value index 2 tap + I/Q
+    };
+    __shared__ DeferCfg s_df;
+    typedef __attribute__((address_space(3))) volatile const int lds_vint;
+    typedef __attribute__((address_space(3))) volatile const long long lds_vi64;
+    auto dfi = [&](const int& f) { return uni((int)*(lds_vint*)&f); };
+    auto NA_ = [&]() { return kDefer ? dfi(s_df.NA) : NV; };
+    auto own_n_ = [&]() { return kDefer ? dfi(s_df.own_n) : 0; };
+    const bool dob = kDefer && b.taps_rec != nullptr;
+    if constexpr (kDefer) {
+        if (tid == 0) {
+            unsigned selA = 0, selB = 0;
+            for (int s = 0; s < NT; s++) {
+                if (s == tk.iE || s == tk.iP || s == tk.iL) selA |= 1u << s;
+                else selB |= 1u << s;
+            }
+            const int nA = __builtin_popcount(selA), nB = __builtin_popcount(selB);
+            const int nBv = 2 * nB, npass = (nB + HT - 1) / HT;
+            int own_lo = 0, own_n = 0;
+            if (dob && nBv > 0) {  // this block's run of B values
+                const int c = (nBv + pbpc - 1) / pbpc;
+                const int nown = (nBv + c - 1) / c;
+                const int r = ((pblk - 3) % pbpc + pbpc) % pbpc;
+                if (r < nown) {
+                    own_lo = r * c;
+                    own_n = nBv - own_lo < c ? nBv - own_lo : c;
+                }
+            }
+            s_df.selA = selA;
+            s_df.selB = selB;
+            s_df.NA = 2 * nA;
+            s_df.nBv = nBv;
+            s_df.hb = npass > 0 ? (nB + npass - 1) / npass : 1;
+            s_df.own_lo = own_lo;
+            s_df.own_n = own_n;
+            s_df.bneg = 0;
+            s_df.bslot = 0;
+            for (int s = 0; s < NT; s++) {
+                const unsigned below = (1u << s) - 1u;
+                const int v = ((selA >> s) & 1u) ? 2 * __builtin_popcount(selA & below)
+                                                 : 2 * nA + 2 * __builtin_popcount(selB & below);
+                s_df.vmap[v] = 2 * s;
+                s_df.vmap[v + 1] = 2 * s + 1;
+            }
+        }
+    }
+    // B taps of pass ps (1-based): ranks (ps - 1) * hb .. ps * hb - 1 among the B taps
+    auto sel_pass = [&](int ps) {
+        const unsigned selB = (unsigned)dfi(*(const int*)&s_df.selB);
+        const int hb = dfi(s_df.hb);
+        unsigned m = 0u;
+        int r = 0;
+        for (int s = 0; s < NT; s++)
+            if ((selB >> s) & 1u) {
+                if (r >= (ps - 1) * hb && r < ps * hb) m |= 1u << s;
+                r++;
+            }
+        return m;
+    };
 
     // step 0's descriptor and the state, as the previous launch left them
     for (int e = tid; e < kDescWords; e += T)
@@ -1519,6 +1707,37 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
     // (profiles/r04_block0_lateness.txt).
     const int duty_b = pbpc > 1 ? 1 : 0, duty_c = pbpc > 2 ? 2 : duty_b;
     int s_now = 0;  // (probe stamps of the flush)
+    // the owned B values of a finished step, swept into pb: summed (8 lanes per value, the
+    // order of channel_sum<NV>) and written to the taps, by one wave
+    auto defer_write = [&](const unsigned* pb) {
+        constexpr int VPW = 64 / CL;  // values per wave pass
+        const int own_n = own_n_(), own_lo = dfi(s_df.own_lo), NA = NA_(), bneg = dfi(s_df.bneg);
+        const int64_t bslot = uni((int64_t)*(lds_vi64*)&s_df.bslot);
+        for (int c0 = 0; c0 < own_n; c0 += VPW) {
+            const double a = channel_sum_l<CL>(bpc, lane, [&](int k, int vl) {
+                const int vv = c0 + vl;
+                if (vv >= own_n) return 0.0;
+                const unsigned lo = pb[(vv * bpc + k) * 2], hi = pb[(vv * bpc + k) * 2 + 1];
+                return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+            });
+            const int vv = c0 + lane / CL;
+            if (lane % CL == 0 && vv < own_n && bslot < p.rec_cap)
+                ((g_dbl*)b.taps_rec)[((int64_t)ch * p.rec_cap + bslot) * NV + s_df.vmap[NA + own_lo + vv]] =
+                    bneg ? -a : a;  // (phase C: negated like every tap, :447-449)
+        }
+    };
+    // after a launch's last flush: the owned B values of finished step sf, swept and written
+    auto defer_final = [&](int sf) {
+        if (!kDefer || sf < 0) return;
+        const int own_n = own_n_();  // (block-uniform)
+        if (own_n <= 0) return;
+        unsigned* pb = reinterpret_cast<unsigned*>(s_mem);
+        if (!sweep16x2(pg, 0, 0, 0u, pb, own_n * bpc,
+                       gran_region_b(NT) + (sf & 3) * gran_slot_b(NT) + dfi(s_df.own_lo) * bpc, tag0 + sf + 1, pb,
+                       tid, T, b.run_err))
+            return;
+        if (wv == 1) defer_write(pb);
+    };
     auto flush = [&]() {
         if (wv == 1) {
             // (probe GNSS_FLUSH_PROBE & 2: block 0's record part twice, stamped at [2000..2002]
@@ -1545,8 +1764,15 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
                 write_record_i(p, b, ch, s_c, s_o, s_u, s_fin, pre, 3);
                 fr[2002] = wall_clock64();
             }
-            if (pblk == duty_b && b.taps_rec && lane < NV && s_c.slot < p.rec_cap)
-                ((g_dbl*)b.taps_rec)[((int64_t)ch * p.rec_cap + s_c.slot) * NV + lane] = s_fin[lane];
+            if (pblk == duty_b && b.taps_rec && lane < NA_() && s_c.slot < p.rec_cap) {
+                // (above 3 taps the loop's values only: the others follow a step later, defer_write)
+                const int v = kDefer ? s_df.vmap[lane] : lane;
+                ((g_dbl*)b.taps_rec)[((int64_t)ch * p.rec_cap + s_c.slot) * NV + v] = s_fin[v];
+            }
+            if (kDefer && lane == 0) {  // the pending step's slot and sign, for its deferred taps
+                s_df.bslot = s_c.slot;
+                s_df.bneg = s_o.phaseC;
+            }
             if (lane == 0) update_state_inplace(p, b, ch, s_c, s_o, s_u, s_fin, pblk == duty_c);
         }
         pend = false;
@@ -1560,7 +1786,9 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         const int bad = D.bad ? D.bad : D.bad_tap;
         const bool stop = !D.phaseC && D.Index + 1 > n1_target;  // 1-ms run of this channel done
         if (bad || stop || D.d * M >= 1.0) {  // (a code rate beyond Fs/M breaks the one-boundary lane)
+            const bool had = pend;
             if (pend) flush();
+            if (had) defer_final(s - 1);
             if (io && tid == 64) desc_rem(tk, &s_d[cur]);  // (complete for a step-kernel follow-up)
             __syncthreads();
             if (io) {  // leave the state and this (unused) descriptor for the host / next launch
@@ -1623,9 +1851,29 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
                 if (srow && tid == 0) srow[1] = wall_clock64();
                 if (brow && tid == 0) brow[40 + 256 + vb] = wall_clock64();
                 // block sum in a fixed order, published as granules
-                const double bsum = block_partial<NT>(s_mem, oI, oQ, tid);
-                if (tid < NV * 4 && (tid & 3) == 0)
-                    publish16(pg, ((s & 1) * kMaxBpcRun + vb) * NV + (tid >> 2), bsum, tag0 + s + 1);
+                if constexpr (!kDefer) {
+                    const double bsum = block_partial<NT>(s_mem, oI, oQ, tid);
+                    if (tid < NV * 4 && (tid & 3) == 0)
+                        publish16(pg, ((s & 1) * kMaxBpcRun + vb) * NV + (tid >> 2), bsum, tag0 + s + 1);
+                } else {
+                    // E / P / L first (region A), then the other taps (region B, slot s mod 4),
+                    // reduced while the exchange is in flight
+                    const double ba = block_pass<NT>(s_mem, oI, oQ, tid, (unsigned)dfi(*(const int*)&s_df.selA));
+                    const int NA = NA_();
+                    if (tid < NA * 4 && (tid & 3) == 0)
+                        publish16(pg, ((s & 1) * kMaxBpcRun + vb) * NA + (tid >> 2), ba, tag0 + s + 1);
+                    if (dob) {
+                        const int hb = dfi(s_df.hb), nB = dfi(s_df.nBv) / 2;
+                        for (int ps = 1; (ps - 1) * hb < nB; ps++) {
+                            const unsigned sel = sel_pass(ps);
+                            const double bb = block_pass<NT>(s_mem, oI, oQ, tid, sel);
+                            if (tid < 2 * __builtin_popcount(sel) * 4 && (tid & 3) == 0)
+                                publish16(pg, gran_region_b(NT) + (s & 3) * gran_slot_b(NT) +
+                                                  (2 * (ps - 1) * hb + (tid >> 2)) * bpc + vb,
+                                          bb, tag0 + s + 1);
+                        }
+                    }
+                }
                 if (srow && tid == 0) srow[2] = wall_clock64();
                 if (kProbe && b.stamps && ch == 0 && tid == 0) {  // latest partial of the channel (all blocks)
                     unsigned long long* r = b.stamps + (size_t)(s % kStampSlots) * kStampRow;
@@ -1639,6 +1887,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         // next tail reads them after the sweep's closing barrier)
         // (by wave 2, a poller, so that wave 1's flush of the previous step starts at once)
         if (wv == (io ? GNSS_IO_DR_WAVE : 2) && lane == 0) desc_rem(tk, &s_d[cur]);
+        const bool bsw = kDefer && pend && own_n_() > 0;  // the previous step's owned B values are due
         if (pend) {
             if (srow && tid == 64) srow[16] = wall_clock64();
             flush();  // (the sweep's closing barrier publishes it)
@@ -1650,9 +1899,20 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         // (waves 0, 2, 3 poll; wave 1 is flushing the previous step meanwhile)
         // (block 0: waves 0, 2, 3 poll while wave 1 writes the record; the other blocks'
         // wave 1 flush is short and it joins the polling after it)
-        if (!sweep16(pg, bpc * NV, tag0 + s + 1, pw, GNSS_SWEEP_IO_ALL || !io ? tid : (wv == 1 ? -1 : tid - (wv > 1 ? 64 : 0)),
-                     GNSS_SWEEP_IO_ALL || !io ? 4 * 64 : 3 * 64, b.run_err, (s & 1) * kMaxBpcRun * NV))
-            return;
+        {
+            const int pid = GNSS_SWEEP_IO_ALL || !io ? tid : (wv == 1 ? -1 : tid - (wv > 1 ? 64 : 0));
+            const int np = GNSS_SWEEP_IO_ALL || !io ? 4 * 64 : 3 * 64;
+            if constexpr (!kDefer) {
+                if (!sweep16(pg, bpc * NV, tag0 + s + 1, pw, pid, np, b.run_err, (s & 1) * kMaxBpcRun * NV)) return;
+            } else {
+                // this step's E / P / L, and the owned B values of the previous step (long published)
+                const int NA = NA_();
+                if (!sweep16x2(pg, bpc * NA, (s & 1) * kMaxBpcRun * NA, tag0 + s + 1, pw, bsw ? own_n_() * bpc : 0,
+                               gran_region_b(NT) + ((s - 1) & 3) * gran_slot_b(NT) + dfi(s_df.own_lo) * bpc, tag0 + s,
+                               pw + 2 * bpc * NA, pid, np, b.run_err))
+                    return;
+            }
+        }
         if (srow && tid == 0) srow[3] = wall_clock64();
         if (brow && tid == 0) brow[40 + 512 + blk] = wall_clock64();  // (probe: this block's all-in)
         // wave 2 issues the whole block's next IF (it starts at A + n, ftell after this
@@ -1664,16 +1924,17 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
                 prefetch_raw<SUB>(iq, ((A + n) >> 3) + ((int64_t)blk * T + h * 64 + lane) * SUB, gmax, s_raw,
                                   h * 64 + lane);
         }
-        constexpr int CL = chan_lanes<NV>();
-        if (tid < CL * NV) {
-            const double a = channel_sum<NV>(bpc, tid, [&](int k, int v) {
-                const unsigned lo = pw[(k * NV + v) * 2], hi = pw[(k * NV + v) * 2 + 1];
+        if (tid < CL * NA_()) {  // (above 3 taps: the E / P / L values, at their value index)
+            const int NA = NA_();
+            const double a = channel_sum_l<CL>(bpc, tid, [&](int k, int v) {
+                const unsigned lo = pw[(k * NA + v) * 2], hi = pw[(k * NA + v) * 2 + 1];
                 return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
             });
+            const int vi = kDefer ? s_df.vmap[tid / CL] : tid / CL;
             if constexpr (GNSS_CORR_PROBE != 0)  // (probe builds: E = P = L = 1, a steady loop)
-                if (tid % CL == 0) s_fin[tid / CL] = ((tid / CL) & 1) ? 0.0 * a : 1.0 + 0.0 * a;
+                if (tid % CL == 0) s_fin[vi] = (vi & 1) ? 0.0 * a : 1.0 + 0.0 * a;
             if constexpr (GNSS_CORR_PROBE == 0)
-                if (tid % CL == 0) s_fin[tid / CL] = D.phaseC ? -a : a;  // :447-449
+                if (tid % CL == 0) s_fin[vi] = D.phaseC ? -a : a;  // :447-449
         }
         const int phaseC = D.phaseC;
         lds_barrier();
@@ -1733,6 +1994,9 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
                 s_o = o;
                 s_u = u;
             }
+            // (idle otherwise: the previous step's owned B values, swept beside this step's
+            // E / P / L, summed and written)
+            if (bsw) defer_write(pw + 2 * bpc * NA_());
         } else {  // wave 2: the next step's scalars and checks, then its IF has landed
             prepare_desc_i(tk, nx, o.pdi, o.phaseC, 3, lane, &s_d[cur ^ 1], s_taps, nullptr, s_post, true);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1748,7 +2012,9 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         b.stamps[21 + 3 * ch] = wall_clock64();
         b.stamps[22 + 3 * ch] = (unsigned long long)nsteps;
     }
+    const bool had = pend;
     if (pend) flush();
+    if (had) defer_final(nsteps - 1);
     if (io && tid == 64) desc_rem(tk, &s_d[cur]);  // (complete for a step-kernel follow-up)
     __syncthreads();
     if (io) {  // the state and the next step's descriptor for the next launch

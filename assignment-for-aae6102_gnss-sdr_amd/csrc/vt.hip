@@ -247,20 +247,34 @@ __global__ __launch_bounds__(kVtStepThreads) void vt_step_kernel(VtRunArgs a)
     __syncthreads();
     if (!s_last) return;
     // the channel's last block: every partial has landed (each was drained before its
-    // ticket); lane k loads partial k past the L2, lane 0 adds them in block order
-    for (int k = tid; k < nb; k += kVtStepThreads) {
-        const double* pp = a.part + ((int64_t)ch * nb + k) * 2;
-        s_r0[k] = __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_r1[k] = __hip_atomic_load(pp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    // ticket); lane k loads partial k past the L2 in chunks of kVtStepThreads (the LDS arrays'
+    // size, so any nb works), lane 0 adds each chunk in block order: the sum is the same
+    // sequential block-order sum for every nb
     __shared__ gnss_vt_out s_o;
+    __shared__ double s_I, s_Q;
+    if (tid == 0) s_I = s_Q = 0.0;
+    for (int k0 = 0; k0 < nb; k0 += kVtStepThreads) {
+        const int m = nb - k0 < kVtStepThreads ? nb - k0 : kVtStepThreads;
+        __syncthreads();  // (the previous chunk's adds are done before its slots are reused)
+        if (tid < m) {
+            const double* pp = a.part + ((int64_t)ch * nb + k0 + tid) * 2;
+            s_r0[tid] = __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_r1[tid] = __hip_atomic_load(pp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            double I = s_I, Q = s_Q;
+            for (int k = 0; k < m; k++) {
+                I += s_r0[k];
+                Q += s_r1[k];
+            }
+            s_I = I;
+            s_Q = Q;
+        }
+    }
     __syncthreads();
     if (tid == 0) {
-        double I = 0.0, Q = 0.0;
-        for (int k = 0; k < nb; k++) {
-            I += s_r0[k];
-            Q += s_r1[k];
-        }
+        const double I = s_I, Q = s_Q;
         __hip_atomic_store(a.ticket + ch, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_o = gnss_vt_out{};
         if (s_bad) {
@@ -305,7 +319,7 @@ hipError_t launch_vt_run(const VtRunArgs& a, hipStream_t s)
 
 hipError_t launch_vt_step(const VtRunArgs& a, hipStream_t s)
 {
-    if (a.nsteps != 1 || a.prec != 1 || a.nb < 1 || !a.part || !a.ticket || a.n > GNSS_VT_MAX_CH)
+    if (a.nsteps != 1 || a.prec != 1 || a.nb < 1 || a.nb > GNSS_VT_MAX_BLOCKS || !a.part || !a.ticket || a.n > GNSS_VT_MAX_CH)
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(vt_step_kernel, dim3(a.nb, a.n), dim3(kVtStepThreads), 0, s, a);
     return hipGetLastError();

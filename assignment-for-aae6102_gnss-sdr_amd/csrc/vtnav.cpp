@@ -577,8 +577,10 @@ int gnss_vt_nav_update(gnss_vt_nav* v, const double* codeError, const double* co
     double xn[8];
     matmul(T, v->total_state, xn, 8, 8, 1);
     for (int k = 0; k < 8; k++) v->total_state[k] = xn[k];
-    // measurement noise from the innovations of the last 200 / pdi steps (:445-467)
-    if (v->counterUptR == 200 / v->pdi) {
+    // measurement noise from the innovations of the last 200 / pdi steps (:445-467); MATLAB
+    // compares the integer counter with the real thresUptR = 200/track.pdi (:63), so a pdi that
+    // does not divide 200 never updates R
+    if (200 % v->pdi == 0 && v->counterUptR == 200 / v->pdi) {
         const double w = 1.0 / v->counterUptR;
         for (int i = 0; i < n; i++) {
             double rc = w * v->recordR2[i] * 10, rr = w * v->recordR2[n + i] * 1;

@@ -57,16 +57,33 @@ def initParameters(fileRoute: str | None = None):
 # device context
 # ---------------------------------------------------------------------------
 class Context:
-    """One gnss_ctx on one HIP device (stream, rocFFT plans, device buffers)."""
+    """One gnss_ctx on one HIP device (stream, rocFFT plans, device buffers), or with
+    `devices` a multi-device context (gnss_ctx_create_multi): acquisition and trackingCT deal
+    their PRNs / channels round-robin over one member context per entry (a device may repeat)
+    and merge the rows, bit-identical to one context; device-resident records and outputs
+    belong to devices[0]."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, devices=None):
         self.lib = abi.load()
         h = C.c_void_p()
-        st = self.lib.gnss_ctx_create(int(device), C.byref(h))
-        if st != abi.OK:
-            raise abi.GnssError(st, f"gnss_ctx_create(device={device}) failed")
+        if devices is not None:
+            devs = [int(d) for d in devices]
+            arr = (C.c_int * len(devs))(*devs)
+            st = self.lib.gnss_ctx_create_multi(arr, len(devs), C.byref(h))
+            if st != abi.OK:
+                raise abi.GnssError(st, f"gnss_ctx_create_multi(devices={devs}) failed")
+            device = devs[0]
+        else:
+            st = self.lib.gnss_ctx_create(int(device), C.byref(h))
+            if st != abi.OK:
+                raise abi.GnssError(st, f"gnss_ctx_create(device={device}) failed")
         self.h = h
         self.device = device
+        self.devices = list(devices) if devices is not None else [device]
+
+    @property
+    def members(self) -> int:
+        return int(self.lib.gnss_ctx_members(self.h))
 
     def close(self):
         if getattr(self, "h", None):

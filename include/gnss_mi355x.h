@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define GNSS_ABI_VERSION 10
+#define GNSS_ABI_VERSION 11
 
 /* ---- status codes (SURVEY §8b "Error conventions") --------------------- */
 #define GNSS_OK         0
@@ -209,6 +209,24 @@ const char *gnss_strerror(int status);
 /* Create a context bound to HIP device `device` (owns stream, device buffers,
  * rocFFT plans). Replaces the MEX's persistent state (freed by mexAtExit). */
 int  gnss_ctx_create(int device, gnss_ctx **out);
+/* Multi-device context (ABI v11): one member context per entry of devices[0..n-1] (a device
+ * may repeat; its members then run one after the other), so a MEX caller of SDR_main.m:22,38
+ * shards over the GPUs of a node with no MATLAB change. gnss_acquisition deals the PRN list
+ * (acquisition.m:47-80) and gnss_tracking_ct / _pos / _mc the channel list (trackingCT.m:22-528)
+ * round-robin over the members, one host thread per device; each member keeps the global
+ * svindex / nsv (quirk A.11), so every row is bit-identical to the one-context call. Results
+ * are merged into the caller's arrays in the reference's order (Acquired and diag in PRN-list
+ * order; tracking rows by channel). GNSS_OUT_DEVICE arrays live on devices[0]; a member on
+ * another device expands its rows in its own HBM and copies them over xGMI (peer copies), and
+ * a gnss_file.dev_data record on another device is copied range by range into each member's
+ * HBM the same way. The status is the one-context call's (group.h). Every other entry point
+ * runs on devices[0] alone. The setters apply to every member. n in 1..GNSS_MAX_DEVICES. */
+#define GNSS_MAX_DEVICES 16
+int  gnss_ctx_create_multi(const int *devices, int n, gnss_ctx **out);
+/* HIP devices visible to this process (0 without a GPU or runtime). */
+int  gnss_device_count(void);
+/* Members of a context (1 for gnss_ctx_create). */
+int  gnss_ctx_members(const gnss_ctx *ctx);
 void gnss_ctx_destroy(gnss_ctx *ctx);
 const char *gnss_last_error(const gnss_ctx *ctx);
 int  gnss_last_timing(const gnss_ctx *ctx, gnss_timing *out);
@@ -246,8 +264,13 @@ int  gnss_ctx_set_window(gnss_ctx *ctx, uint64_t bytes);
                                     order on one stream, 2 = pipelined over two streams
                                     (batch b's rows beside batch b+1's columns, two
                                     intermediates); 0 = the engine's choice               */
-#define GNSS_OPT_VT_BLOCKS    9  /* > 0: blocks per channel of gnss_tracking_vt's step      */
-#define GNSS_OPT_COUNT        10
+#define GNSS_OPT_VT_BLOCKS    9  /* 1..GNSS_VT_MAX_BLOCKS: blocks per channel of
+                                    gnss_tracking_vt's step (GNSS_EARG above)             */
+#define GNSS_OPT_FORCE_PEER   10 /* != 0 (multi-device contexts): every member treats
+                                    dev_data and GNSS_OUT_DEVICE arrays as on another
+                                    device (range copies in, row copies out), so one GPU
+                                    exercises the peer-copy path                          */
+#define GNSS_OPT_COUNT        11
 int  gnss_ctx_set_option(gnss_ctx *ctx, int key, int64_t value);
 
 /* Device memory owned by the ctx, for callers that keep an IF record resident
@@ -453,6 +476,7 @@ int gnss_vt_prepare(const gnss_signal *signal, int32_t pdi, const gnss_vt_chan *
  * BLAS-backed matrix products and inv() round differently in the last place, so the values
  * match the reference within the ulp bounds stated in tests/test_vt_nav_kat.py. */
 #define GNSS_VT_MAX_CH 32
+#define GNSS_VT_MAX_BLOCKS 1024  /* blocks per channel of one VT step (GNSS_OPT_VT_BLOCKS)  */
 
 /* ephemeris(prn).*(eph_idx) -- the fields svPosVel.m:23-44 reads (eph_idx = 1, :36). */
 typedef struct gnss_eph_sv {

@@ -1787,7 +1787,7 @@ int or_vtnav_init(or_vtnav *v, int n, int pdi, const int *prn, const double *eph
         v->mesurement_noise[i][i] = 3e-1;
         v->mesurement_noise[n + i][n + i] = 1e-1;
     }
-    v->thresUptR = 200 / pdi;                                      /* :63 */
+    v->thresUptR = 200 % pdi == 0 ? 200 / pdi : -1; /* :63 (real 200/pdi: never met otherwise) */
     for (int k = 0; k < 3; k++) {
         v->estPos[k] = usrPos[k];
         v->estVel[k] = usrVel[k];
@@ -1917,7 +1917,8 @@ int or_vtnav_update(or_vtnav *v, const double *codeError, const double *codeFreq
     if (!or_inv(S, N, Si)) return GNSS_EINDEX;
     or_mm(PHt, Si, K, 8, N, N);
     v->counterUptR = v->counterUptR + 1;
-    for (int k = 0; k < N; k++) v->recordR[v->counterUptR - 1][k] = Z[k] - 0.0; /* newZ' - H*0 (:395) */
+    if (v->counterUptR <= 200) /* (rows past 200 are never read: thresUptR <= 200) */
+        for (int k = 0; k < N; k++) v->recordR[v->counterUptR - 1][k] = Z[k] - 0.0; /* newZ' - H*0 (:395) */
     double inno[2 * OR_VT_MAXCH];
     for (int k = 0; k < N; k++) inno[k] = Z[k];
     double Kz[8];

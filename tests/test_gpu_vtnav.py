@@ -191,11 +191,12 @@ def test_vector_tracking_formats(pkg, po, ctx, opensky_short, prec, dtyp):
     print(prec, dtyp, "worst sum / |P|", _compare(pkg, po, z, tck, nsol, rec, onav))
 
 
-@pytest.mark.parametrize("nb", [1, 7, 64])
+@pytest.mark.parametrize("nb", [1, 7, 64, 300, 1024])
 def test_vector_tracking_step_blocks(pkg, po, ctx, opensky_short, opts, nb):
     """The multi-block step (vt_step_kernel) at other block counts per channel
     (GNSS_OPT_VT_BLOCKS; the engine's is 29): another fixed association of the same per-sample
-    terms, the same loop against the oracle."""
+    terms, the same loop against the oracle. nb > 256 (more partials than the
+    last block's LDS arrays hold) is summed in chunks, in the same block order."""
     skip, cfg, data = opensky_short
     file, signal, acq, track = params(pkg, skip, data)
     _, _, _, _, solu, cmn = pkg.initParameters()
@@ -208,6 +209,16 @@ def test_vector_tracking_step_blocks(pkg, po, ctx, opensky_short, opts, nb):
     status, rec, onav = _oracle_loop(pkg, po, z, ct, data, nsteps)
     assert status == 0
     print(nb, "worst sum / |P|", _compare(pkg, po, z, tck, nsol, rec, onav))
+
+
+def test_vector_tracking_block_option_bound(pkg, ctx):
+    """GNSS_OPT_VT_BLOCKS takes 0 (the engine's choice) .. GNSS_VT_MAX_BLOCKS and refuses
+    anything else with GNSS_EARG."""
+    abi = pkg.abi
+    for bad in (-1, 1025, 1 << 20):
+        assert ctx.lib.gnss_ctx_set_option(ctx.h, abi.OPT_VT_BLOCKS, bad) == abi.EARG
+    assert ctx.lib.gnss_ctx_set_option(ctx.h, abi.OPT_VT_BLOCKS, 1024) == 0
+    assert ctx.lib.gnss_ctx_set_option(ctx.h, abi.OPT_VT_BLOCKS, 0) == 0
 
 
 def test_vector_tracking_channel_bound(pkg, ctx):

@@ -44,3 +44,17 @@ def test_div_const_equals_ieee_division(tmp_path):
     r = subprocess.run([str(exe), "2000000"], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches 0" in r.stdout
+
+
+def test_multi_device_bookkeeping(tmp_path):
+    """gnss_ctx_create_multi's dealing and merging (csrc/group.h): the PRN / channel deal, the
+    Acquired / diag rows merged back into PRN-list order, and a sharded call's status equal the
+    one-context results (acquisition.m:47-80,84-85; trackingCT.m:22-528 and the channel loop's
+    status rule in gnss_api.cpp). Host C++ only."""
+    cxx = shutil.which("g++") or HIPCC
+    src = os.path.join(ROOT, "tests", "native", "group_test.cpp")
+    exe = tmp_path / "group_test"
+    subprocess.run([cxx, "-O2", "-std=c++17", "-o", str(exe), src], check=True, capture_output=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches 0" in r.stdout
