@@ -1449,8 +1449,17 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
     // resident (config 5: 32 channels x 11 taps), each block correlates vpb of the step's
     // blocks in turn -- the lane geometry and so the bits stay those of bpc blocks.
     // GNSS_OPT_FORCE_VPB (test hook) asks for at least that many.
+    // above 3 taps the persistent loop's lanes keep at most kQcapMax interior tap boundaries
+    // (lane_correlate's capture queue): checked here for code rates up to cps_max, and a step
+    // beyond that rate stops the channel with GNSS_EINDEX in the kernel (as d*M >= 1 does)
+    P.qcap_dmax = cps_max;
+    auto qcap_ok = [&](int sub) {
+        return !GNSS_QCAP || P.ntaps <= 3 ||
+               max_taps_in_lane(P.taps, P.tap_post, P.ntaps, 8 * sub, cps_max) <= kQcapMax;
+    };
     auto vpb_for = [&](int pdi, int sub) {
-        if (ctx->opt[GNSS_OPT_NO_PERSIST] || P.fmt != 0 || bpc_for(pdi, sub) > run_bpc_cap(P.ntaps)) return 0;
+        if (ctx->opt[GNSS_OPT_NO_PERSIST] || P.fmt != 0 || bpc_for(pdi, sub) > run_bpc_cap(P.ntaps) || !qcap_ok(sub))
+            return 0;
         const int bpc = bpc_for(pdi, sub);
         int v0 = 1;
         if (ctx->opt[GNSS_OPT_FORCE_VPB] > 0) v0 = (int)std::min<int64_t>(ctx->opt[GNSS_OPT_FORCE_VPB], kMaxVpb);

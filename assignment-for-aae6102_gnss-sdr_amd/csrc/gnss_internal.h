@@ -206,6 +206,10 @@ struct TrkParams {
     const long long* pref_q;  //   (8-sample groups from buf_base), Q likewise
     const short* stage16;     // fmt 1: the staged int16 I/Q (absolute: stage16[2k] = I of k)
     double taps[GNSS_MAX_TAPS];
+    // the persistent loop above 3 taps (lane_correlate's capture queue, at most kQcapMax
+    // interior boundaries per lane): the host checked that bound for code rates up to this many
+    // chips per sample; a step beyond it stops the channel with GNSS_EINDEX, as d*M >= 1 does
+    double qcap_dmax;
     // Loop conventions: 0 = trackingCT.m; 1 = trackingCT_POS_updated.m:179-408 (numSample
     // by ceil, prompt replica Code(ceil(t + 0.05) + 1), codeFreq = f0 + codeNco, loop T =
     // signal.ms for every pdi, Index + 1 per step, no phase-C negation or re-seek,
@@ -325,6 +329,34 @@ constexpr int kMaxBpcRun = 256;  // blocks per channel of the persistent kernel
 // blocks per CU; 192 blocks of 24-sample lanes = 1.18 M samples per step)
 constexpr int run_bpc_cap(int ntaps) { return ntaps > 3 ? 192 : kMaxBpcRun; }
 constexpr int kMaxVpb = 16;      // virtual blocks per resident block of the persistent kernel
+// lane_correlate's capture queue (A/B knob): 0 = every tap's prefix read after every 8-sample
+// subgroup (the default: the queue measured 8-16 % slower at 11 taps and 8 % at 3,
+// profiles/r05_ab_cfg5_variants.txt); 1 = the queue above 3 taps; 2 = at 3 taps too
+#ifndef GNSS_QCAP
+#define GNSS_QCAP 0
+#endif
+constexpr int kQcapMax = 8;      // capture-queue entries per lane (lane_correlate, the LDS slots)
+
+// The most taps whose replica boundary can fall inside one lane of M samples when the code
+// advances at most dmax chips per sample: tap s's boundaries sit where frac(t + off_s) wraps,
+// so a lane spanning (M - 1) dmax chips holds a boundary of every tap whose fractional offset
+// lies in a window of that width (taps whose offsets differ by whole chips count once each).
+inline int max_taps_in_lane(const double* taps, const double* post, int n, int M, double dmax)
+{
+    const double w = (M - 1) * dmax + 1e-9;
+    int best = 0;
+    for (int a = 0; a < n; a++) {
+        const double x = taps[a] + (post ? post[a] : 0.0);
+        int c = 0;
+        for (int b = 0; b < n; b++) {
+            double f = (taps[b] + (post ? post[b] : 0.0)) - x;
+            f -= floor(f);
+            if (f < w || f > 1.0 - 1e-9) c++;
+        }
+        best = c > best ? c : best;
+    }
+    return best;
+}
 // The persistent kernel's 16-B hand-off granules per channel. 3 taps: [2 (step parity)]
 // [kMaxBpcRun][6]. Above 3 taps only the loop's E/P/L go through the step's exchange
 // ([2][kMaxBpcRun][<= 6], region A); the other taps' partials (region B) are published after

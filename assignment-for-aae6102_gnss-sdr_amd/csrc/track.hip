@@ -105,7 +105,7 @@ __device__ __forceinline__ unsigned long long load_agent(const unsigned long lon
 // runs in the persistent loop).
 struct TailK {
     double Fs, inv_Fs, codelength, S, codeFreqBasis, ms;
-    double dll_r, dll_t1, dll_t10, pll_r, pll_t1, pll_t10, tau1code, tau1carr;
+    double dll_r, dll_t1, dll_t10, pll_r, pll_t1, pll_t10, tau1code, tau1carr, qcap_dmax;
     int32_t exact_div, conv, given, chip_off, ntaps, iE, iP, iL, bps;
     int64_t file_len, buf_base, buf_len;
     const double* taps;
@@ -129,7 +129,7 @@ __device__ __forceinline__ TailK tail_k(const TrkParams& p)
     k.codeFreqBasis = p.codeFreqBasis; k.ms = p.ms;
     k.dll_r = p.dll_r; k.dll_t1 = p.dll_t1; k.dll_t10 = p.dll_t10;
     k.pll_r = p.pll_r; k.pll_t1 = p.pll_t1; k.pll_t10 = p.pll_t10;
-    k.tau1code = p.tau1code; k.tau1carr = p.tau1carr;
+    k.tau1code = p.tau1code; k.tau1carr = p.tau1carr; k.qcap_dmax = p.qcap_dmax;
     k.exact_div = p.exact_div; k.conv = p.conv; k.given = p.given; k.chip_off = p.chip_off;
     k.ntaps = p.ntaps; k.iE = p.iE; k.iP = p.iP; k.iL = p.iL; k.bps = p.bps;
     k.file_len = p.file_len; k.buf_base = p.buf_base; k.buf_len = p.buf_len;
@@ -138,7 +138,7 @@ __device__ __forceinline__ TailK tail_k(const TrkParams& p)
     launder_s(k.codeFreqBasis); launder_s(k.ms);
     launder_s(k.dll_r); launder_s(k.dll_t1); launder_s(k.dll_t10);
     launder_s(k.pll_r); launder_s(k.pll_t1); launder_s(k.pll_t10);
-    launder_s(k.tau1code); launder_s(k.tau1carr);
+    launder_s(k.tau1code); launder_s(k.tau1carr); launder_s(k.qcap_dmax);
     launder_s(k.exact_div); launder_s(k.conv); launder_s(k.given); launder_s(k.chip_off);
     launder_s(k.ntaps); launder_s(k.iE); launder_s(k.iP); launder_s(k.iL); launder_s(k.bps);
     launder_s(k.file_len); launder_s(k.buf_base); launder_s(k.buf_len);
@@ -784,6 +784,7 @@ struct LdsRaw {
 #define GNSS_FLUSH_PROBE 0  // (A/B probe: 1 = block 0 writes no record)
 #endif
 
+// (GNSS_QCAP: gnss_internal.h)
 template <int NT, int SUB, bool DIVIDE, bool RELOAD, int FMT, class Desc, class Raw>
 __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* dp, const Raw& raw,
                                                int64_t ks, unsigned cabits, double2* myslot,
@@ -791,6 +792,14 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
 {
     constexpr int M = 8 * SUB;
     constexpr int T = kTrkThreads;
+    // Capture queue (the persistent loop above 3 taps, where the host has checked that a lane
+    // holds at most kQcapMax distinct interior boundaries, TrkParams.qcap): a tap's prefix is
+    // the lane's running sum at its last sample before the boundary, cap. Instead of reading
+    // every tap's slot after every 8-sample subgroup (NT x SUB LDS reads and 2 NT x SUB adds),
+    // the running sum is stored at the distinct interior capture samples only (queue entry =
+    // the sample's rank among them), and each tap reads its one entry in the epilogue. The
+    // value is the same running sum, so the same bits (pre = v + 0.0 either way).
+    constexpr bool QC = RELOAD && (GNSS_QCAP == 2 || (GNSS_QCAP && NT > 3));
     if constexpr ((GNSS_CORR_PROBE & 8) != 0) {  // (probe: no correlate at all)
 #pragma unroll
         for (int s = 0; s < NT; s++) { oI[s] = 0.0; oQ[s] = 0.0; }
@@ -820,6 +829,11 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
             neg0 |= (cabits & 1u) << s;
             continue;
         }
+        if constexpr ((GNSS_CORR_PROBE & 64) != 0) {  // (probe: no search; a runtime cap, the captures as usual)
+            cap[s] = (int)((ks + 5 * s) & 31) - 4;
+            neg0 |= (cabits & 1u) << s;
+            continue;
+        }
         const Colon col{uni(dp->tap_a[s]), d, uni(dp->tap_c[s]), n - 1};
         // the replica index is ceil(t + post): post = 0, or the prompt's +0.05 of
         // trackingCT_POS_updated.m:216 (t + 0.0 is t exactly)
@@ -837,6 +851,7 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
                 pb = ceil(colon_elem(col, kx) + post) > c0 ? ms : ms + 1;
         }
         cap[s] = (pb < M ? pb : M) - 1;  // Prefix(p) = running sum through sample p-1
+        if constexpr ((GNSS_CORR_PROBE & 32) != 0) cap[s] = M - 1 - s;  // (probe: the search runs, its cap is ignored)
         const unsigned i0 = ca_index32((int)c0 + p.chip_off);
         const unsigned i1 = i0 == 1022u ? 0u : i0 + 1u;
         const unsigned w0 = __shfl(cabits, (int)(i0 >> 5), 64);
@@ -857,9 +872,17 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
     }
 
     double run_r = 0.0, run_i = 0.0;
-    double pre_r[NT], pre_i[NT];
+    double pre_r[QC ? 1 : NT], pre_i[QC ? 1 : NT];
+    if constexpr (!QC) {
 #pragma unroll
-    for (int s = 0; s < NT; s++) { pre_r[s] = 0.0; pre_i[s] = 0.0; }
+        for (int s = 0; s < NT; s++) { pre_r[s] = 0.0; pre_i[s] = 0.0; }
+    }
+    unsigned cmask = 0u;  // QC: the lane's interior capture samples (0 <= cap < M - 1)
+    if constexpr (QC) {
+#pragma unroll
+        for (int s = 0; s < NT; s++)
+            if (cap[s] >= 0 && cap[s] < M - 1) cmask |= 1u << cap[s];
+    }
 
     // fmt 1: I - mean(I), Q - mean(Q) per sample, as the reference forms rawsignal0DC
     double mu_r = 0.0, mu_i = 0.0;
@@ -931,18 +954,27 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
                 run_r += xr;
                 run_i += xi;
             }
-            myslot[mm * T] = make_double2(run_r, run_i);
-
+            if constexpr (QC) {
+                if ((cmask >> m) & 1u)
+                    myslot[__builtin_popcount(cmask & ((1u << m) - 1u)) * T] = make_double2(run_r, run_i);
+            } else {
+                myslot[mm * T] = make_double2(run_r, run_i);
+            }
         }
+        if constexpr (!QC) {
 #pragma unroll
-        for (int s = 0; s < NT; s++) {
-            const unsigned idx = (unsigned)(cap[s] - 8 * j);
-            const double2 v = *(idx < 8u ? myslot + idx * T : zero);
-            pre_r[s] += v.x;
-            pre_i[s] += v.y;
+            for (int s = 0; s < NT; s++) {
+                const unsigned idx = (unsigned)(cap[s] - 8 * j);
+                const double2 v = *(idx < 8u ? myslot + idx * T : zero);
+                pre_r[s] += v.x;
+                pre_i[s] += v.y;
+            }
         }
     };
-    if constexpr (RELOAD && NT > 3) {
+#ifndef GNSS_UNROLL_TAPS
+#define GNSS_UNROLL_TAPS 0  // (A/B: 1 = the > 3-tap subgroup loop unrolled like the 3-tap one)
+#endif
+    if constexpr (RELOAD && NT > 3 && !GNSS_UNROLL_TAPS) {
         // descriptor in LDS: one subgroup at a time (unrolled, the compiler would keep
         // every subgroup's table values live)
 #pragma unroll 1
@@ -962,8 +994,19 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
         const double a0 = ((neg0 >> s) & 1u) ? -1.0 : 1.0;
         const double v1 = ((neg1 >> s) & 1u) ? -1.0 : 1.0;
         const double dv = a0 - v1;
-        const double ur = __builtin_fma(dv, pre_r[s], v1 * run_r);
-        const double ui = __builtin_fma(dv, pre_i[s], v1 * run_i);
+        double pr, pi;
+        if constexpr (QC) {
+            const int cs = cap[s];
+            const int q = __builtin_popcount(cmask & ((1u << (cs > 0 ? cs : 0)) - 1u));
+            const double2 v = myslot[(q < 8 ? q : 7) * T];  // (read even where unused: no divergence)
+            pr = (cs < 0 ? 0.0 : cs == M - 1 ? run_r : v.x) + 0.0;
+            pi = (cs < 0 ? 0.0 : cs == M - 1 ? run_i : v.y) + 0.0;
+        } else {
+            pr = pre_r[s];
+            pi = pre_i[s];
+        }
+        const double ur = __builtin_fma(dv, pr, v1 * run_r);
+        const double ui = __builtin_fma(dv, pi, v1 * run_i);
         oI[s] = __builtin_fma(cb, ui, sb * ur);
         oQ[s] = __builtin_fma(cb, ur, -(sb * ui));
     }
@@ -1537,6 +1580,9 @@ __device__ __forceinline__ void prefetch_raw(const int8_t* iq, int64_t g0, int64
 // (the same fp64 code on the same sums: bit-identical copies), so a step needs one
 // exchange only: each block publishes its partial sums and reads everyone's. Block 0
 // of the channel writes the records, C/N0 and, at the end, the state.
+#ifndef GNSS_DEFER
+#define GNSS_DEFER 0  // (A/B: 0 = every tap through the step's exchange, the round-4 form)
+#endif
 #ifndef GNSS_WPE_TAPS
 #define GNSS_WPE_TAPS 2  // (A/B: waves per EU of the > 3-tap persistent forms; 3 = three blocks per CU)
 #endif
@@ -1572,7 +1618,17 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
     constexpr int kSlot = 8 * T * 2;                  // running sums [8][T] double2
     constexpr int kRed = red_words<NT>();             // block reduction
     constexpr int kPart = run_bpc_cap(NT) * NV;       // everyone's partials (as words)
-    constexpr int kMem0 = kSlot > kRed ? kSlot : kRed;
+    // Above 3 taps only E / P / L cross the step's exchange (kDefer, below); GNSS_DEFER 2 (one
+    // block of the step per resident block) has one wave reduce the other taps' block partials
+    // while the rest poll: their lane values staged at s_mem + kPwD, [value][T], and that wave's
+    // run sums after them. The exchange's words then need bpc * (E/P/L values + owned values).
+    constexpr bool kDefer = GNSS_DEFER && NT > 3;
+    constexpr bool kWave1 = GNSS_DEFER == 2 && kDefer && !VB;
+    constexpr int kPwD = run_bpc_cap(NT) * 8 + 2 * NT;  // (pbpc = bpc: own_n <= nBv / bpc + 1)
+    constexpr int kStage = 2 * (NT - 1) * T;
+    constexpr int kMemW = kWave1 ? kPwD + kStage + 2 * NT * 32 : 0;
+    constexpr int kMem1 = kSlot > kRed ? kSlot : kRed;
+    constexpr int kMem0 = kMem1 > kMemW ? kMem1 : kMemW;
     constexpr int kMem = kMem0 > kPart + 16 * NV ? kMem0 : kPart + 16 * NV;
     __shared__ __attribute__((aligned(16))) double s_mem[kMem];
     __shared__ __attribute__((aligned(16))) int4 s_raw[SUB * T];   // this step's IF
@@ -1601,11 +1657,10 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
     // they are reduced, published and swept first (region A); the other taps' values (B,
     // only when the caller asked for the taps) are reduced after that publication, overlapping
     // the exchange, and the previous step's are swept beside this step's E/P/L by the blocks
-    // that own them (a run of B values per block, blocks 3, 4, ...), whose idle tail wave
+    // that own them (a run of B values per block, blocks 4, 5, ...), whose idle tail wave
     // sums them and writes the taps one step late. Every value keeps its reduction lanes and
     // order (block_pass, channel_sum_l with the whole tap set's lane count), so the records
     // and taps are the bits of the one-exchange form and of the per-step kernel.
-    constexpr bool kDefer = NT > 3;
     constexpr int CL = chan_lanes<NV>();
     constexpr int HT = red_taps<NT>();
     // The configuration lives in LDS and is read where it is used (volatile LDS loads, never
@@ -1639,7 +1694,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
             if (dob && nBv > 0) {  // this block's run of B values
                 const int c = (nBv + pbpc - 1) / pbpc;
                 const int nown = (nBv + c - 1) / c;
-                const int r = ((pblk - 3) % pbpc + pbpc) % pbpc;
+                const int r = ((pblk - 4) % pbpc + pbpc) % pbpc;
                 if (r < nown) {
                     own_lo = r * c;
                     own_n = nBv - own_lo < c ? nBv - own_lo : c;
@@ -1687,25 +1742,28 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         s_post[tid] = p.tap_post[tid];
     }
     __syncthreads();
-    // block 0, wave 1, lane 0: dvpre[s_c.nstep], the running delayValue prefix its flushes
-    // extend (no read-back of its own stores)
+    // The record's parts, the taps and the C/N0 value go to different blocks (one when the channel
+    // has one), so that no block's flush outlasts the exchange it overlaps: one block doing all of
+    // it measured ~1.7 us, and that block then started every step last
+    // (profiles/r04_block0_lateness.txt). Part 1 (the sums and the codedelay bookkeeping) is not
+    // on block 0 either (round 5): block 0 then polls with all four waves like
+    // the others, and in the 1-ms phase it was still the last to finish its correlate.
+    const int duty_a = pbpc > 3 ? 3 : 0, duty_b = pbpc > 1 ? 1 : 0, duty_c = pbpc > 2 ? 2 : duty_b;
+    const bool dio = pblk == duty_a;  // the block holding the record's part 1
+    // (that block's wave 1, lane 0: dvpre[s_c.nstep], the running delayValue prefix its flushes
+    // extend -- no read-back of its own stores)
     int64_t dvrun = 0;
-    if (io && wv == 1 && lane == 0) dvrun = ((const g_i64*)(b.dvpre + (int64_t)ch * (p.rec_cap + 1)))[s_c.nstep];
+    if (dio && wv == 1 && lane == 0) dvrun = ((const g_i64*)(b.dvpre + (int64_t)ch * (p.rec_cap + 1)))[s_c.nstep];
     if (!s_d[0].bad && !s_d[0].bad_tap)
         prefetch_raw<SUB>(iq, s_d[0].g_first + ((int64_t)blk * T + tid) * SUB, gmax, s_raw, tid);
 
     int cur = 0;   // s_d[cur]: this step
     bool pend = false;  // a finished step's state / record still to write (s_o, s_u, s_fin)
-    int64_t pre[2] = {0, 0};  // block 0: its record's delayValue prefix reads, issued early
+    int64_t pre[2] = {0, 0};  // the part-1 block: its record's delayValue prefix reads, issued early
     bool pre_ok = false;      //   (for the pending step)
     // The pending step's side effects, by wave 1 while the next step's partials are in
-    // flight (off the critical path): the state replica (every block, in place) and, in
-    // block 0, the record, C/N0 and taps.
-    // The record's halves, the taps and the C/N0 value go to three different blocks (one when
-    // the channel has one), so that no block's flush outlasts the exchange it overlaps: one
-    // block doing all of it measured ~1.7 us, and that block then started every step last
-    // (profiles/r04_block0_lateness.txt).
-    const int duty_b = pbpc > 1 ? 1 : 0, duty_c = pbpc > 2 ? 2 : duty_b;
+    // flight (off the critical path): the state replica (every block, in place) and, in the
+    // duty blocks above, the record, C/N0 and taps.
     int s_now = 0;  // (probe stamps of the flush)
     // the owned B values of a finished step, swept into pb: summed (8 lanes per value, the
     // order of channel_sum<NV>) and written to the taps, by one wave
@@ -1738,6 +1796,34 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
             return;
         if (wv == 1) defer_write(pb);
     };
+    // GNSS_DEFER 2: one wave's reduction of the staged other-tap lane values of step `step`,
+    // exactly block_partial's order per value (8-lane runs in order, four runs per lane, the
+    // DPP quad butterfly), published to region B
+    auto defer_reduce = [&](int step) {
+        const double* stg = s_mem + kPwD;
+        double* r2 = s_mem + kPwD + kStage;  // [value][32] run sums
+        const int nbv = dfi(s_df.nBv);
+        for (int e = lane; e < nbv * 32; e += 64) {
+            const double* r = stg + (e >> 5) * T + (e & 31) * 8;
+            double x = r[0];
+#pragma unroll
+            for (int k = 1; k < 8; k++) x += r[k];
+            r2[e] = x;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the run sums are in LDS (this wave's)
+        double a = 0.0;
+        if (lane < nbv * 4) {
+            const double* r = r2 + (lane >> 2) * 32 + (lane & 3) * 8;
+            a = r[0];
+#pragma unroll
+            for (int k = 1; k < 8; k++) a += r[k];
+            a += dpp_f64<0xB1>(a);  // quad_perm [1,0,3,2]
+            a += dpp_f64<0x4E>(a);  // quad_perm [2,3,0,1]
+            if ((lane & 3) == 0)
+                publish16(pg, gran_region_b(NT) + (step & 3) * gran_slot_b(NT) + (lane >> 2) * bpc + blk, a,
+                          tag0 + step + 1);
+        }
+    };
     auto flush = [&]() {
         if (wv == 1) {
             // (probe GNSS_FLUSH_PROBE & 2: block 0's record part twice, stamped at [2000..2002]
@@ -1746,7 +1832,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
                                          ? b.stamps + (size_t)(s_now % kStampSlots) * kStampRow : nullptr;
             if (fr) fr[2000] = wall_clock64();
             if (lane == 0 && !(GNSS_FLUSH_PROBE & 1)) {
-                if (io) {
+                if (dio) {
                     if (!pre_ok) {  // (a launch's last flush: the column's prefix read here)
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         const g_i64* dvp = (const g_i64*)(b.dvpre + (int64_t)ch * (p.rec_cap + 1));
@@ -1754,7 +1840,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
                         pre[1] = cols < s_c.nstep + 1 ? dvp[cols] : 0;
                     }
                     pre[0] = dvrun;
-                    write_record_i(p, b, ch, s_c, s_o, s_u, s_fin, pre, duty_b == 0 ? 3 : 1);
+                    write_record_i(p, b, ch, s_c, s_o, s_u, s_fin, pre, duty_b == duty_a ? 3 : 1);
                     dvrun += s_o.delayValue;  // = dvpre[nstep + 1], the value just stored
                 }
                 else if (pblk == duty_b) write_record_i(p, b, ch, s_c, s_o, s_u, s_fin, nullptr, 2);
@@ -1785,7 +1871,9 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         const StepDesc& D = s_d[cur];
         const int bad = D.bad ? D.bad : D.bad_tap;
         const bool stop = !D.phaseC && D.Index + 1 > n1_target;  // 1-ms run of this channel done
-        if (bad || stop || D.d * M >= 1.0) {  // (a code rate beyond Fs/M breaks the one-boundary lane)
+        // (a code rate beyond Fs/M breaks the one-boundary lane; above 3 taps one beyond the
+        // capture queue's checked rate would overflow the queue)
+        if (bad || stop || D.d * M >= 1.0 || (GNSS_QCAP && NT > kQcapMax && D.d > tk.qcap_dmax)) {
             const bool had = pend;
             if (pend) flush();
             if (had) defer_final(s - 1);
@@ -1833,7 +1921,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
                 lane_correlate<NT, SUB, DIVIDE, true, 0>(p, &D, LdsRaw{s_raw + tid}, 8 * g0 - A, cabits,
                                                       reinterpret_cast<double2*>(s_mem) + tid, &s_zero, oI, oQ);
                 __syncthreads();  // slots and s_raw free
-                if (pend && io && wv == 1 && lane == 0 && jv == 0) {
+                if (pend && dio && wv == 1 && lane == 0 && jv == 0) {
                     // the pending record's older delayValue prefix (quirk A.11's column), loaded
                     // here and not at the step's start: an outstanding load there held this
                     // wave at the correlate's vmcnt(0) wait (its IF landed long before)
@@ -1862,7 +1950,20 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
                     const int NA = NA_();
                     if (tid < NA * 4 && (tid & 3) == 0)
                         publish16(pg, ((s & 1) * kMaxBpcRun + vb) * NA + (tid >> 2), ba, tag0 + s + 1);
-                    if (dob) {
+                    if (kWave1 && dob) {
+                        // the other taps' lane values to LDS ([value][T], value = 2 rank + I/Q);
+                        // one wave reduces them during the sweep (defer_reduce)
+                        double* stg = s_mem + kPwD;
+                        const unsigned sb = (unsigned)dfi(*(const int*)&s_df.selB);
+#pragma unroll
+                        for (int s2 = 0; s2 < NT; s2++)
+                            if ((sb >> s2) & 1u) {
+                                const int r = __builtin_popcount(sb & ((1u << s2) - 1u));
+                                stg[(2 * r) * T + tid] = oI[s2];
+                                stg[(2 * r + 1) * T + tid] = oQ[s2];
+                            }
+                        lds_barrier();
+                    } else if (dob) {
                         const int hb = dfi(s_df.hb), nB = dfi(s_df.nBv) / 2;
                         for (int ps = 1; (ps - 1) * hb < nB; ps++) {
                             const unsigned sel = sel_pass(ps);
@@ -1896,12 +1997,21 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
 
         // ---- every block's partial, summed in a fixed order (bit-identical in all blocks)
         unsigned* pw = reinterpret_cast<unsigned*>(s_mem);
-        // (waves 0, 2, 3 poll; wave 1 is flushing the previous step meanwhile)
-        // (block 0: waves 0, 2, 3 poll while wave 1 writes the record; the other blocks'
-        // wave 1 flush is short and it joins the polling after it)
         {
-            const int pid = GNSS_SWEEP_IO_ALL || !io ? tid : (wv == 1 ? -1 : tid - (wv > 1 ? 64 : 0));
-            const int np = GNSS_SWEEP_IO_ALL || !io ? 4 * 64 : 3 * 64;
+            // (the part-1 block: waves 0, 2, 3 poll while wave 1 writes the record; the other
+            // blocks' wave 1 flush is short and it joins the polling after it)
+            int pid = GNSS_SWEEP_IO_ALL || !dio ? tid : (wv == 1 ? -1 : tid - (wv > 1 ? 64 : 0));
+            int np = GNSS_SWEEP_IO_ALL || !dio ? 4 * 64 : 3 * 64;
+            if (kWave1 && dob) {
+                // the B wave (wave 1, or wave 3 in the part-1 block, whose wave 1 writes the
+                // record) reduces the other taps and publishes them; the rest poll
+                const int bw = dio ? 3 : 1;
+                if (wv == bw) defer_reduce(s);
+                // pollers: waves 0, 2, 3 (ranks 0, 1, 2); in the part-1 block waves 0, 2
+                const int rank = wv == 0 ? 0 : wv - 1;
+                pid = (wv == bw || wv == 1) ? -1 : rank * 64 + lane;
+                np = dio ? 2 * 64 : 3 * 64;
+            }
             if constexpr (!kDefer) {
                 if (!sweep16(pg, bpc * NV, tag0 + s + 1, pw, pid, np, b.run_err, (s & 1) * kMaxBpcRun * NV)) return;
             } else {

@@ -2,7 +2,8 @@
 (taps -0.5:0.1:0.5, trackingCT_multiCorr-GIVEN.m:25 tap semantics on trackingCT.m's loop)
 over the FULL benchmarked length -- 1000 ms @1 ms + countinx + 90 000 ms @10 ms
 (trackingCT.m:73-171, :178-213, :377-525) -- on the bench's own 32-SV record, for eight of
-the 32 channels (round 4; rounds 2-3: three).
+the 32 channels (round 4; rounds 2-3: three), and from round 5 the other 24 in two sets
+(--set b / c, compact_lite: integer fields, E / P / L and the NCO fields).
 
 Runs ON THE GPU BOX (the record is the HIP synthetic generator's, resident in HBM: it is
 downloaded there and fed to the CPU oracle, one OpenMP thread per channel, ~13-15 min), e.g.
@@ -77,20 +78,49 @@ def compact(j, r, tp, cn0, F):
             f"taps_{j}": qt.astype(np.int32), f"nco_{j}": r[nco], f"CN0_{j}": cn0}
 
 
+def compact_lite(j, r, cn0, F):
+    """The other 24 channels (round 5) in a smaller form: the integer fields
+    exact as above, E / P / L (r[:6]) as int32 quanta of QREL x RMS, the NCO fields as float32
+    (their test tolerance, 1e-7 relative, is above float32's 6e-8) -- no non-loop taps."""
+    ints, nco = field_rows(F)
+    rms = float(np.sqrt(np.mean(r[0] ** 2 + r[1] ** 2)))
+    qe = np.rint(r[:6] / (QREL * rms))
+    assert np.abs(qe).max() < 2 ** 31
+    iv = r[ints].astype(np.int64)
+    d = np.diff(iv, axis=1)
+    assert np.abs(d).max() < 2 ** 31
+    return {f"rms_{j}": rms, f"int0_{j}": iv[:, 0], f"intd_{j}": d.astype(np.int32),
+            f"epl_{j}": qe.astype(np.int32), f"nco32_{j}": r[nco].astype(np.float32), f"CN0_{j}": cn0}
+
+
 def expand(z, j):
     """(integer fields [5][steps], taps [2][11][steps] as floats, nco [7][steps], rms)."""
     iv = np.concatenate([z[f"int0_{j}"][:, None], z[f"intd_{j}"].astype(np.int64)], axis=1).cumsum(axis=1)
     rms = float(z[f"rms_{j}"])
+    if f"taps_{j}" not in z:  # (compact_lite: E / P / L only, as the [2][11] tap array's rows 0 / 5 / 10)
+        e = z[f"epl_{j}"] * (float(z["qrel"]) * rms)
+        taps = np.full((2, 11, e.shape[1]), np.nan)
+        for k in range(6):
+            taps[k % 2, (5, 5, 0, 0, 10, 10)[k]] = e[k]
+        return iv, taps, z[f"nco32_{j}"].astype(np.float64), rms
     return iv, z[f"taps_{j}"] * (float(z["qrel"]) * rms), z[f"nco_{j}"], rms
 
 
-def main(out):
-    ctx = pkg.Context(0)
+# round 5: the other 24 channels in two sets (one GPU-box call each: 12 oracle threads, ~15 min)
+CHANNEL_SETS = {"b": (1, 3, 4, 5, 6, 8, 9, 10, 11, 13, 14, 15),
+                "c": (16, 18, 19, 20, 21, 23, 24, 25, 26, 28, 29, 30)}
+
+
+def main(out, channels=CHANNELS, lite=False, cpu=False):
     file, signal, acq, track = pkg.initParameters()[:4]
     cfg = pkg.synth.all_prn(NSV, skip_ms=SKIP)
-    dev = pkg.DeviceRecord(ctx, record_bytes(signal.Sample))
-    pkg.synth.generate_device(ctx, cfg, dev)
-    data = dev.download()
+    if cpu:  # (tools/synth_cmp.py showed or_synth_if == gnss_synth_if_device for this scenario)
+        data = po.synth_if(cfg, 0, record_bytes(signal.Sample) // 2)
+    else:
+        ctx = pkg.Context(0)
+        dev = pkg.DeviceRecord(ctx, record_bytes(signal.Sample))
+        pkg.synth.generate_device(ctx, cfg, dev)
+        data = dev.download()
     dg = mgl.digest(data)
     print("record", len(data), "bytes, xxh64", dg, flush=True)
     file.skip, file.data = SKIP, data
@@ -100,15 +130,15 @@ def main(out):
     stop = threading.Event()
     threading.Thread(target=mgl.beat, args=(stop,), daemon=True).start()
     t = time.time()
-    b = po.trackingCT(file, signal, track, A, taps=taps, channels=list(CHANNELS), nthreads=len(CHANNELS),
+    b = po.trackingCT(file, signal, track, A, taps=taps, channels=list(channels), nthreads=len(channels),
                       raw=True)
     stop.set()
     assert b.status == 0, b.status
-    print(f"oracle channels {CHANNELS}: {time.time() - t:.1f} s", flush=True)
-    save = dict(digest=dg, skip=SKIP, N1=N1, N10=N10, nsv=NSV, channels=np.array(CHANNELS), qrel=QREL,
-                taps=taps, countinx=np.array([int(b.countinx[c]) for c in CHANNELS]),
-                len=np.array([int(b.len[c]) for c in CHANNELS]))
-    for j, c in enumerate(CHANNELS):
+    print(f"oracle channels {channels}: {time.time() - t:.1f} s", flush=True)
+    save = dict(digest=dg, skip=SKIP, N1=N1, N10=N10, nsv=NSV, channels=np.array(channels), qrel=QREL,
+                taps=taps, countinx=np.array([int(b.countinx[c]) for c in channels]),
+                len=np.array([int(b.len[c]) for c in channels]))
+    for j, c in enumerate(channels):
         n1 = N1 + int(b.countinx[c])
         L = int(b.len[c])
         assert L == n1 + N10
@@ -116,7 +146,10 @@ def main(out):
         assert np.array_equal(rec[:, n1::10], rec[:, n1 + 9::10])  # 10x replication
         r = distinct_steps(rec, n1)
         tp = distinct_steps(b.taps[c, :, :, :L], n1)  # [2][11][steps]
-        save.update(compact(j, r, tp, b.CN0[: b.c.cn0_rows, c], pkg.abi.FIELDS))
+        if lite:
+            save.update(compact_lite(j, r, b.CN0[: b.c.cn0_rows, c], pkg.abi.FIELDS))
+        else:
+            save.update(compact(j, r, tp, b.CN0[: b.c.cn0_rows, c], pkg.abi.FIELDS))
         lock = float(np.mean(np.abs(r[0, n1:]) > np.abs(r[1, n1:])))  # |P_i| > |P_q| in the 10-ms phase
         save[f"lock_{j}"] = lock
         print(f"channel {c} (PRN {int(A.sv[c])}): countinx {int(b.countinx[c])}, 10-ms lock {lock:.3f}", flush=True)
@@ -125,4 +158,12 @@ def main(out):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "golden_cfg5_long.npz"))
+    # make_golden_cfg5.py [OUT]                -> the eight channels of CHANNELS, full taps
+    # make_golden_cfg5.py --set b|c [--cpu]    -> CHANNEL_SETS[b|c], compact_lite, golden_cfg5_long_<set>.npz
+    args = sys.argv[1:]
+    if args and args[0] == "--set":
+        st = args[1]
+        main(os.path.join(ROOT, "gpurun_out", f"golden_cfg5_long_{st}.npz"), CHANNEL_SETS[st], lite=True,
+             cpu="--cpu" in args)
+    else:
+        main(args[0] if args else os.path.join(ROOT, "gpurun_out", "golden_cfg5_long.npz"))
