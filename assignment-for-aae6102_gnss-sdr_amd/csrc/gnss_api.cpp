@@ -1287,6 +1287,14 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
     if (pos) { P.iE = 0; P.iP = 1; P.iL = 2; }
     if ((pos && pos->mc_pdi) || gv) { P.iE = 2; P.iP = 12; P.iL = 22; }
     if (P.iE < 0 || P.iP < 0 || P.iL < 0) return fail(ctx, GNSS_EARG, "taps must contain -spacing, 0, +spacing");
+    {
+        double lo_t = 1e300, hi_t = -1e300;
+        for (int s = 0; s < ntaps; s++) {
+            lo_t = std::min(lo_t, taps[s] + P.tap_post[s]);
+            hi_t = std::max(hi_t, taps[s] + P.tap_post[s]);
+        }
+        if (!(hi_t - lo_t <= kTapSpan)) return fail(ctx, GNSS_EARG, "tap offsets must lie within %g chips", kTapSpan);
+    }
     P.ntaps = ntaps;
 
     std::vector<int32_t> chans;

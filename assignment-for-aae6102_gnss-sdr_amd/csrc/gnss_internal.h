@@ -335,6 +335,9 @@ constexpr int kMaxVpb = 16;      // virtual blocks per resident block of the per
 #ifndef GNSS_QCAP
 #define GNSS_QCAP 0
 #endif
+// the persistent loop's tap window (lane_correlate): tap offsets (+ prompt post) within this
+// many chips of each other, so every tap's chip at a lane's start lies in one 32-chip run
+constexpr double kTapSpan = 30.0;
 constexpr int kQcapMax = 8;      // capture-queue entries per lane (lane_correlate, the LDS slots)
 
 // The most taps whose replica boundary can fall inside one lane of M samples when the code

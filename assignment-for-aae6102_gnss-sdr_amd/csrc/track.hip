@@ -785,10 +785,28 @@ struct LdsRaw {
 #endif
 
 // (GNSS_QCAP: gnss_internal.h)
+// The C/A code bits as the lanes hold them (lane w < 32: word w, bit i of word w = chip
+// 32 w + i of the 1023, bit set = -1) extended circularly for the tap window below: bit 31 of
+// word 31 (index 1023) = chip 0, word 32 (lane 32) = chips 1..32, word 33 = chips 33..64, so
+// any 64-bit run starting at an index <= 1022 reads the code without a wrap. Call with every
+// lane of the wave active; lanes < 31 keep their word.
+__device__ __forceinline__ unsigned ca_bits_ext(unsigned cabits, int lane)
+{
+    const unsigned w0 = __shfl(cabits, 0, 64), w1 = __shfl(cabits, 1, 64), w2 = __shfl(cabits, 2, 64);
+    if (lane == 31) return cabits | ((w0 & 1u) << 31);
+    if (lane == 32) return (w0 >> 1) | (w1 << 31);
+    if (lane == 33) return (w1 >> 1) | (w2 << 31);
+    return cabits;
+}
+
+#ifndef GNSS_TAPWIN
+#define GNSS_TAPWIN 1  // (A/B: 0 = per-tap colon element, scalar tap loads and two code shuffles)
+#endif
 template <int NT, int SUB, bool DIVIDE, bool RELOAD, int FMT, class Desc, class Raw>
 __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* dp, const Raw& raw,
                                                int64_t ks, unsigned cabits, double2* myslot,
-                                               const double2* zero, double (&oI)[NT], double (&oQ)[NT])
+                                               const double2* zero, double (&oI)[NT], double (&oQ)[NT],
+                                               const double* posts = nullptr)
 {
     constexpr int M = 8 * SUB;
     constexpr int T = kTrkThreads;
@@ -822,8 +840,54 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
     // code values around each tap's boundary as sign bits (bit s set: -1): a0 before it,
     // a1 after; v1 = a1 and dv = a0 - a1 are rebuilt in the epilogue (2 VGPRs, not 4*NT)
     unsigned neg0 = 0u, neg1 = 0u;
+    // Tap window (GNSS_TAPWIN, the persistent loop: descriptor and tap offsets in LDS): the
+    // parts of colon_elem(col_s, kf) that no tap changes (which end of the colon kf is counted
+    // from, (double)kf * d, (double)(n - 1 - kf) * d) once per lane; every tap's colon ends read
+    // from LDS into vector registers (broadcast reads, no scalar round trip per tap); and the
+    // code bits of all taps from ONE 64-bit window of the circularly extended code table
+    // (ca_bits_ext) instead of two shuffles per tap: the taps' chips at the lane start lie within
+    // kTapSpan chips of each other (the host checks the tap offsets). The same values as
+    // colon_elem and ca_index32, so the same bits.
+    constexpr bool TW = GNSS_TAPWIN && RELOAD && (GNSS_CORR_PROBE & 66) == 0;
+    if constexpr (TW) {
+        const int64_t nn = n - 1;
+        const bool mid = 2 * kf == nn, lower = kf <= nn / 2;
+        const double KD = (double)kf * d, NKD = (double)(nn - kf) * d;
+        int c0i[NT];
+        int cmin = 0x7fffffff;
 #pragma unroll
-    for (int s = 0; s < NT; s++) {
+        for (int s = 0; s < NT; s++) {
+            const double a = lds_at(dp->tap_a, s), c = lds_at(dp->tap_c, s);
+            const double post = lds_at(posts, s);
+            const double t0 = (mid ? (a + c) / 2 : lower ? a + KD : c - NKD) + post;
+            const double c0 = ceil(t0);
+            const double R = (double)(kf - ks) + (c0 - t0) * inv_d;  // samples to the boundary
+            const double rr = rint(R);
+            int pb = (int)floor(R) + 1;
+            if (fabs(R - rr) < 1e-6) {  // too close to call in floating point: exact colon value
+                const int ms = (int)rr;
+                pb = ms;
+                const int64_t kx = ks + ms;
+                if (ms >= 0 && ms < M && kx >= 0 && kx <= n - 1)
+                    pb = ceil(colon_elem(Colon{a, d, c, nn}, kx) + post) > c0 ? ms : ms + 1;
+            }
+            cap[s] = (pb < M ? pb : M) - 1;  // Prefix(p) = running sum through sample p-1
+            if constexpr ((GNSS_CORR_PROBE & 32) != 0) cap[s] = M - 1 - s;
+            c0i[s] = (int)c0;
+            cmin = c0i[s] < cmin ? c0i[s] : cmin;
+        }
+        const unsigned ib = ca_index32(cmin + p.chip_off);
+        const unsigned wlo = __shfl(cabits, (int)(ib >> 5), 64), whi = __shfl(cabits, (int)(ib >> 5) + 1, 64);
+        const unsigned long long W = (((unsigned long long)whi << 32) | wlo) >> (ib & 31);
+#pragma unroll
+        for (int s = 0; s < NT; s++) {
+            const int o = c0i[s] - cmin;
+            neg0 |= (unsigned)((W >> o) & 1ull) << s;
+            neg1 |= (unsigned)((W >> (o + 1)) & 1ull) << s;
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < (TW ? 0 : NT); s++) {
         if constexpr ((GNSS_CORR_PROBE & 2) != 0) {
             cap[s] = M - 1 - s;
             neg0 |= (cabits & 1u) << s;
@@ -1646,7 +1710,8 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
     const int64_t n1_target = cp->n1_target;
     const int8_t* iq = b.iq - p.buf_base;  // absolute-byte addressing
     const int64_t gmax = (p.buf_base + p.buf_len) / 16 - 1;  // last resident 16-B group
-    const unsigned cabits = lane < 32 ? ((g_cu32*)b.ca_bits)[ch * 32 + lane] : 0u;
+    // (circularly extended for lane_correlate's tap window, ca_bits_ext)
+    const unsigned cabits = ca_bits_ext(lane < 32 ? ((g_cu32*)b.ca_bits)[ch * 32 + lane] : 0u, lane);
     // this channel's granules (gran_per_chan): 3 taps [parity][block][value] x 16 B; above,
     // region A [parity][block][E/P/L value] and region B [step mod 4][value][block]
     const __amdgpu_buffer_rsrc_t pg = __builtin_amdgcn_make_buffer_rsrc(
@@ -1919,7 +1984,8 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's global_load_lds landed
                 double oI[NT], oQ[NT];
                 lane_correlate<NT, SUB, DIVIDE, true, 0>(p, &D, LdsRaw{s_raw + tid}, 8 * g0 - A, cabits,
-                                                      reinterpret_cast<double2*>(s_mem) + tid, &s_zero, oI, oQ);
+                                                      reinterpret_cast<double2*>(s_mem) + tid, &s_zero, oI, oQ,
+                                                      s_post);
                 __syncthreads();  // slots and s_raw free
                 if (pend && dio && wv == 1 && lane == 0 && jv == 0) {
                     // the pending record's older delayValue prefix (quirk A.11's column), loaded
