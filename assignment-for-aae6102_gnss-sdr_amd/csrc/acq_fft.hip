@@ -25,7 +25,11 @@
 // storage index s = tau2*2000 + tau1 to the code phase tau = tau2 + P*tau1.
 #include "gnss_internal.h"
 
-// FFT values need no bit-for-bit replay of the reference: let the compiler fuse.
+// FFT values need no bit-for-bit replay of the reference: let the compiler fuse a product
+// into the sum it feeds. Where a sum has two products (a*b + c*d) the contraction could fuse
+// either one, chosen by the schedule, so two kernels running the same source (the fused
+// and the two-launch correlators, a refactored body) could round differently: those sums are
+// written with the fused product fixed (fma2 below).
 #pragma clang fp contract(fast)
 
 namespace gnss {
@@ -60,15 +64,18 @@ template <class V> __device__ __forceinline__ V mk(Re<V> x, Re<V> y)
     r.y = y;
     return r;
 }
+// a*b + cd (cd = c*d rounded): the fused product fixed, whatever the schedule
+__device__ __forceinline__ float fma2(float a, float b, float cd) { return __builtin_fmaf(a, b, cd); }
+__device__ __forceinline__ double fma2(double a, double b, double cd) { return __builtin_fma(a, b, cd); }
 template <class V> __device__ __forceinline__ V cadd(V a, V b) { return mk<V>(a.x + b.x, a.y + b.y); }
 template <class V> __device__ __forceinline__ V csub(V a, V b) { return mk<V>(a.x - b.x, a.y - b.y); }
 template <class V> __device__ __forceinline__ V cmul(V a, V b)
 {
-    return mk<V>(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+    return mk<V>(fma2(a.x, b.x, -(a.y * b.y)), fma2(a.x, b.y, a.y * b.x));
 }
 template <class V> __device__ __forceinline__ V cmulc(V a, V b)  // a * conj(b)
 {
-    return mk<V>(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
+    return mk<V>(fma2(a.x, b.x, a.y * b.y), fma2(a.y, b.x, -(a.x * b.y)));
 }
 // multiply by -j (DIR = -1, forward) or +j (DIR = +1, inverse)
 template <int DIR, class V> __device__ __forceinline__ V mul_dj(V a)
@@ -100,8 +107,8 @@ template <int DIR, class V> __device__ __forceinline__ void dft5(V (&v)[5])
     const V t3 = csub(v[1], v[4]), t4 = csub(v[2], v[3]);
     const V b1 = mk<V>(v[0].x + c1 * t1.x + c2 * t2.x, v[0].y + c1 * t1.y + c2 * t2.y);
     const V b2 = mk<V>(v[0].x + c2 * t1.x + c1 * t2.x, v[0].y + c2 * t1.y + c1 * t2.y);
-    const V e1 = mul_dj<DIR>(mk<V>(s1 * t3.x + s2 * t4.x, s1 * t3.y + s2 * t4.y));
-    const V e2 = mul_dj<DIR>(mk<V>(s2 * t3.x - s1 * t4.x, s2 * t3.y - s1 * t4.y));
+    const V e1 = mul_dj<DIR>(mk<V>(fma2(s1, t3.x, s2 * t4.x), fma2(s1, t3.y, s2 * t4.y)));
+    const V e2 = mul_dj<DIR>(mk<V>(fma2(s2, t3.x, -(s1 * t4.x)), fma2(s2, t3.y, -(s1 * t4.y))));
     v[0] = mk<V>(v[0].x + t1.x + t2.x, v[0].y + t1.y + t2.y);
     v[1] = cadd(b1, e1);
     v[4] = csub(b1, e1);
@@ -481,7 +488,7 @@ __global__ __launch_bounds__(kRowThreads) void fwd_rows_kernel(
             }
             const double2 r = src.at((int64_t)idx * S + n);
             const R xr = (R)r.x, xi = (R)r.y;
-            s_a[n1] = mk<V>(xr * c - xi * sn, xr * sn + xi * c);
+            s_a[n1] = mk<V>(fma2(xr, c, -(xi * sn)), fma2(xr, sn, xi * c));
         }
     } else {
         const float* cp = ca + (int64_t)(s - nsig) * 1023;
@@ -536,19 +543,16 @@ template <> __device__ __forceinline__ float2 buf_ld<float2>(__amdgpu_buffer_rsr
 #ifndef GNSS_TW_ROWS
 #define GNSS_TW_ROWS 1  // (A/B: 0 = the column pass multiplies by the four-step twiddle)
 #endif
-template <int P, class V>
 #ifndef GNSS_INVCOLS_WPE
 #define GNSS_INVCOLS_WPE 0  // (A/B: waves per EU asked of inv_cols; 0 = the compiler's choice)
 #endif
-__global__ __launch_bounds__(kColThreads)
-#if GNSS_INVCOLS_WPE > 0
-__attribute__((amdgpu_waves_per_eu(GNSS_INVCOLS_WPE, GNSS_INVCOLS_WPE)))
-#endif
-void inv_cols_kernel(
-    const V* __restrict__ C, const V* __restrict__ X, int nbins, int nprn, int datalen,
+// (the body takes its block coordinates: inv_cols_kernel and the paired launch run it)
+template <int P, class V>
+__device__ __forceinline__ void inv_cols_body(
+    int bx, int t, const V* __restrict__ C, const V* __restrict__ X, int nbins, int nprn, int datalen,
     int first_pair, const V* __restrict__ tw_col, V* __restrict__ A)
 {
-    const int k1 = blockIdx.x * kColThreads + threadIdx.x, t = blockIdx.y;
+    const int k1 = bx * kColThreads + threadIdx.x;
     if (k1 >= kRow) return;
     const int q = first_pair + t / datalen, idx = t % datalen;
     const int bin = q / nprn, p = q - bin * nprn;
@@ -634,6 +638,18 @@ void inv_cols_kernel(
     });
 }
 
+template <int P, class V>
+__global__ __launch_bounds__(kColThreads)
+#if GNSS_INVCOLS_WPE > 0
+__attribute__((amdgpu_waves_per_eu(GNSS_INVCOLS_WPE, GNSS_INVCOLS_WPE)))
+#endif
+void inv_cols_kernel(
+    const V* __restrict__ C, const V* __restrict__ X, int nbins, int nprn, int datalen,
+    int first_pair, const V* __restrict__ tw_col, V* __restrict__ A)
+{
+    inv_cols_body<P, V>(blockIdx.x, blockIdx.y, C, X, nbins, nprn, datalen, first_pair, tw_col, A);
+}
+
 // ---- I2: inverse rows, |.|^2/S^2 summed over the ms in order, stored tau2-major. Two
 // ms per pass (their 2000-point transforms side by side, fft2000_batch): half the
 // barriers per transform, every lane busy in the radix-20 pass.
@@ -700,8 +716,8 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel(
         for (int i = 0; i < Q; i++) {  // the ms in order (acquisition.m:53-61)
             const int t1 = tid + i * kRowThreads, t = t1 < kRow ? t1 : kRow - 1;
             const float2 v = s_a[t], w = s_a[kRow + t];
-            acc[i] += (v.x * v.x + v.y * v.y) * scale;
-            if (second) acc[i] += (w.x * w.x + w.y * w.y) * scale;
+            acc[i] += fma2(v.x, v.x, v.y * v.y) * scale;
+            if (second) acc[i] += fma2(w.x, w.x, w.y * w.y) * scale;
         }
         __syncthreads();
     }
@@ -725,13 +741,13 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel(
 // of the LDS cycles by SQ_LDS_BANK_CONFLICT): 350 -> 481 us per launch (index divisions);
 // radix 10-10-20 (conflict-free first pass, twiddles in the radix-20 pass): 350 -> 367 us.
 template <int P>
-__global__ __launch_bounds__(kRowThreads) void inv_rows_kernel_f64(
-    const double2* __restrict__ A, int nprn, int datalen, int first_pair, double scale,
+__device__ __forceinline__ void inv_rows_f64_body(
+    int tau2, int g, const double2* __restrict__ A, int nprn, int datalen, int first_pair, double scale,
     const double2* __restrict__ tw_row, const double2* __restrict__ tw_col, double* __restrict__ corr, int nbins)
 {
     constexpr int Q = (kRow + kRowThreads - 1) / kRowThreads;
     __shared__ double2 s_a[kRowPad], s_tw[kTwIK];
-    const int tau2 = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
+    const int tid = threadIdx.x;
     const TwIK<double2> twk = load_row_tw_ik(s_tw, tw_row, tid);
     double acc[kInvOut];
 #pragma unroll
@@ -777,6 +793,43 @@ __global__ __launch_bounds__(kRowThreads) void inv_rows_kernel_f64(
     if (tid < kRow / kInvOut) {
 #pragma unroll
         for (int i = 0; i < kInvOut; i++) o[tid + i * (kRow / kInvOut)] = acc[i];
+    }
+}
+
+template <int P>
+__global__ __launch_bounds__(kRowThreads) void inv_rows_kernel_f64(
+    const double2* __restrict__ A, int nprn, int datalen, int first_pair, double scale,
+    const double2* __restrict__ tw_row, const double2* __restrict__ tw_col, double* __restrict__ corr, int nbins)
+{
+    inv_rows_f64_body<P>(blockIdx.x, blockIdx.y, A, nprn, datalen, first_pair, scale, tw_row, tw_col, corr, nbins);
+}
+
+// ---- The two passes in one launch (fp64, GNSS_OPT_ACQ_PIPE 3): launch k holds the column
+// pass of batch k and the row pass of batch k-1, their blocks interleaved in the grid, so a
+// CU runs a column block (bound by the intermediate's streaming stores) beside a row block
+// (bound by its fp64 LDS transforms) instead of two of a kind. Block i is a row block iff
+// floor((i+1) nr / F) > floor(i nr / F) for i < F (F = front * grid / 100: the long row blocks
+// are all dispatched in the grid's first `front` percent, none left for the launch's tail);
+// its index is floor(i nr / F), a column block's is i minus the row blocks before it. Each
+// block runs the plain kernels' body unchanged: the bits are the two-launch path's.
+template <int P>
+__global__ __launch_bounds__(kRowThreads) void inv_pair_kernel_f64(
+    const double2* __restrict__ C, const double2* __restrict__ X, int nbins, int nprn, int datalen,
+    int cols_first, int cols_n, double2* __restrict__ Acols, int rows_first, int rows_n,
+    const double2* __restrict__ Arows, double scale, const double2* __restrict__ tw_row,
+    const double2* __restrict__ tw_col, double* __restrict__ corr, int front)
+{
+    constexpr int kCx = (kRow + kColThreads - 1) / kColThreads;
+    const int64_t nr = (int64_t)P * rows_n, T = nr + (int64_t)kCx * cols_n * datalen;
+    const int64_t F = nr ? std::max<int64_t>(nr, T * front / 100) : 1;
+    const int64_t i = blockIdx.x;
+    const int64_t r0 = i < F ? i * nr / F : nr, r1 = i < F ? (i + 1) * nr / F : nr;
+    if (r1 > r0) {
+        const int g = (int)(r0 / P), tau2 = (int)(r0 - (int64_t)g * P);
+        inv_rows_f64_body<P>(tau2, g, Arows, nprn, datalen, rows_first, scale, tw_row, tw_col, corr, nbins);
+    } else {
+        const int c = (int)(i - r0), t = c / kCx;
+        inv_cols_body<P, double2>(c - t * kCx, t, C, X, nbins, nprn, datalen, cols_first, tw_col, Acols);
     }
 }
 
@@ -1179,6 +1232,32 @@ hipError_t launch_acq_fft_correlate(const double2* C, const double2* X, int64_t 
     }
     GNSS_INV(13) GNSS_INV(29)
 #undef GNSS_INV
+    return hipErrorInvalidValue;
+}
+
+// One paired launch (fp64): the column pass of pairs [cols_first, +cols_n) into Acols and the
+// row pass of [rows_first, +rows_n) from Arows (a different intermediate: the previous launch's).
+hipError_t launch_acq_fft_pair(const double2* C, const double2* X, int64_t S, int datalen, int nbins, int nprn,
+                               int cols_first, int cols_n, double2* Acols, int rows_first, int rows_n,
+                               const double2* Arows, const double2* tw_row, const double2* tw_col, double* corr,
+                               int front, hipStream_t s)
+{
+    if (front < 1 || front > 100 || cols_n < 0 || rows_n < 0) return hipErrorInvalidValue;
+    const double scale = 1.0 / ((double)S * (double)S);
+    constexpr int kCx = (kRow + kColThreads - 1) / kColThreads;
+#define GNSS_PAIR(P_)                                                                           \
+    if (S == (int64_t)P_ * kRow) {                                                              \
+        const int64_t nblk = (int64_t)P_ * rows_n + (int64_t)kCx * cols_n * datalen;             \
+        if (nblk == 0) return hipSuccess;                                                       \
+        if (nblk > INT32_MAX) return hipErrorInvalidConfiguration;                              \
+        hipLaunchKernelGGL(inv_pair_kernel_f64<P_>, dim3((unsigned)nblk), dim3(kRowThreads), 0, s, C, X, nbins, \
+                           nprn, datalen, cols_first, cols_n, Acols, rows_first, rows_n, Arows, scale, tw_row, \
+                           tw_col, corr, front);                                                \
+        return hipGetLastError();                                                               \
+    }
+    static_assert(kColThreads == kRowThreads, "the paired launch runs both bodies in one block shape");
+    GNSS_PAIR(13) GNSS_PAIR(29)
+#undef GNSS_PAIR
     return hipErrorInvalidValue;
 }
 

@@ -75,7 +75,9 @@ namespace {
 // The acquisition's split correlator pipelines its batches over two streams by default
 // (GNSS_OPT_ACQ_PIPE; config-2 fp64 correlation 10.10-10.18 -> 9.75-9.88 ms on MI355X,
 // profiles/r03_ab_acq_pipe.txt).
-constexpr bool kAcqPipeDefault = true;
+constexpr int kAcqPipeDefault = 2;
+// the paired launch's row blocks sit in the grid's first kAcqPairFront percent (acq_fft.hip)
+constexpr int kAcqPairFront = 60;
 
 // The context's pinned host buffer `key`, at least `bytes` (contents undefined).
 template <class T>
@@ -518,17 +520,36 @@ int acq_search(gnss_ctx* ctx, const int8_t* blk, const double2* xa, int64_t S, i
         // in its own half of a double intermediate; the column pass of b+2 waits for the rows
         // of b. Every pair is in one batch and its corr entries are written by its row pass
         // alone, so the surface is bit-identical to the one-stream order.
-        const int64_t pipe = ctx->opt[GNSS_OPT_ACQ_PIPE];
-        const bool two = (pipe == 2 || (pipe == 0 && kAcqPipeDefault)) && npairs > batch;
+        // Paired launches (fp64, = 3): one launch per batch boundary holding batch b's column
+        // blocks and batch b-1's row blocks interleaved, so the two passes share every CU.
+        const int64_t pipe = ctx->opt[GNSS_OPT_ACQ_PIPE] ? ctx->opt[GNSS_OPT_ACQ_PIPE] : kAcqPipeDefault;
+        const bool pair = dbl && pipe == 3 && npairs > batch;
+        const bool two = (pipe == 2 || (pipe == 3 && !dbl)) && npairs > batch;
         hipStream_t s_cols = ctx->stream, s_rows = ctx->stream2;
         const size_t abuf = (size_t)batch * dl * S;
-        HIP_TRY(A.alloc(ctx, "acq.A", csz * abuf * (two ? 2 : 1)));
+        HIP_TRY(A.alloc(ctx, "acq.A", csz * abuf * (two || pair ? 2 : 1)));
         HIP_TRY(hipStreamSynchronize(ctx->stream));
         HIP_TRY(hipEventRecord(e_all.a, ctx->stream));
         HIP_TRY(launch_acq_fft_forward<V>(blk, xa, S, dl, nb, sg->IF, acq->freqMin, acq->freqStep, sg->Fs, ca, np,
                                           sg->codeFreqBasis, d_twr.as<V>(), d_twc.as<V>(), B.as<V>(), X.as<V>(),
                                           ctx->stream));
         const V* C = X.as<V>() + (size_t)nsig * S;
+        if (pair) {
+            const char* fe = probe_env("GNSS_PAIR_FRONT");  // (probe builds: the A/B knob)
+            const int front = fe ? atoi(fe) : kAcqPairFront;
+            const int nbt = (npairs + batch - 1) / batch;
+            double2* Ah[2] = {reinterpret_cast<double2*>(A.p), reinterpret_cast<double2*>(A.p) + abuf};
+            for (int b = 0; b <= nbt; b++) {
+                const int cq = b * batch, rq = (b - 1) * batch;
+                const int nc = b < nbt ? std::min(batch, npairs - cq) : 0;
+                const int nr = b > 0 ? std::min(batch, npairs - rq) : 0;
+                HIP_TRY(launch_acq_fft_pair(reinterpret_cast<const double2*>(C), X.as<double2>(), S, dl, nb, np, cq,
+                                            nc, Ah[b & 1], rq, nr, Ah[(b + 1) & 1], d_twr.as<double2>(),
+                                            d_twc.as<double2>(), reinterpret_cast<double*>(corr), front,
+                                            ctx->stream));
+            }
+            return GNSS_OK;
+        }
         if (!two) {
             for (int q0 = 0; q0 < npairs; q0 += batch) {
                 const int nq = std::min(batch, npairs - q0);

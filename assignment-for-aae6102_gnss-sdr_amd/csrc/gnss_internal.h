@@ -426,6 +426,12 @@ hipError_t launch_acq_fft_correlate(const double2* C, const double2* X, int64_t 
                                     int nbins, int nprn, int first_pair, int npair,
                                     const double2* tw_row, const double2* tw_col, double2* A,
                                     double* corr, hipStream_t s, int parts = kAcqCols | kAcqRows);
+// fp64, the column pass of one batch and the row pass of the previous one in one launch, their
+// blocks interleaved (the row blocks within the grid's first `front` percent); see acq_fft.hip
+hipError_t launch_acq_fft_pair(const double2* C, const double2* X, int64_t S, int datalen, int nbins, int nprn,
+                               int cols_first, int cols_n, double2* Acols, int rows_first, int rows_n,
+                               const double2* Arows, const double2* tw_row, const double2* tw_col, double* corr,
+                               int front, hipStream_t s);
 // fp64, every (bin, PRN) pair in one persistent launch with the column/row intermediate
 // kept in each XCD's L2 (nslot ring slots per XCD, 2..4); see acq_fft.hip
 size_t acq_fused_sync_bytes();

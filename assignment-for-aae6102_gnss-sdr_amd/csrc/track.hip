@@ -1113,7 +1113,7 @@ template <int NT>
 __device__ __forceinline__ double block_partial(double* s_mem, const double (&oI)[NT],
                                                 const double (&oQ)[NT], int tid)
 {
-    constexpr int NV = 2 * NT, T = kTrkThreads, HT = red_taps<NT>();
+    constexpr int T = kTrkThreads, HT = red_taps<NT>();
     double* red = s_mem;                 // [2 HT][T]
     double* red2 = s_mem + 2 * HT * T;   // [2 HT][32]
     double a = 0.0;
@@ -1671,9 +1671,14 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
     const int pbpc = (bpc + vpb_ - 1) / vpb_;
     // (A/B knob GNSS_XCD_LOCAL: with 8 channels, channel = the block's XCD (blocks are dealt
     // round-robin over the 8 XCDs), so a channel's exchange stays in one L2)
-    const bool xl = GNSS_XCD_LOCAL && !VB && p.nch == 8;
-    const int ch = xl ? (int)(blockIdx.x & 7) : (int)(blockIdx.x / pbpc);
-    const int pblk = xl ? (int)(blockIdx.x >> 3) : (int)(blockIdx.x - ch * pbpc);
+    // (GNSS_XCD_LOCAL 2, the control experiment: with 8 channels x 96 blocks, a CU's three
+    // blocks b, b + 256, b + 512 (profiles/r03_channel_lockstep.txt) are one channel's, as
+    // XCD-local placement makes them, but each channel's 32 CUs span all 8 XCDs)
+    const bool xl = GNSS_XCD_LOCAL == 1 && !VB && p.nch == 8;
+    const bool cul = GNSS_XCD_LOCAL == 2 && !VB && p.nch == 8 && pbpc == 96;
+    const int ch = xl ? (int)(blockIdx.x & 7) : cul ? (int)((blockIdx.x & 255) >> 5) : (int)(blockIdx.x / pbpc);
+    const int pblk = xl ? (int)(blockIdx.x >> 3)
+                    : cul ? (int)((blockIdx.x & 31) * 3 + (blockIdx.x >> 8)) : (int)(blockIdx.x - ch * pbpc);
     const int blk = pblk * vpb_;
     const int nvb = VB ? (bpc - blk < vpb_ ? bpc - blk : vpb_) : 1;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1815,6 +1820,12 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
     // the others, and in the 1-ms phase it was still the last to finish its correlate.
     const int duty_a = pbpc > 3 ? 3 : 0, duty_b = pbpc > 1 ? 1 : 0, duty_c = pbpc > 2 ? 2 : duty_b;
     const bool dio = pblk == duty_a;  // the block holding the record's part 1
+    // blocks whose wave 1 flush is long (record part 1; part 2 and the tap record, ~1 us against
+    // ~0.5 elsewhere, profiles/r05_stamps_1ms.txt) poll with waves 0, 2, 3 only
+#ifndef GNSS_DSW_B
+#define GNSS_DSW_B 1  // (A/B: 0 = only the part-1 block polls without wave 1)
+#endif
+    const bool dsw = dio || (GNSS_DSW_B && pblk == duty_b);
     // (that block's wave 1, lane 0: dvpre[s_c.nstep], the running delayValue prefix its flushes
     // extend -- no read-back of its own stores)
     int64_t dvrun = 0;
@@ -2057,26 +2068,28 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
         const bool bsw = kDefer && pend && own_n_() > 0;  // the previous step's owned B values are due
         if (pend) {
             if (srow && tid == 64) srow[16] = wall_clock64();
+            if (brow && tid == 64) brow[40 + 1024 + blk] = wall_clock64();  // (probe: every block's flush)
             flush();  // (the sweep's closing barrier publishes it)
             if (srow && tid == 64) srow[17] = wall_clock64();
+            if (brow && tid == 64) brow[40 + 1280 + blk] = wall_clock64();
         }
 
         // ---- every block's partial, summed in a fixed order (bit-identical in all blocks)
         unsigned* pw = reinterpret_cast<unsigned*>(s_mem);
         {
-            // (the part-1 block: waves 0, 2, 3 poll while wave 1 writes the record; the other
-            // blocks' wave 1 flush is short and it joins the polling after it)
-            int pid = GNSS_SWEEP_IO_ALL || !dio ? tid : (wv == 1 ? -1 : tid - (wv > 1 ? 64 : 0));
-            int np = GNSS_SWEEP_IO_ALL || !dio ? 4 * 64 : 3 * 64;
+            // (the part-1 and part-2 blocks: waves 0, 2, 3 poll while wave 1 writes the record;
+            // the other blocks' wave 1 flush is short and it joins the polling after it)
+            int pid = GNSS_SWEEP_IO_ALL || !dsw ? tid : (wv == 1 ? -1 : tid - (wv > 1 ? 64 : 0));
+            int np = GNSS_SWEEP_IO_ALL || !dsw ? 4 * 64 : 3 * 64;
             if (kWave1 && dob) {
                 // the B wave (wave 1, or wave 3 in the part-1 block, whose wave 1 writes the
                 // record) reduces the other taps and publishes them; the rest poll
-                const int bw = dio ? 3 : 1;
+                const int bw = dsw ? 3 : 1;
                 if (wv == bw) defer_reduce(s);
                 // pollers: waves 0, 2, 3 (ranks 0, 1, 2); in the part-1 block waves 0, 2
                 const int rank = wv == 0 ? 0 : wv - 1;
                 pid = (wv == bw || wv == 1) ? -1 : rank * 64 + lane;
-                np = dio ? 2 * 64 : 3 * 64;
+                np = dsw ? 2 * 64 : 3 * 64;
             }
             if constexpr (!kDefer) {
                 if (!sweep16(pg, bpc * NV, tag0 + s + 1, pw, pid, np, b.run_err, (s & 1) * kMaxBpcRun * NV)) return;

@@ -263,7 +263,10 @@ int  gnss_ctx_set_window(gnss_ctx *ctx, uint64_t bytes);
 #define GNSS_OPT_ACQ_PIPE     8  /* split path: 1 = column and row passes of every batch in
                                     order on one stream, 2 = pipelined over two streams
                                     (batch b's rows beside batch b+1's columns, two
-                                    intermediates); 0 = the engine's choice               */
+                                    intermediates), 3 = paired launches (fp64: batch
+                                    b+1's column blocks and batch b's row blocks in one
+                                    grid, interleaved; fp32 runs 2); 0 = the engine's
+                                    choice                                                */
 #define GNSS_OPT_VT_BLOCKS    9  /* 1..GNSS_VT_MAX_BLOCKS: blocks per channel of
                                     gnss_tracking_vt's step (GNSS_EARG above)             */
 #define GNSS_OPT_FORCE_PEER   10 /* != 0 (multi-device contexts): every member treats

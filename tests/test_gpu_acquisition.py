@@ -233,7 +233,9 @@ def test_fused_correlator_equals_split_path(pkg, ctx, opts, shape):
 @pytest.mark.parametrize("shape", ["cfg2", "cfg4"])
 def test_pipelined_batches_equal_one_stream(pkg, ctx, opts, shape, precision):
     """The split correlator's batches pipelined over two streams (GNSS_OPT_ACQ_PIPE = 2:
-    batch b's row pass beside batch b+1's column pass, two intermediates) against the
+    batch b's row pass beside batch b+1's column pass, two intermediates) and in paired
+    launches (= 3: batch b+1's column blocks and batch b's row blocks in one grid; fp64, the
+    fp32 mode runs 2) against the
     same batches in order on one stream (= 1): every PRN's SNR, peak, second peak, bin and
     code phase identical bit for bit at the benchmarked shapes, with the engine's batch
     size and with 7 pairs per batch (an odd batch count and a short tail batch)
@@ -254,12 +256,13 @@ def test_pipelined_batches_equal_one_stream(pkg, ctx, opts, shape, precision):
     for batch in (0, 7):
         opts(abi.OPT_ACQ_BATCH, batch)
         res = []
-        for pipe in (1, 2):
+        for pipe in (1, 2, 3):
             opts(abi.OPT_ACQ_PIPE, pipe)
             res.append(pkg.acquisition(file, signal, acq, ctx=ctx, diag=True))
-        (g0, d0), (g1, d1) = res
-        for f in ("prn", "SNR", "peak", "peak2", "fbin", "codePhase"):
-            a, b = np.asarray(getattr(d0, f)), np.asarray(getattr(d1, f))
-            assert np.array_equal(a, b), (batch, f, a, b)
-        assert np.array_equal(g0.sv, g1.sv) and np.array_equal(g0.fineFreq, g1.fineFreq)
+        (g0, d0) = res[0]
+        for pipe, (g1, d1) in zip((2, 3), res[1:]):
+            for f in ("prn", "SNR", "peak", "peak2", "fbin", "codePhase"):
+                a, b = np.asarray(getattr(d0, f)), np.asarray(getattr(d1, f))
+                assert np.array_equal(a, b), (batch, pipe, f, a, b)
+            assert np.array_equal(g0.sv, g1.sv) and np.array_equal(g0.fineFreq, g1.fineFreq)
         assert len(d0.prn) == 32

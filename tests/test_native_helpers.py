@@ -58,3 +58,19 @@ def test_multi_device_bookkeeping(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches 0" in r.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_acq_fft_contraction_is_fixed_by_source():
+    """acq_fft.hip lets the compiler fuse products into sums (`fp contract(fast)`), but no sum
+    of two products is left to it: the backend would fuse either one by the schedule, so the
+    fused and two-launch correlators (or one kernel after a refactor) could round differently
+    and their bit-identity tests fail for no arithmetic reason (round 5: 2 482 such sums, the
+    fused-vs-split test failed after a no-op refactor). tools/contract_scan.py over the device
+    LLVM IR (acquisition.m:47-61, 103-116 arithmetic)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("contract_scan", os.path.join(ROOT, "tools", "contract_scan.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    n = mod.main(os.path.join(ROOT, "assignment-for-aae6102_gnss-sdr_amd", "csrc", "acq_fft.hip"))
+    assert n == 0

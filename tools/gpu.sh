@@ -167,6 +167,14 @@ for step in "$@"; do
         python3 -c "import json; d=json.load(open('gpurun_out/xsq_$v.json')); k=[x for x in d if not x.startswith('_')][0]; print('   SQ', {c: round(w['median_per_dispatch']) for c, w in d[k].items() if isinstance(w, dict) and 'median_per_dispatch' in w})" | cut -c1-1200
         rm -f gpurun_out/xsq*_$v/**/*kernel_trace.csv
       done ;;
+    acqpair)  # config-2 fp64 correlation by ACQ_PIPE:front (GNSS_PAIR_FRONT, probe library PAIRLIB):
+              # PAIRS="2:60 3:100 3:60 3:40" -> corr_ms of the three calls and a digest of the decisions
+      for v in ${PAIRS:-2:60 3:100 3:60 3:40}; do
+        pp=${v%%:*}; fr=${v##*:}
+        GNSS_LIB=$R/tools/probe_lib/libgnss_${PAIRLIB:-pair}.so ACQ_PIPE=$pp GNSS_PAIR_FRONT=$fr timeout -k 10 200 python3 tools/acq_only.py > gpurun_out/acqpair_${pp}_$fr.txt 2>&1 \
+          && echo "acqpair pipe=$pp front=$fr: corr_ms $(grep -o "'acq_corr_ms': [0-9.]*" gpurun_out/acqpair_${pp}_$fr.txt | cut -d' ' -f2 | tr '\n' ' ') acq_ms $(grep -o "'acq_ms': [0-9.]*" gpurun_out/acqpair_${pp}_$fr.txt | cut -d' ' -f2 | tr '\n' ' ') $(grep -E '^(fbin|snr|sv)' gpurun_out/acqpair_${pp}_$fr.txt | md5sum | cut -c1-8)" \
+          || { tail -5 gpurun_out/acqpair_${pp}_$fr.txt; exit 1; }
+      done ;;
     acqlib)  # config-2 acquisition (tools/acq_only.py, fp64) under each library of ACQLIBS (tools/probe_lib/libgnss_<name>.so,
              # "prod" = the product): correlation ms of the three calls and a digest of the decisions
       for v in ${ACQLIBS:-prod}; do

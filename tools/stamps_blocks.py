@@ -53,6 +53,17 @@ if m.any():
     print(f"  tail (all-in -> ready): blk0 {np.median(rd[:, 0] - ai[:, 0]) * us:.2f}, others {np.median(rd[:, 1:] - ai[:, 1:]) * us:.2f}")
     ai_late = np.argsort(np.median(ai - ai.min(1, keepdims=True), axis=0))[::-1][:6]
     print("  latest all-in: " + ", ".join(f"blk {b} +{np.median(ai[:, b] - ai.min(1)) * us:.2f}" for b in ai_late))
+# every block's flush of the previous step (wave 1: [1064 + blk] start, [1320 + blk] end)
+f0, f1 = a[:, 1064:1064 + nb], a[:, 1320:1320 + nb]
+m = (f0 > 0).all(axis=1) & (f1 > 0).all(axis=1)
+if m.any():
+    fd = (f1[m] - f0[m]) * us
+    fs = (f0[m] - st[m].min(1, keepdims=True)) * us
+    top = np.argsort(np.median(fd, axis=0))[::-1][:6]
+    print("  longest median flush: " + ", ".join(f"blk {b} {np.median(fd[:, b]):.2f}" for b in top)
+          + f"; others median {np.median(fd):.2f}")
+    print("  flush start after the earliest step start: " + ", ".join(
+        f"blk {b} {np.median(fs[:, b]):+.2f}" for b in top))
 # (GNSS_FLUSH_PROBE & 2 builds) block 0's record part cold, then the whole record again warm
 f0, f1, f2 = a[:, 2000], a[:, 2001], a[:, 2002]
 m = (f0 > 0) & (f1 > 0) & (f2 > 0)
