@@ -1109,10 +1109,73 @@ __device__ __forceinline__ void lds_barrier()
 template <int NT> constexpr int red_taps() { return NT > 3 ? (NT + 1) / 2 : NT; }
 template <int NT> constexpr int red_words() { return 2 * red_taps<NT>() * (kTrkThreads + 32); }
 
+// GNSS_RED 1 (round 5, A/B knob, off): each value summed over a wave without LDS -- the DPP
+// butterfly over quads, half rows and rows (every lane of a row ends with the row's sum, the
+// same bits in each: IEEE addition commutes), the four rows' sums read from lanes 0 / 16 / 32 /
+// 48 and added as (r0 + r1) + (r2 + r3) -- then the four waves' sums through LDS as
+// (w0 + w1) + (w2 + w3). One barrier instead of three, but 8 lane reads per value: measured
+// slower (block partial 0.48 -> 0.68 us; 10-ms launch 36.8-37.0 -> 37.8-38.0 ms at 3 taps,
+// 203 -> 217 ms at 32 channels x 11 taps; profiles/r05_ab_block_tree.txt). A different order
+// also moves the last bits, so the full-length goldens' tie flips move (config 3 channel 5
+// parts at step 3 944 with it).
+#ifndef GNSS_RED
+#define GNSS_RED 0
+#endif
+// a double read from one lane (the result is uniform)
+__device__ __forceinline__ double readlane_f64(double v, int l)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// one value's sum over the wave's 64 lanes in the fixed order above (every lane active)
+__device__ __forceinline__ double wave_sum(double a)
+{
+    a += dpp_f64<0xB1>(a);   // quad_perm [1,0,3,2]
+    a += dpp_f64<0x4E>(a);   // quad_perm [2,3,0,1]
+    a += dpp_f64<0x141>(a);  // row_half_mirror: the other quad of the 8
+    a += dpp_f64<0x140>(a);  // row_mirror: the other 8 of the 16
+    return (readlane_f64(a, 0) + readlane_f64(a, 16)) + (readlane_f64(a, 32) + readlane_f64(a, 48));
+}
+
+// the waves' sums of the values of mask `sel` (pass value w = the w-th selected I / Q), combined:
+// value w in lanes 4w .. 4w + 3 on return; s_mem free on entry and on return
+template <int NT>
+__device__ __forceinline__ double block_tree(double* s_mem, const double (&oI)[NT], const double (&oQ)[NT],
+                                             int tid, unsigned sel)
+{
+    constexpr int NV = 2 * NT;
+    const int wv = tid >> 6, lane = tid & 63;
+    double* ws = s_mem;  // [4][NV]
+    int w = 0;
+#pragma unroll
+    for (int s = 0; s < NT; s++) {
+        if ((sel >> s) & 1u) {  // (sel uniform)
+            const double si = wave_sum(oI[s]), sq = wave_sum(oQ[s]);
+            if (lane == 0) {
+                ws[wv * NV + 2 * w] = si;
+                ws[wv * NV + 2 * w + 1] = sq;
+            }
+            w++;
+        }
+    }
+    lds_barrier();
+    double a = 0.0;
+    if (tid < 2 * w * 4) {
+        const int v = tid >> 2;
+        a = (ws[v] + ws[NV + v]) + (ws[2 * NV + v] + ws[3 * NV + v]);
+    }
+    lds_barrier();  // ws read before the caller reuses s_mem
+    return a;
+}
+
 template <int NT>
 __device__ __forceinline__ double block_partial(double* s_mem, const double (&oI)[NT],
                                                 const double (&oQ)[NT], int tid)
 {
+    if constexpr (GNSS_RED) return block_tree<NT>(s_mem, oI, oQ, tid, (1u << NT) - 1u);
     constexpr int T = kTrkThreads, HT = red_taps<NT>();
     double* red = s_mem;                 // [2 HT][T]
     double* red2 = s_mem + 2 * HT * T;   // [2 HT][32]
@@ -1164,6 +1227,7 @@ template <int NT>
 __device__ __forceinline__ double block_pass(double* s_mem, const double (&oI)[NT], const double (&oQ)[NT],
                                              int tid, unsigned sel)
 {
+    if constexpr (GNSS_RED) return block_tree<NT>(s_mem, oI, oQ, tid, sel);
     constexpr int T = kTrkThreads;
     constexpr int HT = red_taps<NT>();
     double* red = s_mem;                 // [2 HT][T]
@@ -1693,6 +1757,8 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
     // run sums after them. The exchange's words then need bpc * (E/P/L values + owned values).
     constexpr bool kDefer = GNSS_DEFER && NT > 3;
     constexpr bool kWave1 = GNSS_DEFER == 2 && kDefer && !VB;
+    // (defer_reduce restates the round-4 block order for its one wave)
+    static_assert(!kWave1 || GNSS_RED == 0, "GNSS_DEFER 2 needs GNSS_RED 0");
     constexpr int kPwD = run_bpc_cap(NT) * 8 + 2 * NT;  // (pbpc = bpc: own_n <= nBv / bpc + 1)
     constexpr int kStage = 2 * (NT - 1) * T;
     constexpr int kMemW = kWave1 ? kPwD + kStage + 2 * NT * 32 : 0;

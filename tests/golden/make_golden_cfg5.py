@@ -81,7 +81,8 @@ def compact(j, r, tp, cn0, F):
 def compact_lite(j, r, cn0, F):
     """The other 24 channels (round 5) in a smaller form: the integer fields
     exact as above, E / P / L (r[:6]) as int32 quanta of QREL x RMS, the NCO fields as float32
-    (their test tolerance, 1e-7 relative, is above float32's 6e-8) -- no non-loop taps."""
+    (their test tolerance, 1e-7 relative, is above float32's 6e-8) and remChip / codeFreq again as
+    float64 -- no non-loop taps."""
     ints, nco = field_rows(F)
     rms = float(np.sqrt(np.mean(r[0] ** 2 + r[1] ** 2)))
     qe = np.rint(r[:6] / (QREL * rms))
@@ -89,8 +90,12 @@ def compact_lite(j, r, cn0, F):
     iv = r[ints].astype(np.int64)
     d = np.diff(iv, axis=1)
     assert np.abs(d).max() < 2 ** 31
+    # remChip and codeFreq also at full precision: the test's tie-flip check rebuilds the replica
+    # coordinates from the oracle's state to 1e-9 chip (float32 would give ~1e-3 chip)
+    tie = [F.index("remChip"), F.index("codeFreq")]
     return {f"rms_{j}": rms, f"int0_{j}": iv[:, 0], f"intd_{j}": d.astype(np.int32),
-            f"epl_{j}": qe.astype(np.int32), f"nco32_{j}": r[nco].astype(np.float32), f"CN0_{j}": cn0}
+            f"epl_{j}": qe.astype(np.int32), f"nco32_{j}": r[nco].astype(np.float32),
+            f"ncotie_{j}": r[tie], f"CN0_{j}": cn0}
 
 
 def expand(z, j):
@@ -102,7 +107,13 @@ def expand(z, j):
         taps = np.full((2, 11, e.shape[1]), np.nan)
         for k in range(6):
             taps[k % 2, (5, 5, 0, 0, 10, 10)[k]] = e[k]
-        return iv, taps, z[f"nco32_{j}"].astype(np.float64), rms
+        nv = z[f"nco32_{j}"].astype(np.float64)
+        if f"ncotie_{j}" in z:  # (remChip, codeFreq at full precision)
+            F = pkg.abi.FIELDS
+            nco = field_rows(F)[1]
+            for k, f in enumerate(("remChip", "codeFreq")):
+                nv[nco.index(F.index(f))] = z[f"ncotie_{j}"][k]
+        return iv, taps, nv, rms
     return iv, z[f"taps_{j}"] * (float(z["qrel"]) * rms), z[f"nco_{j}"], rms
 
 

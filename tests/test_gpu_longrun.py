@@ -160,66 +160,92 @@ def test_config5_full_length_against_oracle(pkg, ctx):
     F = pkg.abi.FIELDS
     ints, nco = mg.field_rows(F)
     S = float(signal.Fs)
-    diverged, checked = {}, []
+    diverged, checked, problems = {}, [], []
     for zz in zs:
         for j, c in enumerate(zz["channels"]):
             c = int(c)
             checked.append(c)
-            n1 = N1 + int(zz["countinx"][j])
-            assert int(b.countinx[c]) == int(zz["countinx"][j]) and int(b.len[c]) == int(zz["len"][j])
-            _structure_checks(pkg, b, c, n1, N10)
-            L = int(b.len[c])
-            got = mg.distinct_steps(b.rec[c, :, :L], n1)
-            gtaps = mg.distinct_steps(b.taps[c, :, :, :L], n1)
-            iv, rtaps, rnco, rms = mg.expand(zz, j)
-            have = ~np.isnan(rtaps[:, :, 0])  # [2][11]: the taps this golden holds (lite: E / P / L)
-            # (1) where the GPU and the oracle part: a tap value off by more than 1e-8 of the RMS,
-            # or an integer field off
-            dev_t = np.where(have[:, :, None], np.abs(gtaps - np.nan_to_num(rtaps)) / rms, 0.0)
-            tap_off = (dev_t > 1e-8).any(axis=0)  # [11][steps]
-            int_off = np.zeros(got.shape[1], dtype=bool)
-            for k, i in enumerate(ints):
-                int_off |= got[i] != iv[k]
-            end = got.shape[1]  # steps compared strictly: all, or up to a loop tap's tie flip
-            for st in np.nonzero(tap_off.any(axis=0) | int_off)[0]:
-                # (2) every such step must be a tie flip: both runs' NCO states agree to rounding
-                # (the sums' summation order differs: tree vs sequential), and one sample's replica
-                # coordinate t lies on the GPU's side of an integer in one run and on the other side
-                # in the other -- ceil(t) differs for that sample alone. Integer fields may only
-                # part after a loop tap (E / P / L: taps 0 / 5 / 10) did.
-                assert st > 0, (c, "the first step cannot part: both runs start from the same state")
-                assert not int_off[st], (c, int(st), "integer field parted without a tie flip")
-                for t in np.nonzero(tap_off[:, st])[0]:
-                    assert _tie_flip(got, rnco, F, nco, st, float(taps[t]), S), (c, int(st), int(t))
-                if tap_off[[0, 5, 10], st].any():
-                    end = int(st) + 1  # the closed loop now runs on a (legitimately) different value
-                    diverged[c] = int(st)
-                    break
-            for k, i in enumerate(ints):
-                bad = np.nonzero(got[i, :end] != iv[k, :end])[0]
-                assert len(bad) == 0, (c, F[i], bad[:5])
-            keep = have[:, :, None] & ~tap_off[None, :, :end]  # (tie-flipped taps judged above)
-            ee = end if end == got.shape[1] else end - 1  # (E / P / L up to the loop tap's tie flip)
-            repl = np.stack([rtaps[k % 2, (5, 5, 0, 0, 10, 10)[k], :ee] for k in range(6)])
-            e_epl = np.max(np.abs(got[:6, :ee] - repl)) / rms
-            e_taps = np.max((np.abs(gtaps[:, :, :end] - np.nan_to_num(rtaps[:, :, :end])) / rms)[keep])
-            print(f"channel {c}: E/P/L max err / rms {e_epl:.2e}, taps {e_taps:.2e} (quantum 2e-9), "
-                  f"{int(tap_off[:, :end].any(axis=0).sum())} tie-flip steps, strict over {end} of {got.shape[1]} steps")
-            assert e_taps < 1e-8 and e_epl < 1e-8, (c, e_epl, e_taps)
-            assert np.allclose(got[nco][:, :ee], rnco[:, :ee], rtol=1e-7, atol=1e-9), c  # (the loop
-            # update of a tie-flip step in E / P / L already runs on the flipped sums)
-            ref_cn0 = zz[f"CN0_{j}"]
-            rows = len(ref_cn0) if end == got.shape[1] else max(0, (end - 1 - n1) // 20)
-            assert np.allclose(b.CN0[:rows, c], ref_cn0[:rows], rtol=0, atol=1e-6)
-            if end < got.shape[1]:  # (3) after the flip, to full length
-                lock = _post_flip_checks(pkg, b, c, got, iv, rtaps, rnco, F, ints, nco, n1, end - 1, ref_cn0,
-                                         float(zz[f"lock_{j}"]))
-                print(f"channel {c}: parted at step {end - 1} (tie flip in E/P/L); after it locked "
-                      f"{lock:.3f} (oracle {float(zz[f'lock_{j}']):.3f}), frequencies / offsets near the oracle's")
+            try:
+                _check_cfg5_channel(pkg, b, zz, j, c, N1, N10, mg, taps, F, ints, nco, S, diverged)
+            except AssertionError as e:  # (every channel is checked and reported before the verdict)
+                problems.append((c, repr(e)[:400]))
+                print(f"channel {c}: FAILED {repr(e)[:400]}")
     print(f"{len(checked)} channels checked; closed loops parted at a tie flip (channel: step): {diverged}")
+    assert not problems, problems
     assert set(diverged) <= set(CFG5_PARTED), diverged
     for c, st in diverged.items():
         assert st == CFG5_PARTED[c], (c, st)
+
+
+def _check_cfg5_channel(pkg, b, zz, j, c, N1, N10, mg, taps, F, ints, nco, S, diverged):
+    """One golden channel of test_config5_full_length_against_oracle (its docstring)."""
+    n1 = N1 + int(zz["countinx"][j])
+    assert int(b.countinx[c]) == int(zz["countinx"][j]) and int(b.len[c]) == int(zz["len"][j])
+    _structure_checks(pkg, b, c, n1, N10)
+    L = int(b.len[c])
+    got = mg.distinct_steps(b.rec[c, :, :L], n1)
+    gtaps = mg.distinct_steps(b.taps[c, :, :, :L], n1)
+    iv, rtaps, rnco, rms = mg.expand(zz, j)
+    have = ~np.isnan(rtaps[:, :, 0])  # [2][11]: the taps this golden holds (lite: E / P / L)
+    # (1) where the GPU and the oracle part: a tap value off by more than 1e-8 of the RMS,
+    # or an integer field off
+    dev_t = np.where(have[:, :, None], np.abs(gtaps - np.nan_to_num(rtaps)) / rms, 0.0)
+    tap_off = (dev_t > 1e-8).any(axis=0)  # [11][steps]
+    int_off = np.zeros(got.shape[1], dtype=bool)
+    for k, i in enumerate(ints):
+        int_off |= got[i] != iv[k]
+    end = got.shape[1]  # steps compared strictly: all, or up to a loop tap's tie flip
+    for st in np.nonzero(tap_off.any(axis=0) | int_off)[0]:
+        # (2) every such step must be a tie flip: both runs' NCO states agree to rounding
+        # (the sums' summation order differs: tree vs sequential), and one sample's replica
+        # coordinate t lies on the GPU's side of an integer in one run and on the other side
+        # in the other -- ceil(t) differs for that sample alone. Integer fields may only
+        # part after a loop tap (E / P / L: taps 0 / 5 / 10) did.
+        assert st > 0, (c, "the first step cannot part: both runs start from the same state")
+        assert not int_off[st], (c, int(st), "integer field parted without a tie flip")
+        for t in np.nonzero(tap_off[:, st])[0]:
+            assert _tie_flip(got, rnco, F, nco, st, float(taps[t]), S), (
+                c, int(st), int(t), "no tie flip found; nearest-integer distance (GPU, oracle state):",
+                _tie_margin(got, rnco, F, nco, st, float(taps[t]), S))
+        if tap_off[[0, 5, 10], st].any():
+            end = int(st) + 1  # the closed loop now runs on a (legitimately) different value
+            diverged[c] = int(st)
+            break
+    for k, i in enumerate(ints):
+        bad = np.nonzero(got[i, :end] != iv[k, :end])[0]
+        assert len(bad) == 0, (c, F[i], bad[:5])
+    keep = have[:, :, None] & ~tap_off[None, :, :end]  # (tie-flipped taps judged above)
+    ee = end if end == got.shape[1] else end - 1  # (E / P / L up to the loop tap's tie flip)
+    repl = np.stack([rtaps[k % 2, (5, 5, 0, 0, 10, 10)[k], :ee] for k in range(6)])
+    e_epl = np.max(np.abs(got[:6, :ee] - repl)) / rms
+    e_taps = np.max((np.abs(gtaps[:, :, :end] - np.nan_to_num(rtaps[:, :, :end])) / rms)[keep])
+    print(f"channel {c}: E/P/L max err / rms {e_epl:.2e}, taps {e_taps:.2e} (quantum 2e-9), "
+          f"{int(tap_off[:, :end].any(axis=0).sum())} tie-flip steps, strict over {end} of {got.shape[1]} steps")
+    assert e_taps < 1e-8 and e_epl < 1e-8, (c, e_epl, e_taps)
+    assert np.allclose(got[nco][:, :ee], rnco[:, :ee], rtol=1e-7, atol=1e-9), c  # (the loop
+    # update of a tie-flip step in E / P / L already runs on the flipped sums)
+    ref_cn0 = zz[f"CN0_{j}"]
+    rows = len(ref_cn0) if end == got.shape[1] else max(0, (end - 1 - n1) // 20)
+    assert np.allclose(b.CN0[:rows, c], ref_cn0[:rows], rtol=0, atol=1e-6)
+    if end < got.shape[1]:  # (3) after the flip, to full length
+        lock = _post_flip_checks(pkg, b, c, got, iv, rtaps, rnco, F, ints, nco, n1, end - 1, ref_cn0,
+                                 float(zz[f"lock_{j}"]))
+        print(f"channel {c}: parted at step {end - 1} (tie flip in E/P/L); after it locked "
+              f"{lock:.3f} (oracle {float(zz[f'lock_{j}']):.3f}), frequencies / offsets near the oracle's")
+
+
+def _tie_margin(got, rnco, F, nco, st, tap, Fs):
+    """(diagnostic for a failed _tie_flip) the smallest |t - round(t)| over the step's samples from
+    the GPU's state and from the oracle's, and how many samples take a different chip."""
+    ir, icf, ins = F.index("remChip"), F.index("codeFreq"), F.index("numSample")
+    n = int(got[ins, st])
+    out = []
+    for rc, cf in ((got[ir, st - 1], got[icf, st - 1]), (rnco[nco.index(ir), st - 1], rnco[nco.index(icf), st - 1])):
+        t = (tap + rc) + np.arange(n) * (cf / Fs)
+        out.append(float(np.min(np.abs(t - np.round(t)))))
+        out.append(t)
+    nd = int(np.sum(np.ceil(out[1]) != np.ceil(out[3]))) if len(out[1]) == len(out[3]) else -1
+    return out[0], out[2], nd
 
 
 def _tie_flip(got, rnco, F, nco, st, tap, Fs):
