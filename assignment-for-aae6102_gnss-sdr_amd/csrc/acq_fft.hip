@@ -1020,13 +1020,17 @@ __global__ void fine_twiddle_kernel(double2* __restrict__ t, int64_t len, int64_
     t[x] = make_double2(c, s);
 }
 
+// (blockIdx.z = the SV of a batched launch: its code delay, code table and transform slab)
 template <int P, class Src>
 __global__ __launch_bounds__(kRowThreads) void fine_rows_kernel(
-    const Src src, int64_t base, const float* __restrict__ ca, double invFs,
+    const Src src, const int32_t* __restrict__ cd, int64_t S, const float* __restrict__ ca0, double invFs,
     double invFc, double codelength, int D, int64_t N, const double2* __restrict__ tw_row,
-    const double2* __restrict__ tabA, const double2* __restrict__ tabB, double2* __restrict__ E)
+    const double2* __restrict__ tabA, const double2* __restrict__ tabB, double2* __restrict__ E0)
 {
     constexpr int T = kFineT;
+    const int64_t base = S - cd[blockIdx.z] - 1;  // 0-based sample of CarrSignal(1) (acquisition.m:105)
+    const float* ca = ca0 + (int64_t)blockIdx.z * 1023;
+    double2* E = E0 + (int64_t)blockIdx.z * N;
     // twiddles read from the (L2-resident) global table: 32 KB of LDS per block instead of
     // 64, five blocks per CU instead of two
     __shared__ double2 s_a[kRowPad];
@@ -1062,10 +1066,12 @@ __device__ __forceinline__ void best_merge(double& m, int64_t& i, double m2, int
 
 template <int P>
 __global__ __launch_bounds__(kColThreads) void fine_cols_kernel(
-    const double2* __restrict__ E, int D, int64_t N, int shifted, const double2* __restrict__ tabK,
-    const double2* __restrict__ tabS, FineBest* __restrict__ part)
+    const double2* __restrict__ E0, int D, int64_t N, int shifted, const double2* __restrict__ tabK,
+    const double2* __restrict__ tabS, FineBest* __restrict__ part0)
 {
     constexpr int T = kFineT, JC = kFineJC;
+    const double2* E = E0 + (int64_t)blockIdx.z * N;
+    FineBest* part = part0 + (int64_t)blockIdx.z * gridDim.x * gridDim.y;
     // 29 x 10 x 16 x 16 B = 74 KB of LDS: two blocks per CU on gfx950's 160 KiB (above the
     // 64 KiB per-workgroup limit of earlier gfx9 parts; this file is built for gfx950 only)
     static_assert(P * T * JC * sizeof(double2) + (kColThreads / 64) * sizeof(double) * 2 <= 80 * 1024,
@@ -1128,9 +1134,11 @@ __global__ __launch_bounds__(kColThreads) void fine_cols_kernel(
     }
 }
 
-__global__ void fine_best_final_kernel(const FineBest* __restrict__ part, int nblk,
-                                       int64_t* __restrict__ kbest)
+__global__ void fine_best_final_kernel(const FineBest* __restrict__ part0, int nblk,
+                                       int64_t* __restrict__ kbest0)
 {
+    const FineBest* part = part0 + (int64_t)blockIdx.x * nblk;  // (one block per SV)
+    int64_t* kbest = kbest0 + blockIdx.x;
     double bm = -1.0;
     int64_t bi = INT64_MAX;
     for (int k = threadIdx.x; k < nblk; k += blockDim.x) best_merge(bm, bi, part[k].m, part[k].i);
@@ -1298,20 +1306,35 @@ hipError_t launch_acq_fft_correlate_fused(const double2* C, const double2* X, in
 
 bool fine_fft_supported(int64_t S, int L) { return acq_fft_supported(S) && L == kFineT; }
 
-size_t fine_fft_scratch_bytes(int64_t S, int L, int datalen)
+// Scratch of the fine search: the twiddle tables, then per SV of a batch its N-point slab of
+// transform values and its column blocks' arg-max candidates.
+namespace {
+struct FineLayout {
+    int64_t M, N, tabs, slab, part;  // element counts (double2) / offsets
+};
+FineLayout fine_layout(int64_t S, int L, int datalen)
 {
-    const int64_t M = (int64_t)L * S;
-    return sizeof(double2) * (size_t)(M * datalen + kRow + (int64_t)kRow * datalen +
-                                      (int64_t)kFineT * kRow + M) +
-           sizeof(FineBest) * (size_t)datalen * (kRow / kFineJC);
+    FineLayout f;
+    f.M = (int64_t)L * S;
+    f.N = f.M * datalen;
+    f.tabs = kRow + (int64_t)kRow * datalen + (int64_t)kFineT * kRow + S + f.M / kRow;
+    f.slab = f.N;
+    f.part = (int64_t)datalen * (kRow / kFineJC);  // FineBest entries per SV
+    return f;
+}
+}  // namespace
+
+size_t fine_fft_scratch_bytes(int64_t S, int L, int datalen, int nsv)
+{
+    const FineLayout f = fine_layout(S, L, datalen);
+    return sizeof(double2) * (size_t)(f.tabs + (int64_t)nsv * f.slab) + sizeof(FineBest) * (size_t)(nsv * f.part);
 }
 
 // Twiddle tables of the fine search, once per call: w_2000, w_{2000*D}, w_{T*2000}, w_M, w_{P*T}.
 hipError_t launch_fine_fft_tables(int64_t S, int L, int datalen, void* scratch, hipStream_t s)
 {
     const int64_t M = (int64_t)L * S;
-    double2* E = static_cast<double2*>(scratch);
-    double2* tw_row = E + M * datalen;
+    double2* tw_row = static_cast<double2*>(scratch);
     double2* tabA = tw_row + kRow;
     double2* tabB = tabA + (int64_t)kRow * datalen;
     double2* tabK = tabB + (int64_t)kFineT * kRow;  // [P][2000] w_M^(-n2*k), then w_{P*T}
@@ -1329,34 +1352,37 @@ hipError_t launch_fine_fft_tables(int64_t S, int L, int datalen, void* scratch, 
     return hipGetLastError();
 }
 
-// First fftshift-ed argmax (1-based) of |fft(CarrSignal, N)| for one SV (acquisition.m:103-116).
-hipError_t launch_fine_fft_argmax(const int8_t* iq, const double2* xs, int64_t S, int L, int datalen, int64_t base,
-                                  const float* ca, double Fs, double codeFreqBasis,
-                                  double codelength, int shifted, void* scratch, int64_t* kbest,
-                                  hipStream_t s)
+// First fftshift-ed argmax (1-based) of |fft(CarrSignal, N)| for nsv SVs in one batch of
+// launches (acquisition.m:103-116): SV k's code delay cd[k] (device), its code table
+// ca + 1023 k, its result kbest[k]. Every SV's arithmetic is the one-SV launch's.
+hipError_t launch_fine_fft_argmax(const int8_t* iq, const double2* xs, int64_t S, int L, int datalen,
+                                  const int32_t* cd, int nsv, const float* ca, double Fs, double codeFreqBasis,
+                                  double codelength, int shifted, void* scratch, int64_t* kbest, hipStream_t s)
 {
-    const int64_t M = (int64_t)L * S, N = M * datalen;
-    double2* E = static_cast<double2*>(scratch);
-    double2* tw_row = E + M * datalen;
+    if (nsv < 1 || nsv > 65535) return hipErrorInvalidValue;
+    const FineLayout f = fine_layout(S, L, datalen);
+    const int64_t N = f.N;
+    double2* tw_row = static_cast<double2*>(scratch);
     double2* tabA = tw_row + kRow;
     double2* tabB = tabA + (int64_t)kRow * datalen;
     double2* tabK = tabB + (int64_t)kFineT * kRow;
     double2* tabS = tabK + S;
-    FineBest* part = reinterpret_cast<FineBest*>(tabK + M);  // (tabK + tabS < M entries)
+    double2* E = tw_row + f.tabs;
+    FineBest* part = reinterpret_cast<FineBest*>(E + (int64_t)nsv * f.slab);
     const int nblk = kRow / kFineJC;
 #define GNSS_FINE(P_)                                                                           \
     if (S == (int64_t)P_ * kRow) {                                                              \
         if (xs)                                                                                 \
-            hipLaunchKernelGGL((fine_rows_kernel<P_, SrcC64>), dim3(P_ * kFineT, datalen), dim3(kRowThreads), \
-                               0, s, SrcC64{xs}, base, ca, 1 / Fs, 1 / codeFreqBasis, codelength, datalen, N, \
+            hipLaunchKernelGGL((fine_rows_kernel<P_, SrcC64>), dim3(P_ * kFineT, datalen, nsv), dim3(kRowThreads), \
+                               0, s, SrcC64{xs}, cd, S, ca, 1 / Fs, 1 / codeFreqBasis, codelength, datalen, N, \
                                tw_row, tabA, tabB, E);                                          \
         else                                                                                    \
-            hipLaunchKernelGGL((fine_rows_kernel<P_, SrcIQ8>), dim3(P_ * kFineT, datalen), dim3(kRowThreads), \
-                               0, s, SrcIQ8{iq}, base, ca, 1 / Fs, 1 / codeFreqBasis, codelength, datalen, N, \
+            hipLaunchKernelGGL((fine_rows_kernel<P_, SrcIQ8>), dim3(P_ * kFineT, datalen, nsv), dim3(kRowThreads), \
+                               0, s, SrcIQ8{iq}, cd, S, ca, 1 / Fs, 1 / codeFreqBasis, codelength, datalen, N, \
                                tw_row, tabA, tabB, E);                                          \
-        hipLaunchKernelGGL(fine_cols_kernel<P_>, dim3(nblk, datalen), dim3(kColThreads), 0, s, E, \
+        hipLaunchKernelGGL(fine_cols_kernel<P_>, dim3(nblk, datalen, nsv), dim3(kColThreads), 0, s, E, \
                            datalen, N, shifted, tabK, tabS, part);                                    \
-        hipLaunchKernelGGL(fine_best_final_kernel, dim3(1), dim3(256), 0, s, part, nblk * datalen, \
+        hipLaunchKernelGGL(fine_best_final_kernel, dim3(nsv), dim3(256), 0, s, part, nblk * datalen, \
                            kbest);                                                              \
         return hipGetLastError();                                                               \
     }

@@ -78,6 +78,8 @@ namespace {
 constexpr int kAcqPipeDefault = 2;
 // the paired launch's row blocks sit in the grid's first kAcqPairFront percent (acq_fft.hip)
 constexpr int kAcqPairFront = 60;
+// SVs per launch of the fine-frequency search (scratch ~186 MB per SV at config 2)
+constexpr int kFineBatch = 16;
 
 // The context's pinned host buffer `key`, at least `bytes` (contents undefined).
 template <class T>
@@ -1138,15 +1140,17 @@ int gnss_acquisition(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     const bool own_fine = fine_fft_supported(S, L) && !ctx->opt[GNSS_OPT_FINE_ROCFFT];
     Events e_fine;
     if (own_fine) {
-        // per-SV zero-padded FFT as datalen three-level transforms (acq_fft.hip)
-        HIP_TRY(fx.alloc(ctx, "acq.fx", fine_fft_scratch_bytes(S, L, dl)));
+        // per-SV zero-padded FFT as datalen three-level transforms (acq_fft.hip), up to
+        // kFineBatch SVs per launch (each SV's N-point slab, 186 MB at config 2, in one scratch)
+        const int fb = std::min(na, kFineBatch);
+        HIP_TRY(fx.alloc(ctx, "acq.fx", fine_fft_scratch_bytes(S, L, dl, fb)));
         HIP_TRY(hipEventRecord(e_fine.a, ctx->stream));
         HIP_TRY(launch_fine_fft_tables(S, L, dl, fx.p, ctx->stream));
-        for (int k = 0; k < na; k++) {
-            const int64_t base = S - cdh[k] - 1;  // 0-based sample of CarrSignal(1) (:105)
-            HIP_TRY(launch_fine_fft_argmax(blk, xf, S, L, dl, base, fca.as<float>() + (size_t)k * 1023, sg->Fs,
-                                           sg->codeFreqBasis, sg->codelength, fshift, fx.p,
-                                           kb.as<int64_t>() + k, ctx->stream));
+        for (int k0 = 0; k0 < na; k0 += fb) {
+            const int nk = std::min(fb, na - k0);
+            HIP_TRY(launch_fine_fft_argmax(blk, xf, S, L, dl, fcd.as<int32_t>() + k0, nk,
+                                           fca.as<float>() + (size_t)k0 * 1023, sg->Fs, sg->codeFreqBasis,
+                                           sg->codelength, fshift, fx.p, kb.as<int64_t>() + k0, ctx->stream));
         }
     } else {
         HIP_TRY(fx.alloc(ctx, "acq.fx", sizeof(double2) * (size_t)na * N));

@@ -441,12 +441,13 @@ hipError_t launch_acq_fft_correlate_fused(const double2* C, const double2* X, in
                                           int nprn, int nslot, const double2* tw_row, const double2* tw_col,
                                           double2* ring, void* sync, double* corr, hipStream_t s);
 bool fine_fft_supported(int64_t S, int L);
-size_t fine_fft_scratch_bytes(int64_t S, int L, int datalen);
+// (a batch of nsv SVs per launch: scratch for nsv, SV k's code delay cd[k] on the device, its
+// code table ca + 1023 k, its 1-based arg-max kbest[k])
+size_t fine_fft_scratch_bytes(int64_t S, int L, int datalen, int nsv);
 hipError_t launch_fine_fft_tables(int64_t S, int L, int datalen, void* scratch, hipStream_t s);
-hipError_t launch_fine_fft_argmax(const int8_t* iq, const double2* xs, int64_t S, int L, int datalen, int64_t base,
-                                  const float* ca, double Fs, double codeFreqBasis,
-                                  double codelength, int shifted, void* scratch, int64_t* kbest,
-                                  hipStream_t s);
+hipError_t launch_fine_fft_argmax(const int8_t* iq, const double2* xs, int64_t S, int L, int datalen,
+                                  const int32_t* cd, int nsv, const float* ca, double Fs, double codeFreqBasis,
+                                  double codelength, int shifted, void* scratch, int64_t* kbest, hipStream_t s);
 hipError_t launch_fine_build(const int8_t* iq, const double2* xs, int64_t S, int L, const int32_t* codedelay,
                              const float* ca, int nsv, double Fs, double codeFreqBasis,
                              double codelength, int64_t N, double2* out, hipStream_t s);
