@@ -1464,6 +1464,10 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
         const int v = atoi(fs);
         if (v >= 1 && v <= 4 && sub_ok(v) && P.fmt == 0 && ntaps != 25) sub10 = v;
     }
+    if (const char* fs = probe_env("GNSS_FORCE_SUB1")) {  // probe hook: the 1-ms lane span alone
+        const int v = atoi(fs);
+        if (v >= 1 && v <= 4 && sub_ok(v) && P.fmt == 0 && ntaps != 25) sub1 = v;
+    }
     if (const int v = (int)ctx->opt[GNSS_OPT_FORCE_SUB]) {  // test hook: exercise every kernel variant
         if (v >= 1 && v <= 4 && sub_ok(v) && ((P.fmt == 0 && ntaps != 25) || v == 1 || v == 3)) sub1 = sub10 = v;
     }

@@ -1117,7 +1117,8 @@ template <int NT> constexpr int red_words() { return 2 * red_taps<NT>() * (kTrkT
 // slower (block partial 0.48 -> 0.68 us; 10-ms launch 36.8-37.0 -> 37.8-38.0 ms at 3 taps,
 // 203 -> 217 ms at 32 channels x 11 taps; profiles/r05_ab_block_tree.txt). A different order
 // also moves the last bits, so the full-length goldens' tie flips move (config 3 channel 5
-// parts at step 3 944 with it).
+// parts at step 3 944 with it). GNSS_RED 2 combines the rows by DPP broadcasts instead of
+// lane reads (same bits as 1): +1 % at 3 taps, equal at 11.
 #ifndef GNSS_RED
 #define GNSS_RED 0
 #endif
@@ -1130,9 +1131,31 @@ __device__ __forceinline__ double readlane_f64(double v, int l)
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
+// a double moved across lanes by a DPP control with a row mask; lanes of disabled rows get 0
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_f64_rows(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROWS, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWS, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 // one value's sum over the wave's 64 lanes in the fixed order above (every lane active)
 __device__ __forceinline__ double wave_sum(double a)
 {
+    if constexpr (GNSS_RED == 2) {
+        // (GNSS_RED 2: the rows combined by DPP broadcasts instead of lane reads -- row 1 +=
+        // row 0 and row 3 += row 2 (row_bcast:15), then rows 2, 3 += row 1 (row_bcast:31): lane
+        // 63 ends with (r3 + r2) + (r1 + r0); the other lanes' values are not used)
+        a += dpp_f64<0xB1>(a);
+        a += dpp_f64<0x4E>(a);
+        a += dpp_f64<0x141>(a);
+        a += dpp_f64<0x140>(a);
+        a += dpp_f64_rows<0x142, 0xA>(a);
+        a += dpp_f64_rows<0x143, 0xC>(a);
+        return a;
+    }
     a += dpp_f64<0xB1>(a);   // quad_perm [1,0,3,2]
     a += dpp_f64<0x4E>(a);   // quad_perm [2,3,0,1]
     a += dpp_f64<0x141>(a);  // row_half_mirror: the other quad of the 8
@@ -1154,7 +1177,7 @@ __device__ __forceinline__ double block_tree(double* s_mem, const double (&oI)[N
     for (int s = 0; s < NT; s++) {
         if ((sel >> s) & 1u) {  // (sel uniform)
             const double si = wave_sum(oI[s]), sq = wave_sum(oQ[s]);
-            if (lane == 0) {
+            if (lane == (GNSS_RED == 2 ? 63 : 0)) {
                 ws[wv * NV + 2 * w] = si;
                 ws[wv * NV + 2 * w + 1] = sq;
             }
