@@ -321,14 +321,33 @@ __device__ __forceinline__ V tw_get(const TwIK<V>& tw, int i, int k, int m)
     return NS == 20 ? tw.t2[(i - 1) * 20 + k] : tw.t3[(i - 1) * 200 + k];
 }
 constexpr int kTwIK = 9 * 20 + 9 * 200;  // entries of the split layout
+// (every load of the block's prologue issued before the first LDS store: a loop of load ->
+// wait -> store paid one L2 round trip per iteration, 8 per table, GNSS_STAGED_LOADS 0)
+#ifndef GNSS_STAGED_LOADS
+#define GNSS_STAGED_LOADS 1
+#endif
 template <class V>
 __device__ __forceinline__ TwIK<V> load_row_tw_ik(V* s_t, const V* tw_row, int tid)
 {
-    for (int e = tid; e < kTwIK; e += kRowThreads) {
+    auto src = [&](int e) {
         const bool t2 = e < 9 * 20;
         const int f = t2 ? e : e - 9 * 20;
         const int i = t2 ? f / 20 + 1 : f / 200 + 1, k = t2 ? f % 20 : f % 200;
-        s_t[e] = tw_row[t2 ? 10 * i * k : i * k];
+        return t2 ? 10 * i * k : i * k;
+    };
+    if constexpr (GNSS_STAGED_LOADS) {
+        constexpr int NIT = (kTwIK + kRowThreads - 1) / kRowThreads;
+        V r[NIT];
+#pragma unroll
+        for (int q = 0; q < NIT; q++) {
+            const int e0 = tid + q * kRowThreads;
+            r[q] = tw_row[src(e0 < kTwIK ? e0 : kTwIK - 1)];
+        }
+#pragma unroll
+        for (int q = 0; q < NIT; q++)
+            if (tid + q * kRowThreads < kTwIK) s_t[tid + q * kRowThreads] = r[q];
+    } else {
+        for (int e = tid; e < kTwIK; e += kRowThreads) s_t[e] = tw_row[src(e)];
     }
     return TwIK<V>{s_t, s_t + 9 * 20};
 }
@@ -471,10 +490,11 @@ __global__ __launch_bounds__(kRowThreads) void fwd_rows_kernel(
     __shared__ V s_a[kRowPad], s_tw[kTwIK];
     const int n2 = blockIdx.x, s = blockIdx.y, tid = threadIdx.x;
     const TwIK<V> twk = load_row_tw_ik(s_tw, tw_row, tid);
+    constexpr int NIT = (kRow + kRowThreads - 1) / kRowThreads;
     if (s < nsig) {
         const int idx = s / nbins, bin = s - idx * nbins;
         const double f = (IF + (freqMin + freqStep * (double)bin)) / Fs;  // cycles per sample
-        for (int n1 = tid; n1 < kRow; n1 += kRowThreads) {
+        auto put = [&](int n1, double2 r) {
             const int64_t n = (int64_t)P * n1 + n2;
             double cyc = f * (double)(n + 1);  // n is 1-based in the reference
             cyc -= floor(cyc);
@@ -486,16 +506,41 @@ __global__ __launch_bounds__(kRowThreads) void fwd_rows_kernel(
             } else {
                 sincospi(2.0 * cyc, &sn, &c);
             }
-            const double2 r = src.at((int64_t)idx * S + n);
             const R xr = (R)r.x, xi = (R)r.y;
             s_a[n1] = mk<V>(fma2(xr, c, -(xi * sn)), fma2(xr, sn, xi * c));
+        };
+        if constexpr (GNSS_STAGED_LOADS) {
+            double2 raw[NIT];
+#pragma unroll
+            for (int q = 0; q < NIT; q++) {
+                const int m0 = tid + q * kRowThreads, n1 = m0 < kRow ? m0 : kRow - 1;
+                raw[q] = src.at((int64_t)idx * S + (int64_t)P * n1 + n2);
+            }
+#pragma unroll
+            for (int q = 0; q < NIT; q++)
+                if (tid + q * kRowThreads < kRow) put(tid + q * kRowThreads, raw[q]);
+        } else {
+            for (int n1 = tid; n1 < kRow; n1 += kRowThreads) put(n1, src.at((int64_t)idx * S + (int64_t)P * n1 + n2));
         }
     } else {
         const float* cp = ca + (int64_t)(s - nsig) * 1023;
-        for (int n1 = tid; n1 < kRow; n1 += kRowThreads) {
+        auto chip = [&](int n1) {
             const int64_t n = (int64_t)P * n1 + n2;
             const int64_t ci = (int64_t)ceil((double)(n + 1) * code_step);  // 1-based into [CA CA]
-            s_a[n1] = mk<V>((R)cp[(ci - 1) % 1023], (R)0);
+            return (ci - 1) % 1023;
+        };
+        if constexpr (GNSS_STAGED_LOADS) {
+            float cv[NIT];
+#pragma unroll
+            for (int q = 0; q < NIT; q++) {
+                const int m0 = tid + q * kRowThreads;
+                cv[q] = cp[chip(m0 < kRow ? m0 : kRow - 1)];
+            }
+#pragma unroll
+            for (int q = 0; q < NIT; q++)
+                if (tid + q * kRowThreads < kRow) s_a[tid + q * kRowThreads] = mk<V>((R)cv[q], (R)0);
+        } else {
+            for (int n1 = tid; n1 < kRow; n1 += kRowThreads) s_a[n1] = mk<V>((R)cp[chip(n1)], (R)0);
         }
     }
     __syncthreads();
@@ -1036,13 +1081,38 @@ __global__ __launch_bounds__(kRowThreads) void fine_rows_kernel(
     __shared__ double2 s_a[kRowPad];
     const int rho = blockIdx.x, r = blockIdx.y, tid = threadIdx.x;
     const int m2 = rho / P, n2 = rho - m2 * P;
-    for (int m1 = tid; m1 < kRow; m1 += kRowThreads) {
-        const int64_t n = (int64_t)P * T * m1 + (int64_t)P * m2 + n2;
+    auto sample = [&](int m1) { return (int64_t)P * T * m1 + (int64_t)P * m2 + n2; };
+    auto code_of = [&](int64_t n) {
         const double cvi = floor((invFs * (double)(n + 1)) / invFc);
-        const double code = (double)ca[(int64_t)fmod(cvi, codelength)];
-        const double2 raw = src.at(base + n);
-        const double2 x = make_double2(raw.x * code, raw.y * code);
-        s_a[m1] = cmul(x, tabA[(int64_t)r * kRow + m1]);  // w_RD^(-m1*r), [r][m1]: coalesced
+        return (int64_t)fmod(cvi, codelength);
+    };
+    if constexpr (GNSS_STAGED_LOADS) {
+        constexpr int NIT = (kRow + kRowThreads - 1) / kRowThreads;
+        double2 raw[NIT], ta[NIT];
+        float cv[NIT];
+#pragma unroll
+        for (int q = 0; q < NIT; q++) {
+            const int m10 = tid + q * kRowThreads, m1 = m10 < kRow ? m10 : kRow - 1;
+            const int64_t n = sample(m1);
+            cv[q] = ca[code_of(n)];
+            raw[q] = src.at(base + n);
+            ta[q] = tabA[(int64_t)r * kRow + m1];
+        }
+#pragma unroll
+        for (int q = 0; q < NIT; q++) {
+            const int m1 = tid + q * kRowThreads;
+            const double code = (double)cv[q];
+            const double2 x = make_double2(raw[q].x * code, raw[q].y * code);
+            if (m1 < kRow) s_a[m1] = cmul(x, ta[q]);  // w_RD^(-m1*r), [r][m1]: coalesced
+        }
+    } else {
+        for (int m1 = tid; m1 < kRow; m1 += kRowThreads) {
+            const int64_t n = sample(m1);
+            const double code = (double)ca[code_of(n)];
+            const double2 raw = src.at(base + n);
+            const double2 x = make_double2(raw.x * code, raw.y * code);
+            s_a[m1] = cmul(x, tabA[(int64_t)r * kRow + m1]);  // w_RD^(-m1*r), [r][m1]: coalesced
+        }
     }
     __syncthreads();
     double sn, cs;
@@ -1079,9 +1149,23 @@ __global__ __launch_bounds__(kColThreads) void fine_cols_kernel(
     __shared__ double2 s_e[P * T * JC];  // [n2][m2 -> j2][jj]
     __shared__ FineBest s_b[kColThreads / 64];
     const int r = blockIdx.y, j10 = blockIdx.x * JC, tid = threadIdx.x;
-    for (int e = tid; e < P * T * JC; e += kColThreads) {
+    auto at = [&](int e) {
         const int jj = e % JC, nm = e / JC;  // nm = n2*T + m2
-        s_e[e] = E[((int64_t)r * P * T + nm) * kRow + j10 + jj];
+        return E + ((int64_t)r * P * T + nm) * kRow + j10 + jj;
+    };
+    if constexpr (GNSS_STAGED_LOADS) {
+        constexpr int NE = P * T * JC, NIT = (NE + kColThreads - 1) / kColThreads;
+        double2 st[NIT];
+#pragma unroll
+        for (int q = 0; q < NIT; q++) {
+            const int e0 = tid + q * kColThreads;
+            st[q] = *at(e0 < NE ? e0 : NE - 1);
+        }
+#pragma unroll
+        for (int q = 0; q < NIT; q++)
+            if (tid + q * kColThreads < NE) s_e[tid + q * kColThreads] = st[q];
+    } else {
+        for (int e = tid; e < P * T * JC; e += kColThreads) s_e[e] = *at(e);
     }
     __syncthreads();
     // DFT_T over m2 for each (n2, jj), twiddle w_M^(-n2*k1), k1 = k + 2000*j2:
