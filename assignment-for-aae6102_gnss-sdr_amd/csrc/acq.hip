@@ -132,10 +132,6 @@ __device__ __forceinline__ int64_t natural_col(int64_t k, int perm)
     return perm ? k / 2000 + (int64_t)perm * (k % 2000) : k;
 }
 
-__device__ __forceinline__ int64_t storage_of(int64_t col, int perm)
-{
-    return perm ? (col % perm) * 2000 + col / perm : col;
-}
 
 template <class R>
 __global__ void acq_peak_part_kernel(const R* __restrict__ corr, int nbins, int64_t S,
@@ -145,10 +141,20 @@ __global__ void acq_peak_part_kernel(const R* __restrict__ corr, int nbins, int6
     const R* c = corr + (int64_t)p * nbins * S;
     R m = (R)-1;
     int bin = 0x7fffffff, col = 0x7fffffff;
-    for (int b = 0; b < nbins; b++)
-        for (int64_t k = (int64_t)blk * blockDim.x + threadIdx.x; k < S;
-             k += (int64_t)nblk * blockDim.x)
-            peak_merge(m, bin, col, c[(int64_t)b * S + k], b, (int)natural_col(k, perm));
+    // (a column's bins loaded 8 at a time before they are merged: the merge keeps the maximum
+    // with the lowest bin / column on ties, so its order does not matter; one load per merge
+    // waited for each L2 round trip)
+    for (int64_t k = (int64_t)blk * blockDim.x + threadIdx.x; k < S; k += (int64_t)nblk * blockDim.x) {
+        const int ck = (int)natural_col(k, perm);
+        for (int b0 = 0; b0 < nbins; b0 += 8) {
+            R v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = c[(int64_t)(b0 + u < nbins ? b0 + u : nbins - 1) * S + k];
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (b0 + u < nbins) peak_merge(m, bin, col, v[u], b0 + u, ck);
+        }
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const R m2 = __shfl_xor(m, o, 64);
@@ -190,13 +196,16 @@ __global__ void acq_peak_final_kernel(const R* __restrict__ corr, int nbins, int
     const int64_t cp1 = (int64_t)s_col + 1;  // 1-based codePhase
     const R* row = corr + ((int64_t)p * nbins + fbin) * S;
     double sum = 0, cnt = 0, mx = 0;
-    for (int64_t k = threadIdx.x + 1; k <= S; k += blockDim.x) {
-        if (k <= cp1 - cshift || k >= cp1 + cshift) {
-            const double v = (double)row[storage_of(k - 1, perm)];
-            sum += v * v;
-            cnt += 1;
-            mx = fmax(mx, v);
-        }
+    // in storage order (coalesced; the permuted surface's natural order strides 2 000 entries
+    // across a wave), 8 loads in flight
+#pragma unroll 8
+    for (int64_t q = threadIdx.x; q < S; q += blockDim.x) {
+        const int64_t k = natural_col(q, perm) + 1;  // 1-based column
+        const double v = (double)row[q];
+        const bool off = k <= cp1 - cshift || k >= cp1 + cshift;
+        sum += off ? v * v : 0.0;  // (+0.0 leaves a non-negative sum unchanged)
+        cnt += off ? 1.0 : 0.0;
+        mx = off ? fmax(mx, v) : mx;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
