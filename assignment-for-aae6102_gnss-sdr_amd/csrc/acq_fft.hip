@@ -479,16 +479,30 @@ __device__ __forceinline__ void load_row_tw(V* s_tw, const V* tw_row, int tid)
 // ---- F1: forward rows. Transform s < nsig: rawsignal(ms) .* carrier(bin) (acquisition.m:41-44,56);
 // s >= nsig: the code replica of PRN s - nsig (acquisition.m:49-51). Row n2 holds
 // x[P*n1 + n2]; output B[s][n2][k1] * w_S^(-n2*k1).
+// The forward transforms of one launch: the nprn code transforms first when `codes`, then the
+// signal transforms of bins [bin0, bin0 + nbc) of every ms (the whole pass: bin0 = 0, nbc = nbins);
+// launch-local index y -> transform s (s = ms * nbins + bin for signals, nsig + p for codes).
+struct FwdSet {
+    int nbins, nsig, nprn, bin0, nbc, codes;
+    __device__ __forceinline__ int transform(int y) const
+    {
+        if (codes && y < nprn) return nsig + y;
+        const int u = y - (codes ? nprn : 0), idx = u / nbc;
+        return idx * nbins + bin0 + (u - idx * nbc);
+    }
+};
+
 template <int P, class Src, class V>
 __global__ __launch_bounds__(kRowThreads) void fwd_rows_kernel(
-    const Src src, int nbins, int nsig, double IF, double freqMin, double freqStep,
+    const Src src, FwdSet fs, double IF, double freqMin, double freqStep,
     double Fs, const float* __restrict__ ca, double code_step, const V* __restrict__ tw_row,
     const V* __restrict__ tw_col, V* __restrict__ B)
 {
     using R = Re<V>;
     constexpr int64_t S = (int64_t)P * kRow;
     __shared__ V s_a[kRowPad], s_tw[kTwIK];
-    const int n2 = blockIdx.x, s = blockIdx.y, tid = threadIdx.x;
+    const int nbins = fs.nbins, nsig = fs.nsig;
+    const int n2 = blockIdx.x, s = fs.transform(blockIdx.y), tid = threadIdx.x;
     const TwIK<V> twk = load_row_tw_ik(s_tw, tw_row, tid);
     constexpr int NIT = (kRow + kRowThreads - 1) / kRowThreads;
     if (s < nsig) {
@@ -551,9 +565,9 @@ __global__ __launch_bounds__(kRowThreads) void fwd_rows_kernel(
 
 // ---- F2: forward columns: X[s][k1 + 2000*k2] = DFT_P over n2 of B[s][n2][k1]
 template <int P, class V>
-__global__ __launch_bounds__(kColThreads) void fwd_cols_kernel(const V* __restrict__ B, V* __restrict__ X)
+__global__ __launch_bounds__(kColThreads) void fwd_cols_kernel(FwdSet fs, const V* __restrict__ B, V* __restrict__ X)
 {
-    const int k1 = blockIdx.x * kColThreads + threadIdx.x, s = blockIdx.y;
+    const int k1 = blockIdx.x * kColThreads + threadIdx.x, s = fs.transform(blockIdx.y);
     if (k1 >= kRow) return;
     const V* b = B + (int64_t)s * P * kRow + k1;
     V v[P];
@@ -1251,20 +1265,25 @@ template <class V>
 hipError_t launch_acq_fft_forward(const int8_t* iq, const double2* xs, int64_t S, int datalen, int nbins,
                                   double IF, double freqMin, double freqStep, double Fs, const float* ca,
                                   int nprn, double codeFreqBasis, const V* tw_row,
-                                  const V* tw_col, V* B, V* X, hipStream_t s)
+                                  const V* tw_col, V* B, V* X, hipStream_t s, int bin0, int nbc, bool codes)
 {
-    const int nsig = datalen * nbins, ntr = nsig + nprn;
+    const int nsig = datalen * nbins;
+    if (nbc < 0) nbc = nbins - bin0;
+    if (bin0 < 0 || nbc < 0 || bin0 + nbc > nbins) return hipErrorInvalidValue;
+    const FwdSet fs{nbins, nsig, nprn, bin0, nbc > 0 ? nbc : 1, codes ? 1 : 0};
+    const int ntr = (codes ? nprn : 0) + datalen * nbc;
+    if (ntr == 0) return hipSuccess;
     const double step = codeFreqBasis / Fs;
 #define GNSS_FWD(P_)                                                                            \
     if (S == (int64_t)P_ * kRow) {                                                              \
         if (xs)                                                                                 \
             hipLaunchKernelGGL((fwd_rows_kernel<P_, SrcC64, V>), dim3(P_, ntr), dim3(kRowThreads), 0, s, \
-                               SrcC64{xs}, nbins, nsig, IF, freqMin, freqStep, Fs, ca, step, tw_row, tw_col, B); \
+                               SrcC64{xs}, fs, IF, freqMin, freqStep, Fs, ca, step, tw_row, tw_col, B); \
         else                                                                                    \
             hipLaunchKernelGGL((fwd_rows_kernel<P_, SrcIQ8, V>), dim3(P_, ntr), dim3(kRowThreads), 0, s, \
-                               SrcIQ8{iq}, nbins, nsig, IF, freqMin, freqStep, Fs, ca, step, tw_row, tw_col, B); \
+                               SrcIQ8{iq}, fs, IF, freqMin, freqStep, Fs, ca, step, tw_row, tw_col, B); \
         hipLaunchKernelGGL((fwd_cols_kernel<P_, V>), dim3((kRow + kColThreads - 1) / kColThreads, ntr), \
-                           dim3(kColThreads), 0, s, B, X);                                      \
+                           dim3(kColThreads), 0, s, fs, B, X);                                  \
         return hipGetLastError();                                                               \
     }
     GNSS_FWD(13) GNSS_FWD(29)
@@ -1273,11 +1292,12 @@ hipError_t launch_acq_fft_forward(const int8_t* iq, const double2* xs, int64_t S
 }
 template hipError_t launch_acq_fft_forward<float2>(const int8_t*, const double2*, int64_t, int, int, double,
                                                    double, double, double, const float*, int, double,
-                                                   const float2*, const float2*, float2*, float2*, hipStream_t);
+                                                   const float2*, const float2*, float2*, float2*, hipStream_t, int,
+                                                   int, bool);
 template hipError_t launch_acq_fft_forward<double2>(const int8_t*, const double2*, int64_t, int, int, double,
                                                     double, double, double, const float*, int, double,
                                                     const double2*, const double2*, double2*, double2*,
-                                                    hipStream_t);
+                                                    hipStream_t, int, int, bool);
 
 // Correlation of (bin, PRN) pairs [first_pair, first_pair + npair) (pair = bin*nprn + p)
 // over every ms: corr[p][bin] (tau2-major) = sum_ms |ifft(C_p .* conj(X_{ms,bin}))|^2.

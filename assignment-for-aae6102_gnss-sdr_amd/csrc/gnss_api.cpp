@@ -76,6 +76,11 @@ namespace {
 // (GNSS_OPT_ACQ_PIPE; config-2 fp64 correlation 10.10-10.18 -> 9.75-9.88 ms on MI355X,
 // profiles/r03_ab_acq_pipe.txt).
 constexpr int kAcqPipeDefault = 2;
+// the pipeline's forward spectra in bin chunks, each before the first column pass that reads it
+#ifndef GNSS_ACQ_FWD_SPLIT
+#define GNSS_ACQ_FWD_SPLIT 1
+#endif
+constexpr bool kAcqFwdSplit = GNSS_ACQ_FWD_SPLIT;
 // the paired launch's row blocks sit in the grid's first kAcqPairFront percent (acq_fft.hip)
 constexpr int kAcqPairFront = 60;
 // SVs per launch of the fine-frequency search (scratch ~186 MB per SV at config 2)
@@ -532,9 +537,26 @@ int acq_search(gnss_ctx* ctx, const int8_t* blk, const double2* xa, int64_t S, i
         HIP_TRY(A.alloc(ctx, "acq.A", csz * abuf * (two || pair ? 2 : 1)));
         HIP_TRY(hipStreamSynchronize(ctx->stream));
         HIP_TRY(hipEventRecord(e_all.a, ctx->stream));
-        HIP_TRY(launch_acq_fft_forward<V>(blk, xa, S, dl, nb, sg->IF, acq->freqMin, acq->freqStep, sg->Fs, ca, np,
-                                          sg->codeFreqBasis, d_twr.as<V>(), d_twc.as<V>(), B.as<V>(), X.as<V>(),
-                                          ctx->stream));
+        // the forward spectra: all at once, or (the two-stream pipeline, GNSS_ACQ_FWD_SPLIT) the
+        // codes and the bins batch 0 reads first and each later batch's new bins just before its
+        // column pass, on the column stream, where they run beside the previous batch's row pass
+        // (the column stream waits on the rows anyway); every spectrum is the same transform of the
+        // same data, so the bits do not change
+        const bool fwd_split = kAcqFwdSplit && two;
+        auto fwd = [&](int bin0, int nbc, bool codes) {
+            return launch_acq_fft_forward<V>(blk, xa, S, dl, nb, sg->IF, acq->freqMin, acq->freqStep, sg->Fs, ca, np,
+                                             sg->codeFreqBasis, d_twr.as<V>(), d_twc.as<V>(), B.as<V>(), X.as<V>(),
+                                             ctx->stream, bin0, nbc, codes);
+        };
+        int fwd_bins = 0;  // bins [0, fwd_bins) transformed so far
+        if (fwd_split) {
+            const int need = std::min(nb, (std::min(batch, npairs) - 1) / np + 1);
+            HIP_TRY(fwd(0, need, true));
+            fwd_bins = need;
+        } else {
+            HIP_TRY(fwd(0, -1, true));
+            fwd_bins = nb;
+        }
         const V* C = X.as<V>() + (size_t)nsig * S;
         if (pair) {
             const char* fe = probe_env("GNSS_PAIR_FRONT");  // (probe builds: the A/B knob)
@@ -568,6 +590,11 @@ int acq_search(gnss_ctx* ctx, const int8_t* blk, const double2* xa, int64_t S, i
                 const int nq = std::min(batch, npairs - q0);
                 const int h = b & 1;
                 V* Ah = A.as<V>() + (size_t)h * abuf;
+                if (fwd_split) {  // this batch's bins not transformed yet (pairs q0 .. q0 + nq - 1)
+                    const int need = std::min(nb, (q0 + nq - 1) / np + 1);
+                    if (need > fwd_bins) HIP_TRY(fwd(fwd_bins, need - fwd_bins, false));
+                    fwd_bins = std::max(fwd_bins, need);
+                }
                 if (b >= 2) HIP_TRY(hipStreamWaitEvent(s_cols, ctx->ev_rows[h], 0));  // rows of b-2 read Ah
                 HIP_TRY(launch_acq_fft_correlate(C, X.as<V>(), S, dl, nb, np, q0, nq, d_twr.as<V>(), d_twc.as<V>(),
                                                  Ah, corr, s_cols, kAcqCols));

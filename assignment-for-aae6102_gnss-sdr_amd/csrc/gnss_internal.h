@@ -411,11 +411,14 @@ hipError_t launch_acq_peak(const double* corr, int nprn, int nbins, int64_t S, i
 // Two-pass FFT correlator for S = P * 2000 (acq_fft.hip)
 bool acq_fft_supported(int64_t S);
 // V = float2 (fp32 fast mode) or double2 (fp64, the reference's precision)
+// (a subset: the code spectra when `codes`, and the signal spectra of bins [bin0, bin0 + nbc) of
+// every ms; nbc < 0 = to the last bin. The defaults: the whole pass)
 template <class V>
 hipError_t launch_acq_fft_forward(const int8_t* iq, const double2* xs, int64_t S, int datalen, int nbins, double IF,
                                   double freqMin, double freqStep, double Fs, const float* ca,
                                   int nprn, double codeFreqBasis, const V* tw_row,
-                                  const V* tw_col, V* B, V* X, hipStream_t s);
+                                  const V* tw_col, V* B, V* X, hipStream_t s, int bin0 = 0, int nbc = -1,
+                                  bool codes = true);
 // parts: kAcqCols (the column pass into A), kAcqRows (the row pass out of A into corr), or both
 constexpr int kAcqCols = 1, kAcqRows = 2;
 hipError_t launch_acq_fft_correlate(const float2* C, const float2* X, int64_t S, int datalen,
