@@ -116,3 +116,25 @@ def test_multi_context_errors_match_one(pkg, ctx, mctx, opensky_short):
     track.msToProcessCT_1ms, track.msToProcessCT_10ms = 700, 100
     T, cn0, cx = pkg.trackingCT(file, signal, track, A, ctx=mctx)
     assert T.prns() == [16, 26]
+
+
+def test_multi_context_pos_and_mc_equal_one(pkg, ctx, mctx, opensky_short):
+    """The sibling loops through the group context: trackingCT_POS_updated (per-channel
+    1 000 + countinx 1-ms steps, then 10-ms to ctPOS) and the 25-tap
+    trackingCT_POS_updated_multicorrelator (pdi 10) with the 8 Opensky channels dealt over three
+    members: every record, tap, C/N0 row and length equal the one-context call bit for bit
+    (trackingCT_POS_updated.m:179-413; trackingCT_POS_updated_multicorrelator.m)."""
+    from test_gpu_pos import OPENSKY
+    skip, cfg, data = opensky_short
+    file, signal, acq, track = params(pkg, skip, data)
+    A = acquired_of(OPENSKY["svs"], OPENSKY["cd"], OPENSKY["ff"])
+    track.msToProcessCT_1ms, track.ctPOS = 1000, 1000 + 12 + 80
+    one = pkg.trackingCT_POS(file, signal, track, A, OPENSKY["cx"], ctx=ctx, raw=True)
+    grp = pkg.trackingCT_POS(file, signal, track, A, OPENSKY["cx"], ctx=mctx, raw=True)
+    assert np.array_equal(one.rec, grp.rec) and np.array_equal(one.CN0, grp.CN0)
+    assert np.array_equal(one.len, grp.len)
+    track.msPosCT, track.pdi = 800, 10
+    one = pkg.trackingCT_POS_updated_multicorrelator(file, signal, track, A, ctx=ctx, raw=True)
+    grp = pkg.trackingCT_POS_updated_multicorrelator(file, signal, track, A, ctx=mctx, raw=True)
+    assert np.array_equal(one.rec, grp.rec) and np.array_equal(one.taps, grp.taps)
+    assert np.array_equal(one.CN0, grp.CN0) and np.array_equal(one.len, grp.len)
