@@ -1079,12 +1079,86 @@ __global__ void fine_twiddle_kernel(double2* __restrict__ t, int64_t len, int64_
     t[x] = make_double2(c, s);
 }
 
+// t[e] = the split layout's entry e of the w_2000 table (load_row_tw_ik's order), in global memory
+__global__ void fine_twik_kernel(const double2* __restrict__ tw_row, double2* __restrict__ t)
+{
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= kTwIK) return;
+    const bool t2 = e < 9 * 20;
+    const int f = t2 ? e : e - 9 * 20;
+    const int i = t2 ? f / 20 + 1 : f / 200 + 1, k = t2 ? f % 20 : f % 200;
+    t[e] = tw_row[t2 ? 10 * i * k : i * k];
+}
+
+// CA chip index of sample n of CarrSignal (acquisition.m:104: rem(floor((n+1)/Fs*fc), 1023))
+__device__ __forceinline__ int64_t fine_code_of(int64_t n, double invFs, double invFc, double codelength)
+{
+    const double cvi = floor((invFs * (double)(n + 1)) / invFc);
+    return (int64_t)fmod(cvi, codelength);
+}
+
+// A row of the fine search reads the samples n = P*T*m1 + rho, m1 < 2000: a lane stride of
+// P*T samples, one cache line per lane for 2 bytes of it, and each of the D row passes of a
+// column rho reads them again. GNSS_FINE_PREP: one pass per SV first copies CarrSignal's
+// samples (unconverted) and their chips (the CA table's float at the chip index) into the
+// row order [rho][m1] through an LDS tile (TM consecutive m1 x every rho: a contiguous run of
+// the record), so the row pass reads both contiguously and with no dependent table read;
+// the values are the ones it computed itself.
+#ifndef GNSS_FINE_PREP
+#define GNSS_FINE_PREP 1
+#endif
+#ifndef GNSS_FINE_TWIK
+#define GNSS_FINE_TWIK 1
+#endif
+template <class Src> struct SrcElem;
+template <> struct SrcElem<SrcIQ8> {
+    using T = char2;
+    static constexpr int kTM = 32;  // m1 per prep tile: 32 x 290 x (2 + 4) B = 56 KB of LDS
+    __device__ static T get(const SrcIQ8& s, int64_t n) { return reinterpret_cast<const char2*>(s.p)[n]; }
+    static SrcIQ8 wrap(const T* p) { return SrcIQ8{reinterpret_cast<const int8_t*>(p)}; }
+};
+template <> struct SrcElem<SrcC64> {
+    using T = double2;
+    static constexpr int kTM = 8;  // 8 x 290 x (16 + 4) B = 46 KB
+    __device__ static T get(const SrcC64& s, int64_t n) { return s.p[n]; }
+    static SrcC64 wrap(const T* p) { return SrcC64{p}; }
+};
+template <int P, class Src>
+__global__ __launch_bounds__(kRowThreads) void fine_prep_kernel(
+    const Src src, const int32_t* __restrict__ cd, int64_t S, double invFs, double invFc, double codelength,
+    const float* __restrict__ ca0, typename SrcElem<Src>::T* __restrict__ xt0, float* __restrict__ ct0)
+{
+    using T = typename SrcElem<Src>::T;
+    constexpr int PT = P * kFineT, TM = SrcElem<Src>::kTM;
+    constexpr int64_t M = (int64_t)PT * kRow;
+    __shared__ T s_x[TM * PT];
+    __shared__ float s_c[TM * PT];
+    const float* ca = ca0 + (int64_t)blockIdx.y * 1023;
+    const int m0 = blockIdx.x * TM, tid = threadIdx.x;
+    const int tm = kRow - m0 < TM ? kRow - m0 : TM;
+    const int64_t base = S - cd[blockIdx.y] - 1, n0 = (int64_t)PT * m0;
+    for (int e = tid; e < tm * PT; e += kRowThreads) {  // e = (m1 - m0)*PT + rho: the record in order
+        s_x[e] = SrcElem<Src>::get(src, base + n0 + e);
+        s_c[e] = ca[fine_code_of(n0 + e, invFs, invFc, codelength)];
+    }
+    __syncthreads();
+    T* xt = xt0 + (int64_t)blockIdx.y * M;
+    float* ct = ct0 + (int64_t)blockIdx.y * M;
+    for (int e = tid; e < tm * PT; e += kRowThreads) {  // e = rho*tm + c: tm consecutive m1 of a row
+        const int rho = e / tm, c = e - rho * tm;
+        xt[(int64_t)rho * kRow + m0 + c] = s_x[c * PT + rho];
+        ct[(int64_t)rho * kRow + m0 + c] = s_c[c * PT + rho];
+    }
+}
+
 // (blockIdx.z = the SV of a batched launch: its code delay, code table and transform slab)
+// GNSS_FINE_PREP: `src` is the prep pass's [sv][rho][m1] copy and ct its chips.
 template <int P, class Src>
 __global__ __launch_bounds__(kRowThreads) void fine_rows_kernel(
-    const Src src, const int32_t* __restrict__ cd, int64_t S, const float* __restrict__ ca0, double invFs,
-    double invFc, double codelength, int D, int64_t N, const double2* __restrict__ tw_row,
-    const double2* __restrict__ tabA, const double2* __restrict__ tabB, double2* __restrict__ E0)
+    const Src src, const float* __restrict__ ct, const int32_t* __restrict__ cd, int64_t S,
+    const float* __restrict__ ca0, double invFs, double invFc, double codelength, int D, int64_t N,
+    const double2* __restrict__ tw_row, const double2* __restrict__ twik, const double2* __restrict__ tabA,
+    const double2* __restrict__ tabB, double2* __restrict__ E0)
 {
     constexpr int T = kFineT;
     const int64_t base = S - cd[blockIdx.z] - 1;  // 0-based sample of CarrSignal(1) (acquisition.m:105)
@@ -1096,11 +1170,27 @@ __global__ __launch_bounds__(kRowThreads) void fine_rows_kernel(
     const int rho = blockIdx.x, r = blockIdx.y, tid = threadIdx.x;
     const int m2 = rho / P, n2 = rho - m2 * P;
     auto sample = [&](int m1) { return (int64_t)P * T * m1 + (int64_t)P * m2 + n2; };
-    auto code_of = [&](int64_t n) {
-        const double cvi = floor((invFs * (double)(n + 1)) / invFc);
-        return (int64_t)fmod(cvi, codelength);
-    };
-    if constexpr (GNSS_STAGED_LOADS) {
+    auto code_of = [&](int64_t n) { return fine_code_of(n, invFs, invFc, codelength); };
+    if constexpr (GNSS_FINE_PREP) {
+        constexpr int NIT = (kRow + kRowThreads - 1) / kRowThreads;
+        const int64_t row0 = ((int64_t)blockIdx.z * P * T + rho) * kRow;
+        double2 raw[NIT], ta[NIT];
+        float cv[NIT];
+#pragma unroll
+        for (int q = 0; q < NIT; q++) {
+            const int m10 = tid + q * kRowThreads, m1 = m10 < kRow ? m10 : kRow - 1;
+            cv[q] = ct[row0 + m1];
+            raw[q] = src.at(row0 + m1);
+            ta[q] = tabA[(int64_t)r * kRow + m1];
+        }
+#pragma unroll
+        for (int q = 0; q < NIT; q++) {
+            const int m1 = tid + q * kRowThreads;
+            const double code = (double)cv[q];
+            const double2 x = make_double2(raw[q].x * code, raw[q].y * code);
+            if (m1 < kRow) s_a[m1] = cmul(x, ta[q]);
+        }
+    } else if constexpr (GNSS_STAGED_LOADS) {
         constexpr int NIT = (kRow + kRowThreads - 1) / kRowThreads;
         double2 raw[NIT], ta[NIT];
         float cv[NIT];
@@ -1135,7 +1225,14 @@ __global__ __launch_bounds__(kRowThreads) void fine_rows_kernel(
     const double2 cb = make_double2(cs, sn);
     double2* o = E + (((int64_t)r * P + n2) * T + m2) * kRow;
     const double2* tb = tabB + m2 * kRow;  // w_{T*2000}^(-m2*j1), [m2][j1]
-    fft2000_r20first_put<-1>(s_a, tw_row, tid, [&](int, int j1, double2 v) { o[j1] = cmul(cmul(v, cb), tb[j1]); });
+    auto put = [&](int, int j1, double2 v) { o[j1] = cmul(cmul(v, cb), tb[j1]); };
+    // GNSS_FINE_TWIK: the stages' twiddles from the global split table (coalesced: lanes read
+    // consecutive entries) instead of the plain table (a gather at a lane stride of i or 10 i
+    // entries: up to a cache line per lane); the same values
+    if constexpr (GNSS_FINE_TWIK)
+        fft2000_r20first_put<-1>(s_a, TwIK<double2>{twik, twik + 9 * 20}, tid, put);
+    else
+        fft2000_r20first_put<-1>(s_a, tw_row, tid, put);
 }
 
 struct FineBest {
@@ -1421,17 +1518,25 @@ FineLayout fine_layout(int64_t S, int L, int datalen)
     FineLayout f;
     f.M = (int64_t)L * S;
     f.N = f.M * datalen;
-    f.tabs = kRow + (int64_t)kRow * datalen + (int64_t)kFineT * kRow + S + f.M / kRow;
+    f.tabs = kRow + (int64_t)kRow * datalen + (int64_t)kFineT * kRow + S + f.M / kRow + kTwIK;
     f.slab = f.N;
     f.part = (int64_t)datalen * (kRow / kFineJC);  // FineBest entries per SV
     return f;
 }
 }  // namespace
 
+// (GNSS_FINE_PREP) the row-order copies after the candidates: nsv x M samples (sized for the
+// widest source, complex fp64), then nsv x M chips (float)
+static size_t fine_prep_offset(const FineLayout& f, int nsv)
+{
+    const size_t b = sizeof(double2) * (size_t)(f.tabs + (int64_t)nsv * f.slab) + sizeof(FineBest) * (size_t)(nsv * f.part);
+    return (b + 255) & ~(size_t)255;
+}
 size_t fine_fft_scratch_bytes(int64_t S, int L, int datalen, int nsv)
 {
     const FineLayout f = fine_layout(S, L, datalen);
-    return sizeof(double2) * (size_t)(f.tabs + (int64_t)nsv * f.slab) + sizeof(FineBest) * (size_t)(nsv * f.part);
+    if (!GNSS_FINE_PREP) return fine_prep_offset(f, nsv);
+    return fine_prep_offset(f, nsv) + (size_t)nsv * f.M * (sizeof(double2) + sizeof(float));
 }
 
 // Twiddle tables of the fine search, once per call: w_2000, w_{2000*D}, w_{T*2000}, w_M, w_{P*T}.
@@ -1453,6 +1558,9 @@ hipError_t launch_fine_fft_tables(int64_t S, int L, int datalen, void* scratch, 
     for (int t = 0; t < 5; t++)
         hipLaunchKernelGGL(fine_twiddle_kernel, dim3((unsigned)((lens[t] + 255) / 256)), dim3(256), 0,
                            s, tabs[t], lens[t], divs[t], rows[t]);
+    // the row transforms' twiddles in the split layout (TwIK: a stage's lanes read consecutive
+    // entries), copied from w_2000 after it (the same stream)
+    hipLaunchKernelGGL(fine_twik_kernel, dim3((kTwIK + 255) / 256), dim3(256), 0, s, tw_row, tabS + M / kRow);
     return hipGetLastError();
 }
 
@@ -1473,17 +1581,29 @@ hipError_t launch_fine_fft_argmax(const int8_t* iq, const double2* xs, int64_t S
     double2* tabS = tabK + S;
     double2* E = tw_row + f.tabs;
     FineBest* part = reinterpret_cast<FineBest*>(E + (int64_t)nsv * f.slab);
+    char* prep = static_cast<char*>(scratch) + fine_prep_offset(f, nsv);
+    float* ct = reinterpret_cast<float*>(prep + (size_t)nsv * f.M * sizeof(double2));
     const int nblk = kRow / kFineJC;
+    // the row pass over source Src: from the record itself, or (GNSS_FINE_PREP) from its row-order copy
+    auto rows = [&](auto src, auto* xt, auto kern, auto prep_kern, int tm) {
+        using SrcT = decltype(src);
+        if (GNSS_FINE_PREP) {
+            hipLaunchKernelGGL(prep_kern, dim3((kRow + tm - 1) / tm, nsv), dim3(kRowThreads), 0, s, src, cd, S, 1 / Fs,
+                               1 / codeFreqBasis, codelength, ca, xt, ct);
+            src = SrcElem<SrcT>::wrap(xt);
+        }
+        hipLaunchKernelGGL(kern, dim3((unsigned)(f.M / kRow), datalen, nsv), dim3(kRowThreads), 0, s, src, ct, cd, S,
+                           ca, 1 / Fs, 1 / codeFreqBasis, codelength, datalen, N, tw_row, tabS + f.M / kRow, tabA,
+                           tabB, E);
+    };
 #define GNSS_FINE(P_)                                                                           \
     if (S == (int64_t)P_ * kRow) {                                                              \
         if (xs)                                                                                 \
-            hipLaunchKernelGGL((fine_rows_kernel<P_, SrcC64>), dim3(P_ * kFineT, datalen, nsv), dim3(kRowThreads), \
-                               0, s, SrcC64{xs}, cd, S, ca, 1 / Fs, 1 / codeFreqBasis, codelength, datalen, N, \
-                               tw_row, tabA, tabB, E);                                          \
+            rows(SrcC64{xs}, reinterpret_cast<double2*>(prep), fine_rows_kernel<P_, SrcC64>,    \
+                 fine_prep_kernel<P_, SrcC64>, SrcElem<SrcC64>::kTM);                           \
         else                                                                                    \
-            hipLaunchKernelGGL((fine_rows_kernel<P_, SrcIQ8>), dim3(P_ * kFineT, datalen, nsv), dim3(kRowThreads), \
-                               0, s, SrcIQ8{iq}, cd, S, ca, 1 / Fs, 1 / codeFreqBasis, codelength, datalen, N, \
-                               tw_row, tabA, tabB, E);                                          \
+            rows(SrcIQ8{iq}, reinterpret_cast<char2*>(prep), fine_rows_kernel<P_, SrcIQ8>,      \
+                 fine_prep_kernel<P_, SrcIQ8>, SrcElem<SrcIQ8>::kTM);                           \
         hipLaunchKernelGGL(fine_cols_kernel<P_>, dim3(nblk, datalen, nsv), dim3(kColThreads), 0, s, E, \
                            datalen, N, shifted, tabK, tabS, part);                                    \
         hipLaunchKernelGGL(fine_best_final_kernel, dim3(nsv), dim3(256), 0, s, part, nblk * datalen, \
