@@ -370,12 +370,15 @@ def main():
     prns = list(range(1, 33))
     my_prns = [prns[i] for i in D.shard(len(prns), world, rank)]
     outs = [None]  # the trackingCT output buffers (HBM), reused from step to step
+    gather_s = [0.0]  # host wall time inside the result gathers (distributed path only)
 
     def one_step():
         A = pkg.acquisition(file, signal, acq, ctx=ctx, prn_list=my_prns)
         ta = ctx.timing()
         if dist is not None:
+            g0 = time.perf_counter()
             A = D.gather_acquired(A, my_prns, prns, device=f"cuda:{local}")
+            gather_s[0] += time.perf_counter() - g0
         nsv = len(A.sv)
         shards = [D.shard(nsv, world, r) for r in range(world)]
         if outs[0] is None or not outs[0].fits(nsv, track, 0):
@@ -383,12 +386,15 @@ def main():
         buf = pkg.trackingCT(file, signal, track, A, ctx=ctx, channels=shards[rank], raw=True, out=outs[0])
         tt = ctx.timing()
         if dist is not None:
+            g0 = time.perf_counter()
             D.gather_tracking_rows_device(buf, shards)
+            gather_s[0] += time.perf_counter() - g0
         return A, ta, tt, buf, shards
 
     for _ in range(args.warmup):
         one_step()
     barrier(dist, local)
+    gather_s[0] = 0.0
     t0 = time.perf_counter()
     acq_units = trk_units = 0
     acq_ms = trk_ms = acq_corr_ms = acq_fine_ms = 0.0
@@ -510,6 +516,8 @@ def main():
         "track_Msamples_s": round(trk_units / (trk_ms * 1e-3) / 1e6, 2) if trk_ms else None,
         "acq_ms": round(acq_ms / args.steps, 3),
         "track_ms": round(trk_ms / args.steps, 3),
+        # (distributed path) rank 0's host wall time inside the result gathers per timed step
+        "gather_ms": round(gather_s[0] / args.steps * 1e3, 3) if dist is not None else None,
         # device-busy evidence of the timed steps: the ctx stream's event-timed acquisition +
         # tracking spans over the step's wall time (rank 0)
         "device_busy_frac": round((acq_ms + trk_ms) / args.steps / step_ms, 4),
