@@ -33,7 +33,7 @@ dev = pkg.DeviceRecord(ctx, (skip + 40) * S * 2)
 pkg.synth.generate_device(ctx, cfg, dev)
 file.skip, file.dev = skip, dev
 c = []
-between = os.environ.get("BETWEEN", "")  # torch work between the calls: copy | gather
+between = os.environ.get("BETWEEN", "")  # between the calls: copy | gather | sleep<ms>
 if between == "gather":
     D = importlib.import_module("assignment-for-aae6102_gnss-sdr_amd.dist")
 for it in range(4):
@@ -41,6 +41,8 @@ for it in range(4):
     c.append(ctx.timing()["acq_corr_ms"])
     if between == "copy":
         y = torch.arange(160, dtype=torch.float64).to("cuda:0").cpu()
+    elif between.startswith("sleep"):  # the GPU idle for that many ms before the next call
+        time.sleep(float(between[5:]) * 1e-3)
     elif between == "gather":
         A = D.gather_acquired(A, list(range(1, 33)), list(range(1, 33)), device="cuda:0")
 print(f"mode={mode} between={between} pipe={os.environ.get('ACQ_PIPE', 'default')} corr_ms", " ".join(f"{v:.3f}" for v in c), "sv", list(A.sv), flush=True)
