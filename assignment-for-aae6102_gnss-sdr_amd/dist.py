@@ -107,12 +107,17 @@ def _gather_into(out, t, group):
         dist.all_gather_into_tensor(out, t, group=group)
 
 
-def gather_tracking_rows_device(buf, shards, group=None):
+def gather_tracking_rows_device(buf, shards, group=None, defer=False):
     """gather_tracking_rows for DeviceTrackOutBuffers: the TckResultCT series (rec, and
     taps when present) never leave HBM -- each rank packs its own channels' rows on the GPU
     and one all_gather_into_tensor (RCCL over xGMI on MI355X) delivers every rank's rows,
     scattered back in place. The small host arrays (len, countinx, CN0 columns, cn0_rows)
-    travel in one packed device tensor of their own."""
+    travel in one packed device tensor of their own.
+
+    defer=True: enqueue the device work and return a function that completes the gather
+    (the one host round trip: the packed metadata's copy back and its scatter into the host
+    arrays), so the caller can start other GPU work first. Call it before anything writes or
+    reads `buf` again."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
@@ -140,20 +145,24 @@ def gather_tracking_rows_device(buf, shards, group=None):
     for j, c in enumerate(shards[me]):
         meta[j, 0], meta[j, 1], meta[j, 2] = buf.len[c], buf.countinx[c], buf.c.cn0_rows
         meta[j, 3:] = buf.CN0[:, c]
-    mt = torch.from_numpy(meta).to(dev)
-    allm = torch.empty((world * width, 3 + nc), dtype=mt.dtype, device=dev)
-    _gather_into(allm, mt, group)
-    allm = allm.cpu().numpy()
-    crows = buf.c.cn0_rows
-    for r in range(world):
-        for j, c in enumerate(shards[r]):
-            m = allm[r * width + j]
-            crows = max(crows, int(m[2]))
-            if r != me:
-                buf.len[c], buf.countinx[c] = int(m[0]), int(m[1])
-                buf.CN0[:, c] = m[3:]
-    buf.c.cn0_rows = crows
-    return buf
+    mt = torch.from_numpy(meta).to(dev, non_blocking=False)
+    allm_d = torch.empty((world * width, 3 + nc), dtype=mt.dtype, device=dev)
+    _gather_into(allm_d, mt, group)
+
+    def finish():
+        allm = allm_d.cpu().numpy()
+        crows = buf.c.cn0_rows
+        for r in range(world):
+            for j, c in enumerate(shards[r]):
+                m = allm[r * width + j]
+                crows = max(crows, int(m[2]))
+                if r != me:
+                    buf.len[c], buf.countinx[c] = int(m[0]), int(m[1])
+                    buf.CN0[:, c] = m[3:]
+        buf.c.cn0_rows = crows
+        return buf
+
+    return finish if defer else finish()
 
 
 def gather_tracking(buf, nsv: int, group=None, device=None):

@@ -371,11 +371,26 @@ def main():
     my_prns = [prns[i] for i in D.shard(len(prns), world, rank)]
     outs = [None]  # the trackingCT output buffers (HBM), reused from step to step
     gather_s = [0.0]  # host wall time inside the result gathers (distributed path only)
+    # (distributed path) the previous step's tracking gather, enqueued on the GPU and completed
+    # after this step's acquisition: its host round trip would otherwise leave the GPU idle right
+    # before the acquisition, which then starts slower (profiles/r05_dist_overhead.txt); the last
+    # step's is completed inside the timed region (finish_gather)
+    pending = [None]
+
+    def finish_gather():
+        if pending[0] is not None:
+            g0 = time.perf_counter()
+            pending[0]()
+            pending[0] = None
+            gather_s[0] += time.perf_counter() - g0
+
+    skip_gathers = bool(os.environ.get("BENCH_DIAG_NO_GATHER")) and world == 1  # (diagnostic hook)
 
     def one_step():
         A = pkg.acquisition(file, signal, acq, ctx=ctx, prn_list=my_prns)
         ta = ctx.timing()
-        if dist is not None:
+        finish_gather()
+        if dist is not None and not skip_gathers:
             g0 = time.perf_counter()
             A = D.gather_acquired(A, my_prns, prns, device=f"cuda:{local}")
             gather_s[0] += time.perf_counter() - g0
@@ -385,14 +400,15 @@ def main():
             outs[0] = pkg.DeviceTrackOutBuffers(nsv, track, 0, device=f"cuda:{local}")
         buf = pkg.trackingCT(file, signal, track, A, ctx=ctx, channels=shards[rank], raw=True, out=outs[0])
         tt = ctx.timing()
-        if dist is not None:
+        if dist is not None and not skip_gathers:
             g0 = time.perf_counter()
-            D.gather_tracking_rows_device(buf, shards)
+            pending[0] = D.gather_tracking_rows_device(buf, shards, defer=True)
             gather_s[0] += time.perf_counter() - g0
         return A, ta, tt, buf, shards
 
     for _ in range(args.warmup):
         one_step()
+    finish_gather()
     barrier(dist, local)
     gather_s[0] = 0.0
     t0 = time.perf_counter()
@@ -406,6 +422,7 @@ def main():
         acq_corr_ms += ta["acq_corr_ms"]
         acq_fine_ms += ta["acq_fine_ms"]
         trk_ms += tt["track_ms"]
+    finish_gather()  # (the last step's tracking gather, inside the timed region)
     barrier(dist, local)
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(dist, local, elapsed)

@@ -60,14 +60,21 @@ def _worker(rank, world, port, out_dir):
     tv = SimpleNamespace(rec=torch.from_numpy(bt.rec.copy()), taps=torch.from_numpy(bt.taps.copy()),
                          len=bt.len.copy(), countinx=bt.countinx.copy(), CN0=bt.CN0.copy(),
                          c=SimpleNamespace(cn0_rows=bt.c.cn0_rows))
+    # the deferred form (bench.py's N > 1 step): device work enqueued, the host half completed later
+    tw = SimpleNamespace(rec=tv.rec.clone(), taps=tv.taps.clone(), len=tv.len.copy(), countinx=tv.countinx.copy(),
+                         CN0=tv.CN0.copy(), c=SimpleNamespace(cn0_rows=tv.c.cn0_rows))
     D.gather_tracking_rows(bt, shards)
     D.gather_tracking_rows_device(tv, shards)
+    fin = D.gather_tracking_rows_device(tw, shards, defer=True)
+    assert callable(fin) and fin() is tw
     if rank == 0:
         np.savez(os.path.join(out_dir, "dist.npz"), sv=A.sv, codedelay=A.codedelay,
                  fineFreq=A.fineFreq, SNR=A.SNR, rec=G.rec, len=G.len, countinx=G.countinx, CN0=G.CN0,
                  rec_rows=B.rec, len_rows=B.len, cx_rows=B.countinx, CN0_rows=B.CN0[: B.c.cn0_rows],
                  taps_rows=bt.taps, trec_rows=bt.rec, tv_rec=tv.rec.numpy(), tv_taps=tv.taps.numpy(),
-                 tv_len=tv.len, tv_cx=tv.countinx, tv_CN0=tv.CN0[: tv.c.cn0_rows])
+                 tv_len=tv.len, tv_cx=tv.countinx, tv_CN0=tv.CN0[: tv.c.cn0_rows],
+                 tw_rec=tw.rec.numpy(), tw_taps=tw.taps.numpy(), tw_len=tw.len, tw_cx=tw.countinx,
+                 tw_CN0=tw.CN0[: tw.c.cn0_rows])
     dist.barrier()
     dist.destroy_process_group()
 
@@ -103,3 +110,6 @@ def test_sharded_equals_single_process(tmp_path, pkg, po):
     assert np.array_equal(z["tv_taps"], full.taps) and np.array_equal(z["tv_rec"], full.rec)
     assert np.array_equal(z["tv_len"], full.len) and np.array_equal(z["tv_cx"], full.countinx)
     assert np.array_equal(z["tv_CN0"], full.CN0[: full.c.cn0_rows])
+    assert np.array_equal(z["tw_taps"], full.taps) and np.array_equal(z["tw_rec"], full.rec)
+    assert np.array_equal(z["tw_len"], full.len) and np.array_equal(z["tw_cx"], full.countinx)
+    assert np.array_equal(z["tw_CN0"], full.CN0[: full.c.cn0_rows])

@@ -18,6 +18,8 @@ if mode in ("gloo", "nccl"):
         dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
     else:
         dist.init_process_group("gloo")
+    if os.environ.get("PROBE_BARRIER"):  # one collective before the context (what bench.py's barrier does)
+        dist.barrier()
 pkg = importlib.import_module("assignment-for-aae6102_gnss-sdr_amd")
 ctx = pkg.Context(0)
 if mode == "torch_after":
@@ -45,6 +47,6 @@ for it in range(4):
         time.sleep(float(between[5:]) * 1e-3)
     elif between == "gather":
         A = D.gather_acquired(A, list(range(1, 33)), list(range(1, 33)), device="cuda:0")
-print(f"mode={mode} between={between} pipe={os.environ.get('ACQ_PIPE', 'default')} corr_ms", " ".join(f"{v:.3f}" for v in c), "sv", list(A.sv), flush=True)
+print(f"mode={mode} barrier={os.environ.get('PROBE_BARRIER', '')} between={between} pipe={os.environ.get('ACQ_PIPE', 'default')} corr_ms", " ".join(f"{v:.3f}" for v in c), "sv", list(A.sv), flush=True)
 if mode in ("gloo", "nccl"):
     dist.destroy_process_group()
