@@ -18,10 +18,12 @@ if mode in ("gloo", "nccl"):
         dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
     else:
         dist.init_process_group("gloo")
-    if os.environ.get("PROBE_BARRIER"):  # one collective before the context (what bench.py's barrier does)
+    if os.environ.get("PROBE_BARRIER") == "1":  # one collective before the context
         dist.barrier()
 pkg = importlib.import_module("assignment-for-aae6102_gnss-sdr_amd")
 ctx = pkg.Context(0)
+if os.environ.get("PROBE_BARRIER") == "after":  # the first collective after the context (bench.py's order)
+    dist.barrier()
 if mode == "torch_after":
     torch.cuda.set_device(0)
     x = torch.ones(16, device="cuda:0")
