@@ -22,6 +22,7 @@
 #include <vector>
 #include <fcntl.h>
 #include <map>
+#include <mutex>
 #include <string>
 #include <tuple>
 #include <unistd.h>
@@ -379,23 +380,7 @@ int run_fft(gnss_ctx* ctx, void* data, size_t len, size_t batch, int dbl, int in
 // The kernels form CarrTime = k/Fs (trackingCT.m:104) as q = k*RN(1/Fs) corrected by
 // one FMA; that equals the IEEE quotient for every k we check here (exhaustive over
 // the step's sample range, cached per Fs). Otherwise they divide.
-int fast_div_exact(double Fs, int64_t kmax)
-{
-    static std::map<std::pair<double, int64_t>, int> cache;
-    auto key = std::make_pair(Fs, kmax);
-    auto it = cache.find(key);
-    if (it != cache.end()) return it->second;
-    const double y = 1.0 / Fs;
-    int ok = 1;
-    for (int64_t k = 0; k <= kmax && ok; k++) {
-        const double a = (double)k;
-        const double q = a * y;
-        const double e = std::fma(-q, Fs, a);
-        if (std::fma(e, y, q) != a / Fs) ok = 0;
-    }
-    cache[key] = ok;
-    return ok;
-}
+int fast_div_exact(double Fs, int64_t kmax) { return group::reciprocal_exact_cached(Fs, kmax); }
 
 void generate_ca(int prn, float* out);
 
@@ -794,7 +779,9 @@ static int group_tracking(gnss_ctx* g, const gnss_file* file, const gnss_signal*
             o.taps = out->taps ? ltap.as<double>() : nullptr;
         }
         const int st = tracking_impl(m, file, sg, &t, acq, &o, pos, nullptr, remote ? slot.data() : nullptr);
-        ts[(size_t)k] = group::TrackStatus{st, m->fail_chan};
+        // the failing channel's POSITION in the call's channel list (the one-context rule picks the
+        // first failing channel in tr->chan order, which need not be ascending)
+        ts[(size_t)k] = group::TrackStatus{st, group::fail_position(shards[(size_t)k], chans, m->fail_chan)};
         rows[(size_t)k] = o.cn0_rows;
         if (st != GNSS_OK || !remote) return;
         bool copied = true;
@@ -1339,13 +1326,17 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
     if (pos) { P.iE = 0; P.iP = 1; P.iL = 2; }
     if ((pos && pos->mc_pdi) || gv) { P.iE = 2; P.iP = 12; P.iL = 22; }
     if (P.iE < 0 || P.iP < 0 || P.iL < 0) return fail(ctx, GNSS_EARG, "taps must contain -spacing, 0, +spacing");
+    bool wide_taps = false;
     {
         double lo_t = 1e300, hi_t = -1e300;
         for (int s = 0; s < ntaps; s++) {
             lo_t = std::min(lo_t, taps[s] + P.tap_post[s]);
             hi_t = std::max(hi_t, taps[s] + P.tap_post[s]);
         }
-        if (!(hi_t - lo_t <= kTapSpan)) return fail(ctx, GNSS_EARG, "tap offsets must lie within %g chips", kTapSpan);
+        // the persistent loop's tap window needs every tap's chip at a lane start within one
+        // 32-chip run; a wider tap set runs on the per-step path (a path choice, not
+        // an argument error)
+        wide_taps = !(hi_t - lo_t <= kTapSpan);
     }
     P.ntaps = ntaps;
 
@@ -1522,7 +1513,8 @@ static int tracking_impl(gnss_ctx* ctx, const gnss_file* file, const gnss_signal
                max_taps_in_lane(P.taps, P.tap_post, P.ntaps, 8 * sub, cps_max) <= kQcapMax;
     };
     auto vpb_for = [&](int pdi, int sub) {
-        if (ctx->opt[GNSS_OPT_NO_PERSIST] || P.fmt != 0 || bpc_for(pdi, sub) > run_bpc_cap(P.ntaps) || !qcap_ok(sub))
+        if (ctx->opt[GNSS_OPT_NO_PERSIST] || P.fmt != 0 || wide_taps || bpc_for(pdi, sub) > run_bpc_cap(P.ntaps) ||
+            !qcap_ok(sub))
             return 0;
         const int bpc = bpc_for(pdi, sub);
         int v0 = 1;

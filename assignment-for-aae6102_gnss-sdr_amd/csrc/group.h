@@ -10,7 +10,11 @@
 #define GNSS_GROUP_H
 
 #include <algorithm>
+#include <cmath>
 #include <cstdint>
+#include <map>
+#include <mutex>
+#include <utility>
 #include <vector>
 
 #include "../../include/gnss_mi355x.h"
@@ -84,13 +88,21 @@ inline int acquisition_status(const std::vector<int>& st, int merged_n)
 // The status of a sharded tracking call. One context decides it over its channels in
 // order (gnss_api.cpp, tracking_impl): GNSS_ENODATA ("Not enough raw data") if any channel
 // ran short, else the status of the first failing channel. Member k reports its status and
-// the global index of the channel that set it (-1: failed before any channel ran, i.e. an
-// argument error that every member shares). The same rule over the members' reports gives
+// the position, in the call's channel list, of the channel that set it (-1: failed before any
+// channel ran, i.e. an argument error that every member shares). The same rule over the members' reports gives
 // the one-context answer.
 struct TrackStatus {
     int status;
     int chan;
 };
+// A member tracks the channels chans[shard[i]] in shard order and reports the channel id that
+// failed first (fail_chan, -1: none); its position in the call's list is what the rule compares.
+inline int fail_position(const std::vector<int>& shard, const std::vector<int32_t>& chans, int fail_chan)
+{
+    for (int i : shard)
+        if (chans[(size_t)i] == fail_chan) return i;
+    return -1;
+}
 inline int tracking_status(const std::vector<TrackStatus>& st)
 {
     int best = GNSS_OK, best_chan = 0;
@@ -106,6 +118,41 @@ inline int tracking_status(const std::vector<TrackStatus>& st)
         }
     }
     return best;
+}
+
+// CarrTime = k/Fs as the tracking kernels form it (k * RN(1/Fs) plus one FMA correction)
+// equals the IEEE quotient for every k in [0, kmax] (exhaustive; gnss_api.cpp caches it per
+// (Fs, kmax) behind a mutex, since a group's member threads reach it concurrently).
+inline int reciprocal_exact(double Fs, int64_t kmax)
+{
+    const double y = 1.0 / Fs;
+    for (int64_t k = 0; k <= kmax; k++) {
+        const double a = (double)k;
+        const double q = a * y;
+        const double e = std::fma(-q, Fs, a);
+        if (std::fma(e, y, q) != a / Fs) return 0;
+    }
+    return 1;
+}
+
+// reciprocal_exact, cached per (Fs, kmax). A multi-device context reaches it from one host
+// thread per device (gnss_api.cpp, for_members), so the cache is guarded: the check
+// runs outside the lock (a pure function of the key: two threads that miss together compute
+// the same answer), the lookup and the insert under it.
+inline int reciprocal_exact_cached(double Fs, int64_t kmax)
+{
+    static std::mutex mu;
+    static std::map<std::pair<double, int64_t>, int> cache;
+    const auto key = std::make_pair(Fs, kmax);
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = cache.find(key);
+        if (it != cache.end()) return it->second;
+    }
+    const int ok = reciprocal_exact(Fs, kmax);
+    std::lock_guard<std::mutex> lk(mu);
+    cache.emplace(key, ok);
+    return ok;
 }
 
 // Timing of a group call: the members ran side by side, so durations are the slowest

@@ -30,7 +30,9 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-pkg = importlib.import_module("assignment-for-aae6102_gnss-sdr_amd")
+# the package (and with it the HIP library) is imported in main(), after the N-rank launcher
+# has decided whether this process is a parent that only spawns ranks (it never touches the GPU)
+pkg = None
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X vector fp64 (half the 157.3 TF fp32 vector rate: 4-cycle wave64 fp64 ops)
@@ -107,12 +109,55 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--no-profile-pass", action="store_true")
-    ap.add_argument("--workload", choices=["cfg2+3", "cfg4", "cfg5"], default="cfg2+3",
+    ap.add_argument("--workload", choices=["cfg2+3", "cfg4", "cfg5", "dist-selftest"], default="cfg2+3",
                     help="cfg2+3: the headline step (default); cfg4: BASELINE config 4, 32-PRN Urban "
                          "acquisition, PRNs sharded over the ranks; cfg5: BASELINE config 5, 32-channel "
-                         "11-tap trackingCT, channels sharded over the ranks")
+                         "11-tap trackingCT, channels sharded over the ranks; dist-selftest: the launcher, "
+                         "shards and result gathers on host arrays only (no GPU, no library: a CPU check "
+                         "of the N-rank path, never a bench line)")
     ap.add_argument("--n10-cfg5", type=int, default=90000, help="cfg5 msToProcessCT_10ms")
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n):
+    """`python3 bench.py --gpus N` without a launcher (RANK unset): start N child processes of
+    this same command, one rank per GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR 127.0.0.1 /
+    MASTER_PORT in their environment), and return the job's exit status. This parent runs before
+    anything imports the HIP library or torch, so it never touches a GPU; the children are new
+    processes (no fork of GPU state, no exec). Rank 0 prints the one JSON line. If a child fails,
+    the others are terminated and the parent exits with that child's status."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                print(f"bench.py: rank {procs.index(p)} exited with status {rc}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return status
 
 
 def setup_dist(args):
@@ -250,7 +295,9 @@ def run_cfg5(args, rank, world, local, dist, ctx):
             "data": "synthetic 32-SV IF at Opensky rates (int8 I/Q), resident in HBM",
             "config": {"workload": f"trackingCT cfg5 (32 ch, 11 taps -0.5:0.1:0.5, 1000 ms @1ms + "
                                    f"{args.n10_cfg5} ms @10ms)", "parallelism": f"channels x{world}",
-                       "channels_per_rank": len(mine)},
+                       "channels_per_rank": len(mine),
+                       "channels_by_rank": [len(x) for x in shards]},
+            **dist_world(dist),
             "code": code_stamp(),
             "roofline": roof, "cpu_baseline": cpu}
     if rank == 0:
@@ -326,7 +373,9 @@ def run_cfg4(args, rank, world, local, dist, ctx):
             "dtype": "int8 in, f64 correlation / f64 fine search",
             "data": "synthetic Urban-shape IF (int8 I/Q, Fs 26 MHz, IF 0), resident in HBM",
             "config": {"workload": "acquisition cfg4 (32 PRN, +-10kHz/250Hz, 10 ms, L 10)",
-                       "parallelism": f"PRNs x{world}", "prns_per_rank": len(mine)},
+                       "parallelism": f"PRNs x{world}", "prns_per_rank": len(mine),
+                       "prns_by_rank": [len(D.shard(len(prns), world, r)) for r in range(world)]},
+            **dist_world(dist),
             "acquired": [int(x) for x in A.sv], "acq_ms_rank0": round(ta["acq_ms"], 3),
             "code": code_stamp(),
             "roofline": roof, "cpu_baseline": cpu}
@@ -337,8 +386,81 @@ def run_cfg4(args, rank, world, local, dist, ctx):
         dist.destroy_process_group()
 
 
+def dist_world(dist):
+    """What the line says about the process group: its size and backend (RCCL = "nccl")."""
+    if dist is None:
+        return {"rccl_world": 1, "backend": None}
+    return {"rccl_world": dist.get_world_size(), "backend": dist.get_backend()}
+
+
+def run_dist_selftest(args):
+    """The N-rank path without a GPU (CPU test of the launcher): each rank takes its round-robin
+    shard of 32 PRNs and of 8 channels, fills its rows of host result tables with a seeded
+    function of the unit index (the same values whatever rank computes them), and runs the bench's
+    result gathers (dist.gather_acquired, dist.gather_tracking_rows) over the process group; rank 0
+    prints a digest of the gathered tables, which must equal the N = 1 run's."""
+    import hashlib
+    import torch.distributed as tdist
+    from types import SimpleNamespace
+    D = importlib.import_module("assignment-for-aae6102_gnss-sdr_amd.dist")
+    dist = None
+    rank, world = 0, 1
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        tdist.init_process_group("gloo")
+        dist, rank, world = tdist, tdist.get_rank(), tdist.get_world_size()
+    if os.environ.get("BENCH_SELFTEST_FAIL_RANK") == str(rank):  # (test hook: a failing rank)
+        sys.exit(3)
+    t0 = time.perf_counter()
+    prns = list(range(1, 33))
+    mine = [prns[i] for i in D.shard(32, world, rank)]
+    acq_prns = [p for p in mine if p % 3]  # "acquired": a rank-independent rule per PRN
+    A = SimpleNamespace(sv=np.array(acq_prns, dtype=np.int64), SNR=np.array([17.0 + p / 7 for p in acq_prns]),
+                        Doppler=np.array([500.0 * (p % 29 - 14) for p in acq_prns]),
+                        codedelay=np.array([1000 * p + 7 for p in acq_prns], dtype=np.int64),
+                        fineFreq=np.array([4.58e6 + 13.0 * p for p in acq_prns]))
+    if dist is not None:
+        A = D.gather_acquired(A, mine, prns)
+    nch, nrow, nlen = 8, 18, 50
+    rec = np.zeros((nch, nrow, nlen))
+    buf = SimpleNamespace(rec=rec, len=np.zeros(nch, dtype=np.int64), countinx=np.zeros(nch, dtype=np.int64),
+                          CN0=np.zeros((4, nch)), taps=None, c=SimpleNamespace(cn0_rows=0))
+    shards = [D.shard(nch, world, r) for r in range(world)]
+    for c in shards[rank]:
+        buf.rec[c] = np.random.default_rng(c).standard_normal((nrow, nlen))
+        buf.len[c], buf.countinx[c] = 1000 + c, c % 20
+        buf.CN0[:, c] = 40.0 + c + np.arange(4)
+    buf.c.cn0_rows = 4
+    if dist is not None:
+        D.gather_tracking_rows(buf, shards)
+    h = hashlib.sha256()
+    for a in (A.sv, A.SNR, A.Doppler, A.codedelay, A.fineFreq, buf.rec, buf.len, buf.countinx, buf.CN0):
+        h.update(np.ascontiguousarray(a).tobytes())
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = __import__("torch").tensor([elapsed], dtype=__import__("torch").float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    line = {"metric": "dist-selftest (not a bench line)", "n_gpus": world, "digest": h.hexdigest(),
+            "acquired": [int(x) for x in A.sv], "ms": round(elapsed * 1e3, 3),
+            "spawned": bool(os.environ.get("BENCH_SPAWNED")),
+            "config": {"prns_per_rank": [len(D.shard(32, world, r)) for r in range(world)],
+                       "channels_per_rank": [len(s) for s in shards]}, **dist_world(dist)}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
+    global pkg
     args = parse()
+    # N ranks with no launcher: this process only spawns them (before any GPU or library import)
+    if args.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+    pkg = importlib.import_module("assignment-for-aae6102_gnss-sdr_amd")
+    if args.workload == "dist-selftest":
+        return run_dist_selftest(args)
     rank, world, local, dist = setup_dist(args)
     import torch  # noqa: F401  (before the library: device-resident outputs are torch tensors)
     ctx = pkg.Context(local)
@@ -398,6 +520,9 @@ def main():
         shards = [D.shard(nsv, world, r) for r in range(world)]
         if outs[0] is None or not outs[0].fits(nsv, track, 0):
             outs[0] = pkg.DeviceTrackOutBuffers(nsv, track, 0, device=f"cuda:{local}")
+        # the previous step's deferred gather still scatters into outs[0] until finish_gather()
+        # has run; trackingCT must not write the buffers before that
+        assert pending[0] is None, "tracking gather still pending on the output buffers"
         buf = pkg.trackingCT(file, signal, track, A, ctx=ctx, channels=shards[rank], raw=True, out=outs[0])
         tt = ctx.timing()
         if dist is not None and not skip_gathers:
@@ -525,7 +650,10 @@ def main():
         "config": {"workload": "acquisition cfg2 (32 PRN, +-7kHz/500Hz, 20 ms) + trackingCT cfg3 "
                                f"({nch} ch, 1000 ms @1ms + {args.n10} ms @10ms, E/P/L)",
                    "parallelism": f"PRNs and channels x{world} (one record, strong scaling)",
-                   "prns_per_rank": len(my_prns), "channels_per_rank": len(mine)},
+                   "prns_per_rank": len(my_prns), "channels_per_rank": len(mine),
+                   "prns_by_rank": [len(D.shard(len(prns), world, r)) for r in range(world)],
+                   "channels_by_rank": [len(x) for x in shards]},
+        **dist_world(dist),
         "outputs_ok": outputs_ok,
         "acquired": [int(x) for x in A.sv],
         "per_gpu_Msamples_s": round(value / world, 2),

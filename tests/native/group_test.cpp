@@ -3,7 +3,9 @@
 // sharded call returns, each against the one-context answer computed directly.
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <random>
+#include <thread>
 #include <vector>
 
 #include "../../assignment-for-aae6102_gnss-sdr_amd/csrc/group.h"
@@ -134,6 +136,47 @@ int main()
             ts.push_back({serial_status(sub), first});
         }
         CHECK(group::tracking_status(ts) == serial_status(st));
+    }
+    // the same with the call's channel list permuted (tr->chan need not be ascending): each
+    // member reports the CHANNEL id that failed first, converted to its list position
+    // (fail_position); the one-context rule is the first failing channel in LIST order
+    for (int it = 0; it < 20000; it++) {
+        const int n = 1 + (int)(rng() % 33), m = 1 + (int)(rng() % 9);
+        std::vector<int32_t> chans((size_t)n);
+        for (int i = 0; i < n; i++) chans[(size_t)i] = i;
+        std::shuffle(chans.begin(), chans.end(), rng);
+        std::vector<int> st_of((size_t)n, GNSS_OK);  // status by channel id
+        for (int c = 0; c < n; c++) {
+            const unsigned r = rng() % 12;
+            st_of[(size_t)c] = r == 0 ? GNSS_EIO : r == 1 ? GNSS_EINDEX : r == 2 ? GNSS_EDEVICE : GNSS_OK;
+        }
+        std::vector<int> in_order;
+        for (int32_t c : chans) in_order.push_back(st_of[(size_t)c]);
+        const auto shards = group::deal(n, m);
+        std::vector<group::TrackStatus> ts;
+        for (int k = 0; k < m; k++) {
+            std::vector<int> sub;
+            int fail_chan = -1;
+            for (int i : shards[(size_t)k]) {
+                const int c = chans[(size_t)i];
+                sub.push_back(st_of[(size_t)c]);
+                if (st_of[(size_t)c] && fail_chan < 0) fail_chan = c;
+            }
+            ts.push_back({serial_status(sub), group::fail_position(shards[(size_t)k], chans, fail_chan)});
+        }
+        CHECK(group::tracking_status(ts) == serial_status(in_order));
+    }
+    // reciprocal_exact_cached from many threads at once (the group's member threads): one
+    // answer per key, equal to the uncached check (run under -fsanitize=thread by the test)
+    {
+        const double fs[4] = {58e6, 26e6, 38.192e6, 5.714e6};
+        std::vector<int> got(32, -1);
+        std::vector<std::thread> th;
+        for (int t = 0; t < 32; t++)
+            th.emplace_back([&, t]() { got[(size_t)t] = group::reciprocal_exact_cached(fs[t % 4], 20000 + 1000 * (t % 4)); });
+        for (auto& x : th) x.join();
+        for (int t = 0; t < 32; t++) CHECK(got[(size_t)t] == group::reciprocal_exact(fs[t % 4], 20000 + 1000 * (t % 4)));
+        CHECK(group::reciprocal_exact(58e6, 600000) == 1);
     }
     // by_device: first-appearance order, members of a device in order
     {

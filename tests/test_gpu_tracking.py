@@ -258,6 +258,24 @@ def test_argument_errors_raise(pkg, ctx, opensky_short):
     assert T.prns() == [26]
 
 
+def test_wide_tap_set_is_an_index_error(pkg, ctx, opensky_short):
+    """11 taps spanning more than the persistent loop's 30-chip tap window (kTapSpan) are no
+    argument error: they take the per-step path, where a tap 16 chips early indexes
+    Code(ceil(t) + 1) below 1 on the first step, MATLAB's index error (trackingCT.m:96-100) ->
+    GNSS_EINDEX. The context stays usable."""
+    skip, cfg, data = opensky_short
+    file, signal, acq, track = params(pkg, skip, data[: 2 * 58000 * 1400])
+    track.msToProcessCT_1ms, track.msToProcessCT_10ms = 700, 200
+    A = acquired_of([26], [57908], [4581800.0])
+    taps = list(pkg.colon(-0.5, 0.1, 0.5))
+    taps[1], taps[-2] = -16.0, 16.0  # (E, P, L at -0.5, 0, 0.5 stay)
+    with pytest.raises(pkg.abi.GnssError) as e:
+        pkg.trackingCT(file, signal, track, A, ctx=ctx, taps=taps)
+    assert e.value.status == pkg.abi.EINDEX
+    T, cn0, cx = pkg.trackingCT(file, signal, track, A, ctx=ctx)
+    assert T.prns() == [26]
+
+
 def test_file_route_positioned_reads(pkg, ctx, opensky_short, tmp_path):
     """file.fileRoute path (positioned reads) == in-memory record."""
     skip, cfg, data = opensky_short

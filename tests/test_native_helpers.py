@@ -54,10 +54,19 @@ def test_multi_device_bookkeeping(tmp_path):
     cxx = shutil.which("g++") or HIPCC
     src = os.path.join(ROOT, "tests", "native", "group_test.cpp")
     exe = tmp_path / "group_test"
-    subprocess.run([cxx, "-O2", "-std=c++17", "-o", str(exe), src], check=True, capture_output=True)
+    subprocess.run([cxx, "-O2", "-std=c++17", "-pthread", "-o", str(exe), src], check=True, capture_output=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches 0" in r.stdout
+    # the same under ThreadSanitizer: the member threads' shared host state (the reciprocal
+    # cache) has no data race
+    tsan = tmp_path / "group_test_tsan"
+    b = subprocess.run([cxx, "-O1", "-g", "-std=c++17", "-pthread", "-fsanitize=thread", "-o", str(tsan), src],
+                       capture_output=True, text=True)
+    if b.returncode == 0:
+        r = subprocess.run([str(tsan)], capture_output=True, text=True)
+        if "FATAL: ThreadSanitizer: unexpected memory mapping" not in r.stderr:  # (TSan vs this kernel's ASLR)
+            assert r.returncode == 0 and "WARNING: ThreadSanitizer" not in r.stderr, r.stdout + r.stderr[-3000:]
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
