@@ -14,6 +14,7 @@
 #   acqpmc4      FETCH / WRITE passes of the config-4 acquisition's correlator kernels -> gpurun_out/traffic_cfg4.json
 #   acqprof1     kernel stats of the config-2 acquisition, passes on one stream -> gpurun_out/acq_onestream_summary.txt
 #   acqpipe      config-2 / config-4 acquisition timing, batches on one stream vs pipelined (tools/acq_only.py)
+#   spawn        bench.py --gpus 2 without a launcher (own ranks, gloo, one device)
 #   cfg4         bench --workload cfg4 -> gpurun_out/bench_cfg4.json
 #   cfg5         bench --workload cfg5 -> gpurun_out/bench_cfg5.json
 #   vt           tools/vt_only.py: the VT loop's wall / kernel time per step -> gpurun_out/vt_only.txt
@@ -77,6 +78,10 @@ for step in "$@"; do
         "tools/acq_only.py with ACQ_CFG=4 (the bench's config-4 record, 32 PRNs x 81 bins x 10 ms, fp64), the correlator's kernels (forward rows/cols, inverse cols/rows)" \
         "fwd_rows_kernel<13" "fwd_cols_kernel<13" "inv_cols_kernel<13" "inv_rows_kernel_f64<13>" || exit 1
       rm -f gpurun_out/a4_*/**/*kernel_trace.csv ;;
+    spawn)  # bench.py --gpus 2 with no launcher: its own two ranks, both on device 0 over gloo (the
+      # one-GPU rehearsal of the driver's `python3 bench.py --gpus N`; SPAWN_WL = workload)
+      BENCH_FORCE_DEVICE=0 BENCH_DIST_BACKEND=gloo timeout -k 10 500 python3 bench.py --gpus 2 --workload ${SPAWN_WL:-cfg2+3} --steps 2 --warmup 1 --no-cpu --no-profile-pass $BENCH_ARGS > gpurun_out/bench_spawn.json 2> gpurun_out/bench_spawn.err \
+        && tail -1 gpurun_out/bench_spawn.json | cut -c1-900 || { tail -20 gpurun_out/bench_spawn.err; exit 1; } ;;
     cfg4)
       timeout -k 10 400 python3 bench.py --workload cfg4 $BENCH_ARGS > gpurun_out/bench_cfg4.json 2> gpurun_out/bench_cfg4.err \
         && tail -1 gpurun_out/bench_cfg4.json | cut -c1-500 || { tail -20 gpurun_out/bench_cfg4.err; exit 1; } ;;
