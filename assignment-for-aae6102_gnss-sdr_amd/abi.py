@@ -179,6 +179,8 @@ PROTOTYPES = {
     "gnss_ctx_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
     "gnss_ctx_create_multi": (C.c_int, [C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_void_p)]),
     "gnss_ctx_members": (C.c_int, [C.c_void_p]),
+    "gnss_ctx_drop_record": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "gnss_ctx_resident_records": (C.c_int, [C.c_void_p]),
     "gnss_device_count": (C.c_int, []),
     "gnss_ctx_destroy": (None, [C.c_void_p]),
     "gnss_last_error": (C.c_char_p, [C.c_void_p]),

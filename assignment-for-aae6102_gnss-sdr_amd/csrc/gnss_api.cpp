@@ -60,7 +60,35 @@ struct gnss_ctx {
     std::vector<gnss_ctx*> members;
     bool member = false;  // a group's member: dev_data on another device is copied in (xGMI)
     int fail_chan = -1;   // tracking: the channel whose status the last call returned (group.h)
+    // (a member) its resident copies of dev_data records on another device: one peer copy per
+    // record, kept across calls (group.h ResidentCache; the copy is a hipMalloc of this device)
+    gnss::group::ResidentCache<void*> resident;
 };
+
+// frees a member's resident record copy (on that member's device)
+static void release_resident(void* p)
+{
+    if (p) (void)hipFree(p);
+}
+
+// drops the resident copies of every member of ctx that overlap [p, p + n) (n == 0: the records
+// containing p; p == nullptr: all of them); returns how many were dropped
+static int drop_resident(gnss_ctx* ctx, const void* p, uint64_t n)
+{
+    int k = 0;
+    for (gnss_ctx* m : ctx->members) {
+        (void)hipSetDevice(m->device);
+        if (m->stream) (void)hipStreamSynchronize(m->stream);  // (no kernel still reads a copy)
+        if (!p) {
+            k += (int)m->resident.m.size();
+            m->resident.clear(release_resident);
+        } else {
+            k += m->resident.drop_overlapping(p, n, release_resident);
+        }
+    }
+    (void)hipSetDevice(ctx->device);
+    return k;
+}
 
 // Timing-probe hooks read from the environment in probe builds only (tools/build_probe.sh
 // passes -DGNSS_PROBE_BUILD=1); the product library reads no environment variable.
@@ -309,21 +337,31 @@ int stage_window(gnss_ctx* ctx, const gnss_file* f, int64_t lo, int64_t hi, IfWi
             return GNSS_OK;
         }
         // a group member whose record lives on another device of the node (devices[0]): the
-        // range [lo, hi) into this device's HBM by one peer copy over xGMI
-        const int64_t n = hi - lo;
-        HIP_TRY(w.own.alloc((size_t)n + 64));
-        Events ev;
-        HIP_TRY(hipEventRecord(ev.a, ctx->stream));
-        if (n > 0)
-            HIP_TRY(hipMemcpyPeerAsync(w.own.p, ctx->device, static_cast<const int8_t*>(f->dev_data) + lo,
-                                       pd < 0 ? ctx->device : pd, (size_t)n, ctx->stream));
-        HIP_TRY(hipEventRecord(ev.b, ctx->stream));
-        HIP_TRY(hipEventSynchronize(ev.b));
-        ctx->timing.h2d_bytes += n;
-        ctx->timing.h2d_ms += ev.ms();
-        w.ptr = w.own.as<int8_t>();
-        w.base = lo;
-        w.len = n;
+        // whole record into this device's HBM by one peer copy over xGMI, on the first call that
+        // reads it; it stays resident for the later calls (group.h ResidentCache) until the
+        // library writes into the record or the caller drops it (gnss_ctx_drop_record)
+        const void* const* hit = ctx->resident.find(f->dev_data, (uint64_t)flen);
+        if (!hit) {
+            void* copy = nullptr;
+            HIP_TRY(hipMalloc(&copy, (size_t)flen + 64));
+            Events ev;
+            HIP_TRY(hipEventRecord(ev.a, ctx->stream));
+            if (flen > 0 && hipMemcpyPeerAsync(copy, ctx->device, f->dev_data, pd < 0 ? ctx->device : pd,
+                                               (size_t)flen, ctx->stream) != hipSuccess) {
+                (void)hipStreamSynchronize(ctx->stream);
+                (void)hipFree(copy);
+                return fail(ctx, GNSS_EDEVICE, "peer copy of the IF record (%lld bytes)", (long long)flen);
+            }
+            HIP_TRY(hipEventRecord(ev.b, ctx->stream));
+            HIP_TRY(hipEventSynchronize(ev.b));
+            ctx->timing.h2d_bytes += flen;
+            ctx->timing.h2d_ms += ev.ms();
+            ctx->resident.put(f->dev_data, (uint64_t)flen, copy, release_resident);
+            hit = ctx->resident.find(f->dev_data, (uint64_t)flen);
+        }
+        w.ptr = static_cast<const int8_t*>(*hit);
+        w.base = 0;
+        w.len = flen;
         return GNSS_OK;
     }
     const int64_t n = hi - lo;
@@ -911,6 +949,7 @@ void gnss_ctx_destroy(gnss_ctx* ctx)
     ctx->members.clear();
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    ctx->resident.clear(release_resident);
     if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
     for (auto& kv : ctx->plans) rocfft_plan_destroy(kv.second);
     if (ctx->fft_work) (void)hipFree(ctx->fft_work);
@@ -978,9 +1017,25 @@ int gnss_dev_alloc(gnss_ctx* ctx, uint64_t nbytes, void** dev_ptr)
     return GNSS_OK;
 }
 
+int gnss_ctx_drop_record(gnss_ctx* ctx, const void* dev_ptr)
+{
+    if (!ctx) return GNSS_EARG;
+    drop_resident(ctx, dev_ptr, 0);
+    return GNSS_OK;
+}
+
+int gnss_ctx_resident_records(const gnss_ctx* ctx)
+{
+    if (!ctx) return 0;
+    int k = 0;
+    for (const gnss_ctx* m : ctx->members) k += (int)m->resident.m.size();
+    return k;
+}
+
 int gnss_dev_free(gnss_ctx* ctx, void* p)
 {
     if (!ctx) return GNSS_EARG;
+    drop_resident(ctx, p, 0);  // (the pointer may be handed out again by a later allocation)
     HIP_TRY(hipSetDevice(ctx->device));
     HIP_TRY(hipFree(p));
     return GNSS_OK;
@@ -989,6 +1044,7 @@ int gnss_dev_free(gnss_ctx* ctx, void* p)
 int gnss_dev_upload(gnss_ctx* ctx, void* dst, const void* src, uint64_t n)
 {
     if (!ctx) return GNSS_EARG;
+    drop_resident(ctx, dst, n);  // (a member's copy of these bytes is stale now)
     HIP_TRY(hipSetDevice(ctx->device));
     HIP_TRY(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
@@ -2373,6 +2429,7 @@ int gnss_synth_if_device(gnss_ctx* ctx, const gnss_synth* cfg, uint64_t sample0,
                          void* dev_dst)
 {
     if (!ctx || !cfg || !dev_dst || cfg->n_sv < 0 || cfg->n_sv > GNSS_MAX_SV) return GNSS_EARG;
+    drop_resident(ctx, dev_dst, 2 * nsamples);  // (int8 I/Q: a member's copy of these bytes is stale now)
     HIP_TRY(hipSetDevice(ctx->device));
     std::vector<float> cah((size_t)std::max(1, cfg->n_sv) * 1023);
     for (int i = 0; i < cfg->n_sv; i++) {

@@ -155,6 +155,67 @@ inline int reciprocal_exact_cached(double Fs, int64_t kmax)
     return ok;
 }
 
+// A member's resident copies of IF records that live on another device (gnss_file.dev_data on
+// devices[0]): one peer copy per record, kept across calls. Keyed by the record's device pointer;
+// an entry also holds the record's length (a call naming the same pointer with another length
+// re-copies) and the member-side copy (`copy`, owned by the caller: release(copy) frees it). A
+// library write into a record's bytes (gnss_dev_upload, gnss_synth_if_device, gnss_dev_free)
+// drops every copy that overlaps it; gnss_ctx_drop_record drops one record or all.
+template <class Copy>
+struct ResidentCache {
+    struct Entry {
+        uint64_t len;
+        Copy copy;
+    };
+    std::map<uintptr_t, Entry> m;
+    // the copy of [key, key + len) if resident with that length, else nullptr
+    const Copy* find(const void* key, uint64_t len) const
+    {
+        auto it = m.find(reinterpret_cast<uintptr_t>(key));
+        return it != m.end() && it->second.len == len ? &it->second.copy : nullptr;
+    }
+    // the entry of `key` (its old copy, if any, released first)
+    template <class Release>
+    void put(const void* key, uint64_t len, Copy copy, Release release)
+    {
+        drop(key, release);
+        m.emplace(reinterpret_cast<uintptr_t>(key), Entry{len, copy});
+    }
+    template <class Release>
+    int drop(const void* key, Release release)
+    {
+        auto it = m.find(reinterpret_cast<uintptr_t>(key));
+        if (it == m.end()) return 0;
+        release(it->second.copy);
+        m.erase(it);
+        return 1;
+    }
+    // drop every record whose bytes overlap [p, p + n) (n == 0: the records containing p)
+    template <class Release>
+    int drop_overlapping(const void* p, uint64_t n, Release release)
+    {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p), b = a + (n ? n : 1);
+        int k = 0;
+        for (auto it = m.begin(); it != m.end();) {
+            const uintptr_t lo = it->first, hi = it->first + (it->second.len ? it->second.len : 1);
+            if (lo < b && a < hi) {
+                release(it->second.copy);
+                it = m.erase(it);
+                k++;
+            } else {
+                ++it;
+            }
+        }
+        return k;
+    }
+    template <class Release>
+    void clear(Release release)
+    {
+        for (auto& kv : m) release(kv.second.copy);
+        m.clear();
+    }
+};
+
 // Timing of a group call: the members ran side by side, so durations are the slowest
 // member's and counts are summed.
 inline gnss_timing combine_timing(const std::vector<gnss_timing>& t)

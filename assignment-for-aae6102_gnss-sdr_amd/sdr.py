@@ -118,6 +118,22 @@ class Context:
         """Test hook: force one engine path (abi.OPT_*, gnss_ctx_set_option)."""
         self.check(self.lib.gnss_ctx_set_option(self.h, int(key), int(value)))
 
+    def drop_record(self, dev=None):
+        """Multi-device contexts: drop the members' resident copies of a device record (a
+        DeviceRecord, a device pointer, or None for all), gnss_ctx_drop_record; needed only when
+        the record's bytes were rewritten outside the library."""
+        if dev is None:
+            ptr = None
+        else:
+            v = getattr(dev, "ptr", dev)
+            ptr = v.value if isinstance(v, C.c_void_p) else int(v)
+        self.check(self.lib.gnss_ctx_drop_record(self.h, C.c_void_p(ptr)))
+
+    @property
+    def resident_records(self) -> int:
+        """Resident record copies held by the members (gnss_ctx_resident_records)."""
+        return int(self.lib.gnss_ctx_resident_records(self.h))
+
     def set_acq_precision(self, fp64: bool):
         """Acquisition correlation at fp64 (the reference's precision, default) or the fp32
         fast mode (gnss_ctx_set_acq_precision)."""
@@ -141,6 +157,14 @@ class DeviceRecord:
         ctx.check(ctx.lib.gnss_dev_upload(ctx.h, r.ptr, data.ctypes.data_as(C.c_void_p),
                                           C.c_uint64(data.nbytes)))
         return r
+
+    def upload(self, data: np.ndarray, offset: int = 0):
+        """Host bytes into the record at `offset` (gnss_dev_upload; a multi-device context's
+        members drop their resident copies of the record)."""
+        data = np.ascontiguousarray(data, dtype=np.int8)
+        dst = C.c_void_p(self.ptr.value + int(offset))
+        self.ctx.check(self.ctx.lib.gnss_dev_upload(self.ctx.h, dst, data.ctypes.data_as(C.c_void_p),
+                                                    C.c_uint64(data.nbytes)))
 
     def download(self, offset: int = 0, nbytes: int | None = None) -> np.ndarray:
         n = self.nbytes - offset if nbytes is None else int(nbytes)

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define GNSS_ABI_VERSION 11
+#define GNSS_ABI_VERSION 12
 
 /* ---- status codes (SURVEY §8b "Error conventions") --------------------- */
 #define GNSS_OK         0
@@ -223,6 +223,18 @@ int  gnss_ctx_create(int device, gnss_ctx **out);
  * runs on devices[0] alone. The setters apply to every member. n in 1..GNSS_MAX_DEVICES. */
 #define GNSS_MAX_DEVICES 16
 int  gnss_ctx_create_multi(const int *devices, int n, gnss_ctx **out);
+/* Record residency of a multi-device context (ABI v12): a member on another device than a
+ * gnss_file.dev_data record copies the WHOLE record into its own HBM by one peer copy (xGMI) the
+ * first time a call reads it, and keeps that copy for every later call naming the same pointer
+ * and length (gnss_timing.h2d_bytes counts the copy once). The library drops the copies that a
+ * write of its own makes stale (gnss_dev_upload, gnss_synth_if_device into the record,
+ * gnss_dev_free of it); a caller that rewrites the record by other means (its own hipMemcpy, a
+ * MATLAB gpuArray) drops it here first. dev_ptr NULL drops every resident copy. The members'
+ * copies are freed by gnss_ctx_destroy. No-ops for a one-device context. Replaces nothing in the
+ * reference (SDR_main.m:22,38 re-read the file on every call). */
+int  gnss_ctx_drop_record(gnss_ctx *ctx, const void *dev_ptr);
+/* Resident record copies held by the context's members (0 for a one-device context). */
+int  gnss_ctx_resident_records(const gnss_ctx *ctx);
 /* HIP devices visible to this process (0 without a GPU or runtime). */
 int  gnss_device_count(void);
 /* Members of a context (1 for gnss_ctx_create). */

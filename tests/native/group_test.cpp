@@ -178,6 +178,30 @@ int main()
         for (int t = 0; t < 32; t++) CHECK(got[(size_t)t] == group::reciprocal_exact(fs[t % 4], 20000 + 1000 * (t % 4)));
         CHECK(group::reciprocal_exact(58e6, 600000) == 1);
     }
+    // ResidentCache (a member's resident copies of dev_data records): hit only with the same
+    // pointer and length; a re-put releases the old copy; writes drop every overlapping record
+    {
+        int released = 0;
+        auto rel = [&](int c) { released += c; };
+        group::ResidentCache<int> rc;
+        char rec[4096];
+        CHECK(rc.find(rec, 1000) == nullptr);
+        rc.put(rec, 1000, 7, rel);
+        CHECK(rc.find(rec, 1000) && *rc.find(rec, 1000) == 7);
+        CHECK(rc.find(rec, 999) == nullptr && rc.find(rec + 1, 1000) == nullptr);
+        rc.put(rec, 999, 8, rel);  // same pointer, other length: the old copy is released
+        CHECK(released == 7 && rc.m.size() == 1 && *rc.find(rec, 999) == 8);
+        rc.put(rec + 2000, 100, 100, rel);
+        CHECK(rc.drop_overlapping(rec + 1500, 500, rel) == 0);           // between the two records
+        CHECK(rc.drop_overlapping(rec + 2099, 1, rel) == 1 && released == 107);  // the last byte of the second
+        CHECK(rc.drop_overlapping(rec + 998, 0, rel) == 1 && released == 115);   // a pointer inside the first
+        CHECK(rc.m.empty());
+        rc.put(rec, 10, 1, rel);
+        rc.put(rec + 10, 10, 2, rel);
+        CHECK(rc.drop(rec + 5, rel) == 0 && rc.drop(rec + 10, rel) == 1 && released == 117);
+        rc.clear(rel);
+        CHECK(rc.m.empty() && released == 118);
+    }
     // by_device: first-appearance order, members of a device in order
     {
         const auto g = group::by_device({0, 1, 0, 2, 1, 0});

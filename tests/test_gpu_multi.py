@@ -91,6 +91,54 @@ def test_multi_context_device_io_peer_path(pkg, ctx, mctx, opensky_short, tmp_pa
     dev_keep.free()
 
 
+def test_multi_context_record_stays_resident(pkg, ctx, mctx, opensky_short):
+    """a member copies a dev_data record on another device (here: the
+    FORCE_PEER path on one GPU) ONCE and keeps it -- the second call moves no bytes
+    (h2d_bytes == 0) and gives the same bits; a write into the record through the library
+    (gnss_dev_upload) drops the stale copies, the next call copies again and sees the new bytes;
+    gnss_ctx_drop_record drops them explicitly (SDR_main.m:22,38 through INTEGRATION.md's MEX)."""
+    skip, cfg, data = opensky_short
+    file, signal, acq, track = params(pkg, skip, data)
+    track.msToProcessCT_1ms, track.msToProcessCT_10ms = 700, 200
+    A = acquired_of([3, 16, 22, 26], [3684, 26051, 2611, 57908], [4580975.0, 4579675.0, 4581525.0, 4581800.0])
+    one = pkg.trackingCT(file, signal, track, A, ctx=ctx, raw=True)
+    dev = pkg.DeviceRecord.from_host(mctx, data)
+    file.data, file.dev = None, dev
+    mctx.set_option(pkg.abi.OPT_FORCE_PEER, 1)
+    try:
+        assert mctx.resident_records == 0
+        a = pkg.trackingCT(file, signal, track, A, ctx=mctx, raw=True)
+        t1 = mctx.timing()
+        assert mctx.resident_records == 3  # (one copy per member: every member read the record)
+        b = pkg.trackingCT(file, signal, track, A, ctx=mctx, raw=True)
+        t2 = mctx.timing()
+        assert t1["h2d_bytes"] == 3 * data.nbytes and t2["h2d_bytes"] == 0
+        assert np.array_equal(a.rec, one.rec) and np.array_equal(b.rec, one.rec)
+        # the acquisition reads the same resident copies
+        acq.freqMin, acq.freqNum, acq.freqStep, acq.datalen, acq.L = -7000, 29, 500, 4, 10
+        g1 = pkg.acquisition(file, signal, acq, ctx=mctx, prn_list=[3, 16, 22, 26])
+        assert mctx.timing()["h2d_bytes"] == 0
+        # rewrite the record through the library (every byte negated): the copies are dropped and
+        # the next call tracks the new bytes
+        z = np.clip(-data.astype(np.int16), -128, 127).astype(np.int8)
+        dev.upload(z)
+        assert mctx.resident_records == 0
+        c = pkg.trackingCT(file, signal, track, A, ctx=mctx, raw=True)
+        assert mctx.timing()["h2d_bytes"] == 3 * data.nbytes
+        ref = pkg.trackingCT(params(pkg, skip, z)[0], signal, track, A, ctx=ctx, raw=True)
+        assert np.array_equal(c.rec, ref.rec) and not np.array_equal(c.rec, one.rec)
+        mctx.drop_record(dev)
+        assert mctx.resident_records == 0
+        pkg.acquisition(file, signal, acq, ctx=mctx, prn_list=[3, 16, 22, 26])
+        assert mctx.resident_records == 3 and mctx.timing()["h2d_bytes"] == 3 * data.nbytes
+        mctx.drop_record(None)
+        assert mctx.resident_records == 0
+        del g1
+    finally:
+        mctx.set_option(pkg.abi.OPT_FORCE_PEER, 0)
+        dev.free()
+
+
 def test_multi_context_errors_match_one(pkg, ctx, mctx, opensky_short):
     """A short record: the sharded call returns the one-context status (GNSS_EIO for the 10-ms
     phase's read past EOF, trackingCT.m:442) and the group stays usable; bad device lists are
