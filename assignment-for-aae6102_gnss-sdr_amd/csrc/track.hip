@@ -164,6 +164,54 @@ __device__ __forceinline__ double wave_at(double kd, double f, double phi0, doub
     return y + phi0;
 }
 
+// sin and cos of a small argument (|x| <= ~40 rad: the lane's reduced carrier phase, the rotation
+// table's phi[m]) with a short dependent chain, for the correlator's lane rotation and the
+// rotation table (GNSS_FAST_SINCOS; 0 = the device library's sincos). Reduction by pi/2 in two
+// parts (q * PIO2_HI exact for |q| < 2^20: PIO2_HI has 33 significant bits), then the classic
+// fdlibm minimax kernels on [-pi/4, pi/4] (__kernel_sin / __kernel_cos, error < 1 ulp), the two
+// polynomials evaluated side by side, and the quadrant's swap / negation by selects. Accuracy is
+// the library's (< 1 ulp); the bits differ from it in the last place for some arguments, which
+// moves the tracking sums by rounding only (the parity tests judge them against the oracle).
+#ifndef GNSS_FAST_SINCOS
+#define GNSS_FAST_SINCOS 0
+#endif
+__device__ __forceinline__ void sincos_small(double x, double* sn, double* cs)
+{
+    constexpr double kTwoOverPi = 6.36619772367581382433e-01;
+    constexpr double kPio2Hi = 1.57079632673412561417e+00;  // first 33 bits of pi/2
+    constexpr double kPio2Lo = 6.07710050650619224932e-11;  // RN(pi/2 - kPio2Hi)
+    const double q = rint(x * kTwoOverPi);
+    double y = __builtin_fma(-q, kPio2Hi, x);  // exact (q * kPio2Hi exact, |x - q*kPio2Hi| small)
+    const double t = q * kPio2Lo;              // (fdlibm __ieee754_rem_pio2's first round)
+    const double yh = y - t;
+    const double yl = (y - yh) - t;            // the tail of the reduced argument
+    y = yh;
+    const double z = y * y;
+    // __kernel_sin(y, yl, 1) and __kernel_cos(y, yl) (fdlibm, public domain)
+    const double rs = __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z,
+        1.58969099521155010221e-10, -2.50507602534068634195e-08), 2.75573137070700676789e-06),
+        -1.98412698298579493134e-04), 8.33333333332248946124e-03);
+    const double rc = z * __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z,
+        __builtin_fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
+        -2.75573143513906633035e-07), 2.48015872894767294178e-05), -1.38888888888741095749e-03),
+        4.16666666666666019037e-02);
+    const double v = z * y;
+    const double s = y - ((z * (0.5 * yl - v * rs) - yl) - v * -1.66666666666666324348e-01);
+    const double hz = 0.5 * z;
+    const double w = 1.0 - hz;
+    const double c = w + (((1.0 - w) - hz) + (z * rc - y * yl));
+    const int n = (int)q & 3;
+    const double a = (n & 1) ? c : s, b = (n & 1) ? s : c;
+    *sn = (n & 2) ? -a : a;
+    *cs = ((n + 1) & 2) ? -b : b;
+}
+
+__device__ __forceinline__ void sincos_table(double x, double* sn, double* cs)
+{
+    if constexpr (GNSS_FAST_SINCOS) sincos_small(x, sn, cs);
+    else sincos(x, sn, cs);
+}
+
 // sin/cos of a carrier phase Wave (up to ~3e5 rad): reduced by 2*pi as a double-double
 // first (W - k*kTwoPi is exact: both are multiples of 2^-50 below 8 in magnitude), so the
 // library's small-argument path runs instead of its Payne-Hanek reduction.
@@ -172,7 +220,7 @@ __device__ __forceinline__ void sincos_wave(double W, double* sn, double* cs)
     const double k = rint(W * (1.0 / kTwoPi));
     double r = __builtin_fma(-k, kTwoPi, W);
     r = __builtin_fma(-k, kTwoPiLo, r);
-    sincos(r, sn, cs);
+    sincos_table(r, sn, cs);
 }
 
 // The NCO state a step is prepared from.
@@ -414,7 +462,7 @@ __device__ __forceinline__ void prepare_desc_i(const P& p, const NcoState& c, in
             // phi[m] rounds once (m*dhi is exact)
             const double ph = (double)lane * dhi + (double)lane * dlo;
             double sn, cs;
-            sincos(ph, &sn, &cs);
+            sincos_table(ph, &sn, &cs);
             d->phi[lane] = ph;
             d->rcs[lane] = make_double2(cs, sn);
             if (lane == 0) {
@@ -799,6 +847,12 @@ __device__ __forceinline__ unsigned ca_bits_ext(unsigned cabits, int lane)
     return cabits;
 }
 
+#ifndef GNSS_REGCAP
+#define GNSS_REGCAP 0  // (lane_correlate: 1 = tap prefixes captured in registers at 3 taps)
+#endif
+#ifndef GNSS_PHI_REG
+#define GNSS_PHI_REG 0  // (lane_correlate: 1 = the rotation basis phi[m] formed in registers)
+#endif
 #ifndef GNSS_TAPWIN
 #define GNSS_TAPWIN 1  // (A/B: 0 = per-tap colon element, scalar tap loads and two code shuffles)
 #endif
@@ -852,7 +906,7 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
     if constexpr (TW) {
         const int64_t nn = n - 1;
         const bool mid = 2 * kf == nn, lower = kf <= nn / 2;
-        const double KD = (double)kf * d, NKD = (double)(nn - kf) * d;
+        const double KD = (double)(int)kf * d, NKD = (double)(int)(nn - kf) * d;  // (indices < 2^31: 32-bit conversions)
         int c0i[NT];
         int cmin = 0x7fffffff;
 #pragma unroll
@@ -861,7 +915,7 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
             const double post = lds_at(posts, s);
             const double t0 = (mid ? (a + c) / 2 : lower ? a + KD : c - NKD) + post;
             const double c0 = ceil(t0);
-            const double R = (double)(kf - ks) + (c0 - t0) * inv_d;  // samples to the boundary
+            const double R = (double)(int)(kf - ks) + (c0 - t0) * inv_d;  // samples to the boundary
             const double rr = rint(R);
             int pb = (int)floor(R) + 1;
             if (fabs(R - rr) < 1e-6) {  // too close to call in floating point: exact colon value
@@ -904,7 +958,7 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
         const double post = p.tap_post[s];
         const double t0 = colon_elem(col, kf) + post;
         const double c0 = ceil(t0);
-        const double R = (double)(kf - ks) + (c0 - t0) * inv_d;  // samples to the boundary
+        const double R = (double)(int)(kf - ks) + (c0 - t0) * inv_d;  // samples to the boundary
         const double rr = rint(R);
         int pb = (int)floor(R) + 1;
         if (fabs(R - rr) < 1e-6) {  // too close to call in floating point: exact colon value
@@ -925,7 +979,7 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
     }
 
     // ---- carrier base of the lane
-    const double kb = (double)ks;
+    const double kb = (double)(int)ks;
     const double Wb = wave_at<DIVIDE>(kb, f, phi0, Fs, rFs);
     double sb, cb;
     if constexpr ((GNSS_CORR_PROBE & 1) != 0) {
@@ -955,6 +1009,18 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
         mu_i = uni(dp->mu_i);
     }
 
+    // GNSS_REGCAP (3 taps, no capture queue): each tap's prefix is taken from the running sum in
+    // registers at its capture sample by a select, instead of through the LDS slots (a 16-B store
+    // per sample and a read per tap per subgroup): the correlate's only LDS traffic is then the
+    // rotation table's reads, which no store ahead of them delays. Same values, same bits.
+    constexpr bool RC = GNSS_REGCAP && !QC && NT <= 3;
+    // GNSS_PHI_REG: the rotation basis phi[m] = m*dhi + m*dlo formed in registers (as
+    // prepare_desc forms the table entry: the same operations, the same bits) instead of read
+    double dhi_l = 0.0, dlo_l = 0.0;
+    if constexpr (GNSS_PHI_REG) {
+        dhi_l = uni(dp->dhi);
+        dlo_l = uni(dp->dlo);
+    }
     // one 8-sample subgroup: running sums into the LDS slots, tap prefixes captured
     auto subgroup = [&](const int j) {
         // fmt 0: 8 int8 I/Q pairs in one 16-B group; fmt 1: 8 int16 I/Q pairs in two
@@ -1006,7 +1072,10 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
                 // w = x * (rc + i rs) * (1 + i eta): the first-order residue folded into the
                 // rotation, the products accumulated by FMA into the running sums
                 const double W = wave_at<DIVIDE>(kbj + (double)mm, f, phi0, Fs, rFs);
-                const double eta = (W - Wb) - dp->phi[m];
+                double phm;
+                if constexpr (GNSS_PHI_REG) phm = (double)m * dhi_l + (double)m * dlo_l;
+                else phm = dp->phi[m];
+                const double eta = (W - Wb) - phm;
                 const double2 rcs = ld_rcs(dp, m);
                 const double rc = __builtin_fma(-eta, rcs.y, rcs.x);
                 const double rs = __builtin_fma(eta, rcs.x, rcs.y);
@@ -1021,11 +1090,18 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
             if constexpr (QC) {
                 if ((cmask >> m) & 1u)
                     myslot[__builtin_popcount(cmask & ((1u << m) - 1u)) * T] = make_double2(run_r, run_i);
+            } else if constexpr (RC) {
+#pragma unroll
+                for (int s = 0; s < NT; s++) {
+                    const bool at = cap[s] == m;
+                    pre_r[s] = at ? run_r : pre_r[s];
+                    pre_i[s] = at ? run_i : pre_i[s];
+                }
             } else {
                 myslot[mm * T] = make_double2(run_r, run_i);
             }
         }
-        if constexpr (!QC) {
+        if constexpr (!QC && !RC) {
 #pragma unroll
             for (int s = 0; s < NT; s++) {
                 const unsigned idx = (unsigned)(cap[s] - 8 * j);
@@ -1038,7 +1114,7 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
 #ifndef GNSS_UNROLL_TAPS
 #define GNSS_UNROLL_TAPS 0  // (A/B: 1 = the > 3-tap subgroup loop unrolled like the 3-tap one)
 #endif
-    if constexpr (RELOAD && NT > 3 && !GNSS_UNROLL_TAPS) {
+    if constexpr (RELOAD && ((NT > 3 && !GNSS_UNROLL_TAPS) || (RC && GNSS_REGCAP == 2))) {
         // descriptor in LDS: one subgroup at a time (unrolled, the compiler would keep
         // every subgroup's table values live)
 #pragma unroll 1

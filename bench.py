@@ -116,6 +116,11 @@ def parse():
                          "shards and result gathers on host arrays only (no GPU, no library: a CPU check "
                          "of the N-rank path, never a bench line)")
     ap.add_argument("--n10-cfg5", type=int, default=90000, help="cfg5 msToProcessCT_10ms")
+    ap.add_argument("--multi-ctx", type=int, default=0,
+                    help="N > 0: the headline step in ONE process through the C-ABI's multi-device context "
+                         "(gnss_ctx_create_multi over devices 0..N-1, the path INTEGRATION.md's MEX takes for "
+                         "SDR_main.m:22,38) instead of torch.distributed ranks; BENCH_MULTI_DEVICES=0,0 lists "
+                         "the devices explicitly (a one-GPU rehearsal)")
     return ap.parse_args()
 
 
@@ -461,6 +466,14 @@ def main():
     pkg = importlib.import_module("assignment-for-aae6102_gnss-sdr_amd")
     if args.workload == "dist-selftest":
         return run_dist_selftest(args)
+    if args.multi_ctx > 0:
+        if args.gpus > 1 or args.workload != "cfg2+3":
+            sys.exit("bench.py: --multi-ctx runs the cfg2+3 step in one process (no --gpus)")
+        import torch  # noqa: F401
+        devs = [int(x) for x in os.environ.get("BENCH_MULTI_DEVICES", "").split(",") if x.strip()] or \
+            list(range(args.multi_ctx))
+        ctx = pkg.Context(devices=devs)
+        return run_headline(args, 0, 1, devs[0], None, ctx, multi=devs)
     rank, world, local, dist = setup_dist(args)
     import torch  # noqa: F401  (before the library: device-resident outputs are torch tensors)
     ctx = pkg.Context(local)
@@ -468,6 +481,13 @@ def main():
         return run_cfg5(args, rank, world, local, dist, ctx)
     if args.workload == "cfg4":
         return run_cfg4(args, rank, world, local, dist, ctx)
+    return run_headline(args, rank, world, local, dist, ctx)
+
+
+def run_headline(args, rank, world, local, dist, ctx, multi=None):
+    """The headline step (acquisition cfg2 + trackingCT cfg3), on torch.distributed ranks
+    (world > 1), on one GPU, or (multi = the device list) in one process through the C-ABI's
+    multi-device context, whose members deal the PRNs and channels among themselves."""
     import importlib as _il
     D = _il.import_module("assignment-for-aae6102_gnss-sdr_amd.dist")
     file, signal, acq, track, _, _ = pkg.initParameters()
@@ -539,8 +559,10 @@ def main():
     t0 = time.perf_counter()
     acq_units = trk_units = 0
     acq_ms = trk_ms = acq_corr_ms = acq_fine_ms = 0.0
+    h2d = 0  # record bytes copied in the timed steps (multi-device context: 0, the copies stay resident)
     for _ in range(args.steps):
         A, ta, tt, buf, shards = one_step()
+        h2d += int(ta["h2d_bytes"]) + int(tt["h2d_bytes"])
         acq_units += ta["acq_hypothesis_samples"]
         trk_units += tt["track_channel_samples"]
         acq_ms += ta["acq_ms"]
@@ -568,6 +590,8 @@ def main():
     # launch with hipEvents on the ctx stream; algorithmic bytes = 2 B (int8 I + Q) per
     # channel-sample of the launch.
     roof = None
+    if multi:  # (the group's timing combines its members': the per-launch roofline is the N = 1 line's)
+        args.no_profile_pass, args.no_cpu = True, True
     if not args.no_profile_pass:
         ctx.set_profiling(True)
         pkg.trackingCT(file, signal, track, A, ctx=ctx, channels=mine, raw=True, out=outs[0])
@@ -636,7 +660,7 @@ def main():
         "metric": "correlator Msamples/s (acq+track), whole job",
         "value": round(value, 2),
         "unit": "Msamples/s",
-        "n_gpus": world,
+        "n_gpus": world if not multi else len(set(multi)),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(step_ms, 3),
@@ -649,12 +673,16 @@ def main():
         "data": "synthetic Opensky-shape IF (int8 I/Q, Fs 58 MHz, IF 4.58 MHz), resident in HBM",
         "config": {"workload": "acquisition cfg2 (32 PRN, +-7kHz/500Hz, 20 ms) + trackingCT cfg3 "
                                f"({nch} ch, 1000 ms @1ms + {args.n10} ms @10ms, E/P/L)",
-                   "parallelism": f"PRNs and channels x{world} (one record, strong scaling)",
+                   "parallelism": (f"PRNs and channels x{world} (one record, strong scaling)" if not multi else
+                                   f"C-ABI multi-device context, members on devices {multi} (one process; "
+                                   "PRNs and channels dealt over the members, record resident per member)"),
                    "prns_per_rank": len(my_prns), "channels_per_rank": len(mine),
                    "prns_by_rank": [len(D.shard(len(prns), world, r)) for r in range(world)],
                    "channels_by_rank": [len(x) for x in shards]},
         **dist_world(dist),
         "outputs_ok": outputs_ok,
+        **({"multi_ctx": {"devices": multi, "members": ctx.members, "resident_records": ctx.resident_records,
+                          "record_bytes_copied_in_timed_steps": h2d}} if multi else {}),
         "acquired": [int(x) for x in A.sv],
         "per_gpu_Msamples_s": round(value / world, 2),
         "acq_Msamples_s": round(acq_units / (acq_ms * 1e-3) / 1e6, 2) if acq_ms else None,

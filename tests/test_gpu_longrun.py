@@ -85,10 +85,11 @@ PATH5_MORE = [os.path.join(GOLDEN, f"golden_cfg5_long_{k}.npz") for k in ("b", "
 # trackingCT.m:473,480), and the switch kicks their carrier 15-23 Hz off, beyond its pull-in; they
 # were locked through the 1-ms phase (profiles/r06_cfg5_lock.txt, tools/cfg5_lockdiag.py).
 CFG5_MAX_PARTED = 8
-# |t_gpu - t_oracle| bound for a tie (chips): a locked channel's states agree to ~3e-10 chip in
-# remChip, an unlocked one's to ~6e-9 (the loop amplifies the difference); the observed tie margins
-# are printed by the test (profiles/r06_cfg5_parity.txt) and the bounds sit above them
-TIE_TOL = {True: 1e-8, False: 1e-7}  # (locked, unlocked)
+# |t_gpu - t_oracle| bound for a tie (chips), set about ten times above the margins observed on
+# MI355X (printed by the test, profiles/r06_cfg5_parity.txt): locked channels 1.8e-12 .. 3.2e-10
+# (channels 7, 20, 27, 30), the unlocked channel 19 6.1e-9 -- its loop amplifies the states'
+# difference, so a 1e-9 bound would misclassify that observed tie
+TIE_TOL = {True: 3e-9, False: 6e-8}  # (locked, unlocked)
 
 
 def _post_flip_checks(pkg, b, c, got, iv, rtaps, rnco, F, ints, nco, n1, st, ref_cn0, rlock):

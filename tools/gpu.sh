@@ -82,6 +82,10 @@ for step in "$@"; do
       # one-GPU rehearsal of the driver's `python3 bench.py --gpus N`; SPAWN_WL = workload)
       BENCH_FORCE_DEVICE=0 BENCH_DIST_BACKEND=gloo timeout -k 10 500 python3 bench.py --gpus 2 --workload ${SPAWN_WL:-cfg2+3} --steps 2 --warmup 1 --no-cpu --no-profile-pass $BENCH_ARGS > gpurun_out/bench_spawn.json 2> gpurun_out/bench_spawn.err \
         && tail -1 gpurun_out/bench_spawn.json | cut -c1-900 || { tail -20 gpurun_out/bench_spawn.err; exit 1; } ;;
+    multictx)  # the headline through the C-ABI multi-device context in one process (MULTI_DEVICES, default 0,0
+      # on the one-GPU box: two members on device 0, one after the other)
+      BENCH_MULTI_DEVICES=${MULTI_DEVICES:-0,0} timeout -k 10 500 python3 bench.py --multi-ctx 2 --steps 3 --warmup 1 $BENCH_ARGS > gpurun_out/bench_multictx.json 2> gpurun_out/bench_multictx.err \
+        && tail -1 gpurun_out/bench_multictx.json | cut -c1-1200 || { tail -20 gpurun_out/bench_multictx.err; exit 1; } ;;
     cfg4)
       timeout -k 10 400 python3 bench.py --workload cfg4 $BENCH_ARGS > gpurun_out/bench_cfg4.json 2> gpurun_out/bench_cfg4.err \
         && tail -1 gpurun_out/bench_cfg4.json | cut -c1-500 || { tail -20 gpurun_out/bench_cfg4.err; exit 1; } ;;
