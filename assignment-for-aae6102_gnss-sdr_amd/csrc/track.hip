@@ -173,7 +173,7 @@ __device__ __forceinline__ double wave_at(double kd, double f, double phi0, doub
 // the library's (< 1 ulp); the bits differ from it in the last place for some arguments, which
 // moves the tracking sums by rounding only (the parity tests judge them against the oracle).
 #ifndef GNSS_FAST_SINCOS
-#define GNSS_FAST_SINCOS 0
+#define GNSS_FAST_SINCOS 1
 #endif
 __device__ __forceinline__ void sincos_small(double x, double* sn, double* cs)
 {
