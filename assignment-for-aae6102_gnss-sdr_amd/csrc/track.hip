@@ -882,14 +882,18 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
     const double f = uni(dp->f), phi0 = uni(dp->phi0);
     const double Fs = p.Fs, rFs = p.inv_Fs;
 
-    // ---- valid samples of the lane: [lo, hi) (only the window's two end lanes are partial)
-    const int lo = ks < 0 ? (int)(-ks < M ? -ks : M) : 0;
-    const int hi = n - ks < M ? (n - ks > 0 ? (int)(n - ks) : 0) : M;
+    // ---- valid samples of the lane: [lo, hi) (only the window's two end lanes are partial);
+    // window-relative sample indices are below 2^31 (a step reads <= kMaxBpc * 256 * 32 samples),
+    // so the index arithmetic is 32-bit
+    const int ksi = (int)ks, ni = (int)n;
+    const int lo = ksi < 0 ? (-ksi < M ? -ksi : M) : 0;
+    const int hi = ni - ksi < M ? (ni - ksi > 0 ? ni - ksi : 0) : M;
 
     // ---- code replica per tap: chip c0 at the first valid sample, the sample p of the
     // lane's (single) chip boundary, and the two code values around it
-    const int64_t kf0 = ks + lo;
-    const int64_t kf = kf0 < 0 ? 0 : (kf0 > n - 1 ? n - 1 : kf0);
+    const int kfi0 = ksi + lo;
+    const int kfi = kfi0 < 0 ? 0 : (kfi0 > ni - 1 ? ni - 1 : kfi0);
+    const int64_t kf = kfi;
     int cap[NT];
     // code values around each tap's boundary as sign bits (bit s set: -1): a0 before it,
     // a1 after; v1 = a1 and dv = a0 - a1 are rebuilt in the epilogue (2 VGPRs, not 4*NT)
@@ -902,32 +906,56 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
     // (ca_bits_ext) instead of two shuffles per tap: the taps' chips at the lane start lie within
     // kTapSpan chips of each other (the host checks the tap offsets). The same values as
     // colon_elem and ca_index32, so the same bits.
+    // Round 6: every tap's common case straight-line and branch-free (the colon end by selects,
+    // 32-bit indices), and ONE rare branch for the lanes where any tap's boundary is too close to
+    // call in floating point or that hold the colon's middle element: they redo that tap's search
+    // exactly as before (the fast path's R is fused, the exact path's is not; both give the same
+    // cap wherever the fast path is used: its R lies more than 1e-6 from an integer).
     constexpr bool TW = GNSS_TAPWIN && RELOAD && (GNSS_CORR_PROBE & 66) == 0;
     if constexpr (TW) {
-        const int64_t nn = n - 1;
-        const bool mid = 2 * kf == nn, lower = kf <= nn / 2;
-        const double KD = (double)(int)kf * d, NKD = (double)(int)(nn - kf) * d;  // (indices < 2^31: 32-bit conversions)
+        const int nn = ni - 1;
+        const bool mid = 2 * kfi == nn, lower = kfi <= nn / 2;
+        const double KD = (double)kfi * d, NKD = (double)(nn - kfi) * d;
+        const double kend = lower ? KD : -NKD;  // a + KD (lower half), c - NKD = c + (-NKD) (upper)
+        const double dk = (double)(kfi - ksi);
         int c0i[NT];
         int cmin = 0x7fffffff;
+        bool exact = mid;
 #pragma unroll
         for (int s = 0; s < NT; s++) {
             const double a = lds_at(dp->tap_a, s), c = lds_at(dp->tap_c, s);
-            const double post = lds_at(posts, s);
-            const double t0 = (mid ? (a + c) / 2 : lower ? a + KD : c - NKD) + post;
+            const double t0 = ((lower ? a : c) + kend) + lds_at(posts, s);
             const double c0 = ceil(t0);
-            const double R = (double)(int)(kf - ks) + (c0 - t0) * inv_d;  // samples to the boundary
-            const double rr = rint(R);
-            int pb = (int)floor(R) + 1;
-            if (fabs(R - rr) < 1e-6) {  // too close to call in floating point: exact colon value
-                const int ms = (int)rr;
-                pb = ms;
-                const int64_t kx = ks + ms;
-                if (ms >= 0 && ms < M && kx >= 0 && kx <= n - 1)
-                    pb = ceil(colon_elem(Colon{a, d, c, nn}, kx) + post) > c0 ? ms : ms + 1;
-            }
+            const double R = __builtin_fma(c0 - t0, inv_d, dk);  // samples to the boundary
+            exact = exact || fabs(R - rint(R)) < 1e-6;
+            const int pb = (int)floor(R) + 1;
             cap[s] = (pb < M ? pb : M) - 1;  // Prefix(p) = running sum through sample p-1
-            if constexpr ((GNSS_CORR_PROBE & 32) != 0) cap[s] = M - 1 - s;
             c0i[s] = (int)c0;
+        }
+        if (exact) {  // (rare) this lane's search as the general form does it, tap by tap
+#pragma unroll
+            for (int s = 0; s < NT; s++) {
+                const double a = lds_at(dp->tap_a, s), c = lds_at(dp->tap_c, s);
+                const double post = lds_at(posts, s);
+                const double t0 = (mid ? (a + c) / 2 : lower ? a + KD : c - NKD) + post;
+                const double c0 = ceil(t0);
+                const double R = dk + (c0 - t0) * inv_d;
+                const double rr = rint(R);
+                int pb = (int)floor(R) + 1;
+                if (fabs(R - rr) < 1e-6) {  // too close to call in floating point: exact colon value
+                    const int ms = (int)rr;
+                    pb = ms;
+                    const int64_t kx = ks + ms;
+                    if (ms >= 0 && ms < M && kx >= 0 && kx <= n - 1)
+                        pb = ceil(colon_elem(Colon{a, d, c, (int64_t)nn}, kx) + post) > c0 ? ms : ms + 1;
+                }
+                cap[s] = (pb < M ? pb : M) - 1;
+                c0i[s] = (int)c0;
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < NT; s++) {
+            if constexpr ((GNSS_CORR_PROBE & 32) != 0) cap[s] = M - 1 - s;
             cmin = c0i[s] < cmin ? c0i[s] : cmin;
         }
         const unsigned ib = ca_index32(cmin + p.chip_off);
