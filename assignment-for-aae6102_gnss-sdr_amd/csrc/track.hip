@@ -847,6 +847,9 @@ __device__ __forceinline__ unsigned ca_bits_ext(unsigned cabits, int lane)
     return cabits;
 }
 
+#ifndef GNSS_SWP
+#define GNSS_SWP 0  // (lane_correlate: 1 / 2 = the next sample's Wave formed one sample ahead)
+#endif
 #ifndef GNSS_REGCAP
 #define GNSS_REGCAP 0  // (lane_correlate: 1 = tap prefixes captured in registers at 3 taps)
 #endif
@@ -1049,6 +1052,12 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
         dhi_l = uni(dp->dhi);
         dlo_l = uni(dp->dlo);
     }
+    // GNSS_SWP (A/B knob): the next sample's exact Wave formed one sample ahead (before this
+    // sample's rotation and accumulation), so two independent dependency chains are in flight;
+    // 2 also fences each sample's instructions from the next one's (sched_barrier), so the
+    // scheduler interleaves exactly those two chains. Same operations, same bits.
+    double Wpipe = 0.0;
+    if constexpr (GNSS_SWP) Wpipe = wave_at<DIVIDE>(kb + 1.0, f, phi0, Fs, rFs);
     // one 8-sample subgroup: running sums into the LDS slots, tap prefixes captured
     auto subgroup = [&](const int j) {
         // fmt 0: 8 int8 I/Q pairs in one 16-B group; fmt 1: 8 int16 I/Q pairs in two
@@ -1099,7 +1108,13 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
             } else if (m > 0) {
                 // w = x * (rc + i rs) * (1 + i eta): the first-order residue folded into the
                 // rotation, the products accumulated by FMA into the running sums
-                const double W = wave_at<DIVIDE>(kbj + (double)mm, f, phi0, Fs, rFs);
+                double W;
+                if constexpr (GNSS_SWP) {
+                    W = Wpipe;
+                    if (m + 1 < M) Wpipe = wave_at<DIVIDE>(kbj + (double)(mm + 1), f, phi0, Fs, rFs);
+                } else {
+                    W = wave_at<DIVIDE>(kbj + (double)mm, f, phi0, Fs, rFs);
+                }
                 double phm;
                 if constexpr (GNSS_PHI_REG) phm = (double)m * dhi_l + (double)m * dlo_l;
                 else phm = dp->phi[m];
@@ -1128,6 +1143,7 @@ __device__ __forceinline__ void lane_correlate(const TrkParams& p, const Desc* d
             } else {
                 myslot[mm * T] = make_double2(run_r, run_i);
             }
+            if constexpr (GNSS_SWP == 2) __builtin_amdgcn_sched_barrier(0);
         }
         if constexpr (!QC && !RC) {
 #pragma unroll
