@@ -41,12 +41,12 @@ CLOCK_GHZ = 2.4
 SAMPLES_PER_MS = 58000  # Opensky Fs 58 MHz
 # counter evidence read by the bench, newest first; each file carries the source digest it was
 # measured at (tools/srcdigest.py) and the line says whether it matches the running tree
-TRAFFIC_FILES = ("traffic_r05.json", "traffic_r04.json", "traffic_r03.json", "traffic_r02.json")          # PMC bytes per 10-ms launch
-TRACK_SQ_FILES = ("r05_track_sq.json", "r04_track_sq.json", "r03_track_sq.json")                            # SQ counters of the tracking launches
-ACQ_BOUND_FILES = ("acq_bound_r05.json", "acq_bound_r04.json", "acq_bound_r03.json", "acq_bound_r02.json")     # fp64 acquisition kernels (tools/acq_bound.py)
-TRAFFIC_FILES_CFG5 = ("traffic_cfg5_r05.json", "traffic_cfg5_r04.json", "traffic_cfg5_r03.json", "traffic_cfg5_r02.json")  # the 11-tap 10-ms launch
-CFG5_SQ_FILES = ("r05_cfg5_sq.json", "r04_cfg5_sq.json", "r03_cfg5_sq.json")
-TRAFFIC_FILES_CFG4 = ("traffic_cfg4_r05.json", "traffic_cfg4_r04.json", "traffic_cfg4_r03.json")  # the config-4 correlator's kernels, bytes per call
+TRAFFIC_FILES = ("traffic_r06.json", "traffic_r05.json", "traffic_r04.json", "traffic_r03.json", "traffic_r02.json")          # PMC bytes per 10-ms launch
+TRACK_SQ_FILES = ("r06_track_sq.json", "r05_track_sq.json", "r04_track_sq.json", "r03_track_sq.json")                            # SQ counters of the tracking launches
+ACQ_BOUND_FILES = ("acq_bound_r06.json", "acq_bound_r05.json", "acq_bound_r04.json", "acq_bound_r03.json", "acq_bound_r02.json")     # fp64 acquisition kernels (tools/acq_bound.py)
+TRAFFIC_FILES_CFG5 = ("traffic_cfg5_r06.json", "traffic_cfg5_r05.json", "traffic_cfg5_r04.json", "traffic_cfg5_r03.json", "traffic_cfg5_r02.json")  # the 11-tap 10-ms launch
+CFG5_SQ_FILES = ("r06_cfg5_sq.json", "r05_cfg5_sq.json", "r04_cfg5_sq.json", "r03_cfg5_sq.json")
+TRAFFIC_FILES_CFG4 = ("traffic_cfg4_r06.json", "traffic_cfg4_r05.json", "traffic_cfg4_r04.json", "traffic_cfg4_r03.json")  # the config-4 correlator's kernels, bytes per call
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 import srcdigest  # noqa: E402
 
