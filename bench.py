@@ -140,13 +140,30 @@ def spawn_ranks(n):
     anything imports the HIP library or torch, so it never touches a GPU; the children are new
     processes (no fork of GPU state, no exec). Rank 0 prints the one JSON line. If a child fails,
     the others are terminated and the parent exits with that child's status."""
+    import ctypes
+    import signal
     import subprocess
     port = _free_port()
     procs = []
+
+    def die_with_parent():  # (in the child, before exec: SIGTERM when this parent dies, even by SIGKILL)
+        try:
+            ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
+        except OSError:
+            pass
+
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), BENCH_SPAWNED="1")
-        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      preexec_fn=die_with_parent))
+
+    def forward(signum, _frame):  # a launcher's SIGTERM / SIGINT reaches every rank
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signum)
+    signal.signal(signal.SIGTERM, forward)
+    signal.signal(signal.SIGINT, forward)
     status = 0
     live = list(procs)
     while live:
@@ -415,6 +432,10 @@ def run_dist_selftest(args):
         dist, rank, world = tdist, tdist.get_rank(), tdist.get_world_size()
     if os.environ.get("BENCH_SELFTEST_FAIL_RANK") == str(rank):  # (test hook: a failing rank)
         sys.exit(3)
+    if os.environ.get("BENCH_SELFTEST_SLEEP"):  # (test hook: a busy rank, its pid recorded)
+        with open(os.environ["BENCH_SELFTEST_PIDFILE"], "a") as fh:
+            fh.write(f"{os.getpid()}\n")
+        time.sleep(float(os.environ["BENCH_SELFTEST_SLEEP"]))
     t0 = time.perf_counter()
     prns = list(range(1, 33))
     mine = [prns[i] for i in D.shard(32, world, rank)]

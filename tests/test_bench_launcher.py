@@ -44,3 +44,32 @@ def test_failing_rank_fails_the_job():
     p = _run(2, {"BENCH_SELFTEST_FAIL_RANK": "1"})
     assert p.returncode != 0
     assert "rank 1 exited" in p.stderr
+
+
+def test_terminating_the_launcher_stops_the_ranks(tmp_path):
+    """SIGTERM to the parent (a driver's time limit) reaches the spawned ranks: none is left
+    running on its GPU (BENCH_SELFTEST_SLEEP keeps the ranks busy)."""
+    import signal
+    import time
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["BENCH_SELFTEST_SLEEP"] = "60"
+    env["BENCH_SELFTEST_PIDFILE"] = str(tmp_path / "pids")
+    p = subprocess.Popen([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--workload",
+                          "dist-selftest"], env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    deadline = time.time() + 60
+    while time.time() < deadline and len((tmp_path / "pids").read_text().split() if (tmp_path / "pids").exists() else []) < 2:
+        time.sleep(0.2)
+    pids = [int(x) for x in (tmp_path / "pids").read_text().split()]
+    assert len(pids) == 2
+    p.send_signal(signal.SIGTERM)
+    p.wait(timeout=60)
+    assert p.returncode != 0
+    time.sleep(1.0)
+    for pid in pids:
+        try:
+            os.kill(pid, 0)
+            alive = True
+        except ProcessLookupError:
+            alive = False
+        assert not alive, pid
