@@ -22,6 +22,7 @@
 #include <vector>
 #include <fcntl.h>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <tuple>
@@ -116,15 +117,16 @@ constexpr int kAcqPairFront = 60;
 constexpr int kFineBatch = 16;
 
 // The context's pinned host buffer `key`, at least `bytes` (contents undefined).
+// (`flags`: hipHostMalloc's; a key is always asked for with the same flags)
 template <class T>
-T* pinned_buffer(gnss_ctx* ctx, const char* key, size_t count)
+T* pinned_buffer(gnss_ctx* ctx, const char* key, size_t count, unsigned flags = hipHostMallocDefault)
 {
     auto& e = ctx->pinned[key];
     const size_t want = std::max<size_t>(count * sizeof(T), 16);
     if (e.second < want) {
         if (e.first) (void)hipHostFree(e.first);
         e = {nullptr, 0};
-        if (hipHostMalloc(&e.first, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+        if (hipHostMalloc(&e.first, want, flags) != hipSuccess) return nullptr;
         e.second = want;
     }
     return static_cast<T*>(e.first);
@@ -2229,6 +2231,29 @@ int gnss_tracking_vt_step(gnss_ctx* ctx, const gnss_file* file, const gnss_signa
     return gnss_tracking_vt_run(ctx, file, sg, tr, pdi, n, 1, chans, codeFreq_new, out);
 }
 
+namespace {
+// Wait until every channel's record of VT step `seq` is posted (vt_step_kernel's completion
+// words, coherent host memory). The stream is polled now and then, so a grid that ends without
+// posting (a fault) surfaces as its error rather than a hang.
+hipError_t wait_posted(hipStream_t stream, const unsigned* done, int n, unsigned seq)
+{
+    auto posted = [&] {
+        int i = 0;
+        while (i < n && __atomic_load_n(done + i, __ATOMIC_ACQUIRE) == seq) i++;
+        return i == n;
+    };
+    for (unsigned k = 1;; k++) {
+        if (posted()) return hipSuccess;
+        if ((k & 255) == 0) {
+            const hipError_t e = hipStreamQuery(stream);
+            if (e == hipErrorNotReady) continue;
+            if (e != hipSuccess) return e;
+            return posted() ? hipSuccess : hipErrorLaunchFailure;  // (retired: its posts are visible)
+        }
+    }
+}
+}  // namespace
+
 // trackingVT_POS_updated.m:157-476, the whole EKF-driven loop: per step, each channel's read
 // size (:164) and predicted code frequency (:180-227, gnss_vt_nav_predict, host), the
 // correlations and scalar ends of all channels in ONE launch of the VT kernel (the channel
@@ -2282,8 +2307,10 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     HIP_TRY(d_out.alloc(ctx, "vt.out", sizeof(gnss_vt_out) * (size_t)n));
     HIP_TRY(d_ca.alloc(ctx, "vt.ca", sizeof(unsigned) * cab.size()));
     double* h_cf = pinned_buffer<double>(ctx, "vt.cf", (size_t)n);
-    gnss_vt_out* h_out = pinned_buffer<gnss_vt_out>(ctx, "vt.out", (size_t)n);
-    if (!h_cf || !h_out) return fail(ctx, GNSS_EDEVICE, "pinned VT step buffers");
+    gnss_vt_out* h_out = pinned_buffer<gnss_vt_out>(ctx, "vt.out", (size_t)n, hipHostMallocCoherent);
+    unsigned* h_done = pinned_buffer<unsigned>(ctx, "vt.done", (size_t)n, hipHostMallocCoherent);
+    if (!h_cf || !h_out || !h_done) return fail(ctx, GNSS_EDEVICE, "pinned VT step buffers");
+    for (int i = 0; i < n; i++) __atomic_store_n(h_done + i, 0u, __ATOMIC_RELAXED);
     HIP_TRY(hipMemcpyAsync(d_chan.p, chans, sizeof(gnss_vt_chan) * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(d_ca.p, cab.data(), sizeof(unsigned) * cab.size(), hipMemcpyHostToDevice, ctx->stream));
     double t1, t2;
@@ -2320,6 +2347,7 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         A.part = d_part.as<double>();
         A.ticket = d_ticket.as<unsigned>();
         A.out = h_out;
+        A.done = h_done;  // (the step's records are taken as each channel posts them)
     }
     // the host's view of what sizes the next read (:164): remChip / codeFreq / file_ptr of the
     // last step, from the records the kernel returns
@@ -2330,6 +2358,14 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         cf_old[i] = chans[i].codeFreq;
         fptr[i] = chans[i].file_ptr;
     }
+    // While a step's kernel runs, the host does the navigation work that needs none of its
+    // correlations (bit for bit the work it replaces: the same functions on the same inputs):
+    // the EKF's geometry half of this step (vt_nav_gain) and every channel's orbit for the next
+    // step, whose read size follows from this step's without its samples (vt_remchip_next).
+    // An orbit is used only at the transmit time it was computed for.
+    std::vector<VtOrbit> ahead((size_t)n);
+    std::vector<char> have_ahead((size_t)n, 0);
+    std::unique_ptr<VtGain> gain(new VtGain);
     Events ev;
     double kernel_ms = 0;
     int result = GNSS_OK;
@@ -2343,7 +2379,7 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
                 break;
             }
             double cf = cf_old[i], dpr = 0, vel[3];
-            st = gnss_vt_nav_predict(nav, i, p.n, &cf, &dpr, vel);
+            st = vt_nav_predict_at(nav, i, p.n, have_ahead[(size_t)i] ? &ahead[(size_t)i] : nullptr, &cf, &dpr, vel);
             if (st) {
                 result = fail(ctx, st, "step %d channel %d: svPosVel / trop_UNB3 failed", s + 1, i);
                 break;
@@ -2371,6 +2407,7 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         A.len = w.len;
         if (multi) {  // (per-step events only in profiling mode: each is a queue command)
             for (int i = 0; i < n; i++) A.cf_arg[i] = h_cf[i];
+            A.seq = (unsigned)s + 1;
             if (ctx->profiling) HIP_TRY(hipEventRecord(ev.a, ctx->stream));
             HIP_TRY(launch_vt_step(A, ctx->stream));
             if (ctx->profiling) HIP_TRY(hipEventRecord(ev.b, ctx->stream));
@@ -2382,7 +2419,16 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
             HIP_TRY(hipMemcpyAsync(h_out, d_out.p, sizeof(gnss_vt_out) * (size_t)n, hipMemcpyDeviceToHost,
                                    ctx->stream));
         }
-        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        vt_nav_gain(*nav, gain.get());
+        for (int i = 0; i < n && s + 1 < nsteps; i++) {
+            const int64_t ns = nav->numSample[i];
+            const double rc = vt_remchip_next(sg->Fs, pdi, remChip[i], cf_new[i], ns);
+            const VtPrep q = vt_prepare(sg->Fs, sg->codelength, pdi, rc, cf_new[i], cf_new[i]);
+            have_ahead[(size_t)i] = q.n >= 1;
+            if (q.n >= 1) vt_orbit(*nav, i, vt_transmit_next(*nav, i, q.n), &ahead[(size_t)i]);
+        }
+        if (multi && !ctx->profiling) HIP_TRY(wait_posted(ctx->stream, h_done, n, (unsigned)s + 1));
+        else HIP_TRY(hipStreamSynchronize(ctx->stream));
         if (ctx->profiling || !multi) kernel_ms += ev.ms();
         for (int i = 0; i < n; i++) {
             gnss_vt_out& o = out[(size_t)s * n + i];
@@ -2406,7 +2452,7 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         }
         ctx->timing.track_launches += 1;
         if (result) break;
-        st = gnss_vt_nav_update(nav, codeError.data(), cf_new.data(), carrFreq.data(), sol ? sol + s : nullptr);
+        st = vt_nav_correct(nav, *gain, codeError.data(), cf_new.data(), carrFreq.data(), sol ? sol + s : nullptr);
         if (st) result = fail(ctx, st, "step %d: navigation update failed (singular innovation covariance)", s + 1);
     }
     HIP_TRY(hipMemcpyAsync(chans, d_chan.p, sizeof(gnss_vt_chan) * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));

@@ -635,6 +635,43 @@ GNSS_HD int vt_finish(double Fs, double ms, int pdi, int bps, double tau1carr, d
     return GNSS_OK;
 }
 
+// The vector half (vtnav.cpp) split around the VT kernel, so that gnss_tracking_vt can run
+// the parts that need no correlation of the step while the kernel runs. Host only.
+// A channel's orbit (svPosVel.m) at transmit time t: a pure function of the ephemeris and t,
+// so one computed ahead for the t the prediction then forms is the one it would compute.
+struct VtOrbit {
+    double t;
+    double sv[3], vel[3], clkm, clkv, grp;
+    int st;
+};
+// transmitTimeVT + numSample / Fs (trackingVT_POS_updated.m:181), as the prediction forms it
+double vt_transmit_next(const gnss_vt_nav& v, int i, int64_t numSample);
+void vt_orbit(const gnss_vt_nav& v, int i, double t, VtOrbit* o);
+// gnss_vt_nav_predict with an orbit computed ahead (used when its t is the step's; else computed)
+int vt_nav_predict_at(gnss_vt_nav* v, int i, int64_t numSample, const VtOrbit* ahead, double* codeFreq,
+                      double* deltaPr, double sv_vel[3]);
+// The EKF update's geometry half (:357-398 without the measurements): H, the rate prediction
+// of each channel, the gain and the updated covariance; needs the step's predictions only.
+struct VtGain {
+    int st;
+    double H[2 * GNSS_VT_MAX_CH * 8], K[8 * 2 * GNSS_VT_MAX_CH], cov[64], T[64];
+    double prr_pred[GNSS_VT_MAX_CH], clkv[GNSS_VT_MAX_CH], sv_unrot[GNSS_VT_MAX_CH][3];
+    double svr_last[3], vel_last[3], localTime;
+};
+void vt_nav_gain(const gnss_vt_nav& v, VtGain* g);
+// ... and its measurement half: gnss_vt_nav_update == vt_nav_gain then vt_nav_correct
+int vt_nav_correct(gnss_vt_nav* v, const VtGain& g, const double* codeError, const double* codeFreq,
+                   const double* carrFreq, gnss_vt_navsol* sol);
+// remChip after a step of n samples at code frequency codeFreq_new (vt_finish, :284): the read
+// sizes of a VT channel do not depend on its samples, so the next step's is known a step ahead
+inline double vt_remchip_next(double Fs, int pdi, double remChip, double codeFreq_new, int64_t n)
+{
+    const double cps = codeFreq_new / Fs;
+    const double sp = vt_spacing(15);
+    const Colon col = colon_make((0 + sp) + remChip, cps, ((double)(n - 1) * cps + sp) + remChip);
+    return (colon_elem(col, n - 1) + cps) - 1023 * pdi;
+}
+
 // calcLoopCoef.m:41-45
 GNSS_HD void calc_loop_coef(double LBW, double zeta, double k, double& t1, double& t2)
 {
@@ -660,6 +697,11 @@ struct VtRunArgs {
     unsigned* ticket;
     int nb;
     double cf_arg[GNSS_VT_MAX_CH];  // launch_vt_step: the step's code frequencies (kernel args)
+    // launch_vt_step, when set: `out` is coherent host memory, and each channel's last block
+    // writes its record through to it and then posts `seq` to done[ch] (system scope), so the
+    // host takes the step's records without waiting for the grid to retire
+    unsigned* done;
+    unsigned seq;
 };
 hipError_t launch_vt_run(const VtRunArgs& a, hipStream_t s);
 // One step of the n channels over n x nb blocks (int8 records; nsteps must be 1): each block

@@ -305,8 +305,20 @@ __global__ __launch_bounds__(kVtStepThreads) void vt_step_kernel(VtRunArgs a)
     // the record to the caller's buffer (pinned host memory in the EKF loop): one 8-B word per
     // lane, all posted at once
     constexpr int kW = (int)(sizeof(gnss_vt_out) / 8);
-    if (tid < kW)
-        reinterpret_cast<unsigned long long*>(a.out + ch)[tid] = reinterpret_cast<const unsigned long long*>(&s_o)[tid];
+    unsigned long long* o = reinterpret_cast<unsigned long long*>(a.out + ch);
+    const unsigned long long* w = reinterpret_cast<const unsigned long long*>(&s_o);
+    if (!a.done) {
+        if (tid < kW) o[tid] = w[tid];
+        return;
+    }
+    // with a completion word: the record's words written through to host memory and drained,
+    // then the word (the host reads the record once it sees `seq`)
+    if (tid < kW) {
+        __hip_atomic_store(o + tid, w[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(a.done + ch, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace

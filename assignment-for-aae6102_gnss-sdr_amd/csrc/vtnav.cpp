@@ -8,6 +8,7 @@
 // beside the VT correlator kernel (vt.hip); gnss_tracking_vt (gnss_api.cpp) alternates the
 // two. Built with -ffp-contract=off: every operation rounds separately, in the reference's
 // association order (line cites inline).
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 
@@ -351,6 +352,234 @@ void transition(int pdi, double ms, double* T)  // Transistion_Matrix (:40-47)
 
 }  // namespace
 
+// ---- the vector half, split around the VT kernel (gnss_internal.h) ----------------------------
+
+double gnss::vt_transmit_next(const gnss_vt_nav& v, int i, int64_t numSample)
+{
+    return v.transmitTime[i] + (double)numSample / v.Fs;  // :181
+}
+
+void gnss::vt_orbit(const gnss_vt_nav& v, int i, double t, VtOrbit* o)
+{
+    o->t = t;
+    o->st = sv_pos_vel(v.eph[i], t, o->sv, o->vel, &o->clkm, &o->clkv, &o->grp);  // :185-186
+}
+
+// :180-227 for channel i with read size numSample
+int gnss::vt_nav_predict_at(gnss_vt_nav* v, int i, int64_t numSample, const VtOrbit* ahead, double* codeFreq,
+                            double* deltaPr, double sv_vel[3])
+{
+    const double T = v->pdi * v->ms;
+    v->numSample[i] = numSample;
+    v->transmitTime[i] = vt_transmit_next(*v, i, numSample);  // :181
+    v->tot_est_tck[i] = v->transmitTime[i];
+    VtOrbit here;
+    const VtOrbit* o = ahead;
+    if (!o || o->t != v->tot_est_tck[i]) {  // (bitwise: the same t is the same orbit)
+        vt_orbit(*v, i, v->tot_est_tck[i], &here);
+        o = &here;
+    }
+    if (o->st) return o->st;
+    const double* sv = o->sv;
+    const double* estPos = v->total_state;
+    v->counter_corr[i] = v->counter_corr[i] + 1;  // :189-204
+    if (v->counter_corr[i] == 0.1 / T) {
+        double enu[3], llh[3];
+        xyz2enu(sv, estPos, enu);
+        const double el_rad = std::atan(enu[2] / std::sqrt(enu[0] * enu[0] + enu[1] * enu[1]));
+        const double az_rad = std::atan2(enu[0], enu[1]);
+        v->az[i] = az_rad * 180 / kPi;
+        v->el[i] = el_rad * 180 / kPi;
+        xyz2llh(estPos, llh);
+        v->ionodel[i] = ionocorr(v->tot_est_tck[i], sv, v->cnslxyz, v->cfg.ALPHA, v->cfg.BETA);
+        double trop;
+        const int st = trop_unb3(v->cfg.doy, llh[0] * 180 / kPi, llh[2], v->el[i], &trop);
+        if (st) return st;
+        v->tropodel[i] = std::fabs(trop);
+        v->counter_corr[i] = 0;
+    }
+    double svr[3];
+    const double pr = predicted_pr(*v, i, sv, o->clkm, o->grp, svr);  // :208-215
+    double dpr = 0;
+    if (v->msIndex > 1) {  // :218-223
+        dpr = (pr - v->predictedPr_last[i]) / T;
+        *codeFreq = v->codeFreqBasis * (1 - dpr / v->cfg.cSpeed);
+    }
+    v->predictedPr_last[i] = pr;
+    if (deltaPr) *deltaPr = dpr;  // deltaPr(svindex) keeps 0 until step 2 (:141, :221)
+    if (sv_vel)
+        for (int k = 0; k < 3; k++) sv_vel[k] = o->vel[k];
+    return GNSS_OK;
+}
+
+// :357-398 up to the measurements: every channel's geometry at the common epoch, then the
+// covariance propagation, innovation covariance, its inverse and the gain (none of them read
+// newZ: the error state before the update is 0)
+void gnss::vt_nav_gain(const gnss_vt_nav& v, VtGain* g)
+{
+    const int n = v.n, N = 2 * n;
+    g->st = GNSS_OK;
+    double* H = g->H;
+    std::memset(H, 0, sizeof(double) * N * 8);
+    int64_t nmin = v.numSample[0];  // :357-383
+    for (int i = 1; i < n; i++) nmin = std::min(nmin, v.numSample[i]);
+    nmin = nmin - 1;
+    const double* estPos = v.total_state;
+    const double* estVel = v.total_state + 3;
+    g->localTime = 0;
+    for (int i = 0; i < n; i++) {
+        const double tot = v.tot_est_tck[i] - (double)(v.numSample[i] - nmin) / v.Fs;  // :363
+        g->localTime = i == 0 ? tot : std::min(g->localTime, tot);
+        double sv[3], vel[3], clkm, clkv, grp, svr[3];
+        const int st = sv_pos_vel(v.eph[i], tot, sv, vel, &clkm, &clkv, &grp);  // :366-367
+        if (st) {
+            g->st = st;
+            return;
+        }
+        predicted_pr(v, i, sv, clkm, grp, svr);  // :369-372 (svxyzr_pos)
+        const double r = dist3(svr, estPos);
+        double a[3];
+        for (int k = 0; k < 3; k++) a[k] = (svr[k] - estPos[k]) / r;  // :374
+        for (int k = 0; k < 3; k++) {
+            H[i * 8 + k] = -a[k];
+            H[(n + i) * 8 + 3 + k] = -a[k];
+        }
+        H[i * 8 + 6] = 1;
+        H[(n + i) * 8 + 7] = 1;
+        for (int k = 0; k < 3; k++) {
+            g->svr_last[k] = svr[k];
+            g->vel_last[k] = vel[k];
+            g->sv_unrot[i][k] = sv[k];
+        }
+        g->prr_pred[i] = (estVel[0] - vel[0]) * a[0] + (estVel[1] - vel[1]) * a[1] +
+                         (estVel[2] - vel[2]) * a[2];  // :381
+        g->clkv[i] = clkv;
+    }
+    // Kalman filter (:387-398): error_state = T * 0 = 0, so the innovation is newZ itself
+    double* T = g->T;
+    double Tt[64], TP[64], P[64];
+    transition(v.pdi, v.ms, T);
+    for (int r = 0; r < 8; r++)
+        for (int c = 0; c < 8; c++) Tt[r * 8 + c] = T[c * 8 + r];
+    matmul(T, v.state_cov, TP, 8, 8, 8);
+    matmul(TP, Tt, P, 8, 8, 8);
+    const double q[8] = {1e0, 1e0, 1e0, 1e-1, 1e-1, 1e-1, 1e-1, 1e-2};  // process_noise (:51-54)
+    for (int k = 0; k < 8; k++) P[k * 9] = P[k * 9] + q[k];
+    double Ht[8 * 2 * GNSS_VT_MAX_CH], PHt[8 * 2 * GNSS_VT_MAX_CH], HP[2 * GNSS_VT_MAX_CH * 8];
+    double S[4 * GNSS_VT_MAX_CH * GNSS_VT_MAX_CH], Si[4 * GNSS_VT_MAX_CH * GNSS_VT_MAX_CH];
+    for (int r = 0; r < N; r++)
+        for (int c = 0; c < 8; c++) Ht[c * N + r] = H[r * 8 + c];
+    matmul(P, Ht, PHt, 8, 8, N);   // state_cov * H'
+    matmul(H, P, HP, N, 8, 8);
+    matmul(HP, Ht, S, N, 8, N);    // H * state_cov * H'
+    for (int k = 0; k < N; k++) S[k * N + k] = S[k * N + k] + v.R[k];  // + mesurement_noise
+    if (!inv_lu(S, N, Si)) {  // MATLAB: inv of a singular matrix -> Inf
+        g->st = GNSS_EINDEX;
+        return;
+    }
+    matmul(PHt, Si, g->K, 8, N, N);  // kalman_gain
+    double KH[64], IKH[64];
+    matmul(g->K, H, KH, 8, N, 8);
+    for (int k = 0; k < 64; k++) IKH[k] = ((k % 9 == 0) ? 1.0 : 0.0) - KH[k];
+    matmul(IKH, P, g->cov, 8, 8, 8);  // (:398)
+}
+
+// :321, :380-382, :397-467: the measurements into newZ, the state update, the navigation
+// solution row, the next epoch's state and the measurement noise
+int gnss::vt_nav_correct(gnss_vt_nav* v, const VtGain& g, const double* codeError, const double* codeFreq,
+                         const double* carrFreq, gnss_vt_navsol* sol)
+{
+    if (g.st) return g.st;
+    const int n = v->n, N = 2 * n;
+    const double cS = v->cfg.cSpeed;
+    const double* H = g.H;
+    const double* K = g.K;
+    double Z[2 * GNSS_VT_MAX_CH];
+    for (int i = 0; i < n; i++) Z[i] = codeError[i] * cS / codeFreq[i];  // :321
+    const double clkDrift = v->total_state[7];
+    for (int i = 0; i < n; i++) {
+        const double prr_meas = (carrFreq[i] + v->IF) * cS / v->cfg.Fc;  // :380
+        Z[n + i] = g.prr_pred[i] - prr_meas - clkDrift + g.clkv[i];  // :382
+    }
+    double es[8];
+    matmul(K, Z, es, 8, N, 1);     // error_state = 0 + K * (newZ' - H * 0) (:397)
+    for (int k = 0; k < N; k++) v->recordR2[k] = v->recordR2[k] + Z[k] * Z[k];  // recordR (:395)
+    v->counterUptR += 1;
+    for (int k = 0; k < 64; k++) v->state_cov[k] = g.cov[k];  // (:398)
+    for (int k = 0; k < 8; k++) v->total_state[k] = v->total_state[k] + es[k];  // (:400-404)
+    if (sol) {  // navSolutionsVT row (:406-436), at the updated state
+        std::memset(sol, 0, sizeof *sol);
+        const double* x = v->total_state;
+        double llh[3];
+        xyz2llh(v->cnslxyz, llh);
+        const double Lb = llh[0], lb = llh[1];
+        const double Cen[3][3] = {{-std::sin(lb), std::cos(lb), 0},
+                                  {-std::sin(Lb) * std::cos(lb), -std::sin(Lb) * std::sin(lb), std::cos(Lb)},
+                                  {-std::cos(Lb) * std::cos(lb), -std::cos(Lb) * std::sin(lb), -std::sin(Lb)}};
+        mat3_vec(Cen, x + 3, sol->usrVelENU);
+        xyz2enu(x, v->cnslxyz, sol->usrPosENU);
+        xyz2llh(x, sol->usrPosLLH);
+        sol->usrPosLLH[0] = sol->usrPosLLH[0] * 180 / kPi;
+        sol->usrPosLLH[1] = sol->usrPosLLH[1] * 180 / kPi;
+        sol->localTime = g.localTime;
+        for (int k = 0; k < 3; k++) {
+            sol->usrPos[k] = x[k];
+            sol->usrVel[k] = x[3 + k];
+        }
+        sol->clkBias = x[6];
+        sol->clkDrift = x[7];
+        for (int k = 0; k < 8; k++) {
+            sol->state[k] = es[k];
+            sol->state_cov[k] = v->state_cov[k * 9];
+        }
+        double Hes[2 * GNSS_VT_MAX_CH];
+        matmul(H, es, Hes, N, 8, 1);
+        for (int k = 0; k < N; k++) {
+            sol->newZ[k] = Z[k];
+            sol->meas_inno[k] = Z[k] - Hes[k];  // (:432: with the UPDATED error_state)
+            sol->predicted_z[k] = Hes[k];       // (:434)
+        }
+        for (int i = 0; i < n; i++) {
+            sol->satEA[i] = v->el[i];
+            sol->satAZ[i] = v->az[i];
+            for (int k = 0; k < 3; k++) sol->svxyz_pos[i][k] = g.sv_unrot[i][k];
+        }
+        for (int k = 0; k < 3; k++) {
+            sol->satePos[k] = g.svr_last[k];
+            sol->sateVel[k] = g.vel_last[k];
+        }
+        for (int r = 0; r < 8; r++)
+            for (int c = 0; c < N; c++) sol->kalman_gain[r][c] = K[r * N + c];
+    }
+    // predict the state of the next epoch (:440-442)
+    double xn[8];
+    matmul(g.T, v->total_state, xn, 8, 8, 1);
+    for (int k = 0; k < 8; k++) v->total_state[k] = xn[k];
+    // measurement noise from the innovations of the last 200 / pdi steps (:445-467); MATLAB
+    // compares the integer counter with the real thresUptR = 200/track.pdi (:63), so a pdi that
+    // does not divide 200 never updates R
+    if (200 % v->pdi == 0 && v->counterUptR == 200 / v->pdi) {
+        const double w = 1.0 / v->counterUptR;
+        for (int i = 0; i < n; i++) {
+            double rc = w * v->recordR2[i] * 10, rr = w * v->recordR2[n + i] * 1;
+            rc = rc >= 12000 ? 12000 : (rc <= 0.01 ? 0.01 : rc);
+            rr = rr >= 400 ? 400 : (rr <= 0.01 ? 0.01 : rr);
+            v->R[i] = rc;
+            v->R[n + i] = rr;
+        }
+        for (int k = 0; k < N; k++) v->recordR2[k] = 0;
+        v->counterUptR = 0;
+        v->counter_r += 1;
+        if (sol) {
+            sol->r_row = v->counter_r;
+            for (int k = 0; k < N; k++) sol->R[k] = v->R[k];
+        }
+    }
+    v->msIndex += 1;
+    return GNSS_OK;
+}
+
+
 extern "C" {
 
 int gnss_sv_pos_vel(const gnss_eph_sv* eph, double t, double pos[3], double vel[3], double* clkcorr_m,
@@ -418,187 +647,16 @@ int gnss_vt_nav_predict(gnss_vt_nav* v, int32_t i, int64_t numSample, double* co
                         double sv_vel[3])
 {
     if (!v || !codeFreq || i < 0 || i >= v->n || numSample < 1) return GNSS_EARG;
-    const double T = v->pdi * v->ms;
-    v->numSample[i] = numSample;
-    v->transmitTime[i] = v->transmitTime[i] + (double)numSample / v->Fs;  // :181
-    v->tot_est_tck[i] = v->transmitTime[i];
-    double sv[3], vel[3], clkm, clkv, grp;
-    int st = sv_pos_vel(v->eph[i], v->tot_est_tck[i], sv, vel, &clkm, &clkv, &grp);  // :185-186
-    if (st) return st;
-    const double* estPos = v->total_state;
-    v->counter_corr[i] = v->counter_corr[i] + 1;  // :189-204
-    if (v->counter_corr[i] == 0.1 / T) {
-        double enu[3], llh[3];
-        xyz2enu(sv, estPos, enu);
-        const double el_rad = std::atan(enu[2] / std::sqrt(enu[0] * enu[0] + enu[1] * enu[1]));
-        const double az_rad = std::atan2(enu[0], enu[1]);
-        v->az[i] = az_rad * 180 / kPi;
-        v->el[i] = el_rad * 180 / kPi;
-        xyz2llh(estPos, llh);
-        v->ionodel[i] = ionocorr(v->tot_est_tck[i], sv, v->cnslxyz, v->cfg.ALPHA, v->cfg.BETA);
-        double trop;
-        st = trop_unb3(v->cfg.doy, llh[0] * 180 / kPi, llh[2], v->el[i], &trop);
-        if (st) return st;
-        v->tropodel[i] = std::fabs(trop);
-        v->counter_corr[i] = 0;
-    }
-    double svr[3];
-    const double pr = predicted_pr(*v, i, sv, clkm, grp, svr);  // :208-215
-    double dpr = 0;
-    if (v->msIndex > 1) {  // :218-223
-        dpr = (pr - v->predictedPr_last[i]) / T;
-        *codeFreq = v->codeFreqBasis * (1 - dpr / v->cfg.cSpeed);
-    }
-    v->predictedPr_last[i] = pr;
-    if (deltaPr) *deltaPr = dpr;  // deltaPr(svindex) keeps 0 until step 2 (:141, :221)
-    if (sv_vel)
-        for (int k = 0; k < 3; k++) sv_vel[k] = vel[k];
-    return GNSS_OK;
+    return gnss::vt_nav_predict_at(v, i, numSample, nullptr, codeFreq, deltaPr, sv_vel);
 }
 
 int gnss_vt_nav_update(gnss_vt_nav* v, const double* codeError, const double* codeFreq, const double* carrFreq,
                        gnss_vt_navsol* sol)
 {
     if (!v || !codeError || !codeFreq || !carrFreq) return GNSS_EARG;
-    const int n = v->n, N = 2 * n;
-    const double cS = v->cfg.cSpeed;
-    double Z[2 * GNSS_VT_MAX_CH], H[2 * GNSS_VT_MAX_CH * 8];
-    std::memset(H, 0, sizeof(double) * N * 8);
-    for (int i = 0; i < n; i++) Z[i] = codeError[i] * cS / codeFreq[i];  // :321
-    // :357-383, every channel's pseudorange rate measurement at the common epoch
-    int64_t nmin = v->numSample[0];
-    for (int i = 1; i < n; i++) nmin = std::min(nmin, v->numSample[i]);
-    nmin = nmin - 1;
-    const double* estPos = v->total_state;
-    const double* estVel = v->total_state + 3;
-    const double clkDrift = v->total_state[7];
-    double sv_unrot[GNSS_VT_MAX_CH][3];
-    double localTime = 0, svr_last[3] = {0, 0, 0}, vel_last[3] = {0, 0, 0};
-    for (int i = 0; i < n; i++) {
-        const double tot = v->tot_est_tck[i] - (double)(v->numSample[i] - nmin) / v->Fs;  // :363
-        localTime = i == 0 ? tot : std::min(localTime, tot);
-        double sv[3], vel[3], clkm, clkv, grp, svr[3];
-        const int st = sv_pos_vel(v->eph[i], tot, sv, vel, &clkm, &clkv, &grp);  // :366-367
-        if (st) return st;
-        predicted_pr(*v, i, sv, clkm, grp, svr);  // :369-372 (svxyzr_pos)
-        const double r = dist3(svr, estPos);
-        double a[3];
-        for (int k = 0; k < 3; k++) a[k] = (svr[k] - estPos[k]) / r;  // :374
-        for (int k = 0; k < 3; k++) {
-            H[i * 8 + k] = -a[k];
-            H[(n + i) * 8 + 3 + k] = -a[k];
-        }
-        H[i * 8 + 6] = 1;
-        H[(n + i) * 8 + 7] = 1;
-        for (int k = 0; k < 3; k++) {
-            svr_last[k] = svr[k];
-            vel_last[k] = vel[k];
-            sv_unrot[i][k] = sv[k];
-        }
-        const double prr_meas = (carrFreq[i] + v->IF) * cS / v->cfg.Fc;  // :380
-        const double prr_pred = (estVel[0] - vel[0]) * a[0] + (estVel[1] - vel[1]) * a[1] +
-                                (estVel[2] - vel[2]) * a[2];  // :381
-        Z[n + i] = prr_pred - prr_meas - clkDrift + clkv;  // :382
-    }
-    // Kalman filter (:387-398): error_state = T * 0 = 0, so the innovation is newZ itself
-    double T[64], Tt[64], TP[64], P[64];
-    transition(v->pdi, v->ms, T);
-    for (int r = 0; r < 8; r++)
-        for (int c = 0; c < 8; c++) Tt[r * 8 + c] = T[c * 8 + r];
-    matmul(T, v->state_cov, TP, 8, 8, 8);
-    matmul(TP, Tt, P, 8, 8, 8);
-    const double q[8] = {1e0, 1e0, 1e0, 1e-1, 1e-1, 1e-1, 1e-1, 1e-2};  // process_noise (:51-54)
-    for (int k = 0; k < 8; k++) P[k * 9] = P[k * 9] + q[k];
-    double Ht[8 * 2 * GNSS_VT_MAX_CH], PHt[8 * 2 * GNSS_VT_MAX_CH], HP[2 * GNSS_VT_MAX_CH * 8];
-    double S[4 * GNSS_VT_MAX_CH * GNSS_VT_MAX_CH], Si[4 * GNSS_VT_MAX_CH * GNSS_VT_MAX_CH];
-    double K[8 * 2 * GNSS_VT_MAX_CH];
-    for (int r = 0; r < N; r++)
-        for (int c = 0; c < 8; c++) Ht[c * N + r] = H[r * 8 + c];
-    matmul(P, Ht, PHt, 8, 8, N);   // state_cov * H'
-    matmul(H, P, HP, N, 8, 8);
-    matmul(HP, Ht, S, N, 8, N);    // H * state_cov * H'
-    for (int k = 0; k < N; k++) S[k * N + k] = S[k * N + k] + v->R[k];  // + mesurement_noise
-    if (!inv_lu(S, N, Si)) return GNSS_EINDEX;  // MATLAB: inv of a singular matrix -> Inf
-    matmul(PHt, Si, K, 8, N, N);   // kalman_gain
-    double es[8];
-    matmul(K, Z, es, 8, N, 1);     // error_state = 0 + K * (newZ' - H * 0) (:397)
-    for (int k = 0; k < N; k++) v->recordR2[k] = v->recordR2[k] + Z[k] * Z[k];  // recordR (:395)
-    v->counterUptR += 1;
-    double KH[64], IKH[64];
-    matmul(K, H, KH, 8, N, 8);
-    for (int k = 0; k < 64; k++) IKH[k] = ((k % 9 == 0) ? 1.0 : 0.0) - KH[k];
-    matmul(IKH, P, v->state_cov, 8, 8, 8);  // (:398)
-    for (int k = 0; k < 8; k++) v->total_state[k] = v->total_state[k] + es[k];  // (:400-404)
-    if (sol) {  // navSolutionsVT row (:406-436), at the updated state
-        std::memset(sol, 0, sizeof *sol);
-        const double* x = v->total_state;
-        double llh[3];
-        xyz2llh(v->cnslxyz, llh);
-        const double Lb = llh[0], lb = llh[1];
-        const double Cen[3][3] = {{-std::sin(lb), std::cos(lb), 0},
-                                  {-std::sin(Lb) * std::cos(lb), -std::sin(Lb) * std::sin(lb), std::cos(Lb)},
-                                  {-std::cos(Lb) * std::cos(lb), -std::cos(Lb) * std::sin(lb), -std::sin(Lb)}};
-        mat3_vec(Cen, x + 3, sol->usrVelENU);
-        xyz2enu(x, v->cnslxyz, sol->usrPosENU);
-        xyz2llh(x, sol->usrPosLLH);
-        sol->usrPosLLH[0] = sol->usrPosLLH[0] * 180 / kPi;
-        sol->usrPosLLH[1] = sol->usrPosLLH[1] * 180 / kPi;
-        sol->localTime = localTime;
-        for (int k = 0; k < 3; k++) {
-            sol->usrPos[k] = x[k];
-            sol->usrVel[k] = x[3 + k];
-        }
-        sol->clkBias = x[6];
-        sol->clkDrift = x[7];
-        for (int k = 0; k < 8; k++) {
-            sol->state[k] = es[k];
-            sol->state_cov[k] = v->state_cov[k * 9];
-        }
-        double Hes[2 * GNSS_VT_MAX_CH];
-        matmul(H, es, Hes, N, 8, 1);
-        for (int k = 0; k < N; k++) {
-            sol->newZ[k] = Z[k];
-            sol->meas_inno[k] = Z[k] - Hes[k];  // (:432: with the UPDATED error_state)
-            sol->predicted_z[k] = Hes[k];       // (:434)
-        }
-        for (int i = 0; i < n; i++) {
-            sol->satEA[i] = v->el[i];
-            sol->satAZ[i] = v->az[i];
-            for (int k = 0; k < 3; k++) sol->svxyz_pos[i][k] = sv_unrot[i][k];
-        }
-        for (int k = 0; k < 3; k++) {
-            sol->satePos[k] = svr_last[k];
-            sol->sateVel[k] = vel_last[k];
-        }
-        for (int r = 0; r < 8; r++)
-            for (int c = 0; c < N; c++) sol->kalman_gain[r][c] = K[r * N + c];
-    }
-    // predict the state of the next epoch (:440-442)
-    double xn[8];
-    matmul(T, v->total_state, xn, 8, 8, 1);
-    for (int k = 0; k < 8; k++) v->total_state[k] = xn[k];
-    // measurement noise from the innovations of the last 200 / pdi steps (:445-467); MATLAB
-    // compares the integer counter with the real thresUptR = 200/track.pdi (:63), so a pdi that
-    // does not divide 200 never updates R
-    if (200 % v->pdi == 0 && v->counterUptR == 200 / v->pdi) {
-        const double w = 1.0 / v->counterUptR;
-        for (int i = 0; i < n; i++) {
-            double rc = w * v->recordR2[i] * 10, rr = w * v->recordR2[n + i] * 1;
-            rc = rc >= 12000 ? 12000 : (rc <= 0.01 ? 0.01 : rc);
-            rr = rr >= 400 ? 400 : (rr <= 0.01 ? 0.01 : rr);
-            v->R[i] = rc;
-            v->R[n + i] = rr;
-        }
-        for (int k = 0; k < N; k++) v->recordR2[k] = 0;
-        v->counterUptR = 0;
-        v->counter_r += 1;
-        if (sol) {
-            sol->r_row = v->counter_r;
-            for (int k = 0; k < N; k++) sol->R[k] = v->R[k];
-        }
-    }
-    v->msIndex += 1;
-    return GNSS_OK;
+    gnss::VtGain g;
+    gnss::vt_nav_gain(*v, &g);
+    return gnss::vt_nav_correct(v, g, codeError, codeFreq, carrFreq, sol);
 }
 
 }  // extern "C"
