@@ -2232,16 +2232,12 @@ int gnss_tracking_vt_step(gnss_ctx* ctx, const gnss_file* file, const gnss_signa
 }
 
 namespace {
-// Wait until every channel's record of VT step `seq` is posted (vt_step_kernel's completion
-// words, coherent host memory). The stream is polled now and then, so a grid that ends without
-// posting (a fault) surfaces as its error rather than a hang.
-hipError_t wait_posted(hipStream_t stream, const unsigned* done, int n, unsigned seq)
+// Wait until VT step `seq` is posted (vt_step_kernel's completion word, coherent host
+// memory). The stream is polled now and then, so a grid that ends without posting (a fault)
+// surfaces as its error rather than a hang.
+hipError_t wait_posted(hipStream_t stream, const unsigned* done, unsigned seq)
 {
-    auto posted = [&] {
-        int i = 0;
-        while (i < n && __atomic_load_n(done + i, __ATOMIC_ACQUIRE) == seq) i++;
-        return i == n;
-    };
+    auto posted = [&] { return __atomic_load_n(done, __ATOMIC_ACQUIRE) == seq; };
     for (unsigned k = 1;; k++) {
         if (posted()) return hipSuccess;
         if ((k & 255) == 0) {
@@ -2256,8 +2252,10 @@ hipError_t wait_posted(hipStream_t stream, const unsigned* done, int n, unsigned
 
 // trackingVT_POS_updated.m:157-476, the whole EKF-driven loop: per step, each channel's read
 // size (:164) and predicted code frequency (:180-227, gnss_vt_nav_predict, host), the
-// correlations and scalar ends of all channels in ONE launch of the VT kernel (the channel
-// states stay in HBM between steps), then the EKF (:357-467, gnss_vt_nav_update, host).
+// correlations of all channels in ONE launch of the VT kernel, each channel's scalar end
+// (vt_finish, :284-347), then the EKF (:357-467, gnss_vt_nav_update, host). int8 records: the
+// channel states stay on the host and the kernel returns each channel's sums (vt_step_kernel);
+// int16 (per-read means first): vt_run_kernel runs the whole step, states in HBM.
 int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg, const gnss_track* tr, int32_t n,
                      int32_t nsteps, gnss_vt_chan* chans, gnss_vt_nav* nav, gnss_vt_out* out, gnss_vt_navsol* sol)
 {
@@ -2301,20 +2299,44 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     if (st) return st;
     std::vector<unsigned> cab((size_t)n * 32);
     for (int i = 0; i < n; i++) ca_bits(chans[i].prn, &cab[(size_t)i * 32]);
-    DevBuf d_chan, d_cf, d_out, d_ca;
-    HIP_TRY(d_chan.alloc(ctx, "vt.chan", sizeof(gnss_vt_chan) * (size_t)n));
-    HIP_TRY(d_cf.alloc(ctx, "vt.cf", sizeof(double) * (size_t)n));
-    HIP_TRY(d_out.alloc(ctx, "vt.out", sizeof(gnss_vt_out) * (size_t)n));
-    HIP_TRY(d_ca.alloc(ctx, "vt.ca", sizeof(unsigned) * cab.size()));
-    double* h_cf = pinned_buffer<double>(ctx, "vt.cf", (size_t)n);
-    gnss_vt_out* h_out = pinned_buffer<gnss_vt_out>(ctx, "vt.out", (size_t)n, hipHostMallocCoherent);
-    unsigned* h_done = pinned_buffer<unsigned>(ctx, "vt.done", (size_t)n, hipHostMallocCoherent);
-    if (!h_cf || !h_out || !h_done) return fail(ctx, GNSS_EDEVICE, "pinned VT step buffers");
-    for (int i = 0; i < n; i++) __atomic_store_n(h_done + i, 0u, __ATOMIC_RELAXED);
-    HIP_TRY(hipMemcpyAsync(d_chan.p, chans, sizeof(gnss_vt_chan) * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(hipMemcpyAsync(d_ca.p, cab.data(), sizeof(unsigned) * cab.size(), hipMemcpyHostToDevice, ctx->stream));
     double t1, t2;
     calc_loop_coef(tr->PLLBW, tr->PLLDamp, tr->PLLGain, t1, t2);
+    // int8 records: each step over nb blocks per channel (vt_step_kernel), the step's reads
+    // in the kernel arguments and each channel's two sums posted to coherent host memory (no
+    // copy commands per step); int16 (per-read means first): one block per channel (vt_run_kernel)
+    const bool multi = prec == 1;
+    DevBuf d_chan, d_cf, d_out, d_ca, d_part, d_ticket;
+    double* h_cf = pinned_buffer<double>(ctx, "vt.cf", (size_t)n);
+    gnss_vt_out* h_out = pinned_buffer<gnss_vt_out>(ctx, "vt.out", (size_t)n);
+    if (!h_cf || !h_out) return fail(ctx, GNSS_EDEVICE, "pinned VT step buffers");
+    std::vector<gnss_vt_chan> hc(chans, chans + n);  // (int8: the channel states)
+    std::vector<VtPrep> pk((size_t)n);
+    std::vector<int> bad((size_t)n, 0);
+    VtStepArgs B{};
+    int nb = 1;
+    if (multi) {
+        nb = (int)std::min<int64_t>(std::max<int64_t>(1, (nominal + kVtStepSamples - 1) / kVtStepSamples),
+                                    GNSS_VT_MAX_BLOCKS);
+        if (ctx->opt[GNSS_OPT_VT_BLOCKS] > 0) nb = (int)ctx->opt[GNSS_OPT_VT_BLOCKS];
+        B.sums = pinned_buffer<double>(ctx, "vt.sums", 2 * (size_t)n, hipHostMallocCoherent);
+        B.done = pinned_buffer<unsigned>(ctx, "vt.done", 1, hipHostMallocCoherent);
+        if (!B.sums || !B.done) return fail(ctx, GNSS_EDEVICE, "pinned VT step buffers");
+        HIP_TRY(d_part.alloc(ctx, "vt.part", sizeof(double) * 2 * (size_t)n * nb));
+        B.part = d_part.as<double>();
+        __atomic_store_n(B.done, 0u, __ATOMIC_RELAXED);
+        HIP_TRY(d_ticket.alloc(ctx, "vt.ticket", sizeof(unsigned)));
+        HIP_TRY(hipMemsetAsync(d_ticket.p, 0, sizeof(unsigned), ctx->stream));
+        B.ticket = d_ticket.as<unsigned>();
+        B.Fs = sg->Fs;
+        B.real8 = dtyp == 1;
+    } else {
+        HIP_TRY(d_chan.alloc(ctx, "vt.chan", sizeof(gnss_vt_chan) * (size_t)n));
+        HIP_TRY(d_cf.alloc(ctx, "vt.cf", sizeof(double) * (size_t)n));
+        HIP_TRY(d_out.alloc(ctx, "vt.out", sizeof(gnss_vt_out) * (size_t)n));
+        HIP_TRY(d_ca.alloc(ctx, "vt.ca", sizeof(unsigned) * cab.size()));
+        HIP_TRY(hipMemcpyAsync(d_chan.p, chans, sizeof(gnss_vt_chan) * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(d_ca.p, cab.data(), sizeof(unsigned) * cab.size(), hipMemcpyHostToDevice, ctx->stream));
+    }
     VtRunArgs A{};
     A.file_len = flen;
     A.chans = d_chan.as<gnss_vt_chan>();
@@ -2331,24 +2353,6 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     A.pdi = pdi;
     A.prec = prec;
     A.dtype = dtyp;
-    // int8 records: each step over nb blocks per channel (vt_step_kernel), the step's code
-    // frequencies in the kernel arguments and its records written to pinned host memory (no
-    // copy commands per step); int16 (per-read means first): one block per channel
-    // (vt_run_kernel)
-    const bool multi = prec == 1;
-    DevBuf d_part, d_ticket;
-    if (multi) {
-        A.nb = (int)std::min<int64_t>(std::max<int64_t>(1, (nominal + kVtStepSamples - 1) / kVtStepSamples),
-                                      GNSS_VT_MAX_BLOCKS);
-        if (ctx->opt[GNSS_OPT_VT_BLOCKS] > 0) A.nb = (int)ctx->opt[GNSS_OPT_VT_BLOCKS];
-        HIP_TRY(d_part.alloc(ctx, "vt.part", sizeof(double) * 2 * (size_t)n * A.nb));
-        HIP_TRY(d_ticket.alloc(ctx, "vt.ticket", sizeof(unsigned) * (size_t)n));
-        HIP_TRY(hipMemsetAsync(d_ticket.p, 0, sizeof(unsigned) * (size_t)n, ctx->stream));
-        A.part = d_part.as<double>();
-        A.ticket = d_ticket.as<unsigned>();
-        A.out = h_out;
-        A.done = h_done;  // (the step's records are taken as each channel posts them)
-    }
     // the host's view of what sizes the next read (:164): remChip / codeFreq / file_ptr of the
     // last step, from the records the kernel returns
     std::vector<double> remChip(n), cf_old(n), codeError(n), carrFreq(n), cf_new(n);
@@ -2406,10 +2410,29 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         A.base = w.base;
         A.len = w.len;
         if (multi) {  // (per-step events only in profiling mode: each is a queue command)
-            for (int i = 0; i < n; i++) A.cf_arg[i] = h_cf[i];
-            A.seq = (unsigned)s + 1;
+            // the step's reads (:161-176, :217-249): what vt_step_kernel sums, and what stops a
+            // channel (a replica index MATLAB rejects, a read past the end of the record)
+            for (int i = 0; i < n; i++) {
+                const gnss_vt_chan& c = hc[(size_t)i];
+                const double cf = cf_new[i];
+                const VtPrep p = vt_prepare(sg->Fs, sg->codelength, pdi, c.remChip, c.codeFreq, cf);
+                int b = !(cf > 0) ? GNSS_EARG : p.bad;
+                if (!b) {
+                    const int64_t a0 = c.file_ptr, need = p.n * bps;
+                    if (a0 + need > flen) b = GNSS_EIO;
+                    else if (a0 < w.base || a0 + need > w.base + w.len) b = GNSS_EIO;  // (outside the window)
+                }
+                pk[(size_t)i] = p;
+                bad[(size_t)i] = b;
+                B.ns[i] = b ? 0 : p.n;
+                B.off[i] = b ? 0 : c.file_ptr - w.base;
+                B.f[i] = c.carrFreq;
+                B.phi0[i] = c.remCarrPhase;
+            }
+            B.rec = A.rec;
+            B.seq = (unsigned)s + 1;
             if (ctx->profiling) HIP_TRY(hipEventRecord(ev.a, ctx->stream));
-            HIP_TRY(launch_vt_step(A, ctx->stream));
+            HIP_TRY(launch_vt_step(B, n, nb, ctx->stream));
             if (ctx->profiling) HIP_TRY(hipEventRecord(ev.b, ctx->stream));
         } else {
             HIP_TRY(hipMemcpyAsync(d_cf.p, h_cf, sizeof(double) * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
@@ -2427,9 +2450,25 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
             have_ahead[(size_t)i] = q.n >= 1;
             if (q.n >= 1) vt_orbit(*nav, i, vt_transmit_next(*nav, i, q.n), &ahead[(size_t)i]);
         }
-        if (multi && !ctx->profiling) HIP_TRY(wait_posted(ctx->stream, h_done, n, (unsigned)s + 1));
-        else HIP_TRY(hipStreamSynchronize(ctx->stream));
+        if (!multi || ctx->profiling) HIP_TRY(hipStreamSynchronize(ctx->stream));
+        if (multi) HIP_TRY(wait_posted(ctx->stream, B.done, (unsigned)s + 1));
         if (ctx->profiling || !multi) kernel_ms += ev.ms();
+        for (int i = 0; multi && i < n; i++) {  // each channel's scalar end
+            gnss_vt_out& h = h_out[i];
+            h = gnss_vt_out{};
+            if (bad[(size_t)i]) {
+                h.status = bad[(size_t)i];
+                continue;
+            }
+            const double I = B.sums[2 * i], Q = B.sums[2 * i + 1];
+            const unsigned* cb = &cab[(size_t)i * 32];
+            int code[3];
+            for (int t = 0; t < 3; t++)
+                code[t] = vt_code_at(pk[(size_t)i].j[t], pdi, [&](int j) { return ((cb[j >> 5] >> (j & 31)) & 1u) ? -1 : 1; });
+            const int st2 = vt_finish(sg->Fs, sg->ms, pdi, bps, t1, t2, &hc[(size_t)i], pk[(size_t)i], code, cf_new[i],
+                                      I, Q, &h);
+            if (st2) h.status = st2;
+        }
         for (int i = 0; i < n; i++) {
             gnss_vt_out& o = out[(size_t)s * n + i];
             const gnss_vt_out& h = h_out[i];
@@ -2455,8 +2494,9 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         st = vt_nav_correct(nav, *gain, codeError.data(), cf_new.data(), carrFreq.data(), sol ? sol + s : nullptr);
         if (st) result = fail(ctx, st, "step %d: navigation update failed (singular innovation covariance)", s + 1);
     }
-    HIP_TRY(hipMemcpyAsync(chans, d_chan.p, sizeof(gnss_vt_chan) * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+    if (!multi) HIP_TRY(hipMemcpyAsync(chans, d_chan.p, sizeof(gnss_vt_chan) * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (multi) std::copy(hc.begin(), hc.end(), chans);
     ctx->timing.track_kernel_ms = kernel_ms;  // (int8 records: summed in profiling mode only)
     ctx->timing.track_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_loop).count();
     return result;

@@ -691,24 +691,29 @@ struct VtRunArgs {
     const unsigned* ca_bits;  // [n][32] C/A chips as sign bits (bit set: -1)
     double Fs, ms, codelength, tau1carr, tau2carr;
     int n, nsteps, pdi, prec, dtype;
-    // launch_vt_step only: [n][nb][2] block partials, [n] arrival tickets (zero between
-    // launches: the last block of a channel resets its own), nb blocks per channel
-    double* part;
-    unsigned* ticket;
-    int nb;
-    double cf_arg[GNSS_VT_MAX_CH];  // launch_vt_step: the step's code frequencies (kernel args)
-    // launch_vt_step, when set: `out` is coherent host memory, and each channel's last block
-    // writes its record through to it and then posts `seq` to done[ch] (system scope), so the
-    // host takes the step's records without waiting for the grid to retire
-    unsigned* done;
-    unsigned seq;
 };
 hipError_t launch_vt_run(const VtRunArgs& a, hipStream_t s);
-// One step of the n channels over n x nb blocks (int8 records; nsteps must be 1): each block
-// sums a contiguous 1/nb of the channel's read, the channel's last block to arrive adds
-// the nb partials in block order and runs the scalar end. The EKF loop's step (one launch
-// per step: the next code frequencies come from the host between steps).
-hipError_t launch_vt_step(const VtRunArgs& a, hipStream_t s);
+// One step of n channels over n x nb blocks (int8 records), the EKF loop's step: the host
+// sizes each read and keeps the channel states; block b of channel c sums the carrier-wiped
+// samples [b*chunk, (b+1)*chunk) of the read (chunk = ceil(ns / nb)) into part[(c*nb + b)*2 ..];
+// the grid's last block adds each channel's partials in block order into sums[2c ..] and then
+// posts `seq` to *done (coherent host memory, system scope), so the host takes the sums
+// without waiting for the grid to retire.
+struct VtStepArgs {
+    const uint8_t* rec;             // staged record window
+    double Fs;
+    int real8;                      // int8 real samples (else int8 I/Q)
+    unsigned seq;                   // the step's number
+    double* part;                   // [n][nb][2], device memory
+    double* sums;                   // [n][2], coherent host memory
+    unsigned* done;                 // [1], coherent host memory
+    unsigned* ticket;               // [1], device memory, 0 between launches
+    int64_t off[GNSS_VT_MAX_CH];    // the read's first byte in the window
+    int64_t ns[GNSS_VT_MAX_CH];     // samples read (0: the channel sits the step out)
+    double f[GNSS_VT_MAX_CH];       // carrFreq
+    double phi0[GNSS_VT_MAX_CH];    // remCarrPhase
+};
+hipError_t launch_vt_step(const VtStepArgs& a, int n, int nb, hipStream_t s);
 constexpr int kVtStepThreads = 256;
 constexpr int kVtStepSamples = 8 * kVtStepThreads;  // samples per block at the nominal read
 // generateCAcode.m's 1023 +-1 chips of `prn` (host)

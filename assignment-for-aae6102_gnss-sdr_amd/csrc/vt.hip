@@ -151,174 +151,112 @@ __device__ __forceinline__ void tree2s(double* r0, double* r1, int tid)
 // trackingVT_POS_updated.m is a host-driven chain (the EKF predicts every step's code
 // frequency from the last step's correlations), so a step's latency is the loop's rate:
 // spreading a channel's ~58 000 samples over nb blocks turns vt_run_kernel's one-CU step
-// into a chip-wide one. Each block re-derives the step (vt_prepare on the unchanged state,
-// the same bits in every block), sums the carrier-wiped samples of its contiguous slice
-// exactly as vt_run_kernel does per sample, reduces its 256 lanes in a fixed tree, and
-// publishes the partial; the channel's last block to arrive (ticket) adds the nb partials
-// in block order and runs vt_finish. Sums: the same per-sample terms, another (fixed)
-// association than vt_run_kernel's 1 024-lane tree.
-__global__ __launch_bounds__(kVtStepThreads) void vt_step_kernel(VtRunArgs a)
+// into a chip-wide one, and the kernel is nothing but that spread: the host has sized the
+// read and holds the channel state (gnss_tracking_vt), so each block sums the carrier-wiped
+// samples of its contiguous slice exactly as vt_run_kernel does per sample and reduces its 256
+// lanes in a fixed tree; the grid's last block to finish adds each channel's nb partials in
+// block order and writes the channel's two sums through to the caller's coherent host memory
+// with the step's number beside them. No block waits for another; the host runs the scalar
+// end (vt_finish) of each channel.
+__global__ __launch_bounds__(kVtStepThreads) void vt_step_kernel(VtStepArgs a)
 {
     const int b = blockIdx.x, ch = blockIdx.y, nb = gridDim.x, tid = threadIdx.x;
-    __shared__ VtPrep s_p;
-    __shared__ int s_bad, s_last;
     __shared__ double s_r0[kVtStepThreads], s_r1[kVtStepThreads];
-    const gnss_vt_chan* cg = a.chans + ch;  // read-only until the channel's last block
-    const double cf = a.cf_arg[ch];
-    const int bps = a.prec * a.dtype;
-    const bool real8 = a.dtype == 1;
-    if (tid == 0) {
-        VtPrep p = vt_prepare(a.Fs, a.codelength, a.pdi, cg->remChip, cg->codeFreq, cf);
-        int bad = !(cf > 0) ? GNSS_EARG : p.bad;
-        if (!bad) {
-            const int64_t A = cg->file_ptr, need = p.n * bps;
-            if (A + need > a.file_len) bad = GNSS_EIO;
-            else if (A < a.base || A + need > a.base + a.len) bad = GNSS_EIO;  // (outside the window)
+    const int64_t n = a.ns[ch];  // (0: the channel sits the step out)
+    const int64_t chunk = (n + nb - 1) / nb;
+    const int64_t k0 = (int64_t)b * chunk, k1 = k0 + chunk < n ? k0 + chunk : n;
+    const uint8_t* r = a.rec + a.off[ch];
+    const double f = a.f[ch], phi0 = a.phi0[ch], Fs = a.Fs;
+    const bool real8 = a.real8;
+    // the lane's samples k0 + tid + 256 i, four at a time (independent divisions and sincos in
+    // flight together), added in increasing k as the one-at-a-time loop would
+    auto term = [&](int64_t k, double& tI, double& tQ) {
+        const double W = kTwoPi * (f * ((double)k / Fs)) + phi0;  // Wave(k+1) (:275-276)
+        const double q = rint(W * (1.0 / kTwoPi));
+        double rr = __builtin_fma(-q, kTwoPi, W);
+        rr = __builtin_fma(-q, kTwoPiLo, rr);
+        double sn, cs;
+        if constexpr ((GNSS_VT_PROBE & 1) != 0) {  // (A/B probe: no sincos)
+            sn = rr;
+            cs = 1.0;
+        } else {
+            sincos(rr, &sn, &cs);
         }
-        s_p = p;
-        s_bad = bad;
-    }
-    __syncthreads();
+        double xr, xi;
+        if (real8) {
+            xr = (double)(int8_t)r[k];
+            xi = 0.0;
+        } else {
+            xr = (double)(int8_t)r[2 * k];
+            xi = (double)(int8_t)r[2 * k + 1];
+        }
+        tI = xr * sn + xi * cs;  // imag(raw .* carrsig) (:279)
+        tQ = xr * cs - xi * sn;  // real(raw .* carrsig) (:280)
+    };
     double sI = 0.0, sQ = 0.0;
-    if (!s_bad) {
-        const int64_t n = s_p.n;
-        const int64_t chunk = (n + nb - 1) / nb;
-        const int64_t k0 = (int64_t)b * chunk, k1 = k0 + chunk < n ? k0 + chunk : n;
-        const uint8_t* r = a.rec + (cg->file_ptr - a.base);
-        const double f = cg->carrFreq, phi0 = cg->remCarrPhase, Fs = a.Fs;
-        // the lane's samples k0 + tid + 256 i, four at a time (independent divisions and
-        // sincos in flight together), added in increasing k as the one-at-a-time loop would
-        auto term = [&](int64_t k, double& tI, double& tQ) {
-            const double W = kTwoPi * (f * ((double)k / Fs)) + phi0;  // Wave(k+1) (:275-276)
-            const double q = rint(W * (1.0 / kTwoPi));
-            double rr = __builtin_fma(-q, kTwoPi, W);
-            rr = __builtin_fma(-q, kTwoPiLo, rr);
-            double sn, cs;
-            if constexpr ((GNSS_VT_PROBE & 1) != 0) {  // (A/B probe: no sincos)
-                sn = rr;
-                cs = 1.0;
-            } else {
-                sincos(rr, &sn, &cs);
-            }
-            double xr, xi;
-            if (real8) {
-                xr = (double)(int8_t)r[k];
-                xi = 0.0;
-            } else {
-                xr = (double)(int8_t)r[2 * k];
-                xi = (double)(int8_t)r[2 * k + 1];
-            }
-            tI = xr * sn + xi * cs;  // imag(raw .* carrsig) (:279)
-            tQ = xr * cs - xi * sn;  // real(raw .* carrsig) (:280)
-        };
-        constexpr int U = 4, TS = kVtStepThreads;
-        int64_t k = k0 + tid;
-        for (; k + (U - 1) * TS < k1; k += U * TS) {
-            double tI[U], tQ[U];
+    constexpr int U = 4, TS = kVtStepThreads;
+    int64_t k = k0 + tid;
+    for (; k + (U - 1) * TS < k1; k += U * TS) {
+        double tI[U], tQ[U];
 #pragma unroll
-            for (int u = 0; u < U; u++) term(k + u * TS, tI[u], tQ[u]);
+        for (int u = 0; u < U; u++) term(k + u * TS, tI[u], tQ[u]);
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                sI += tI[u];
-                sQ += tQ[u];
-            }
+        for (int u = 0; u < U; u++) {
+            sI += tI[u];
+            sQ += tQ[u];
         }
-        for (; k < k1; k += TS) {
-            double tI, tQ;
-            term(k, tI, tQ);
-            sI += tI;
-            sQ += tQ;
-        }
+    }
+    for (; k < k1; k += TS) {
+        double tI, tQ;
+        term(k, tI, tQ);
+        sI += tI;
+        sQ += tQ;
     }
     s_r0[tid] = sI;
     s_r1[tid] = sQ;
     tree2s(s_r0, s_r1, tid);
+    __shared__ int s_last;
     if (tid == 0) {
+        // device-coherent stores (past this XCD's L2), drained before the block's ticket: the
+        // grid's last block reads them with device-coherent loads. (No agent-scope release /
+        // acquire fences: on gfx950 those write back and invalidate the whole L2.)
         double* pp = a.part + ((int64_t)ch * nb + b) * 2;
-        // device-coherent stores (past this XCD's L2), drained before the ticket: the channel's
-        // last block reads them with device-coherent loads. (No agent-scope release / acquire
-        // fences: on gfx950 those write back and invalidate the whole L2.)
         __hip_atomic_store(pp, s_r0[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(pp + 1, s_r1[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned t = __hip_atomic_fetch_add(a.ticket + ch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = t == (unsigned)nb - 1;
+        const unsigned total = (unsigned)nb * gridDim.y;
+        s_last = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1;
     }
     __syncthreads();
     if (!s_last) return;
-    // the channel's last block: every partial has landed (each was drained before its
-    // ticket); lane k loads partial k past the L2 in chunks of kVtStepThreads (the LDS arrays'
-    // size, so any nb works), lane 0 adds each chunk in block order: the sum is the same
-    // sequential block-order sum for every nb
-    __shared__ gnss_vt_out s_o;
-    __shared__ double s_I, s_Q;
-    if (tid == 0) s_I = s_Q = 0.0;
-    for (int k0 = 0; k0 < nb; k0 += kVtStepThreads) {
-        const int m = nb - k0 < kVtStepThreads ? nb - k0 : kVtStepThreads;
-        __syncthreads();  // (the previous chunk's adds are done before its slots are reused)
-        if (tid < m) {
-            const double* pp = a.part + ((int64_t)ch * nb + k0 + tid) * 2;
-            s_r0[tid] = __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_r1[tid] = __hip_atomic_load(pp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();
-        if (tid == 0) {
-            double I = s_I, Q = s_Q;
-            for (int k = 0; k < m; k++) {
-                I += s_r0[k];
-                Q += s_r1[k];
+    // the grid's last block: lane c adds channel c's nb partials in block order (the same
+    // sequential sum for every nb), writes the two sums through to the caller's host memory,
+    // and once every lane's are drained, lane 0 re-arms the ticket and posts the step's number
+    const int nch = gridDim.y;
+    if (tid < nch) {
+        const double* pp = a.part + (int64_t)tid * nb * 2;
+        double I = 0.0, Q = 0.0;
+        constexpr int kB = 8;  // (loads in flight per batch)
+        for (int b0 = 0; b0 < nb; b0 += kB) {
+            double v[2 * kB];
+            const int m = nb - b0 < kB ? nb - b0 : kB;
+#pragma unroll
+            for (int j = 0; j < 2 * kB; j++)
+                v[j] = j < 2 * m ? __hip_atomic_load(pp + 2 * b0 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+            for (int j = 0; j < m; j++) {
+                I += v[2 * j];
+                Q += v[2 * j + 1];
             }
-            s_I = I;
-            s_Q = Q;
         }
-    }
-    __syncthreads();
-    if (tid == 0) {
-        const double I = s_I, Q = s_Q;
-        __hip_atomic_store(a.ticket + ch, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_o = gnss_vt_out{};
-        if (s_bad) {
-            s_o.status = s_bad;
-        } else {
-            gnss_vt_chan c = *cg;
-            const unsigned* cab = a.ca_bits + 32 * ch;
-            int code[3];
-            for (int t = 0; t < 3; t++)
-                code[t] = vt_code_at(s_p.j[t], a.pdi, [&](int i) { return ((cab[i >> 5] >> (i & 31)) & 1u) ? -1 : 1; });
-            if constexpr ((GNSS_VT_PROBE & 2) != 0) {  // (A/B probe: no scalar end; the state advances by the read)
-                s_o.numSample = s_p.n;
-                s_o.absoluteSample = c.file_ptr + s_p.n * bps;
-                s_o.remChip = c.remChip;
-                s_o.codeFreq = cf;
-                s_o.carrFreq = c.carrFreq;
-                s_o.P_i = I + Q;
-                c.file_ptr += s_p.n * bps;
-                c.codeFreq = cf;
-            } else {
-                const int st = vt_finish(a.Fs, a.ms, a.pdi, bps, a.tau1carr, a.tau2carr, &c, s_p, code, cf, I, Q, &s_o);
-                if (st) s_o.status = st;
-            }
-            a.chans[ch] = c;
-        }
-    }
-    __syncthreads();
-    // the record to the caller's buffer (pinned host memory in the EKF loop): one 8-B word per
-    // lane, all posted at once
-    constexpr int kW = (int)(sizeof(gnss_vt_out) / 8);
-    unsigned long long* o = reinterpret_cast<unsigned long long*>(a.out + ch);
-    const unsigned long long* w = reinterpret_cast<const unsigned long long*>(&s_o);
-    if (!a.done) {
-        if (tid < kW) o[tid] = w[tid];
-        return;
-    }
-    // with a completion word: the record's words written through to host memory and drained,
-    // then the word (the host reads the record once it sees `seq`)
-    if (tid < kW) {
-        __hip_atomic_store(o + tid, w[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(a.sums + 2 * tid, I, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(a.sums + 2 * tid + 1, Q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    if (tid == 0) __hip_atomic_store(a.done + ch, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tid == 0) {
+        __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.done, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 }  // namespace
@@ -329,11 +267,13 @@ hipError_t launch_vt_run(const VtRunArgs& a, hipStream_t s)
     return hipGetLastError();
 }
 
-hipError_t launch_vt_step(const VtRunArgs& a, hipStream_t s)
+hipError_t launch_vt_step(const VtStepArgs& a, int n, int nb, hipStream_t s)
 {
-    if (a.nsteps != 1 || a.prec != 1 || a.nb < 1 || a.nb > GNSS_VT_MAX_BLOCKS || !a.part || !a.ticket || a.n > GNSS_VT_MAX_CH)
+    if (n < 1 || n > GNSS_VT_MAX_CH || nb < 1 || nb > GNSS_VT_MAX_BLOCKS || !a.rec || !a.part || !a.sums || !a.done || !a.ticket)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(vt_step_kernel, dim3(a.nb, a.n), dim3(kVtStepThreads), 0, s, a);
+    for (int i = 0; i < n; i++)
+        if (a.ns[i] < 0 || a.off[i] < 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(vt_step_kernel, dim3(nb, n), dim3(kVtStepThreads), 0, s, a);
     return hipGetLastError();
 }
 

@@ -195,8 +195,8 @@ def test_vector_tracking_formats(pkg, po, ctx, opensky_short, prec, dtyp):
 def test_vector_tracking_step_blocks(pkg, po, ctx, opensky_short, opts, nb):
     """The multi-block step (vt_step_kernel) at other block counts per channel
     (GNSS_OPT_VT_BLOCKS; the engine's is 29): another fixed association of the same per-sample
-    terms, the same loop against the oracle. nb > 256 (more partials than the
-    last block's LDS arrays hold) is summed in chunks, in the same block order."""
+    terms, the same loop against the oracle. The host adds a channel's nb partials in block
+    order whatever nb is (up to GNSS_VT_MAX_BLOCKS, 1 024 x 5 partials)."""
     skip, cfg, data = opensky_short
     file, signal, acq, track = params(pkg, skip, data)
     _, _, _, _, solu, cmn = pkg.initParameters()
