@@ -2305,7 +2305,7 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     // in the kernel arguments and each channel's two sums posted to coherent host memory (no
     // copy commands per step); int16 (per-read means first): one block per channel (vt_run_kernel)
     const bool multi = prec == 1;
-    DevBuf d_chan, d_cf, d_out, d_ca, d_part, d_ticket;
+    DevBuf d_chan, d_cf, d_out, d_ca, d_part, d_ticket, d_loop;
     double* h_cf = pinned_buffer<double>(ctx, "vt.cf", (size_t)n);
     gnss_vt_out* h_out = pinned_buffer<gnss_vt_out>(ctx, "vt.out", (size_t)n);
     if (!h_cf || !h_out) return fail(ctx, GNSS_EDEVICE, "pinned VT step buffers");
@@ -2321,14 +2321,14 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         B.sums = pinned_buffer<double>(ctx, "vt.sums", 2 * (size_t)n, hipHostMallocCoherent);
         B.done = pinned_buffer<unsigned>(ctx, "vt.done", 1, hipHostMallocCoherent);
         if (!B.sums || !B.done) return fail(ctx, GNSS_EDEVICE, "pinned VT step buffers");
-        HIP_TRY(d_part.alloc(ctx, "vt.part", sizeof(double) * 2 * (size_t)n * nb));
-        B.part = d_part.as<double>();
         __atomic_store_n(B.done, 0u, __ATOMIC_RELAXED);
         HIP_TRY(d_ticket.alloc(ctx, "vt.ticket", sizeof(unsigned)));
         HIP_TRY(hipMemsetAsync(d_ticket.p, 0, sizeof(unsigned), ctx->stream));
         B.ticket = d_ticket.as<unsigned>();
         B.Fs = sg->Fs;
         B.real8 = dtyp == 1;
+        HIP_TRY(d_part.alloc(ctx, "vt.part", sizeof(double) * 2 * (size_t)n * nb));
+        B.part = d_part.as<double>();
     } else {
         HIP_TRY(d_chan.alloc(ctx, "vt.chan", sizeof(gnss_vt_chan) * (size_t)n));
         HIP_TRY(d_cf.alloc(ctx, "vt.cf", sizeof(double) * (size_t)n));
@@ -2353,6 +2353,37 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     A.pdi = pdi;
     A.prec = prec;
     A.dtype = dtyp;
+    // Loop mode (int8 records, not profiling, the grid fits on the chip at once): ONE
+    // vt_loop_kernel launch runs the steps, each posted through a mailbox in coherent host
+    // memory, so a step costs no launch; stopped before a re-staging of the IF window and at
+    // the end (also on every early return: `loop_guard`).
+    const bool loop_mode = multi && !ctx->profiling && (int64_t)n * nb <= kVtLoopMaxBlocks;
+    VtMail* mail = nullptr;
+    bool running = false;
+    uint64_t loop_timeout = 0;
+    if (loop_mode) {
+        mail = pinned_buffer<VtMail>(ctx, "vt.mail", 1, hipHostMallocCoherent);
+        if (!mail) return fail(ctx, GNSS_EDEVICE, "pinned VT mailbox");
+        __atomic_store_n(&mail->stop, 0, __ATOMIC_RELAXED);
+        __atomic_store_n(&mail->seq, 0u, __ATOMIC_RELAXED);
+        int khz = 0;
+        HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device));
+        loop_timeout = (uint64_t)(std::max(khz, 1) * 1e3 * kVtLoopTimeoutS);
+        HIP_TRY(d_loop.alloc(ctx, "vt.loop", sizeof(VtBlockStep) * (size_t)n + 64));
+        HIP_TRY(hipMemsetAsync(d_loop.p, 0, sizeof(VtBlockStep) * (size_t)n + 64, ctx->stream));
+    }
+    auto stop_loop = [&]() -> hipError_t {
+        if (!running) return hipSuccess;
+        __atomic_store_n(&mail->stop, 1, __ATOMIC_RELEASE);
+        running = false;
+        const hipError_t e = hipStreamSynchronize(ctx->stream);
+        __atomic_store_n(&mail->stop, 0, __ATOMIC_RELAXED);
+        return e;
+    };
+    struct LoopGuard {
+        std::function<hipError_t()> stop;
+        ~LoopGuard() { (void)stop(); }
+    } loop_guard{stop_loop};
     // the host's view of what sizes the next read (:164): remChip / codeFreq / file_ptr of the
     // last step, from the records the kernel returns
     std::vector<double> remChip(n), cf_old(n), codeError(n), carrFreq(n), cf_new(n);
@@ -2399,6 +2430,7 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         }
         if (result) break;
         if (!file->dev_data && (need_lo < w.base || need_hi > w.base + w.len) && need_hi <= flen) {
+            HIP_TRY(stop_loop());
             HIP_TRY(hipStreamSynchronize(ctx->stream));
             st = restage(need_lo);
             if (st) return st;
@@ -2431,9 +2463,28 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
             }
             B.rec = A.rec;
             B.seq = (unsigned)s + 1;
-            if (ctx->profiling) HIP_TRY(hipEventRecord(ev.a, ctx->stream));
-            HIP_TRY(launch_vt_step(B, n, nb, ctx->stream));
-            if (ctx->profiling) HIP_TRY(hipEventRecord(ev.b, ctx->stream));
+            if (loop_mode) {  // the reads, then the step's number
+                for (int i = 0; i < n; i++) {
+                    mail->off[i] = B.off[i];
+                    mail->ns[i] = B.ns[i];
+                    mail->f[i] = B.f[i];
+                    mail->phi0[i] = B.phi0[i];
+                }
+                if (!running) {  // (the relay word back to 0: a stopped launch left kVtLoopStop)
+                    HIP_TRY(hipMemsetAsync(d_loop.as<char>() + sizeof(VtBlockStep) * (size_t)n, 0, sizeof(unsigned),
+                                           ctx->stream));
+                    const VtLoopArgs L{B.rec, B.Fs, B.real8, B.seq, mail, B.part, B.sums, B.done, B.ticket, loop_timeout,
+                                       reinterpret_cast<unsigned*>(d_loop.as<char>() + sizeof(VtBlockStep) * (size_t)n),
+                                       d_loop.as<VtBlockStep>()};
+                    HIP_TRY(launch_vt_loop(L, n, nb, ctx->stream));
+                    running = true;
+                }
+                __atomic_store_n(&mail->seq, B.seq, __ATOMIC_RELEASE);
+            } else {
+                if (ctx->profiling) HIP_TRY(hipEventRecord(ev.a, ctx->stream));
+                HIP_TRY(launch_vt_step(B, n, nb, ctx->stream));
+                if (ctx->profiling) HIP_TRY(hipEventRecord(ev.b, ctx->stream));
+            }
         } else {
             HIP_TRY(hipMemcpyAsync(d_cf.p, h_cf, sizeof(double) * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
             HIP_TRY(hipEventRecord(ev.a, ctx->stream));
@@ -2494,6 +2545,7 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         st = vt_nav_correct(nav, *gain, codeError.data(), cf_new.data(), carrFreq.data(), sol ? sol + s : nullptr);
         if (st) result = fail(ctx, st, "step %d: navigation update failed (singular innovation covariance)", s + 1);
     }
+    HIP_TRY(stop_loop());
     if (!multi) HIP_TRY(hipMemcpyAsync(chans, d_chan.p, sizeof(gnss_vt_chan) * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     if (multi) std::copy(hc.begin(), hc.end(), chans);

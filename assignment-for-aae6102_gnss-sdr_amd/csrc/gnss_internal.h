@@ -714,6 +714,39 @@ struct VtStepArgs {
     double phi0[GNSS_VT_MAX_CH];    // remCarrPhase
 };
 hipError_t launch_vt_step(const VtStepArgs& a, int n, int nb, hipStream_t s);
+// The EKF loop's steps from one launch (vt_loop_kernel): the host posts each step's reads and
+// then its number (seq0, seq0 + 1, ...) in `mail` (read by one block, which relays them through
+// device memory to the rest); each step completes as a vt_step_kernel
+// launch would (sums, then *done = its number). `stop` != 0 ends the launch, and so does no new
+// step within `timeout` (then the host sees the stream idle with the step not done).
+struct VtMail {
+    unsigned seq;  // the step to run (written after its reads)
+    int stop;
+    int64_t off[GNSS_VT_MAX_CH], ns[GNSS_VT_MAX_CH];
+    double f[GNSS_VT_MAX_CH], phi0[GNSS_VT_MAX_CH];
+};
+struct VtBlockStep {  // one channel's read of a step
+    int64_t off, ns;     // first byte in the window, samples (0: the channel sits the step out)
+    double f, phi0;      // carrFreq, remCarrPhase
+};
+constexpr unsigned kVtLoopStop = 0xffffffffu;
+struct VtLoopArgs {
+    const uint8_t* rec;
+    double Fs;
+    int real8;
+    unsigned seq0;
+    const VtMail* mail;  // coherent host memory
+    double* part;        // [n][nb][2], device memory
+    double* sums;        // [n][2], coherent host memory
+    unsigned* done;      // [1], coherent host memory
+    unsigned* ticket;    // [1], device memory, 0 between steps
+    uint64_t timeout;    // wall-clock ticks (wall_clock64) a block waits for a step
+    unsigned* dseq;      // [1], device memory: the step the lead block has posted (or kVtLoopStop)
+    VtBlockStep* dstep;  // [n], device memory: its reads
+};
+constexpr int kVtLoopMaxBlocks = 1024;  // (co-resident on 256 CUs with room to spare)
+constexpr double kVtLoopTimeoutS = 10;  // seconds a loop block waits for the next step
+hipError_t launch_vt_loop(const VtLoopArgs& a, int n, int nb, hipStream_t s);
 constexpr int kVtStepThreads = 256;
 constexpr int kVtStepSamples = 8 * kVtStepThreads;  // samples per block at the nominal read
 // generateCAcode.m's 1023 +-1 chips of `prn` (host)

@@ -158,16 +158,19 @@ __device__ __forceinline__ void tree2s(double* r0, double* r1, int tid)
 // block order and writes the channel's two sums through to the caller's coherent host memory
 // with the step's number beside them. No block waits for another; the host runs the scalar
 // end (vt_finish) of each channel.
-__global__ __launch_bounds__(kVtStepThreads) void vt_step_kernel(VtStepArgs a)
+// The step of block (b, ch): channel ch's read of ns samples at byte `off` of the window,
+// carrier frequency f and phase phi0 (ns 0: the channel sits the step out); the grid's last
+// block posts `seq`. s_r0 / s_r1: the block's kVtStepThreads-entry LDS arrays.
+__device__ __forceinline__ void vt_step_block(const uint8_t* rec, double Fs, bool real8, const VtBlockStep& st,
+                                              double* part, double* sums, unsigned* done, unsigned* ticket,
+                                              unsigned seq, int b, int ch, int nb, int nch, int tid, double* s_r0,
+                                              double* s_r1, int* s_last)
 {
-    const int b = blockIdx.x, ch = blockIdx.y, nb = gridDim.x, tid = threadIdx.x;
-    __shared__ double s_r0[kVtStepThreads], s_r1[kVtStepThreads];
-    const int64_t n = a.ns[ch];  // (0: the channel sits the step out)
+    const int64_t n = st.ns;
     const int64_t chunk = (n + nb - 1) / nb;
     const int64_t k0 = (int64_t)b * chunk, k1 = k0 + chunk < n ? k0 + chunk : n;
-    const uint8_t* r = a.rec + a.off[ch];
-    const double f = a.f[ch], phi0 = a.phi0[ch], Fs = a.Fs;
-    const bool real8 = a.real8;
+    const uint8_t* r = rec + st.off;
+    const double f = st.f, phi0 = st.phi0;
     // the lane's samples k0 + tid + 256 i, four at a time (independent divisions and sincos in
     // flight together), added in increasing k as the one-at-a-time loop would
     auto term = [&](int64_t k, double& tI, double& tQ) {
@@ -215,47 +218,139 @@ __global__ __launch_bounds__(kVtStepThreads) void vt_step_kernel(VtStepArgs a)
     s_r0[tid] = sI;
     s_r1[tid] = sQ;
     tree2s(s_r0, s_r1, tid);
-    __shared__ int s_last;
     if (tid == 0) {
         // device-coherent stores (past this XCD's L2), drained before the block's ticket: the
         // grid's last block reads them with device-coherent loads. (No agent-scope release /
         // acquire fences: on gfx950 those write back and invalidate the whole L2.)
-        double* pp = a.part + ((int64_t)ch * nb + b) * 2;
+        double* pp = part + ((int64_t)ch * nb + b) * 2;
         __hip_atomic_store(pp, s_r0[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(pp + 1, s_r1[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned total = (unsigned)nb * gridDim.y;
-        s_last = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1;
+        const unsigned total = (unsigned)nb * nch;
+        *s_last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1;
     }
     __syncthreads();
-    if (!s_last) return;
-    // the grid's last block: lane c adds channel c's nb partials in block order (the same
+    if (!*s_last) return;
+    // the grid's last block: the partials come into LDS a block's worth at a time (lane k loads
+    // partial k, all in flight together), lane c adds channel c's in block order (the same
     // sequential sum for every nb), writes the two sums through to the caller's host memory,
-    // and once every lane's are drained, lane 0 re-arms the ticket and posts the step's number
-    const int nch = gridDim.y;
-    if (tid < nch) {
-        const double* pp = a.part + (int64_t)tid * nb * 2;
-        double I = 0.0, Q = 0.0;
-        constexpr int kB = 8;  // (loads in flight per batch)
-        for (int b0 = 0; b0 < nb; b0 += kB) {
-            double v[2 * kB];
-            const int m = nb - b0 < kB ? nb - b0 : kB;
-#pragma unroll
-            for (int j = 0; j < 2 * kB; j++)
-                v[j] = j < 2 * m ? __hip_atomic_load(pp + 2 * b0 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
-            for (int j = 0; j < m; j++) {
-                I += v[2 * j];
-                Q += v[2 * j + 1];
+    // and once every lane's are drained, lane 0 re-arms the ticket (drained too: a later step's
+    // first ticket must see it) and posts the step's number
+    const int tot = nch * nb;
+    double I = 0.0, Q = 0.0;
+    for (int base = 0; base < tot; base += kVtStepThreads) {
+        const int m = tot - base < kVtStepThreads ? tot - base : kVtStepThreads;
+        __syncthreads();  // (the last chunk's adds are done before its slots are reused)
+        if (tid < m) {
+            const double* pp = part + 2 * (int64_t)(base + tid);
+            s_r0[tid] = __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_r1[tid] = __hip_atomic_load(pp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        if (tid < nch) {
+            const int lo = tid * nb > base ? tid * nb : base;
+            const int hi = tid * nb + nb < base + m ? tid * nb + nb : base + m;
+            for (int k = lo; k < hi; k++) {
+                I += s_r0[k - base];
+                Q += s_r1[k - base];
             }
         }
-        __hip_atomic_store(a.sums + 2 * tid, I, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(a.sums + 2 * tid + 1, Q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (tid < nch) {
+        __hip_atomic_store(sums + 2 * tid, I, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(sums + 2 * tid + 1, Q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
     if (tid == 0) {
-        __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(a.done, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+__global__ __launch_bounds__(kVtStepThreads) void vt_step_kernel(VtStepArgs a)
+{
+    __shared__ double s_r0[kVtStepThreads], s_r1[kVtStepThreads];
+    __shared__ int s_last;
+    const int ch = blockIdx.y;
+    const VtBlockStep st{a.off[ch], a.ns[ch], a.f[ch], a.phi0[ch]};
+    vt_step_block(a.rec, a.Fs, a.real8, st, a.part, a.sums, a.done, a.ticket, a.seq, blockIdx.x, ch, gridDim.x,
+                  gridDim.y, threadIdx.x, s_r0, s_r1, &s_last);
+}
+
+// The same steps from ONE launch (gnss_tracking_vt's loop mode). Block (0, 0) waits for the
+// host to post the next step in the mailbox (coherent host memory: the step's reads, then its
+// number), copies the reads to device memory and posts the number there; every other block
+// waits on that device word (so one block, not the grid, polls across PCIe), runs its
+// vt_step_block, and waits again. A stop word, or no new step within a.timeout, ends every
+// block. A step's blocks need no other block of the grid to be running (the last block only
+// counts tickets), so the launch only has to fit on the chip (launch_vt_loop bounds the grid).
+__global__ __launch_bounds__(kVtStepThreads) void vt_loop_kernel(VtLoopArgs a)
+{
+    __shared__ double s_r0[kVtStepThreads], s_r1[kVtStepThreads];
+    __shared__ int s_last, s_go;
+    __shared__ VtBlockStep s_st;
+    const int b = blockIdx.x, ch = blockIdx.y, tid = threadIdx.x, nch = gridDim.y;
+    const bool lead = b == 0 && ch == 0;
+    const VtMail* m = a.mail;
+    for (unsigned seq = a.seq0;; seq++) {
+        if (tid == 0) {
+            const uint64_t t0 = (uint64_t)wall_clock64();
+            int go = 0;
+            for (;;) {
+                if (lead) {  // (system-scope loads: past every cache, to the host's memory)
+                    if (__hip_atomic_load(&m->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+                    if (__hip_atomic_load(&m->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == seq) {
+                        go = 1;
+                        break;
+                    }
+                } else {  // (device-coherent loads of the lead's word)
+                    const unsigned d = __hip_atomic_load(a.dseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (d == kVtLoopStop) break;
+                    if (d == seq) {
+                        go = 1;
+                        break;
+                    }
+                }
+                if ((uint64_t)wall_clock64() - t0 > a.timeout) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            s_go = go;
+        }
+        __syncthreads();
+        if (lead) {
+            // the step's reads to device memory (lane c: channel c; the host wrote them before
+            // the number), drained, then the number -- or the stop word
+            if (s_go && tid < nch) {
+                VtBlockStep c;
+                c.off = __hip_atomic_load(&m->off[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                c.ns = __hip_atomic_load(&m->ns[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                c.f = __hip_atomic_load(&m->f[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                c.phi0 = __hip_atomic_load(&m->phi0[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                VtBlockStep* d = a.dstep + tid;
+                __hip_atomic_store(&d->off, c.off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&d->ns, c.ns, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&d->f, c.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&d->phi0, c.phi0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (tid == 0) s_st = c;
+            }
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store(a.dseq, s_go ? seq : kVtLoopStop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (s_go && tid == 0) {
+            const VtBlockStep* d = a.dstep + ch;
+            s_st.off = __hip_atomic_load(&d->off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_st.ns = __hip_atomic_load(&d->ns, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_st.f = __hip_atomic_load(&d->f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_st.phi0 = __hip_atomic_load(&d->phi0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        if (!s_go) return;
+        const VtBlockStep st = s_st;
+        vt_step_block(a.rec, a.Fs, a.real8, st, a.part, a.sums, a.done, a.ticket, seq, b, ch, gridDim.x, nch, tid,
+                      s_r0, s_r1, &s_last);
+        __syncthreads();  // (every lane is past the step before lane 0 reads the next one)
     }
 }
 
@@ -264,6 +359,15 @@ __global__ __launch_bounds__(kVtStepThreads) void vt_step_kernel(VtStepArgs a)
 hipError_t launch_vt_run(const VtRunArgs& a, hipStream_t s)
 {
     hipLaunchKernelGGL(vt_run_kernel, dim3(a.n), dim3(kVtRun), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_vt_loop(const VtLoopArgs& a, int n, int nb, hipStream_t s)
+{
+    if (n < 1 || n > GNSS_VT_MAX_CH || nb < 1 || (int64_t)n * nb > kVtLoopMaxBlocks || !a.rec || !a.mail || !a.part ||
+        !a.sums || !a.done || !a.ticket || !a.dseq || !a.dstep)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(vt_loop_kernel, dim3(nb, n), dim3(kVtStepThreads), 0, s, a);
     return hipGetLastError();
 }
 
