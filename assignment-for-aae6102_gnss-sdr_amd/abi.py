@@ -253,7 +253,7 @@ LOADED_PATH = None  # the library file the process bound (bench.py digests it)
 
 # gnss_ctx_set_option keys (include/gnss_mi355x.h, ABI v11)
 (OPT_FORCE_SUB, OPT_NO_PERSIST, OPT_FORCE_VPB, OPT_ACQ_ROCFFT, OPT_FINE_ROCFFT, OPT_ACQ_BATCH, OPT_ACQ_FUSED,
- OPT_ACQ_RING, OPT_ACQ_PIPE, OPT_VT_BLOCKS, OPT_FORCE_PEER) = range(11)
+ OPT_ACQ_RING, OPT_ACQ_PIPE, OPT_VT_BLOCKS, OPT_FORCE_PEER, OPT_VT_SPAN) = range(12)
 MAX_DEVICES = 16
 
 

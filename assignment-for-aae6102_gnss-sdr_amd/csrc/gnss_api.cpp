@@ -113,6 +113,8 @@ constexpr int kAcqPipeDefault = 2;
 constexpr bool kAcqFwdSplit = GNSS_ACQ_FWD_SPLIT;
 // the paired launch's row blocks sit in the grid's first kAcqPairFront percent (acq_fft.hip)
 constexpr int kAcqPairFront = 60;
+// steps of gnss_tracking_vt per staged IF window of a host record (GNSS_OPT_VT_SPAN: fewer)
+constexpr int kVtSpan = 2000;
 // SVs per launch of the fine-frequency search (scratch ~186 MB per SV at config 2)
 constexpr int kFineBatch = 16;
 
@@ -998,6 +1000,8 @@ int gnss_ctx_set_option(gnss_ctx* ctx, int key, int64_t value)
     if (!ctx || key < 0 || key >= GNSS_OPT_COUNT) return GNSS_EARG;
     if (key == GNSS_OPT_VT_BLOCKS && (value < 0 || value > GNSS_VT_MAX_BLOCKS))
         return fail(ctx, GNSS_EARG, "GNSS_OPT_VT_BLOCKS outside 0..%d", GNSS_VT_MAX_BLOCKS);
+    if (key == GNSS_OPT_VT_SPAN && (value < 0 || value > kVtSpan))
+        return fail(ctx, GNSS_EARG, "GNSS_OPT_VT_SPAN outside 0..%d", kVtSpan);
     ctx->opt[key] = value;
     for (gnss_ctx* m : ctx->members) m->opt[key] = value;
     return GNSS_OK;
@@ -2284,7 +2288,7 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     // yet, so a window is staged for `span` steps at half the nominal code rate (twice the
     // nominal read) and re-staged when a read would leave it. A resident record is used as is.
     const int64_t nominal = (int64_t)std::ceil(sg->codelength * pdi / (sg->codeFreqBasis / sg->Fs));
-    const int64_t span = std::min<int64_t>(nsteps, 2000);
+    const int64_t span = std::min<int64_t>(nsteps, ctx->opt[GNSS_OPT_VT_SPAN] > 0 ? ctx->opt[GNSS_OPT_VT_SPAN] : kVtSpan);
     IfWindow w;
     auto restage = [&](int64_t lo) -> int {
         const int64_t hi = lo + (span * 2 * nominal + 64) * bps;
@@ -2357,7 +2361,7 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     // vt_loop_kernel launch runs the steps, each posted through a mailbox in coherent host
     // memory, so a step costs no launch; stopped before a re-staging of the IF window and at
     // the end (also on every early return: `loop_guard`).
-    const bool loop_mode = multi && !ctx->profiling && (int64_t)n * nb <= kVtLoopMaxBlocks;
+    const bool loop_mode = multi && !ctx->profiling && !ctx->opt[GNSS_OPT_NO_PERSIST] && (int64_t)n * nb <= kVtLoopMaxBlocks;
     VtMail* mail = nullptr;
     bool running = false;
     uint64_t loop_timeout = 0;

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define GNSS_ABI_VERSION 12
+#define GNSS_ABI_VERSION 13
 
 /* ---- status codes (SURVEY §8b "Error conventions") --------------------- */
 #define GNSS_OK         0
@@ -263,7 +263,8 @@ int  gnss_ctx_set_window(gnss_ctx *ctx, uint64_t bytes);
  * so the parity tests can prove every path gives the reference's results. All default 0
  * (the engine's own choice); GNSS_EARG for an unknown key.                               */
 #define GNSS_OPT_FORCE_SUB    0  /* lane span 8*v samples for both tracking phases (1..4) */
-#define GNSS_OPT_NO_PERSIST   1  /* != 0: one launch per tracking step (no persistent loop) */
+#define GNSS_OPT_NO_PERSIST   1  /* != 0: one launch per tracking step (no persistent loop;
+                                    gnss_tracking_vt too, ABI v13)                        */
 #define GNSS_OPT_FORCE_VPB    2  /* >= 2: virtual blocks per resident block of the loop     */
 #define GNSS_OPT_ACQ_ROCFFT   3  /* != 0: rocFFT instead of the own P x 2000 correlator     */
 #define GNSS_OPT_FINE_ROCFFT  4  /* != 0: rocFFT for the fine-frequency transform           */
@@ -285,7 +286,10 @@ int  gnss_ctx_set_window(gnss_ctx *ctx, uint64_t bytes);
                                     dev_data and GNSS_OUT_DEVICE arrays as on another
                                     device (range copies in, row copies out), so one GPU
                                     exercises the peer-copy path                          */
-#define GNSS_OPT_COUNT        11
+#define GNSS_OPT_VT_SPAN      11 /* 1..2000 (ABI v13): steps per staged IF window of
+                                    gnss_tracking_vt on a host record (2000; GNSS_EARG
+                                    outside), so a short loop exercises the re-staging   */
+#define GNSS_OPT_COUNT        12
 int  gnss_ctx_set_option(gnss_ctx *ctx, int key, int64_t value);
 
 /* Device memory owned by the ctx, for callers that keep an IF record resident

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol(pkg):
 
 def test_abi_version_and_strerror(pkg):
     lib = pkg.abi.load()
-    assert lib.gnss_abi_version() == 12
+    assert lib.gnss_abi_version() == 13
     for code in range(6):
         assert lib.gnss_strerror(code)
 

@@ -211,6 +211,50 @@ def test_vector_tracking_step_blocks(pkg, po, ctx, opensky_short, opts, nb):
     print(nb, "worst sum / |P|", _compare(pkg, po, z, tck, nsol, rec, onav))
 
 
+def _vt_run(pkg, ctx, opts, data, skip, nsteps, **opt):
+    for k, v in opt.items():
+        opts(getattr(pkg.abi, k), v)
+    file, signal, acq, track = params(pkg, skip, data)
+    _, _, _, _, solu, cmn = pkg.initParameters()
+    z = V.fixture()
+    Acquired, eph, sbf, ct, ns = _inputs(pkg, z, skip)
+    tck, nsol = pkg.trackingVT_POS_updated(file, signal, track, cmn, solu, Acquired, V.cnslxyz(pkg), eph, sbf,
+                                           None, ct, ns, ctx=ctx, nsteps=nsteps)
+    return z, ct, tck, nsol, ctx.timing()
+
+
+def test_vector_tracking_loop_mode_equals_step_launches(pkg, po, ctx, opensky_short, opts):
+    """Loop mode (one vt_loop_kernel launch serves the steps through the host mailbox) against
+    one vt_step_kernel launch per step (GNSS_OPT_NO_PERSIST): the same block sums in the same
+    order, so every output is bit-identical. GNSS_OPT_VT_SPAN = 40 re-stages the host record's
+    IF window every ~40 steps, so the loop launch is stopped and relaunched mid-call; the loop
+    run is also held against the oracle's closed loop."""
+    skip, cfg, data = opensky_short
+    nsteps = 300
+    z, ct, tck_l, nsol_l, t_l = _vt_run(pkg, ctx, opts, data, skip, nsteps, OPT_VT_SPAN=40)
+    _, _, tck_s, nsol_s, t_s = _vt_run(pkg, ctx, opts, data, skip, nsteps, OPT_VT_SPAN=40, OPT_NO_PERSIST=1)
+    assert t_l["track_launches"] == t_s["track_launches"] == nsteps
+    assert t_l["h2d_bytes"] > 0 and t_l["h2d_bytes"] == t_s["h2d_bytes"]  # (the same windows staged)
+    for p in (int(x) for x in z["prns"]):
+        a, b = tck_l(p), tck_s(p)
+        for f in ("P_i", "P_q", "E_i", "L_q", "carrFreq", "codeFreq", "remChip", "remCarrPhase", "absoluteSample",
+                  "codeError", "deltaPr", "sv_vel"):
+            assert np.array_equal(getattr(a, f), getattr(b, f)), (p, f)
+    for f in ("usrPos", "usrVel", "clkBias", "clkDrift", "state"):
+        assert np.array_equal(getattr(nsol_l, f), getattr(nsol_s, f)), f
+    status, rec, onav = _oracle_loop(pkg, po, z, ct, data, nsteps)
+    assert status == 0
+    _compare(pkg, po, z, tck_l, nsol_l, rec, onav)
+
+
+def test_vector_tracking_span_option_bound(pkg, ctx):
+    abi = pkg.abi
+    for bad in (-1, 2001):
+        assert ctx.lib.gnss_ctx_set_option(ctx.h, abi.OPT_VT_SPAN, bad) == abi.EARG
+    assert ctx.lib.gnss_ctx_set_option(ctx.h, abi.OPT_VT_SPAN, 2000) == 0
+    assert ctx.lib.gnss_ctx_set_option(ctx.h, abi.OPT_VT_SPAN, 0) == 0
+
+
 def test_vector_tracking_block_option_bound(pkg, ctx):
     """GNSS_OPT_VT_BLOCKS takes 0 (the engine's choice) .. GNSS_VT_MAX_BLOCKS and refuses
     anything else with GNSS_EARG."""
