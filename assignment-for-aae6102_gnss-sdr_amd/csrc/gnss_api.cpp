@@ -2318,6 +2318,8 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     std::vector<int> bad((size_t)n, 0);
     VtStepArgs B{};
     int nb = 1;
+    int64_t kmax_rfs = 0;
+    double rfs = 0;
     if (multi) {
         nb = (int)std::min<int64_t>(std::max<int64_t>(1, (nominal + kVtStepSamples - 1) / kVtStepSamples),
                                     GNSS_VT_MAX_BLOCKS);
@@ -2331,6 +2333,10 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         B.ticket = d_ticket.as<unsigned>();
         B.Fs = sg->Fs;
         B.real8 = dtyp == 1;
+        // k/Fs by Markstein's correction where it is the IEEE quotient (exhaustively verified up
+        // to four nominal reads, cached per Fs; a longer read divides)
+        kmax_rfs = 4 * nominal;
+        rfs = fast_div_exact(sg->Fs, kmax_rfs) ? 1.0 / sg->Fs : 0.0;
         HIP_TRY(d_part.alloc(ctx, "vt.part", sizeof(double) * 2 * (size_t)n * nb));
         B.part = d_part.as<double>();
     } else {
@@ -2409,6 +2415,13 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     double kernel_ms = 0;
     int result = GNSS_OK;
     const auto t_loop = std::chrono::steady_clock::now();
+    // (probe builds, GNSS_VT_STAMPS set: the host's share of a step, printed at the end)
+    const bool stamps = probe_env("GNSS_VT_STAMPS") != nullptr;
+    double st_pre = 0, st_shadow = 0, st_wait = 0, st_post = 0;
+    auto now_us = [] {
+        return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    };
+    double t_a = stamps ? now_us() : 0;
     for (int s = 0; s < nsteps && result == GNSS_OK; s++) {
         int64_t need_lo = INT64_MAX, need_hi = 0;
         for (int i = 0; i < n; i++) {
@@ -2464,6 +2477,7 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
                 B.off[i] = b ? 0 : c.file_ptr - w.base;
                 B.f[i] = c.carrFreq;
                 B.phi0[i] = c.remCarrPhase;
+                B.rfs[i] = B.ns[i] - 1 <= kmax_rfs ? rfs : 0.0;
             }
             B.rec = A.rec;
             B.seq = (unsigned)s + 1;
@@ -2473,6 +2487,7 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
                     mail->ns[i] = B.ns[i];
                     mail->f[i] = B.f[i];
                     mail->phi0[i] = B.phi0[i];
+                    mail->rfs[i] = B.rfs[i];
                 }
                 if (!running) {  // (the relay word back to 0: a stopped launch left kVtLoopStop)
                     HIP_TRY(hipMemsetAsync(d_loop.as<char>() + sizeof(VtBlockStep) * (size_t)n, 0, sizeof(unsigned),
@@ -2497,6 +2512,8 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
             HIP_TRY(hipMemcpyAsync(h_out, d_out.p, sizeof(gnss_vt_out) * (size_t)n, hipMemcpyDeviceToHost,
                                    ctx->stream));
         }
+        double t_b = stamps ? now_us() : 0;
+        if (stamps) st_pre += t_b - t_a;
         vt_nav_gain(*nav, gain.get());
         for (int i = 0; i < n && s + 1 < nsteps; i++) {
             const int64_t ns = nav->numSample[i];
@@ -2505,8 +2522,17 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
             have_ahead[(size_t)i] = q.n >= 1;
             if (q.n >= 1) vt_orbit(*nav, i, vt_transmit_next(*nav, i, q.n), &ahead[(size_t)i]);
         }
+        if (stamps) {
+            const double t = now_us();
+            st_shadow += t - t_b;
+            t_b = t;
+        }
         if (!multi || ctx->profiling) HIP_TRY(hipStreamSynchronize(ctx->stream));
         if (multi) HIP_TRY(wait_posted(ctx->stream, B.done, (unsigned)s + 1));
+        if (stamps) {
+            t_a = now_us();
+            st_wait += t_a - t_b;
+        }
         if (ctx->profiling || !multi) kernel_ms += ev.ms();
         for (int i = 0; multi && i < n; i++) {  // each channel's scalar end
             gnss_vt_out& h = h_out[i];
@@ -2548,7 +2574,15 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         if (result) break;
         st = vt_nav_correct(nav, *gain, codeError.data(), cf_new.data(), carrFreq.data(), sol ? sol + s : nullptr);
         if (st) result = fail(ctx, st, "step %d: navigation update failed (singular innovation covariance)", s + 1);
+        if (stamps) {
+            const double t = now_us();
+            st_post += t - t_a;
+            t_a = t;
+        }
     }
+    if (stamps && nsteps > 0)
+        fprintf(stderr, "vt stamps (us per step): predict+post %.2f, shadow %.2f, wait %.2f, finish+correct %.2f\n",
+                st_pre / nsteps, st_shadow / nsteps, st_wait / nsteps, st_post / nsteps);
     HIP_TRY(stop_loop());
     if (!multi) HIP_TRY(hipMemcpyAsync(chans, d_chan.p, sizeof(gnss_vt_chan) * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));

@@ -157,6 +157,47 @@ GNSS_HD double div_markstein(double x, double b, double rb)
     return __builtin_fma(r, rb, q);
 }
 
+// sin and cos of a small argument (|x| <= ~40 rad: the lane's reduced carrier phase, the rotation
+// table's phi[m], a VT sample's 2*pi-reduced phase) with a short dependent chain, for the
+// correlators' lane rotation and the rotation table (track.hip GNSS_FAST_SINCOS; 0 = the device
+// library's sincos) and the VT step's samples (vt.hip). Reduction by pi/2 in two
+// parts (q * PIO2_HI exact for |q| < 2^20: PIO2_HI has 33 significant bits), then the classic
+// fdlibm minimax kernels on [-pi/4, pi/4] (__kernel_sin / __kernel_cos, error < 1 ulp), the two
+// polynomials evaluated side by side, and the quadrant's swap / negation by selects. Accuracy is
+// the library's (< 1 ulp); the bits differ from it in the last place for some arguments, which
+// moves the tracking sums by rounding only (the parity tests judge them against the oracle).
+__device__ __forceinline__ void sincos_small(double x, double* sn, double* cs)
+{
+    constexpr double kTwoOverPi = 6.36619772367581382433e-01;
+    constexpr double kPio2Hi = 1.57079632673412561417e+00;  // first 33 bits of pi/2
+    constexpr double kPio2Lo = 6.07710050650619224932e-11;  // RN(pi/2 - kPio2Hi)
+    const double q = rint(x * kTwoOverPi);
+    double y = __builtin_fma(-q, kPio2Hi, x);  // exact (q * kPio2Hi exact, |x - q*kPio2Hi| small)
+    const double t = q * kPio2Lo;              // (fdlibm __ieee754_rem_pio2's first round)
+    const double yh = y - t;
+    const double yl = (y - yh) - t;            // the tail of the reduced argument
+    y = yh;
+    const double z = y * y;
+    // __kernel_sin(y, yl, 1) and __kernel_cos(y, yl) (fdlibm, public domain)
+    const double rs = __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z,
+        1.58969099521155010221e-10, -2.50507602534068634195e-08), 2.75573137070700676789e-06),
+        -1.98412698298579493134e-04), 8.33333333332248946124e-03);
+    const double rc = z * __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z,
+        __builtin_fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
+        -2.75573143513906633035e-07), 2.48015872894767294178e-05), -1.38888888888741095749e-03),
+        4.16666666666666019037e-02);
+    const double v = z * y;
+    const double s = y - ((z * (0.5 * yl - v * rs) - yl) - v * -1.66666666666666324348e-01);
+    const double hz = 0.5 * z;
+    const double w = 1.0 - hz;
+    const double c = w + (((1.0 - w) - hz) + (z * rc - y * yl));
+    const int n = (int)q & 3;
+    const double a = (n & 1) ? c : s, b = (n & 1) ? s : c;
+    *sn = (n & 2) ? -a : a;
+    *cs = ((n + 1) & 2) ? -b : b;
+}
+
+
 // ----------------------------------------------------------------------------
 // Tracking state (one per channel, fp64), lives in HBM across step launches.
 // ----------------------------------------------------------------------------
@@ -712,6 +753,7 @@ struct VtStepArgs {
     int64_t ns[GNSS_VT_MAX_CH];     // samples read (0: the channel sits the step out)
     double f[GNSS_VT_MAX_CH];       // carrFreq
     double phi0[GNSS_VT_MAX_CH];    // remCarrPhase
+    double rfs[GNSS_VT_MAX_CH];     // RN(1/Fs) if k/Fs = div_markstein for k < ns (host-verified), else 0
 };
 hipError_t launch_vt_step(const VtStepArgs& a, int n, int nb, hipStream_t s);
 // The EKF loop's steps from one launch (vt_loop_kernel): the host posts each step's reads and
@@ -723,11 +765,12 @@ struct VtMail {
     unsigned seq;  // the step to run (written after its reads)
     int stop;
     int64_t off[GNSS_VT_MAX_CH], ns[GNSS_VT_MAX_CH];
-    double f[GNSS_VT_MAX_CH], phi0[GNSS_VT_MAX_CH];
+    double f[GNSS_VT_MAX_CH], phi0[GNSS_VT_MAX_CH], rfs[GNSS_VT_MAX_CH];
 };
 struct VtBlockStep {  // one channel's read of a step
     int64_t off, ns;     // first byte in the window, samples (0: the channel sits the step out)
     double f, phi0;      // carrFreq, remCarrPhase
+    double rfs;          // VtStepArgs::rfs
 };
 constexpr unsigned kVtLoopStop = 0xffffffffu;
 struct VtLoopArgs {

@@ -170,11 +170,15 @@ __device__ __forceinline__ void vt_step_block(const uint8_t* rec, double Fs, boo
     const int64_t chunk = (n + nb - 1) / nb;
     const int64_t k0 = (int64_t)b * chunk, k1 = k0 + chunk < n ? k0 + chunk : n;
     const uint8_t* r = rec + st.off;
-    const double f = st.f, phi0 = st.phi0;
+    const double f = st.f, phi0 = st.phi0, rfs = st.rfs;
     // the lane's samples k0 + tid + 256 i, four at a time (independent divisions and sincos in
-    // flight together), added in increasing k as the one-at-a-time loop would
+    // flight together), added in increasing k as the one-at-a-time loop would. k/Fs: Markstein's
+    // correction of k * RN(1/Fs), the IEEE quotient for every k of the read (host-verified), or
+    // the division; sin / cos of the 2*pi-reduced phase: sincos_small (< 1 ulp, as the CT
+    // correlator's)
     auto term = [&](int64_t k, double& tI, double& tQ) {
-        const double W = kTwoPi * (f * ((double)k / Fs)) + phi0;  // Wave(k+1) (:275-276)
+        const double t = rfs != 0.0 ? div_markstein((double)k, Fs, rfs) : (double)k / Fs;
+        const double W = kTwoPi * (f * t) + phi0;  // Wave(k+1) (:275-276)
         const double q = rint(W * (1.0 / kTwoPi));
         double rr = __builtin_fma(-q, kTwoPi, W);
         rr = __builtin_fma(-q, kTwoPiLo, rr);
@@ -183,7 +187,7 @@ __device__ __forceinline__ void vt_step_block(const uint8_t* rec, double Fs, boo
             sn = rr;
             cs = 1.0;
         } else {
-            sincos(rr, &sn, &cs);
+            sincos_small(rr, &sn, &cs);
         }
         double xr, xi;
         if (real8) {
@@ -274,7 +278,7 @@ __global__ __launch_bounds__(kVtStepThreads) void vt_step_kernel(VtStepArgs a)
     __shared__ double s_r0[kVtStepThreads], s_r1[kVtStepThreads];
     __shared__ int s_last;
     const int ch = blockIdx.y;
-    const VtBlockStep st{a.off[ch], a.ns[ch], a.f[ch], a.phi0[ch]};
+    const VtBlockStep st{a.off[ch], a.ns[ch], a.f[ch], a.phi0[ch], a.rfs[ch]};
     vt_step_block(a.rec, a.Fs, a.real8, st, a.part, a.sums, a.done, a.ticket, a.seq, blockIdx.x, ch, gridDim.x,
                   gridDim.y, threadIdx.x, s_r0, s_r1, &s_last);
 }
@@ -328,11 +332,13 @@ __global__ __launch_bounds__(kVtStepThreads) void vt_loop_kernel(VtLoopArgs a)
                 c.ns = __hip_atomic_load(&m->ns[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 c.f = __hip_atomic_load(&m->f[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 c.phi0 = __hip_atomic_load(&m->phi0[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                c.rfs = __hip_atomic_load(&m->rfs[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 VtBlockStep* d = a.dstep + tid;
                 __hip_atomic_store(&d->off, c.off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(&d->ns, c.ns, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(&d->f, c.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(&d->phi0, c.phi0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&d->rfs, c.rfs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (tid == 0) s_st = c;
             }
@@ -344,6 +350,7 @@ __global__ __launch_bounds__(kVtStepThreads) void vt_loop_kernel(VtLoopArgs a)
             s_st.ns = __hip_atomic_load(&d->ns, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             s_st.f = __hip_atomic_load(&d->f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             s_st.phi0 = __hip_atomic_load(&d->phi0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_st.rfs = __hip_atomic_load(&d->rfs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
         if (!s_go) return;
