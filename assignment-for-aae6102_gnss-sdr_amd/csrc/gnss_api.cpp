@@ -2244,6 +2244,7 @@ hipError_t wait_posted(hipStream_t stream, const unsigned* done, unsigned seq)
     auto posted = [&] { return __atomic_load_n(done, __ATOMIC_ACQUIRE) == seq; };
     for (unsigned k = 1;; k++) {
         if (posted()) return hipSuccess;
+        __builtin_ia32_pause();
         if ((k & 255) == 0) {
             const hipError_t e = hipStreamQuery(stream);
             if (e == hipErrorNotReady) continue;
