@@ -2371,6 +2371,8 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     const bool loop_mode = multi && !ctx->profiling && !ctx->opt[GNSS_OPT_NO_PERSIST] && (int64_t)n * nb <= kVtLoopMaxBlocks;
     VtMail* mail = nullptr;
     bool running = false;
+    // the loop's 16-B granules: each channel's relayed read, then every block's two sums
+    const size_t gstep_bytes = (size_t)16 * kVtStepWords * n, loop_bytes = gstep_bytes + (size_t)16 * 2 * n * nb;
     uint64_t loop_timeout = 0;
     if (loop_mode) {
         mail = pinned_buffer<VtMail>(ctx, "vt.mail", 1, hipHostMallocCoherent);
@@ -2380,8 +2382,7 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         int khz = 0;
         HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device));
         loop_timeout = (uint64_t)(std::max(khz, 1) * 1e3 * kVtLoopTimeoutS);
-        HIP_TRY(d_loop.alloc(ctx, "vt.loop", sizeof(VtBlockStep) * (size_t)n + 64));
-        HIP_TRY(hipMemsetAsync(d_loop.p, 0, sizeof(VtBlockStep) * (size_t)n + 64, ctx->stream));
+        HIP_TRY(d_loop.alloc(ctx, "vt.loop", loop_bytes));
     }
     auto stop_loop = [&]() -> hipError_t {
         if (!running) return hipSuccess;
@@ -2490,12 +2491,10 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
                     mail->phi0[i] = B.phi0[i];
                     mail->rfs[i] = B.rfs[i];
                 }
-                if (!running) {  // (the relay word back to 0: a stopped launch left kVtLoopStop)
-                    HIP_TRY(hipMemsetAsync(d_loop.as<char>() + sizeof(VtBlockStep) * (size_t)n, 0, sizeof(unsigned),
-                                           ctx->stream));
-                    const VtLoopArgs L{B.rec, B.Fs, B.real8, B.seq, mail, B.part, B.sums, B.done, B.ticket, loop_timeout,
-                                       reinterpret_cast<unsigned*>(d_loop.as<char>() + sizeof(VtBlockStep) * (size_t)n),
-                                       d_loop.as<VtBlockStep>()};
+                if (!running) {  // (every tag back to 0: a stopped launch left kVtLoopStop, a former call its steps)
+                    HIP_TRY(hipMemsetAsync(d_loop.p, 0, loop_bytes, ctx->stream));
+                    const VtLoopArgs L{B.rec, B.Fs, B.real8, B.seq, mail, B.sums, B.done, loop_timeout, d_loop.p,
+                                       d_loop.as<char>() + gstep_bytes};
                     HIP_TRY(launch_vt_loop(L, n, nb, ctx->stream));
                     running = true;
                 }

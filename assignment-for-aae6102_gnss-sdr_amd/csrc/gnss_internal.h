@@ -198,6 +198,30 @@ __device__ __forceinline__ void sincos_small(double x, double* sn, double* cs)
 }
 
 
+// 16-B granules {lo, tag, hi, tag}: one fp64 value per granule, written by one
+// buffer_store_dwordx4 sc1 and read by one buffer_load_dwordx4 sc1 (MI355X_MICROARCH.md
+// hand-off table: 16-B sc1 stores and loads; each half carries the tag, so a torn read
+// is simply not accepted). Half the polls of two 8-B granules per value. The tracking
+// loop's hand-offs (track.hip) and the VT loop's (vt.hip).
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kBufRsrcWord3 = 0x00020000;  // raw buffer, gfx9 family
+constexpr int kPolSc1 = 16;                // cache policy: sc1 (device coherence)
+
+__device__ __forceinline__ void publish16(__amdgpu_buffer_rsrc_t r, int unit, double v, unsigned tag)
+{
+    const unsigned long long w = (unsigned long long)__double_as_longlong(v);
+    const u32x4 g = {(unsigned)w, tag, (unsigned)(w >> 32), tag};
+    __builtin_amdgcn_raw_buffer_store_b128(g, r, unit * 16, 0, kPolSc1);
+}
+__device__ __forceinline__ u32x4 load16(__amdgpu_buffer_rsrc_t r, int unit)
+{
+    return __builtin_amdgcn_raw_buffer_load_b128(r, unit * 16, 0, kPolSc1);
+}
+__device__ __forceinline__ double value16(u32x4 g)
+{
+    return __longlong_as_double((long long)(((unsigned long long)g.z << 32) | g.x));
+}
+
 // ----------------------------------------------------------------------------
 // Tracking state (one per channel, fp64), lives in HBM across step launches.
 // ----------------------------------------------------------------------------
@@ -758,7 +782,7 @@ struct VtStepArgs {
 hipError_t launch_vt_step(const VtStepArgs& a, int n, int nb, hipStream_t s);
 // The EKF loop's steps from one launch (vt_loop_kernel): the host posts each step's reads and
 // then its number (seq0, seq0 + 1, ...) in `mail` (read by one block, which relays them through
-// device memory to the rest); each step completes as a vt_step_kernel
+// device memory to the rest and gathers their sums); each step completes as a vt_step_kernel
 // launch would (sums, then *done = its number). `stop` != 0 ends the launch, and so does no new
 // step within `timeout` (then the host sees the stream idle with the step not done).
 struct VtMail {
@@ -773,19 +797,18 @@ struct VtBlockStep {  // one channel's read of a step
     double rfs;          // VtStepArgs::rfs
 };
 constexpr unsigned kVtLoopStop = 0xffffffffu;
+constexpr int kVtStepWords = 5;  // VtBlockStep's words, relayed as 16-B granules
 struct VtLoopArgs {
     const uint8_t* rec;
     double Fs;
     int real8;
     unsigned seq0;
     const VtMail* mail;  // coherent host memory
-    double* part;        // [n][nb][2], device memory
     double* sums;        // [n][2], coherent host memory
     unsigned* done;      // [1], coherent host memory
-    unsigned* ticket;    // [1], device memory, 0 between steps
     uint64_t timeout;    // wall-clock ticks (wall_clock64) a block waits for a step
-    unsigned* dseq;      // [1], device memory: the step the lead block has posted (or kVtLoopStop)
-    VtBlockStep* dstep;  // [n], device memory: its reads
+    void* gstep;         // [n][kVtStepWords] 16-B granules, device memory: the relayed reads
+    void* gpart;         // [n][nb][2] 16-B granules, device memory: the blocks' sums
 };
 constexpr int kVtLoopMaxBlocks = 1024;  // (co-resident on 256 CUs with room to spare)
 constexpr double kVtLoopTimeoutS = 10;  // seconds a loop block waits for the next step

@@ -1659,20 +1659,7 @@ __device__ bool sweep_words(const unsigned long long* g, int n, unsigned tag, un
     return !__syncthreads_or(todo != 0);
 }
 
-// 16-B granules {lo, tag, hi, tag}: one fp64 partial per granule, written by one
-// buffer_store_dwordx4 sc1 and read by one buffer_load_dwordx4 sc1 (MI355X_MICROARCH.md
-// hand-off table: 16-B sc1 stores and loads; each half carries the tag, so a torn read
-// is simply not accepted). Half the polls of two 8-B granules per value.
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-constexpr int kBufRsrcWord3 = 0x00020000;  // raw buffer, gfx9 family
-constexpr int kPolSc1 = 16;                // cache policy: sc1 (device coherence)
-
-__device__ __forceinline__ void publish16(__amdgpu_buffer_rsrc_t r, int unit, double v, unsigned tag)
-{
-    const unsigned long long w = (unsigned long long)__double_as_longlong(v);
-    const u32x4 g = {(unsigned)w, tag, (unsigned)(w >> 32), tag};
-    __builtin_amdgcn_raw_buffer_store_b128(g, r, unit * 16, 0, kPolSc1);
-}
+// (16-B granules {lo, tag, hi, tag}, publish16: gnss_internal.h, shared with the VT loop)
 
 // Poll n 16-B granules until both tags of each equal `tag`; granule e's words land in
 // dst[2e], dst[2e+1]. Same protocol as sweep_words (pollers pid 0..np-1, n <= 64*np).

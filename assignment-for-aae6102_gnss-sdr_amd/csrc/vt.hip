@@ -158,13 +158,11 @@ __device__ __forceinline__ void tree2s(double* r0, double* r1, int tid)
 // block order and writes the channel's two sums through to the caller's coherent host memory
 // with the step's number beside them. No block waits for another; the host runs the scalar
 // end (vt_finish) of each channel.
-// The step of block (b, ch): channel ch's read of ns samples at byte `off` of the window,
-// carrier frequency f and phase phi0 (ns 0: the channel sits the step out); the grid's last
-// block posts `seq`. s_r0 / s_r1: the block's kVtStepThreads-entry LDS arrays.
-__device__ __forceinline__ void vt_step_block(const uint8_t* rec, double Fs, bool real8, const VtBlockStep& st,
-                                              double* part, double* sums, unsigned* done, unsigned* ticket,
-                                              unsigned seq, int b, int ch, int nb, int nch, int tid, double* s_r0,
-                                              double* s_r1, int* s_last)
+// The sums of block (b, ch) over its slice of channel ch's read (ns samples at byte `off` of
+// the window, carrier frequency f and phase phi0; ns 0: the channel sits the step out), left
+// in s_r0[0] / s_r1[0] (the block's kVtStepThreads-entry LDS arrays; ends with a barrier).
+__device__ __forceinline__ void vt_block_sums(const uint8_t* rec, double Fs, bool real8, const VtBlockStep& st,
+                                              int b, int nb, int tid, double* s_r0, double* s_r1)
 {
     const int64_t n = st.ns;
     const int64_t chunk = (n + nb - 1) / nb;
@@ -222,6 +220,16 @@ __device__ __forceinline__ void vt_step_block(const uint8_t* rec, double Fs, boo
     s_r0[tid] = sI;
     s_r1[tid] = sQ;
     tree2s(s_r0, s_r1, tid);
+}
+
+// The step of block (b, ch) in a one-step launch (vt_step_kernel): its sums, then the hand-off
+// through device memory and a ticket; the grid's last block posts `seq`.
+__device__ __forceinline__ void vt_step_block(const uint8_t* rec, double Fs, bool real8, const VtBlockStep& st,
+                                              double* part, double* sums, unsigned* done, unsigned* ticket,
+                                              unsigned seq, int b, int ch, int nb, int nch, int tid, double* s_r0,
+                                              double* s_r1, int* s_last)
+{
+    vt_block_sums(rec, Fs, real8, st, b, nb, tid, s_r0, s_r1);
     if (tid == 0) {
         // device-coherent stores (past this XCD's L2), drained before the block's ticket: the
         // grid's last block reads them with device-coherent loads. (No agent-scope release /
@@ -283,81 +291,133 @@ __global__ __launch_bounds__(kVtStepThreads) void vt_step_kernel(VtStepArgs a)
                   gridDim.y, threadIdx.x, s_r0, s_r1, &s_last);
 }
 
-// The same steps from ONE launch (gnss_tracking_vt's loop mode). Block (0, 0) waits for the
-// host to post the next step in the mailbox (coherent host memory: the step's reads, then its
-// number), copies the reads to device memory and posts the number there; every other block
-// waits on that device word (so one block, not the grid, polls across PCIe), runs its
-// vt_step_block, and waits again. A stop word, or no new step within a.timeout, ends every
-// block. A step's blocks need no other block of the grid to be running (the last block only
-// counts tickets), so the launch only has to fit on the chip (launch_vt_loop bounds the grid).
+// The same steps from ONE launch (gnss_tracking_vt's loop mode). Block (0, 0), the lead,
+// waits for the host to post the next step in the mailbox (coherent host memory: the step's
+// reads, then its number) and relays each channel's read as kVtStepWords 16-B granules tagged
+// with the step's number (device memory); every other block polls its channel's granules, so
+// one block, not the grid, polls across PCIe. Each block then publishes its two sums as granules
+// of the same tag, and the lead, its own slice done, gathers every block's into LDS, adds each
+// channel's in block order (the sums of vt_step_kernel, bit for bit), writes them through to the
+// host and posts the step's number. A stop word, or no new step within a.timeout, ends the
+// launch (the lead relays the stop as a kVtLoopStop tag). A step's blocks need no other block
+// of the grid to be running but the lead, so the launch only has to fit on the chip
+// (launch_vt_loop bounds the grid).
+// word w of a relayed step (VtBlockStep's order; the integers travel as their bits)
+__device__ __forceinline__ void step_word(VtBlockStep& st, int w, double v)
+{
+    if (w == 0) st.off = __double_as_longlong(v);
+    else if (w == 1) st.ns = __double_as_longlong(v);
+    else if (w == 2) st.f = v;
+    else if (w == 3) st.phi0 = v;
+    else st.rfs = v;
+}
+
 __global__ __launch_bounds__(kVtStepThreads) void vt_loop_kernel(VtLoopArgs a)
 {
     __shared__ double s_r0[kVtStepThreads], s_r1[kVtStepThreads];
-    __shared__ int s_last, s_go;
+    __shared__ double s_part[2 * kVtLoopMaxBlocks];
+    __shared__ int s_go;
     __shared__ VtBlockStep s_st;
-    const int b = blockIdx.x, ch = blockIdx.y, tid = threadIdx.x, nch = gridDim.y;
+    const int b = blockIdx.x, ch = blockIdx.y, tid = threadIdx.x, nb = gridDim.x, nch = gridDim.y;
     const bool lead = b == 0 && ch == 0;
     const VtMail* m = a.mail;
+    const __amdgpu_buffer_rsrc_t gs = __builtin_amdgcn_make_buffer_rsrc(a.gstep, (short)0,
+                                                                        nch * kVtStepWords * 16, kBufRsrcWord3);
+    const __amdgpu_buffer_rsrc_t gp = __builtin_amdgcn_make_buffer_rsrc(a.gpart, (short)0, nch * nb * 2 * 16,
+                                                                        kBufRsrcWord3);
     for (unsigned seq = a.seq0;; seq++) {
-        if (tid == 0) {
-            const uint64_t t0 = (uint64_t)wall_clock64();
-            int go = 0;
-            for (;;) {
-                if (lead) {  // (system-scope loads: past every cache, to the host's memory)
+        if (lead) {
+            if (tid == 0) {
+                const uint64_t t0 = (uint64_t)wall_clock64();
+                int go = 0;
+                for (;;) {  // (system-scope loads: past every cache, to the host's memory)
                     if (__hip_atomic_load(&m->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
                     if (__hip_atomic_load(&m->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == seq) {
                         go = 1;
                         break;
                     }
-                } else {  // (device-coherent loads of the lead's word)
-                    const unsigned d = __hip_atomic_load(a.dseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (d == kVtLoopStop) break;
-                    if (d == seq) {
-                        go = 1;
-                        break;
-                    }
+                    if ((uint64_t)wall_clock64() - t0 > a.timeout) break;
+                    __builtin_amdgcn_s_sleep(2);
                 }
-                if ((uint64_t)wall_clock64() - t0 > a.timeout) break;
-                __builtin_amdgcn_s_sleep(2);
-            }
-            s_go = go;
-        }
-        __syncthreads();
-        if (lead) {
-            // the step's reads to device memory (lane c: channel c; the host wrote them before
-            // the number), drained, then the number -- or the stop word
-            if (s_go && tid < nch) {
-                VtBlockStep c;
-                c.off = __hip_atomic_load(&m->off[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                c.ns = __hip_atomic_load(&m->ns[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                c.f = __hip_atomic_load(&m->f[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                c.phi0 = __hip_atomic_load(&m->phi0[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                c.rfs = __hip_atomic_load(&m->rfs[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                VtBlockStep* d = a.dstep + tid;
-                __hip_atomic_store(&d->off, c.off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&d->ns, c.ns, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&d->f, c.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&d->phi0, c.phi0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&d->rfs, c.rfs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (tid == 0) s_st = c;
+                s_go = go;
             }
             __syncthreads();
-            if (tid == 0) __hip_atomic_store(a.dseq, s_go ? seq : kVtLoopStop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else if (s_go && tid == 0) {
-            const VtBlockStep* d = a.dstep + ch;
-            s_st.off = __hip_atomic_load(&d->off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_st.ns = __hip_atomic_load(&d->ns, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_st.f = __hip_atomic_load(&d->f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_st.phi0 = __hip_atomic_load(&d->phi0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_st.rfs = __hip_atomic_load(&d->rfs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // lane c * kVtStepWords + w: word w of channel c's read (the host wrote them before
+            // the number), relayed as a granule of this step's tag -- or every granule the stop tag
+            if (tid < nch * kVtStepWords) {
+                const int c = tid / kVtStepWords, w = tid - c * kVtStepWords;
+                double v = 0.0;
+                if (s_go) {
+                    if (w == 0) v = __longlong_as_double(__hip_atomic_load(&m->off[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+                    else if (w == 1) v = __longlong_as_double(__hip_atomic_load(&m->ns[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+                    else if (w == 2) v = __hip_atomic_load(&m->f[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    else if (w == 3) v = __hip_atomic_load(&m->phi0[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    else v = __hip_atomic_load(&m->rfs[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+                publish16(gs, tid, v, s_go ? seq : kVtLoopStop);
+                if (c == 0) step_word(s_st, w, v);  // (the lead's own channel)
+            }
+        } else if (tid < 64) {
+            // wave 0: lanes 0..kVtStepWords-1 poll the channel's granules until every one
+            // carries this step's tag (or the stop tag)
+            const bool mine = tid < kVtStepWords;
+            const uint64_t t0 = (uint64_t)wall_clock64();
+            int go = 0;
+            for (;;) {
+                const u32x4 g = mine ? load16(gs, ch * kVtStepWords + tid) : u32x4{0u, 0u, 0u, 0u};
+                const unsigned long long ok = __ballot(mine && g.y == seq && g.w == seq);
+                const unsigned long long stop = __ballot(mine && g.y == kVtLoopStop && g.w == kVtLoopStop);
+                if (stop) break;
+                if ((ok & ((1ull << kVtStepWords) - 1)) == (1ull << kVtStepWords) - 1) {
+                    if (mine) step_word(s_st, tid, value16(g));
+                    go = 1;
+                    break;
+                }
+                if ((uint64_t)wall_clock64() - t0 > a.timeout) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (tid == 0) s_go = go;
         }
         __syncthreads();
         if (!s_go) return;
         const VtBlockStep st = s_st;
-        vt_step_block(a.rec, a.Fs, a.real8, st, a.part, a.sums, a.done, a.ticket, seq, b, ch, gridDim.x, nch, tid,
-                      s_r0, s_r1, &s_last);
-        __syncthreads();  // (every lane is past the step before lane 0 reads the next one)
+        vt_block_sums(a.rec, a.Fs, a.real8, st, b, nb, tid, s_r0, s_r1);
+        if (tid < 2) publish16(gp, 2 * (ch * nb + b) + tid, tid ? s_r1[0] : s_r0[0], seq);
+        if (lead) {
+            // every block's two sums, lane-strided (a granule seen once is not read again), into LDS
+            const int ng = 2 * nch * nb;
+            unsigned long long todo = 0;  // bit k: granule tid + k * kVtStepThreads still missing
+            for (int k = 0, e = tid; e < ng; k++, e += kVtStepThreads) todo |= 1ull << k;
+            const uint64_t t0 = (uint64_t)wall_clock64();
+            while (todo) {
+                for (int k = 0; (todo >> k) != 0; k++) {
+                    if (!((todo >> k) & 1ull)) continue;
+                    const int e = tid + k * kVtStepThreads;
+                    const u32x4 g = load16(gp, e);
+                    if (g.y == seq && g.w == seq) {
+                        s_part[e] = value16(g);
+                        todo &= ~(1ull << k);
+                    }
+                }
+                if (todo && (uint64_t)wall_clock64() - t0 > a.timeout) break;
+            }
+            if (__syncthreads_or(todo != 0)) return;  // (timed out: the host sees the launch end)
+            // lane c adds channel c's partials in block order (vt_step_block's sum), writes the two
+            // sums through to the host; once every lane's are drained, lane 0 posts the number
+            if (tid < nch) {
+                double I = 0.0, Q = 0.0;
+                for (int k = 0; k < nb; k++) {
+                    I += s_part[2 * (tid * nb + k)];
+                    Q += s_part[2 * (tid * nb + k) + 1];
+                }
+                __hip_atomic_store(a.sums + 2 * tid, I, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(a.sums + 2 * tid + 1, Q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store(a.done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __syncthreads();  // (every lane is past the step before the next one's LDS writes)
     }
 }
 
@@ -371,8 +431,8 @@ hipError_t launch_vt_run(const VtRunArgs& a, hipStream_t s)
 
 hipError_t launch_vt_loop(const VtLoopArgs& a, int n, int nb, hipStream_t s)
 {
-    if (n < 1 || n > GNSS_VT_MAX_CH || nb < 1 || (int64_t)n * nb > kVtLoopMaxBlocks || !a.rec || !a.mail || !a.part ||
-        !a.sums || !a.done || !a.ticket || !a.dseq || !a.dstep)
+    if (n < 1 || n > GNSS_VT_MAX_CH || nb < 1 || (int64_t)n * nb > kVtLoopMaxBlocks || !a.rec || !a.mail || !a.sums ||
+        !a.done || !a.gstep || !a.gpart)
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(vt_loop_kernel, dim3(nb, n), dim3(kVtStepThreads), 0, s, a);
     return hipGetLastError();
