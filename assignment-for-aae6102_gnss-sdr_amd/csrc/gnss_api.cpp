@@ -2322,8 +2322,13 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     int64_t kmax_rfs = 0;
     double rfs = 0;
     if (multi) {
-        nb = (int)std::min<int64_t>(std::max<int64_t>(1, (nominal + kVtStepSamples - 1) / kVtStepSamples),
-                                    GNSS_VT_MAX_BLOCKS);
+        // blocks per channel, the engine's choice per path (r06_vt_loop_nb*.txt): one launch per
+        // step pays a ticket per block, the loop's lead gathers every block's granules at once
+        const bool loop_ok = !ctx->profiling && !ctx->opt[GNSS_OPT_NO_PERSIST];
+        nb = loop_ok ? (int)std::min<int64_t>(std::max<int64_t>(1, (nominal + kVtLoopSamples - 1) / kVtLoopSamples),
+                                              std::max(1, kVtLoopMaxBlocks / n))
+                     : (int)std::min<int64_t>(std::max<int64_t>(1, (nominal + kVtStepSamples - 1) / kVtStepSamples),
+                                              GNSS_VT_MAX_BLOCKS);
         if (ctx->opt[GNSS_OPT_VT_BLOCKS] > 0) nb = (int)ctx->opt[GNSS_OPT_VT_BLOCKS];
         B.sums = pinned_buffer<double>(ctx, "vt.sums", 2 * (size_t)n, hipHostMallocCoherent);
         B.done = pinned_buffer<unsigned>(ctx, "vt.done", 1, hipHostMallocCoherent);

@@ -815,6 +815,7 @@ constexpr double kVtLoopTimeoutS = 10;  // seconds a loop block waits for the ne
 hipError_t launch_vt_loop(const VtLoopArgs& a, int n, int nb, hipStream_t s);
 constexpr int kVtStepThreads = 256;
 constexpr int kVtStepSamples = 8 * kVtStepThreads;  // samples per block at the nominal read
+constexpr int kVtLoopSamples = 3 * kVtStepThreads;  // ... in loop mode (vt_loop_kernel)
 // generateCAcode.m's 1023 +-1 chips of `prn` (host)
 void ca_chips(int prn, float* out);
 

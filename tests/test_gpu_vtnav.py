@@ -231,8 +231,10 @@ def test_vector_tracking_loop_mode_equals_step_launches(pkg, po, ctx, opensky_sh
     run is also held against the oracle's closed loop."""
     skip, cfg, data = opensky_short
     nsteps = 300
-    z, ct, tck_l, nsol_l, t_l = _vt_run(pkg, ctx, opts, data, skip, nsteps, OPT_VT_SPAN=40)
-    _, _, tck_s, nsol_s, t_s = _vt_run(pkg, ctx, opts, data, skip, nsteps, OPT_VT_SPAN=40, OPT_NO_PERSIST=1)
+    # (the same blocks per channel on both paths: the engine's choice differs between them)
+    z, ct, tck_l, nsol_l, t_l = _vt_run(pkg, ctx, opts, data, skip, nsteps, OPT_VT_SPAN=40, OPT_VT_BLOCKS=76)
+    _, _, tck_s, nsol_s, t_s = _vt_run(pkg, ctx, opts, data, skip, nsteps, OPT_VT_SPAN=40, OPT_VT_BLOCKS=76,
+                                       OPT_NO_PERSIST=1)
     assert t_l["track_launches"] == t_s["track_launches"] == nsteps
     assert t_l["h2d_bytes"] > 0 and t_l["h2d_bytes"] == t_s["h2d_bytes"]  # (the same windows staged)
     for p in (int(x) for x in z["prns"]):
