@@ -2253,6 +2253,31 @@ hipError_t wait_posted(hipStream_t stream, const unsigned* done, unsigned seq)
         }
     }
 }
+
+// The same for the loop mode's sums: until the n granules all carry `seq`, their values to
+// `out` (a granule seen once is not read again: the scan resumes where it stopped).
+hipError_t wait_granules(hipStream_t stream, const VtGran* g, int n, unsigned seq, double* out)
+{
+    int i = 0;
+    auto posted = [&] {
+        uint64_t bits;
+        while (i < n && vt_gran_get(g + i, seq, &bits)) {
+            std::memcpy(out + i, &bits, sizeof bits);
+            i++;
+        }
+        return i == n;
+    };
+    for (unsigned k = 1;; k++) {
+        if (posted()) return hipSuccess;
+        __builtin_ia32_pause();
+        if ((k & 255) == 0) {
+            const hipError_t e = hipStreamQuery(stream);
+            if (e == hipErrorNotReady) continue;
+            if (e != hipSuccess) return e;
+            return posted() ? hipSuccess : hipErrorLaunchFailure;
+        }
+    }
+}
 }  // namespace
 
 // trackingVT_POS_updated.m:157-476, the whole EKF-driven loop: per step, each channel's read
@@ -2374,27 +2399,29 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     // memory, so a step costs no launch; stopped before a re-staging of the IF window and at
     // the end (also on every early return: `loop_guard`).
     const bool loop_mode = multi && !ctx->profiling && !ctx->opt[GNSS_OPT_NO_PERSIST] && (int64_t)n * nb <= kVtLoopMaxBlocks;
-    VtMail* mail = nullptr;
+    VtGran *mail = nullptr, *gsums = nullptr;
+    std::vector<double> loop_sums(2 * (size_t)n);
     bool running = false;
     // the loop's 16-B granules: each channel's relayed read, then every block's two sums
     const size_t gstep_bytes = (size_t)16 * kVtStepWords * n, loop_bytes = gstep_bytes + (size_t)16 * 2 * n * nb;
     uint64_t loop_timeout = 0;
     if (loop_mode) {
-        mail = pinned_buffer<VtMail>(ctx, "vt.mail", 1, hipHostMallocCoherent);
-        if (!mail) return fail(ctx, GNSS_EDEVICE, "pinned VT mailbox");
-        __atomic_store_n(&mail->stop, 0, __ATOMIC_RELAXED);
-        __atomic_store_n(&mail->seq, 0u, __ATOMIC_RELAXED);
+        mail = pinned_buffer<VtGran>(ctx, "vt.mail", (size_t)kVtStepWords * n, hipHostMallocCoherent);
+        gsums = pinned_buffer<VtGran>(ctx, "vt.gsums", 2 * (size_t)n, hipHostMallocCoherent);
+        if (!mail || !gsums) return fail(ctx, GNSS_EDEVICE, "pinned VT mailbox");
+        for (int k = 0; k < kVtStepWords * n; k++) vt_gran_put(mail + k, 0, 0);
+        for (int k = 0; k < 2 * n; k++) vt_gran_put(gsums + k, 0, 0);
         int khz = 0;
         HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device));
         loop_timeout = (uint64_t)(std::max(khz, 1) * 1e3 * kVtLoopTimeoutS);
         HIP_TRY(d_loop.alloc(ctx, "vt.loop", loop_bytes));
     }
-    auto stop_loop = [&]() -> hipError_t {
+    auto stop_loop = [&]() -> hipError_t {  // (the mailbox's stop tags, then its tags back to 0)
         if (!running) return hipSuccess;
-        __atomic_store_n(&mail->stop, 1, __ATOMIC_RELEASE);
+        for (int k = 0; k < kVtStepWords * n; k++) vt_gran_put(mail + k, 0, kVtLoopStop);
         running = false;
         const hipError_t e = hipStreamSynchronize(ctx->stream);
-        __atomic_store_n(&mail->stop, 0, __ATOMIC_RELAXED);
+        for (int k = 0; k < kVtStepWords * n; k++) vt_gran_put(mail + k, 0, 0);
         return e;
     };
     struct LoopGuard {
@@ -2488,22 +2515,27 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
             }
             B.rec = A.rec;
             B.seq = (unsigned)s + 1;
-            if (loop_mode) {  // the reads, then the step's number
-                for (int i = 0; i < n; i++) {
-                    mail->off[i] = B.off[i];
-                    mail->ns[i] = B.ns[i];
-                    mail->f[i] = B.f[i];
-                    mail->phi0[i] = B.phi0[i];
-                    mail->rfs[i] = B.rfs[i];
-                }
-                if (!running) {  // (every tag back to 0: a stopped launch left kVtLoopStop, a former call its steps)
+            if (loop_mode) {
+                if (!running) {  // (every device tag back to 0: a stopped launch left kVtLoopStop, a former call its steps)
                     HIP_TRY(hipMemsetAsync(d_loop.p, 0, loop_bytes, ctx->stream));
-                    const VtLoopArgs L{B.rec, B.Fs, B.real8, B.seq, mail, B.sums, B.done, loop_timeout, d_loop.p,
+                    const VtLoopArgs L{B.rec, B.Fs, B.real8, B.seq, mail, gsums, loop_timeout, d_loop.p,
                                        d_loop.as<char>() + gstep_bytes};
                     HIP_TRY(launch_vt_loop(L, n, nb, ctx->stream));
                     running = true;
                 }
-                __atomic_store_n(&mail->seq, B.seq, __ATOMIC_RELEASE);
+                // the step's reads as granules tagged with its number (VtBlockStep's word order)
+                for (int i = 0; i < n; i++) {
+                    VtGran* g = mail + (size_t)kVtStepWords * i;
+                    uint64_t f, phi0, rf;
+                    std::memcpy(&f, &B.f[i], 8);
+                    std::memcpy(&phi0, &B.phi0[i], 8);
+                    std::memcpy(&rf, &B.rfs[i], 8);
+                    vt_gran_put(g + 0, (uint64_t)B.off[i], B.seq);
+                    vt_gran_put(g + 1, (uint64_t)B.ns[i], B.seq);
+                    vt_gran_put(g + 2, f, B.seq);
+                    vt_gran_put(g + 3, phi0, B.seq);
+                    vt_gran_put(g + 4, rf, B.seq);
+                }
             } else {
                 if (ctx->profiling) HIP_TRY(hipEventRecord(ev.a, ctx->stream));
                 HIP_TRY(launch_vt_step(B, n, nb, ctx->stream));
@@ -2533,7 +2565,8 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
             t_b = t;
         }
         if (!multi || ctx->profiling) HIP_TRY(hipStreamSynchronize(ctx->stream));
-        if (multi) HIP_TRY(wait_posted(ctx->stream, B.done, (unsigned)s + 1));
+        if (loop_mode) HIP_TRY(wait_granules(ctx->stream, gsums, 2 * n, (unsigned)s + 1, loop_sums.data()));
+        else if (multi) HIP_TRY(wait_posted(ctx->stream, B.done, (unsigned)s + 1));
         if (stamps) {
             t_a = now_us();
             st_wait += t_a - t_b;
@@ -2546,7 +2579,8 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
                 h.status = bad[(size_t)i];
                 continue;
             }
-            const double I = B.sums[2 * i], Q = B.sums[2 * i + 1];
+            const double* sum = loop_mode ? loop_sums.data() : B.sums;
+            const double I = sum[2 * i], Q = sum[2 * i + 1];
             const unsigned* cb = &cab[(size_t)i * 32];
             int code[3];
             for (int t = 0; t < 3; t++)

@@ -217,6 +217,18 @@ __device__ __forceinline__ u32x4 load16(__amdgpu_buffer_rsrc_t r, int unit)
 {
     return __builtin_amdgcn_raw_buffer_load_b128(r, unit * 16, 0, kPolSc1);
 }
+// the same across PCIe to coherent host memory: system coherence (sc0 sc1), past every cache
+constexpr int kPolSys = 17;
+__device__ __forceinline__ void publish16_sys(__amdgpu_buffer_rsrc_t r, int unit, double v, unsigned tag)
+{
+    const unsigned long long w = (unsigned long long)__double_as_longlong(v);
+    const u32x4 g = {(unsigned)w, tag, (unsigned)(w >> 32), tag};
+    __builtin_amdgcn_raw_buffer_store_b128(g, r, unit * 16, 0, kPolSys);
+}
+__device__ __forceinline__ u32x4 load16_sys(__amdgpu_buffer_rsrc_t r, int unit)
+{
+    return __builtin_amdgcn_raw_buffer_load_b128(r, unit * 16, 0, kPolSys);
+}
 __device__ __forceinline__ double value16(u32x4 g)
 {
     return __longlong_as_double((long long)(((unsigned long long)g.z << 32) | g.x));
@@ -780,17 +792,30 @@ struct VtStepArgs {
     double rfs[GNSS_VT_MAX_CH];     // RN(1/Fs) if k/Fs = div_markstein for k < ns (host-verified), else 0
 };
 hipError_t launch_vt_step(const VtStepArgs& a, int n, int nb, hipStream_t s);
-// The EKF loop's steps from one launch (vt_loop_kernel): the host posts each step's reads and
-// then its number (seq0, seq0 + 1, ...) in `mail` (read by one block, which relays them through
-// device memory to the rest and gathers their sums); each step completes as a vt_step_kernel
-// launch would (sums, then *done = its number). `stop` != 0 ends the launch, and so does no new
-// step within `timeout` (then the host sees the stream idle with the step not done).
-struct VtMail {
-    unsigned seq;  // the step to run (written after its reads)
-    int stop;
-    int64_t off[GNSS_VT_MAX_CH], ns[GNSS_VT_MAX_CH];
-    double f[GNSS_VT_MAX_CH], phi0[GNSS_VT_MAX_CH], rfs[GNSS_VT_MAX_CH];
+// The EKF loop's steps from one launch (vt_loop_kernel). Both directions are 16-B granules
+// {lo, tag, hi, tag} in coherent host memory, tagged with the step's number (seq0, seq0 + 1,
+// ...): the host writes each channel's read as kVtStepWords granules (vt_mail_put), read by one
+// block that relays them through device memory to the rest and gathers their sums; the step
+// completes when the channel sums' 2n granules carry its number (vt_sums_get). Read granules
+// tagged kVtLoopStop end the launch, and so does no new step within `timeout` (then the host
+// sees the stream idle with the step not done). Each 8-B half is written and read whole, so a
+// granule read while it is rewritten has one stale tag and is not accepted.
+struct alignas(16) VtGran {
+    uint64_t lo, hi;  // {value bits 0..31, tag}, {value bits 32..63, tag}
 };
+inline void vt_gran_put(VtGran* g, uint64_t bits, unsigned tag)
+{
+    __atomic_store_n(&g->lo, (bits & 0xffffffffull) | ((uint64_t)tag << 32), __ATOMIC_RELAXED);
+    __atomic_store_n(&g->hi, (bits >> 32) | ((uint64_t)tag << 32), __ATOMIC_RELAXED);
+}
+// the value of a granule carrying `tag`, else false
+inline bool vt_gran_get(const VtGran* g, unsigned tag, uint64_t* bits)
+{
+    const uint64_t lo = __atomic_load_n(&g->lo, __ATOMIC_ACQUIRE), hi = __atomic_load_n(&g->hi, __ATOMIC_ACQUIRE);
+    if ((unsigned)(lo >> 32) != tag || (unsigned)(hi >> 32) != tag) return false;
+    *bits = (lo & 0xffffffffull) | (hi << 32);
+    return true;
+}
 struct VtBlockStep {  // one channel's read of a step
     int64_t off, ns;     // first byte in the window, samples (0: the channel sits the step out)
     double f, phi0;      // carrFreq, remCarrPhase
@@ -803,9 +828,8 @@ struct VtLoopArgs {
     double Fs;
     int real8;
     unsigned seq0;
-    const VtMail* mail;  // coherent host memory
-    double* sums;        // [n][2], coherent host memory
-    unsigned* done;      // [1], coherent host memory
+    const VtGran* mail;  // [n][kVtStepWords], coherent host memory: the steps' reads
+    VtGran* sums;        // [n][2], coherent host memory: the channels' sums
     uint64_t timeout;    // wall-clock ticks (wall_clock64) a block waits for a step
     void* gstep;         // [n][kVtStepWords] 16-B granules, device memory: the relayed reads
     void* gpart;         // [n][nb][2] 16-B granules, device memory: the blocks' sums

@@ -291,17 +291,16 @@ __global__ __launch_bounds__(kVtStepThreads) void vt_step_kernel(VtStepArgs a)
                   gridDim.y, threadIdx.x, s_r0, s_r1, &s_last);
 }
 
-// The same steps from ONE launch (gnss_tracking_vt's loop mode). Block (0, 0), the lead,
-// waits for the host to post the next step in the mailbox (coherent host memory: the step's
-// reads, then its number) and relays each channel's read as kVtStepWords 16-B granules tagged
-// with the step's number (device memory); every other block polls its channel's granules, so
-// one block, not the grid, polls across PCIe. Each block then publishes its two sums as granules
-// of the same tag, and the lead, its own slice done, gathers every block's into LDS, adds each
-// channel's in block order (the sums of vt_step_kernel, bit for bit), writes them through to the
-// host and posts the step's number. A stop word, or no new step within a.timeout, ends the
-// launch (the lead relays the stop as a kVtLoopStop tag). A step's blocks need no other block
-// of the grid to be running but the lead, so the launch only has to fit on the chip
-// (launch_vt_loop bounds the grid).
+// The same steps from ONE launch (gnss_tracking_vt's loop mode). Block (0, 0), the lead, polls
+// the host's mailbox granules (coherent host memory: each channel's read as kVtStepWords 16-B
+// granules tagged with the step's number) and relays them as granules of the same tag in device
+// memory; every other block polls its channel's, so one block, not the grid, polls across PCIe.
+// Each block publishes its two sums as granules of the step's tag, and the lead, its own slice
+// done, gathers every block's into LDS, adds each channel's in block order (the sums of
+// vt_step_kernel, bit for bit) and writes them to the host as tagged granules. Mailbox granules
+// tagged kVtLoopStop, or no new step within a.timeout, end the launch (the lead relays the stop
+// tag). A step's blocks need no other block of the grid to be running but the lead, so the
+// launch only has to fit on the chip (launch_vt_loop bounds the grid).
 // word w of a relayed step (VtBlockStep's order; the integers travel as their bits)
 __device__ __forceinline__ void step_word(VtBlockStep& st, int w, double v)
 {
@@ -320,43 +319,38 @@ __global__ __launch_bounds__(kVtStepThreads) void vt_loop_kernel(VtLoopArgs a)
     __shared__ VtBlockStep s_st;
     const int b = blockIdx.x, ch = blockIdx.y, tid = threadIdx.x, nb = gridDim.x, nch = gridDim.y;
     const bool lead = b == 0 && ch == 0;
-    const VtMail* m = a.mail;
     const __amdgpu_buffer_rsrc_t gs = __builtin_amdgcn_make_buffer_rsrc(a.gstep, (short)0,
                                                                         nch * kVtStepWords * 16, kBufRsrcWord3);
     const __amdgpu_buffer_rsrc_t gp = __builtin_amdgcn_make_buffer_rsrc(a.gpart, (short)0, nch * nb * 2 * 16,
                                                                         kBufRsrcWord3);
+    const __amdgpu_buffer_rsrc_t hm = __builtin_amdgcn_make_buffer_rsrc((void*)a.mail, (short)0,
+                                                                        nch * kVtStepWords * 16, kBufRsrcWord3);
+    const __amdgpu_buffer_rsrc_t hs = __builtin_amdgcn_make_buffer_rsrc(a.sums, (short)0, nch * 2 * 16, kBufRsrcWord3);
     for (unsigned seq = a.seq0;; seq++) {
         if (lead) {
-            if (tid == 0) {
+            // lane c * kVtStepWords + w polls word w of channel c's read across PCIe (system
+            // coherence: past every cache) until it carries this step's number, then relays it
+            // as a granule of the same tag -- a stop tag (or the wait's bound) relays the stop
+            const int nw = nch * kVtStepWords;
+            int stop = 0;
+            u32x4 g = {0u, 0u, 0u, 0u};
+            if (tid < nw) {
                 const uint64_t t0 = (uint64_t)wall_clock64();
-                int go = 0;
-                for (;;) {  // (system-scope loads: past every cache, to the host's memory)
-                    if (__hip_atomic_load(&m->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
-                    if (__hip_atomic_load(&m->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == seq) {
-                        go = 1;
+                for (;;) {
+                    g = load16_sys(hm, tid);
+                    if (g.y == seq && g.w == seq) break;
+                    if ((g.y == kVtLoopStop && g.w == kVtLoopStop) || (uint64_t)wall_clock64() - t0 > a.timeout) {
+                        stop = 1;
                         break;
                     }
-                    if ((uint64_t)wall_clock64() - t0 > a.timeout) break;
-                    __builtin_amdgcn_s_sleep(2);
+                    __builtin_amdgcn_s_sleep(1);
                 }
-                s_go = go;
-            }
-            __syncthreads();
-            // lane c * kVtStepWords + w: word w of channel c's read (the host wrote them before
-            // the number), relayed as a granule of this step's tag -- or every granule the stop tag
-            if (tid < nch * kVtStepWords) {
                 const int c = tid / kVtStepWords, w = tid - c * kVtStepWords;
-                double v = 0.0;
-                if (s_go) {
-                    if (w == 0) v = __longlong_as_double(__hip_atomic_load(&m->off[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-                    else if (w == 1) v = __longlong_as_double(__hip_atomic_load(&m->ns[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-                    else if (w == 2) v = __hip_atomic_load(&m->f[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    else if (w == 3) v = __hip_atomic_load(&m->phi0[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    else v = __hip_atomic_load(&m->rfs[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                }
-                publish16(gs, tid, v, s_go ? seq : kVtLoopStop);
-                if (c == 0) step_word(s_st, w, v);  // (the lead's own channel)
+                if (c == 0) step_word(s_st, w, value16(g));  // (the lead's own channel)
             }
+            stop = __syncthreads_or(stop);
+            if (tid < nw) publish16(gs, tid, stop ? 0.0 : value16(g), stop ? kVtLoopStop : seq);
+            if (tid == 0) s_go = !stop;
         } else if (tid < 64) {
             // wave 0: lanes 0..kVtStepWords-1 poll the channel's granules until every one
             // carries this step's tag (or the stop tag)
@@ -402,20 +396,17 @@ __global__ __launch_bounds__(kVtStepThreads) void vt_loop_kernel(VtLoopArgs a)
                 if (todo && (uint64_t)wall_clock64() - t0 > a.timeout) break;
             }
             if (__syncthreads_or(todo != 0)) return;  // (timed out: the host sees the launch end)
-            // lane c adds channel c's partials in block order (vt_step_block's sum), writes the two
-            // sums through to the host; once every lane's are drained, lane 0 posts the number
+            // lane c adds channel c's partials in block order (vt_step_block's sum) and writes the
+            // two sums to the host as granules of the step's tag
             if (tid < nch) {
                 double I = 0.0, Q = 0.0;
                 for (int k = 0; k < nb; k++) {
                     I += s_part[2 * (tid * nb + k)];
                     Q += s_part[2 * (tid * nb + k) + 1];
                 }
-                __hip_atomic_store(a.sums + 2 * tid, I, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                __hip_atomic_store(a.sums + 2 * tid + 1, Q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                publish16_sys(hs, 2 * tid, I, seq);
+                publish16_sys(hs, 2 * tid + 1, Q, seq);
             }
-            __syncthreads();
-            if (tid == 0) __hip_atomic_store(a.done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         __syncthreads();  // (every lane is past the step before the next one's LDS writes)
     }
@@ -432,7 +423,7 @@ hipError_t launch_vt_run(const VtRunArgs& a, hipStream_t s)
 hipError_t launch_vt_loop(const VtLoopArgs& a, int n, int nb, hipStream_t s)
 {
     if (n < 1 || n > GNSS_VT_MAX_CH || nb < 1 || (int64_t)n * nb > kVtLoopMaxBlocks || !a.rec || !a.mail || !a.sums ||
-        !a.done || !a.gstep || !a.gpart)
+        !a.gstep || !a.gpart)
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(vt_loop_kernel, dim3(nb, n), dim3(kVtStepThreads), 0, s, a);
     return hipGetLastError();
