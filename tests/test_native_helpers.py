@@ -83,3 +83,18 @@ def test_acq_fft_contraction_is_fixed_by_source():
     spec.loader.exec_module(mod)
     n = mod.main(os.path.join(ROOT, "assignment-for-aae6102_gnss-sdr_amd", "csrc", "acq_fft.hip"))
     assert n == 0
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_vt_loop_granules_and_next_read(tmp_path):
+    """The VT loop mode's host helpers (gnss_internal.h): a 16-B granule returns its value with
+    its tag, one whose halves carry different tags (read mid-rewrite) is rejected, every read
+    accepted under a concurrent writer is one it wrote; vt_remchip_next equals vt_finish's
+    remChip (trackingVT_POS_updated.m:284), which sizes the next read a step ahead."""
+    src = os.path.join(ROOT, "tests", "native", "vt_gran.cpp")
+    exe = tmp_path / "vt_gran"
+    subprocess.run([HIPCC, "-O2", "-std=c++17", "-ffp-contract=off", "-pthread", "-o", str(exe), src],
+                   check=True, capture_output=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches 0" in r.stdout
