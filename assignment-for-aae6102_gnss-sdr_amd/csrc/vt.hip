@@ -311,6 +311,9 @@ __device__ __forceinline__ void step_word(VtBlockStep& st, int w, double v)
     else st.rfs = v;
 }
 
+static_assert(GNSS_VT_MAX_CH * kVtStepWords <= kVtStepThreads, "the lead relays one mailbox granule per lane");
+static_assert(2 * kVtLoopMaxBlocks <= 64 * kVtStepThreads, "the lead's gather: at most 64 granules per lane");
+
 __global__ __launch_bounds__(kVtStepThreads) void vt_loop_kernel(VtLoopArgs a)
 {
     __shared__ double s_r0[kVtStepThreads], s_r1[kVtStepThreads];
