@@ -249,6 +249,43 @@ def test_vector_tracking_loop_mode_equals_step_launches(pkg, po, ctx, opensky_sh
     _compare(pkg, po, z, tck_l, nsol_l, rec, onav)
 
 
+def test_vector_tracking_loop_mode_at_max_channels(pkg, ctx, opensky_short, opts):
+    """The largest loop-mode grid: GNSS_VT_MAX_CH = 32 channels (the fixture's 5 repeated) at
+    the engine's 32 blocks per channel, 1 024 blocks, the loop kernel's bound: the lead relays
+    160 mailbox granules and gathers 2 048 partial granules per step. Held bit for bit against
+    one vt_step_kernel launch per step at the same blocks per channel (GNSS_OPT_NO_PERSIST):
+    every channel record and every EKF row over 60 steps."""
+    skip, cfg, data = opensky_short
+    file, signal, acq, track = params(pkg, skip, data)
+    _, _, _, _, solu, cmn = pkg.initParameters()
+    z = V.fixture()
+    Acquired, eph, sbf, ct, ns = _inputs(pkg, z, skip)
+    n = pkg.abi.VT_MAX_CH
+    reps = [int(p) for p in z["prns"]]
+    sv = [reps[i % len(reps)] for i in range(n)]
+    Acq = SimpleNamespace(sv=np.array(sv))
+    ns32 = SimpleNamespace(usrPos=ns.usrPos, usrVel=ns.usrVel, clkBias=ns.clkBias, clkDrift=ns.clkDrift,
+                           timeTransmit=np.array([[ns.timeTransmit[0][i % len(reps)] for i in range(n)]]))
+    nsteps = 60
+
+    def run(**opt):
+        for k, v in opt.items():
+            opts(getattr(pkg.abi, k), v)
+        tck, nsol = pkg.trackingVT_POS_updated(file, signal, track, cmn, solu, Acq, V.cnslxyz(pkg), eph, sbf,
+                                               None, ct, ns32, ctx=ctx, nsteps=nsteps)
+        return tck, nsol, ctx.timing()
+
+    tck_l, nsol_l, t_l = run()
+    tck_s, nsol_s, t_s = run(OPT_VT_BLOCKS=1024 // n, OPT_NO_PERSIST=1)
+    assert t_l["track_launches"] == t_s["track_launches"] == nsteps
+    for p in reps:
+        for f in ("P_i", "P_q", "E_q", "L_i", "carrFreq", "codeFreq", "remChip", "absoluteSample", "deltaPr"):
+            assert np.array_equal(getattr(tck_l(p), f), getattr(tck_s(p), f)), (p, f)
+    for f in ("usrPos", "usrVel", "clkBias", "clkDrift", "state", "newZ", "kalman_gain"):
+        assert np.array_equal(getattr(nsol_l, f), getattr(nsol_s, f)), f
+    assert np.all(np.isfinite(nsol_l.usrPos))
+
+
 def test_vector_tracking_span_option_bound(pkg, ctx):
     abi = pkg.abi
     for bad in (-1, 2001):
