@@ -2345,13 +2345,15 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     VtStepArgs B{};
     int nb = 1;
     int64_t kmax_rfs = 0;
+    int loop_cap = 0;  // blocks a loop grid may have (0: no loop mode)
     double rfs = 0;
     if (multi) {
         // blocks per channel, the engine's choice per path (r06_vt_loop_nb*.txt): one launch per
         // step pays a ticket per block, the loop's lead gathers every block's granules at once
         const bool loop_ok = !ctx->profiling && !ctx->opt[GNSS_OPT_NO_PERSIST];
-        nb = loop_ok ? (int)std::min<int64_t>(std::max<int64_t>(1, (nominal + kVtLoopSamples - 1) / kVtLoopSamples),
-                                              std::max(1, kVtLoopMaxBlocks / n))
+        loop_cap = loop_ok ? vt_loop_resident_blocks(ctx->device) : 0;
+        nb = loop_cap >= n ? (int)std::min<int64_t>(std::max<int64_t>(1, (nominal + kVtLoopSamples - 1) / kVtLoopSamples),
+                                                    loop_cap / n)
                      : (int)std::min<int64_t>(std::max<int64_t>(1, (nominal + kVtStepSamples - 1) / kVtStepSamples),
                                               GNSS_VT_MAX_BLOCKS);
         if (ctx->opt[GNSS_OPT_VT_BLOCKS] > 0) nb = (int)ctx->opt[GNSS_OPT_VT_BLOCKS];
@@ -2398,7 +2400,7 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     // vt_loop_kernel launch runs the steps, each posted through a mailbox in coherent host
     // memory, so a step costs no launch; stopped before a re-staging of the IF window and at
     // the end (also on every early return: `loop_guard`).
-    const bool loop_mode = multi && !ctx->profiling && !ctx->opt[GNSS_OPT_NO_PERSIST] && (int64_t)n * nb <= kVtLoopMaxBlocks;
+    const bool loop_mode = multi && loop_cap > 0 && (int64_t)n * nb <= loop_cap;
     VtGran *mail = nullptr, *gsums = nullptr;
     std::vector<double> loop_sums(2 * (size_t)n);
     bool running = false;
@@ -2456,6 +2458,12 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
     };
     double t_a = stamps ? now_us() : 0;
+    DevBuf d_vtst;  // (probe builds with GNSS_VT_STAMPS: the loop kernel's per-step marks)
+    if (stamps && loop_mode) {
+        const size_t nst = (size_t)kVtStampSteps * (8 + 4 * kVtLoopMaxBlocks);
+        HIP_TRY(d_vtst.alloc(ctx, "vt.stamps", sizeof(unsigned long long) * nst));
+        HIP_TRY(hipMemsetAsync(d_vtst.p, 0, sizeof(unsigned long long) * nst, ctx->stream));
+    }
     for (int s = 0; s < nsteps && result == GNSS_OK; s++) {
         int64_t need_lo = INT64_MAX, need_hi = 0;
         for (int i = 0; i < n; i++) {
@@ -2518,8 +2526,8 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
             if (loop_mode) {
                 if (!running) {  // (every device tag back to 0: a stopped launch left kVtLoopStop, a former call its steps)
                     HIP_TRY(hipMemsetAsync(d_loop.p, 0, loop_bytes, ctx->stream));
-                    const VtLoopArgs L{B.rec, B.Fs, B.real8, B.seq, mail, gsums, loop_timeout, d_loop.p,
-                                       d_loop.as<char>() + gstep_bytes};
+                    const VtLoopArgs L{B.rec, w.len, B.Fs, B.real8, B.seq, mail, gsums, loop_timeout, d_loop.p,
+                                       d_loop.as<char>() + gstep_bytes, d_vtst.as<unsigned long long>()};
                     HIP_TRY(launch_vt_loop(L, n, nb, ctx->stream));
                     running = true;
                 }
@@ -2622,6 +2630,41 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     if (stamps && nsteps > 0)
         fprintf(stderr, "vt stamps (us per step): predict+post %.2f, shadow %.2f, wait %.2f, finish+correct %.2f\n",
                 st_pre / nsteps, st_shadow / nsteps, st_wait / nsteps, st_post / nsteps);
+    if (stamps && d_vtst.p) {  // the loop kernel's marks (GNSS_VT_PROBE & 4 builds; zeros otherwise)
+        HIP_TRY(stop_loop());
+        std::vector<unsigned long long> m((size_t)kVtStampSteps * (8 + 4 * kVtLoopMaxBlocks));
+        HIP_TRY(hipMemcpy(m.data(), d_vtst.p, m.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        int khz = 0;
+        HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device));
+        const double us = 1e3 / std::max(khz, 1);
+        double d[6] = {0, 0, 0, 0, 0, 0}, d6 = 0, d7 = 0;
+        int cnt = 0;
+        // the per-block marks as their maximum over the blocks (the step's last block)
+        for (int k = 0; k < std::min(nsteps, kVtStampSteps); k++)
+            for (int q = 0; q < 4; q++) {
+                unsigned long long mx = 0;
+                const unsigned long long* bm = &m[(size_t)kVtStampSteps * 8 + ((size_t)k * 4 + q) * kVtLoopMaxBlocks];
+                for (int bl = 0; bl < kVtLoopMaxBlocks; bl++) mx = std::max(mx, bm[bl]);
+                m[(size_t)8 * k + (q == 0 ? 2 : q == 1 ? 3 : q == 2 ? 6 : 7)] = mx;
+            }
+        for (int k = 10; k + 1 < std::min(nsteps, kVtStampSteps); k++) {
+            const unsigned long long* r = &m[(size_t)8 * k];
+            const unsigned long long* r1 = &m[(size_t)8 * (k + 1)];
+            if (!r[0] || !r[5] || !r1[0]) continue;
+            for (int j = 0; j < 5; j++) d[j] += (double)(long long)(r[j + 1] - r[j]) * us;
+            d[5] += (double)(long long)(r1[0] - r[5]) * us;
+            if (r[6] && r[7]) {
+                d6 += (double)(long long)(r[6] - r[2]) * us;
+                d7 += (double)(long long)(r[7] - r[6]) * us;
+            }
+            cnt++;
+        }
+        if (cnt)
+            fprintf(stderr, "vt loop marks (us per step, %d steps): relay %.2f, to last block %.2f, to last sums %.2f "
+                            "(last terms %.2f after the last block had the step, butterfly %.2f), gather %.2f, "
+                            "sums out %.2f, sums out -> next mailbox seen %.2f\n",
+                    cnt, d[0] / cnt, d[1] / cnt, d[2] / cnt, d6 / cnt, d7 / cnt, d[3] / cnt, d[4] / cnt, d[5] / cnt);
+    }
     HIP_TRY(stop_loop());
     if (!multi) HIP_TRY(hipMemcpyAsync(chans, d_chan.p, sizeof(gnss_vt_chan) * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));

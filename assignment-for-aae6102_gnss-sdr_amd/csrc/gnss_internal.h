@@ -825,6 +825,7 @@ constexpr unsigned kVtLoopStop = 0xffffffffu;
 constexpr int kVtStepWords = 5;  // VtBlockStep's words, relayed as 16-B granules
 struct VtLoopArgs {
     const uint8_t* rec;
+    int64_t rec_len;     // the window's bytes (the next read's prefetch stays inside)
     double Fs;
     int real8;
     unsigned seq0;
@@ -833,10 +834,15 @@ struct VtLoopArgs {
     uint64_t timeout;    // wall-clock ticks (wall_clock64) a block waits for a step
     void* gstep;         // [n][kVtStepWords] 16-B granules, device memory: the relayed reads
     void* gpart;         // [n][nb][2] 16-B granules, device memory: the blocks' sums
+    unsigned long long* stamps;  // probe builds (vt.hip GNSS_VT_PROBE & 4): [kVtStampSteps][8] marks
 };
+constexpr int kVtStampSteps = 2000;
 constexpr int kVtLoopMaxBlocks = 1024;  // (co-resident on 256 CUs with room to spare)
 constexpr double kVtLoopTimeoutS = 10;  // seconds a loop block waits for the next step
 hipError_t launch_vt_loop(const VtLoopArgs& a, int n, int nb, hipStream_t s);
+// blocks of vt_loop_kernel resident at once on `device` (occupancy x CUs, at most
+// kVtLoopMaxBlocks): a loop grid must fit, since a step waits for every block's sums
+int vt_loop_resident_blocks(int device);
 constexpr int kVtStepThreads = 256;
 constexpr int kVtStepSamples = 8 * kVtStepThreads;  // samples per block at the nominal read
 constexpr int kVtLoopSamples = 3 * kVtStepThreads;  // ... in loop mode (vt_loop_kernel)

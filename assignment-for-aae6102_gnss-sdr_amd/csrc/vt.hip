@@ -16,6 +16,7 @@
 #ifndef GNSS_VT_PROBE
 #define GNSS_VT_PROBE 0  // (A/B probe builds only, tools/build_variant.sh)
 #endif
+constexpr bool kVtStamps = (GNSS_VT_PROBE & 4) != 0;
 
 namespace gnss {
 
@@ -134,19 +135,6 @@ __global__ __launch_bounds__(kVtRun) void vt_run_kernel(VtRunArgs a)
 }
 
 
-// Fixed-pairing tree over a kVtStepThreads block
-__device__ __forceinline__ void tree2s(double* r0, double* r1, int tid)
-{
-    for (int h = kVtStepThreads / 2; h > 0; h >>= 1) {
-        __syncthreads();
-        if (tid < h) {
-            r0[tid] += r0[tid + h];
-            r1[tid] += r1[tid + h];
-        }
-    }
-    __syncthreads();
-}
-
 // One step of every channel over nb blocks per channel (grid nb x n). The VT loop of
 // trackingVT_POS_updated.m is a host-driven chain (the EKF predicts every step's code
 // frequency from the last step's correlations), so a step's latency is the loop's rate:
@@ -158,12 +146,40 @@ __device__ __forceinline__ void tree2s(double* r0, double* r1, int tid)
 // block order and writes the channel's two sums through to the caller's coherent host memory
 // with the step's number beside them. No block waits for another; the host runs the scalar
 // end (vt_finish) of each channel.
+// A channel's nb block partials add up in kVtGroups runs of consecutive blocks (run g: blocks
+// [g*len, (g+1)*len), len = ceil(nb / kVtGroups), each added in block order from 0) and then the
+// runs in order: lane 8c + g of the adding block holds run g of channel c, so a channel's sum takes
+// ~nb / 8 dependent adds rather than nb. vt_step_kernel's last block and vt_loop_kernel's lead
+// form the same association: the same bits.
+constexpr int kVtGroups = 8;
+static_assert(GNSS_VT_MAX_CH * kVtGroups <= kVtStepThreads && 64 % kVtGroups == 0, "a channel's runs in one wave");
+__device__ __forceinline__ void vt_run_range(int nb, int g, int* k0, int* k1)
+{
+    const int len = (nb + kVtGroups - 1) / kVtGroups;
+    *k0 = g * len < nb ? g * len : nb;
+    *k1 = *k0 + len < nb ? *k0 + len : nb;
+}
+// the runs of lane 8c + g's channel added in order (every lane of the wave calls it)
+__device__ __forceinline__ double vt_runs_total(double run, int tid)
+{
+    double t = 0.0;
+#pragma unroll
+    for (int g = 0; g < kVtGroups; g++) t += __shfl(run, (tid & ~(kVtGroups - 1)) + g);
+    return t;
+}
+
 // The sums of block (b, ch) over its slice of channel ch's read (ns samples at byte `off` of
 // the window, carrier frequency f and phase phi0; ns 0: the channel sits the step out), left
-// in s_r0[0] / s_r1[0] (the block's kVtStepThreads-entry LDS arrays; ends with a barrier).
+// in s_r0[0] / s_r1[0] (LDS arrays of at least kVtStepThreads / 64 entries; ends with a barrier).
 __device__ __forceinline__ void vt_block_sums(const uint8_t* rec, double Fs, bool real8, const VtBlockStep& st,
-                                              int b, int nb, int tid, double* s_r0, double* s_r1)
+                                              int b, int nb, int tid, double* s_r0, double* s_r1,
+                                              unsigned long long* mark6 = nullptr, unsigned long long* mark7 = nullptr)
 {
+    auto mark = [&](unsigned long long* m) {  // (probe builds: this block's marks 6 / 7, by its lane 0)
+        if constexpr (kVtStamps)
+            if (m && tid == 0)
+                __hip_atomic_store(m, (unsigned long long)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
     const int64_t n = st.ns;
     const int64_t chunk = (n + nb - 1) / nb;
     const int64_t k0 = (int64_t)b * chunk, k1 = k0 + chunk < n ? k0 + chunk : n;
@@ -200,26 +216,45 @@ __device__ __forceinline__ void vt_block_sums(const uint8_t* rec, double Fs, boo
     };
     double sI = 0.0, sQ = 0.0;
     constexpr int U = 4, TS = kVtStepThreads;
-    int64_t k = k0 + tid;
-    for (; k + (U - 1) * TS < k1; k += U * TS) {
+    // (a slice's last few samples per lane in flight together too -- loop mode's slices are 3
+    // samples a lane: the terms past the slice are computed at the lane's first sample of the
+    // batch and not added, so every lane adds the same terms in the same order)
+    for (int64_t k = k0 + tid; k < k1; k += U * TS) {
         double tI[U], tQ[U];
 #pragma unroll
-        for (int u = 0; u < U; u++) term(k + u * TS, tI[u], tQ[u]);
+        for (int u = 0; u < U; u++) term(k + u * TS < k1 ? k + u * TS : k, tI[u], tQ[u]);
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            sI += tI[u];
-            sQ += tQ[u];
+        for (int u = 0; u < U; u++)
+            if (k + u * TS < k1) {
+                sI += tI[u];
+                sQ += tQ[u];
+            }
+    }
+    mark(mark6);
+    // the block's sum: a fixed butterfly within each wave (xor 32, 16, ..., 1), then the four
+    // wave sums in order -- the same bits for the same terms
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        sI += __shfl_xor(sI, m);
+        sQ += __shfl_xor(sQ, m);
+    }
+    mark(mark7);
+    if ((tid & 63) == 0) {
+        s_r0[tid >> 6] = sI;
+        s_r1[tid >> 6] = sQ;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double I = s_r0[0], Q = s_r1[0];
+#pragma unroll
+        for (int w = 1; w < kVtStepThreads / 64; w++) {
+            I += s_r0[w];
+            Q += s_r1[w];
         }
+        s_r0[0] = I;
+        s_r1[0] = Q;
     }
-    for (; k < k1; k += TS) {
-        double tI, tQ;
-        term(k, tI, tQ);
-        sI += tI;
-        sQ += tQ;
-    }
-    s_r0[tid] = sI;
-    s_r1[tid] = sQ;
-    tree2s(s_r0, s_r1, tid);
+    __syncthreads();
 }
 
 // The step of block (b, ch) in a one-step launch (vt_step_kernel): its sums, then the hand-off
@@ -248,7 +283,10 @@ __device__ __forceinline__ void vt_step_block(const uint8_t* rec, double Fs, boo
     // sequential sum for every nb), writes the two sums through to the caller's host memory,
     // and once every lane's are drained, lane 0 re-arms the ticket (drained too: a later step's
     // first ticket must see it) and posts the step's number
-    const int tot = nch * nb;
+    // (lane 8c + g: run g of channel c, accumulated over the chunks in block order)
+    const int tot = nch * nb, c = tid / kVtGroups;
+    int r0 = 0, r1 = 0;
+    vt_run_range(nb, tid % kVtGroups, &r0, &r1);
     double I = 0.0, Q = 0.0;
     for (int base = 0; base < tot; base += kVtStepThreads) {
         const int m = tot - base < kVtStepThreads ? tot - base : kVtStepThreads;
@@ -259,18 +297,20 @@ __device__ __forceinline__ void vt_step_block(const uint8_t* rec, double Fs, boo
             s_r1[tid] = __hip_atomic_load(pp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
-        if (tid < nch) {
-            const int lo = tid * nb > base ? tid * nb : base;
-            const int hi = tid * nb + nb < base + m ? tid * nb + nb : base + m;
+        if (c < nch) {
+            const int lo = c * nb + r0 > base ? c * nb + r0 : base;
+            const int hi = c * nb + r1 < base + m ? c * nb + r1 : base + m;
             for (int k = lo; k < hi; k++) {
                 I += s_r0[k - base];
                 Q += s_r1[k - base];
             }
         }
     }
-    if (tid < nch) {
-        __hip_atomic_store(sums + 2 * tid, I, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(sums + 2 * tid + 1, Q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    I = vt_runs_total(I, tid);
+    Q = vt_runs_total(Q, tid);
+    if (c < nch && tid % kVtGroups == 0) {
+        __hip_atomic_store(sums + 2 * c, I, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(sums + 2 * c + 1, Q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
@@ -312,9 +352,31 @@ __device__ __forceinline__ void step_word(VtBlockStep& st, int w, double v)
 }
 
 static_assert(GNSS_VT_MAX_CH * kVtStepWords <= kVtStepThreads, "the lead relays one mailbox granule per lane");
-static_assert(2 * kVtLoopMaxBlocks <= 64 * kVtStepThreads, "the lead's gather: at most 64 granules per lane");
+static_assert(2 * kVtLoopMaxBlocks <= 8 * kVtStepThreads, "the lead's gather: at most 8 granules per lane");
 
-__global__ __launch_bounds__(kVtStepThreads) void vt_loop_kernel(VtLoopArgs a)
+// (probe builds, GNSS_VT_PROBE & 4: wall-clock marks of a step: 0 the lead has the mailbox, 1 it
+// has relayed it, 2 the last block has it, 3 the last block's sums, 4 the lead has gathered them,
+// 5 the lead has written the channel sums; 6 / 7 the last block's terms / its lanes' butterfly)
+// (lead marks 0, 1, 4, 5 at stamps[step][k]; per-block marks 2, 3, 6, 7 at
+// stamps[kVtStampSteps * 8 + (step * 4 + slot) * kVtLoopMaxBlocks + block]: no two blocks share a
+// word, so the marks do not serialise the step they time)
+__device__ __forceinline__ unsigned long long* vt_mark_slot(const VtLoopArgs& a, unsigned seq, int k, int blk)
+{
+    if (!a.stamps || seq < 1 || seq > (unsigned)kVtStampSteps) return nullptr;
+    if (blk < 0) return a.stamps + (size_t)(seq - 1) * 8 + k;
+    const int slot = k == 2 ? 0 : k == 3 ? 1 : k == 6 ? 2 : 3;
+    return a.stamps + (size_t)kVtStampSteps * 8 + ((size_t)(seq - 1) * 4 + slot) * kVtLoopMaxBlocks + blk;
+}
+__device__ __forceinline__ void vt_mark(const VtLoopArgs& a, unsigned seq, int k, int blk = -1)
+{
+    if constexpr (kVtStamps) {
+        if (unsigned long long* m = vt_mark_slot(a, seq, k, blk))
+            __hip_atomic_store(m, (unsigned long long)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// (at least 4 waves per SIMD: the 1 024-block bound resident on 256 CUs at 4 blocks per CU)
+__global__ __launch_bounds__(kVtStepThreads, 4) void vt_loop_kernel(VtLoopArgs a)
 {
     __shared__ double s_r0[kVtStepThreads], s_r1[kVtStepThreads];
     __shared__ double s_part[2 * kVtLoopMaxBlocks];
@@ -352,8 +414,10 @@ __global__ __launch_bounds__(kVtStepThreads) void vt_loop_kernel(VtLoopArgs a)
                 if (c == 0) step_word(s_st, w, value16(g));  // (the lead's own channel)
             }
             stop = __syncthreads_or(stop);
+            if (tid == 0) vt_mark(a, seq, 0);
             if (tid < nw) publish16(gs, tid, stop ? 0.0 : value16(g), stop ? kVtLoopStop : seq);
             if (tid == 0) s_go = !stop;
+            if (tid == 0) vt_mark(a, seq, 1);
         } else if (tid < 64) {
             // wave 0: lanes 0..kVtStepWords-1 poll the channel's granules until every one
             // carries this step's tag (or the stop tag)
@@ -368,6 +432,7 @@ __global__ __launch_bounds__(kVtStepThreads) void vt_loop_kernel(VtLoopArgs a)
                 if ((ok & ((1ull << kVtStepWords) - 1)) == (1ull << kVtStepWords) - 1) {
                     if (mine) step_word(s_st, tid, value16(g));
                     go = 1;
+                    if (tid == 0) vt_mark(a, seq, 2, ch * nb + b);
                     break;
                 }
                 if ((uint64_t)wall_clock64() - t0 > a.timeout) break;
@@ -378,37 +443,65 @@ __global__ __launch_bounds__(kVtStepThreads) void vt_loop_kernel(VtLoopArgs a)
         __syncthreads();
         if (!s_go) return;
         const VtBlockStep st = s_st;
-        vt_block_sums(a.rec, a.Fs, a.real8, st, b, nb, tid, s_r0, s_r1);
+        vt_block_sums(a.rec, a.Fs, a.real8, st, b, nb, tid, s_r0, s_r1,
+                      kVtStamps ? vt_mark_slot(a, seq, 6, ch * nb + b) : nullptr,
+                      kVtStamps ? vt_mark_slot(a, seq, 7, ch * nb + b) : nullptr);
+        if (tid == 0) vt_mark(a, seq, 3, ch * nb + b);
         if (tid < 2) publish16(gp, 2 * (ch * nb + b) + tid, tid ? s_r1[0] : s_r0[0], seq);
+        // the channel's next read continues this one (:161-176) with about as many samples: the
+        // block touches its slice of it (one word per 64-B line, inside the window) while the
+        // next step is on its way, so the step's loads find it in this XCD's L2
+        {
+            const int bps = a.real8 ? 1 : 2;
+            const int64_t n = st.ns, chunk = (n + nb - 1) / nb;
+            const int64_t lo = st.off + n * bps + (int64_t)b * chunk * bps, hi = lo + chunk * bps;
+            if (n > 0 && hi <= a.rec_len) {
+                const int64_t l0 = lo & ~(int64_t)63;
+                const int64_t at = l0 + (int64_t)tid * 64;
+                if (at < hi) (void)*reinterpret_cast<const volatile unsigned*>(a.rec + at);
+            }
+        }
         if (lead) {
             // every block's two sums, lane-strided (a granule seen once is not read again), into LDS
             const int ng = 2 * nch * nb;
             unsigned long long todo = 0;  // bit k: granule tid + k * kVtStepThreads still missing
             for (int k = 0, e = tid; e < ng; k++, e += kVtStepThreads) todo |= 1ull << k;
             const uint64_t t0 = (uint64_t)wall_clock64();
+            constexpr int kG = 2 * kVtLoopMaxBlocks / kVtStepThreads;  // granules per lane at most
             while (todo) {
-                for (int k = 0; (todo >> k) != 0; k++) {
-                    if (!((todo >> k) & 1ull)) continue;
-                    const int e = tid + k * kVtStepThreads;
-                    const u32x4 g = load16(gp, e);
-                    if (g.y == seq && g.w == seq) {
-                        s_part[e] = value16(g);
+                u32x4 g[kG];  // (every missing granule's load in flight together, then the checks)
+#pragma unroll
+                for (int k = 0; k < kG; k++)
+                    if ((todo >> k) & 1ull) g[k] = load16(gp, tid + k * kVtStepThreads);
+#pragma unroll
+                for (int k = 0; k < kG; k++)
+                    if (((todo >> k) & 1ull) && g[k].y == seq && g[k].w == seq) {
+                        s_part[tid + k * kVtStepThreads] = value16(g[k]);
                         todo &= ~(1ull << k);
                     }
-                }
                 if (todo && (uint64_t)wall_clock64() - t0 > a.timeout) break;
             }
             if (__syncthreads_or(todo != 0)) return;  // (timed out: the host sees the launch end)
-            // lane c adds channel c's partials in block order (vt_step_block's sum) and writes the
-            // two sums to the host as granules of the step's tag
-            if (tid < nch) {
-                double I = 0.0, Q = 0.0;
-                for (int k = 0; k < nb; k++) {
-                    I += s_part[2 * (tid * nb + k)];
-                    Q += s_part[2 * (tid * nb + k) + 1];
+            if (tid == 0) vt_mark(a, seq, 4);
+            // lane 8c + g adds run g of channel c's partials, the runs add up in order (the
+            // association vt_step_block's last block forms), and the channel's two sums go to the
+            // host as granules of the step's tag
+            const int c = tid / kVtGroups;
+            double I = 0.0, Q = 0.0;
+            if (c < nch) {
+                int k0 = 0, k1 = 0;
+                vt_run_range(nb, tid % kVtGroups, &k0, &k1);
+                for (int k = k0; k < k1; k++) {
+                    I += s_part[2 * (c * nb + k)];
+                    Q += s_part[2 * (c * nb + k) + 1];
                 }
-                publish16_sys(hs, 2 * tid, I, seq);
-                publish16_sys(hs, 2 * tid + 1, Q, seq);
+            }
+            I = vt_runs_total(I, tid);
+            Q = vt_runs_total(Q, tid);
+            if (c < nch && tid % kVtGroups == 0) {
+                publish16_sys(hs, 2 * c, I, seq);
+                publish16_sys(hs, 2 * c + 1, Q, seq);
+                if (tid == 0) vt_mark(a, seq, 5);
             }
         }
         __syncthreads();  // (every lane is past the step before the next one's LDS writes)
@@ -421,6 +514,15 @@ hipError_t launch_vt_run(const VtRunArgs& a, hipStream_t s)
 {
     hipLaunchKernelGGL(vt_run_kernel, dim3(a.n), dim3(kVtRun), 0, s, a);
     return hipGetLastError();
+}
+
+int vt_loop_resident_blocks(int device)
+{
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, vt_loop_kernel, kVtStepThreads, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+        return 0;
+    return std::min(per_cu * cus, kVtLoopMaxBlocks);
 }
 
 hipError_t launch_vt_loop(const VtLoopArgs& a, int n, int nb, hipStream_t s)
