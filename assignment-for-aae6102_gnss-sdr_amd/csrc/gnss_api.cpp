@@ -2408,10 +2408,10 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     const size_t gstep_bytes = (size_t)16 * kVtStepWords * n, loop_bytes = gstep_bytes + (size_t)16 * 2 * n * nb;
     uint64_t loop_timeout = 0;
     if (loop_mode) {
-        mail = pinned_buffer<VtGran>(ctx, "vt.mail", (size_t)kVtStepWords * n, hipHostMallocCoherent);
+        mail = pinned_buffer<VtGran>(ctx, "vt.mail", 2 * (size_t)kVtStepWords * n, hipHostMallocCoherent);
         gsums = pinned_buffer<VtGran>(ctx, "vt.gsums", 2 * (size_t)n, hipHostMallocCoherent);
         if (!mail || !gsums) return fail(ctx, GNSS_EDEVICE, "pinned VT mailbox");
-        for (int k = 0; k < kVtStepWords * n; k++) vt_gran_put(mail + k, 0, 0);
+        for (int k = 0; k < 2 * kVtStepWords * n; k++) vt_gran_put(mail + k, 0, 0);
         for (int k = 0; k < 2 * n; k++) vt_gran_put(gsums + k, 0, 0);
         int khz = 0;
         HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device));
@@ -2420,10 +2420,10 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     }
     auto stop_loop = [&]() -> hipError_t {  // (the mailbox's stop tags, then its tags back to 0)
         if (!running) return hipSuccess;
-        for (int k = 0; k < kVtStepWords * n; k++) vt_gran_put(mail + k, 0, kVtLoopStop);
+        for (int k = 0; k < 2 * kVtStepWords * n; k++) vt_gran_put(mail + k, 0, kVtLoopStop);
         running = false;
         const hipError_t e = hipStreamSynchronize(ctx->stream);
-        for (int k = 0; k < kVtStepWords * n; k++) vt_gran_put(mail + k, 0, 0);
+        for (int k = 0; k < 2 * kVtStepWords * n; k++) vt_gran_put(mail + k, 0, 0);
         return e;
     };
     struct LoopGuard {
@@ -2447,6 +2447,15 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     std::vector<VtOrbit> ahead((size_t)n);
     std::vector<char> have_ahead((size_t)n, 0);
     std::unique_ptr<VtGain> gain(new VtGain);
+    // Loop mode posts the next step early: of a channel's read only the carrier frequency waits
+    // for the step's sums (the PLL, :305-311); its start, size, phase and divisor follow from the
+    // step's own read (:161-176, :284-285), so those four words go out while the kernel runs and
+    // the frequency right after vt_finish -- the EKF update and the next prediction then run
+    // beside the next step's kernel. `early`: step s's words are all out; e_*: what was posted,
+    // held against what the step computes when it comes (the same functions: the same bits).
+    bool early = false;
+    std::vector<int64_t> e_off((size_t)n), e_ns((size_t)n);
+    std::vector<double> e_phi0((size_t)n), e_rfs((size_t)n);
     Events ev;
     double kernel_ms = 0;
     int result = GNSS_OK;
@@ -2489,6 +2498,8 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
         }
         if (result) break;
         if (!file->dev_data && (need_lo < w.base || need_hi > w.base + w.len) && need_hi <= flen) {
+            if (early)  // (an early post checked the same reads against this window)
+                return fail(ctx, GNSS_EDEVICE, "step %d: posted early, then re-staged", s + 1);
             HIP_TRY(stop_loop());
             HIP_TRY(hipStreamSynchronize(ctx->stream));
             st = restage(need_lo);
@@ -2523,7 +2534,15 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
             }
             B.rec = A.rec;
             B.seq = (unsigned)s + 1;
-            if (loop_mode) {
+            if (loop_mode && early) {  // (the kernel has the step: its words were posted early)
+                for (int i = 0; i < n; i++) {
+                    if (bad[(size_t)i]) continue;  // (it sums the read; the channel stops below)
+                    if (B.off[i] != e_off[(size_t)i] || B.ns[i] != e_ns[(size_t)i] ||
+                        std::memcmp(&B.phi0[i], &e_phi0[(size_t)i], 8) || std::memcmp(&B.rfs[i], &e_rfs[(size_t)i], 8))
+                        return fail(ctx, GNSS_EDEVICE, "step %d channel %d: the early post differs from the step", s + 1,
+                                    i);
+                }
+            } else if (loop_mode) {
                 if (!running) {  // (every device tag back to 0: a stopped launch left kVtLoopStop, a former call its steps)
                     HIP_TRY(hipMemsetAsync(d_loop.p, 0, loop_bytes, ctx->stream));
                     const VtLoopArgs L{B.rec, w.len, B.Fs, B.real8, B.seq, mail, gsums, loop_timeout, d_loop.p,
@@ -2533,7 +2552,7 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
                 }
                 // the step's reads as granules tagged with its number (VtBlockStep's word order)
                 for (int i = 0; i < n; i++) {
-                    VtGran* g = mail + (size_t)kVtStepWords * i;
+                    VtGran* g = mail + (size_t)kVtStepWords * ((B.seq & 1) * n + i);
                     uint64_t f, phi0, rf;
                     std::memcpy(&f, &B.f[i], 8);
                     std::memcpy(&phi0, &B.phi0[i], 8);
@@ -2567,6 +2586,39 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
             have_ahead[(size_t)i] = q.n >= 1;
             if (q.n >= 1) vt_orbit(*nav, i, vt_transmit_next(*nav, i, q.n), &ahead[(size_t)i]);
         }
+        // the next step's words that need no sums of this one (`early` above)
+        bool early_next = loop_mode && s + 1 < nsteps;
+        for (int i = 0; i < n && early_next; i++) {
+            const gnss_vt_chan& c = hc[(size_t)i];
+            if (bad[(size_t)i]) {
+                early_next = false;
+                break;
+            }
+            const int64_t n0 = pk[(size_t)i].n;
+            const double rc = vt_remchip_next(sg->Fs, pdi, c.remChip, cf_new[i], n0);
+            const VtPrep q = vt_prepare(sg->Fs, sg->codelength, pdi, rc, cf_new[i], cf_new[i]);
+            const int64_t a0 = c.file_ptr + n0 * bps, need = q.n * bps;
+            if (q.n < 1 || a0 + need > flen || a0 < w.base || a0 + need > w.base + w.len) {
+                early_next = false;
+                break;
+            }
+            e_off[(size_t)i] = a0 - w.base;
+            e_ns[(size_t)i] = q.n;
+            e_phi0[(size_t)i] = vt_rem_carr_phase(c.carrFreq, n0, sg->Fs, c.remCarrPhase);
+            e_rfs[(size_t)i] = q.n - 1 <= kmax_rfs ? rfs : 0.0;
+        }
+        if (early_next) {
+            for (int i = 0; i < n; i++) {
+                VtGran* g = mail + (size_t)kVtStepWords * (((B.seq + 1) & 1) * n + i);
+                uint64_t phi0, rf;
+                std::memcpy(&phi0, &e_phi0[(size_t)i], 8);
+                std::memcpy(&rf, &e_rfs[(size_t)i], 8);
+                vt_gran_put(g + 0, (uint64_t)e_off[(size_t)i], B.seq + 1);
+                vt_gran_put(g + 1, (uint64_t)e_ns[(size_t)i], B.seq + 1);
+                vt_gran_put(g + 3, phi0, B.seq + 1);
+                vt_gran_put(g + 4, rf, B.seq + 1);
+            }
+        }
         if (stamps) {
             const double t = now_us();
             st_shadow += t - t_b;
@@ -2596,6 +2648,20 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
             const int st2 = vt_finish(sg->Fs, sg->ms, pdi, bps, t1, t2, &hc[(size_t)i], pk[(size_t)i], code, cf_new[i],
                                       I, Q, &h);
             if (st2) h.status = st2;
+        }
+        // the next step's carrier frequencies (the PLL's output): the kernel starts it now
+        early = false;
+        if (early_next) {
+            bool ok = true;
+            for (int i = 0; i < n; i++) ok = ok && !h_out[i].status;
+            if (ok) {
+                for (int i = 0; i < n; i++) {
+                    uint64_t f;
+                    std::memcpy(&f, &hc[(size_t)i].carrFreq, 8);
+                    vt_gran_put(mail + (size_t)kVtStepWords * (((B.seq + 1) & 1) * n + i) + 2, f, B.seq + 1);
+                }
+                early = true;
+            }
         }
         for (int i = 0; i < n; i++) {
             gnss_vt_out& o = out[(size_t)s * n + i];

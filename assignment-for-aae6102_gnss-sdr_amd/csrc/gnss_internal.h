@@ -647,6 +647,14 @@ GNSS_HD int vt_code_at(int64_t j, int pdi, CaAt ca)
     return j == 1 ? ca(1022) : j == len ? ca(0) : ca((int)((j - 2) % 1023));
 }
 
+// remCarrPhase after a read of n samples: rem(Wave(numSample+1), 2*pi) (:275-276, :285) --
+// vt_finish's, and gnss_tracking_vt's for the next step's read before the sums are in
+GNSS_HD double vt_rem_carr_phase(double carrFreq, int64_t n, double Fs, double remCarrPhase)
+{
+    const double W = kTwoPi * (carrFreq * ((double)n / Fs)) + remCarrPhase;
+    return fmod(W, kTwoPi);
+}
+
 // The rest of the step from its sums (:247-249, :284-347): E / P / L, remChip, remCarrPhase,
 // the C/N0 estimator, PLL, DLL discriminator, the record; advances `c`. bps = bytes per
 // sample (dataPrecision * dataType), code[3] = the E / P / L chip values.
@@ -661,8 +669,7 @@ GNSS_HD int vt_finish(double Fs, double ms, int pdi, int bps, double tau1carr, d
     if (col.n != n - 1) return GNSS_EINDEX;
     const double remChip = (colon_elem(col, n - 1) + cps) - 1023 * pdi;  // :284
     // Wave(numSample+1) = 2*pi*(carrFreq * (numSample/Fs)) + remCarrPhase (:275-276, :285)
-    const double W = kTwoPi * (c->carrFreq * ((double)n / Fs)) + c->remCarrPhase;
-    const double remCarrPhase = fmod(W, kTwoPi);
+    const double remCarrPhase = vt_rem_carr_phase(c->carrFreq, n, Fs, c->remCarrPhase);
     o->E_i = code[0] * sI;
     o->E_q = code[0] * sQ;
     o->P_i = code[1] * sI;
@@ -794,7 +801,7 @@ struct VtStepArgs {
 hipError_t launch_vt_step(const VtStepArgs& a, int n, int nb, hipStream_t s);
 // The EKF loop's steps from one launch (vt_loop_kernel). Both directions are 16-B granules
 // {lo, tag, hi, tag} in coherent host memory, tagged with the step's number (seq0, seq0 + 1,
-// ...): the host writes each channel's read as kVtStepWords granules (vt_mail_put), read by one
+// ...): the host writes each channel's read as kVtStepWords granules (vt_gran_put), read by one
 // block that relays them through device memory to the rest and gathers their sums; the step
 // completes when the channel sums' 2n granules carry its number (vt_sums_get). Read granules
 // tagged kVtLoopStop end the launch, and so does no new step within `timeout` (then the host
@@ -829,7 +836,9 @@ struct VtLoopArgs {
     double Fs;
     int real8;
     unsigned seq0;
-    const VtGran* mail;  // [n][kVtStepWords], coherent host memory: the steps' reads
+    const VtGran* mail;  // [2][n][kVtStepWords], coherent host memory: the steps' reads, step seq in
+                         // half seq & 1 (the next step's early words never overwrite a step the
+                         // lead may not have read yet)
     VtGran* sums;        // [n][2], coherent host memory: the channels' sums
     uint64_t timeout;    // wall-clock ticks (wall_clock64) a block waits for a step
     void* gstep;         // [n][kVtStepWords] 16-B granules, device memory: the relayed reads

@@ -389,7 +389,7 @@ __global__ __launch_bounds__(kVtStepThreads, 4) void vt_loop_kernel(VtLoopArgs a
     const __amdgpu_buffer_rsrc_t gp = __builtin_amdgcn_make_buffer_rsrc(a.gpart, (short)0, nch * nb * 2 * 16,
                                                                         kBufRsrcWord3);
     const __amdgpu_buffer_rsrc_t hm = __builtin_amdgcn_make_buffer_rsrc((void*)a.mail, (short)0,
-                                                                        nch * kVtStepWords * 16, kBufRsrcWord3);
+                                                                        2 * nch * kVtStepWords * 16, kBufRsrcWord3);
     const __amdgpu_buffer_rsrc_t hs = __builtin_amdgcn_make_buffer_rsrc(a.sums, (short)0, nch * 2 * 16, kBufRsrcWord3);
     for (unsigned seq = a.seq0;; seq++) {
         if (lead) {
@@ -402,7 +402,7 @@ __global__ __launch_bounds__(kVtStepThreads, 4) void vt_loop_kernel(VtLoopArgs a
             if (tid < nw) {
                 const uint64_t t0 = (uint64_t)wall_clock64();
                 for (;;) {
-                    g = load16_sys(hm, tid);
+                    g = load16_sys(hm, (int)(seq & 1) * nw + tid);  // (step seq's half of the mailbox)
                     if (g.y == seq && g.w == seq) break;
                     if ((g.y == kVtLoopStop && g.w == kVtLoopStop) || (uint64_t)wall_clock64() - t0 > a.timeout) {
                         stop = 1;
