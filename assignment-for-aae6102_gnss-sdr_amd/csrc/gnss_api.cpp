@@ -2455,7 +2455,7 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
     // held against what the step computes when it comes (the same functions: the same bits).
     bool early = false;
     std::vector<int64_t> e_off((size_t)n), e_ns((size_t)n);
-    std::vector<double> e_phi0((size_t)n), e_rfs((size_t)n);
+    std::vector<double> e_phi0((size_t)n), e_rfs((size_t)n), e_f((size_t)n);
     Events ev;
     double kernel_ms = 0;
     int result = GNSS_OK;
@@ -2632,6 +2632,23 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
             st_wait += t_a - t_b;
         }
         if (ctx->profiling || !multi) kernel_ms += ev.ms();
+        // loop mode, the next step posted early: its carrier frequencies first (the PLL alone; the
+        // rest of vt_finish and the EKF run beside the next step's kernel)
+        early = false;
+        if (early_next) {
+            for (int i = 0; i < n; i++) {
+                const double I = loop_sums[2 * i], Q = loop_sums[2 * i + 1];
+                const int cp = vt_code_at(pk[(size_t)i].j[1], pdi, [&](int j) {
+                    return ((cab[(size_t)i * 32 + (j >> 5)] >> (j & 31)) & 1u) ? -1 : 1;
+                });
+                const double f = vt_pll(hc[(size_t)i], pdi, t1, t2, cp * I, cp * Q).carrFreq;
+                uint64_t fb;
+                std::memcpy(&fb, &f, 8);
+                e_f[(size_t)i] = f;
+                vt_gran_put(mail + (size_t)kVtStepWords * (((B.seq + 1) & 1) * n + i) + 2, fb, B.seq + 1);
+            }
+            early = true;
+        }
         for (int i = 0; multi && i < n; i++) {  // each channel's scalar end
             gnss_vt_out& h = h_out[i];
             h = gnss_vt_out{};
@@ -2649,20 +2666,9 @@ int gnss_tracking_vt(gnss_ctx* ctx, const gnss_file* file, const gnss_signal* sg
                                       I, Q, &h);
             if (st2) h.status = st2;
         }
-        // the next step's carrier frequencies (the PLL's output): the kernel starts it now
-        early = false;
-        if (early_next) {
-            bool ok = true;
-            for (int i = 0; i < n; i++) ok = ok && !h_out[i].status;
-            if (ok) {
-                for (int i = 0; i < n; i++) {
-                    uint64_t f;
-                    std::memcpy(&f, &hc[(size_t)i].carrFreq, 8);
-                    vt_gran_put(mail + (size_t)kVtStepWords * (((B.seq + 1) & 1) * n + i) + 2, f, B.seq + 1);
-                }
-                early = true;
-            }
-        }
+        for (int i = 0; early && i < n; i++)  // (vt_finish's frequency is the one posted: the same vt_pll)
+            if (!h_out[i].status && std::memcmp(&hc[(size_t)i].carrFreq, &e_f[(size_t)i], 8))
+                return fail(ctx, GNSS_EDEVICE, "step %d channel %d: the early carrier frequency differs", s + 1, i);
         for (int i = 0; i < n; i++) {
             gnss_vt_out& o = out[(size_t)s * n + i];
             const gnss_vt_out& h = h_out[i];

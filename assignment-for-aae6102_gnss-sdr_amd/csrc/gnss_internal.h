@@ -655,6 +655,21 @@ GNSS_HD double vt_rem_carr_phase(double carrFreq, int64_t n, double Fs, double r
     return fmod(W, kTwoPi);
 }
 
+// The PLL of a step (:305-311) from its prompt sums: carrError, carrNco and the next carrFreq --
+// vt_finish's, and gnss_tracking_vt's to post the next step's frequency first
+struct VtPll {
+    double carrError, carrNco, carrFreq;
+};
+GNSS_HD VtPll vt_pll(const gnss_vt_chan& c, int pdi, double tau1carr, double tau2carr, double P_i, double P_q)
+{
+    VtPll r;
+    r.carrError = atan(P_q / P_i) / (2.0 * 3.14159265358979323846);
+    r.carrNco = c.oldCarrNco + (tau2carr / tau1carr) * (r.carrError - c.oldCarrError) +
+                r.carrError * (pdi * 1e-3 / tau1carr);
+    r.carrFreq = c.carrFreqBasis + r.carrNco;
+    return r;
+}
+
 // The rest of the step from its sums (:247-249, :284-347): E / P / L, remChip, remCarrPhase,
 // the C/N0 estimator, PLL, DLL discriminator, the record; advances `c`. bps = bytes per
 // sample (dataPrecision * dataType), code[3] = the E / P / L chip values.
@@ -688,10 +703,8 @@ GNSS_HD int vt_finish(double Fs, double ms, int pdi, int bps, double tau1carr, d
         c->snrIndex += 1;
     }
     // PLL (:305-311)
-    const double carrError = atan(o->P_q / o->P_i) / (2.0 * 3.14159265358979323846);
-    const double carrNco = c->oldCarrNco + (tau2carr / tau1carr) * (carrError - c->oldCarrError) +
-                           carrError * (pdi * 1e-3 / tau1carr);
-    const double carrFreq = c->carrFreqBasis + carrNco;
+    const VtPll pll = vt_pll(*c, pdi, tau1carr, tau2carr, o->P_i, o->P_q);
+    const double carrError = pll.carrError, carrNco = pll.carrNco, carrFreq = pll.carrFreq;
     // DLL discriminator (:314-316)
     const double E = sqrt(o->E_i * o->E_i + o->E_q * o->E_q);
     const double L = sqrt(o->L_i * o->L_i + o->L_q * o->L_q);
