@@ -186,3 +186,24 @@ def test_multi_context_pos_and_mc_equal_one(pkg, ctx, mctx, opensky_short):
     grp = pkg.trackingCT_POS_updated_multicorrelator(file, signal, track, A, ctx=mctx, raw=True)
     assert np.array_equal(one.rec, grp.rec) and np.array_equal(one.taps, grp.taps)
     assert np.array_equal(one.CN0, grp.CN0) and np.array_equal(one.len, grp.len)
+
+
+def test_multi_context_vector_tracking_equals_one(pkg, ctx, mctx, opensky_short):
+    """trackingVT_POS_updated on the multi-device context (the VT loop is one host-driven chain:
+    it runs on devices[0]) equals the one-context call bit for bit over 200 steps, in
+    loop mode (the persistent VT launch) on both."""
+    import vt_nav_common as V
+    from test_gpu_vtnav import _inputs
+    skip, cfg, data = opensky_short
+    file, signal, acq, track = params(pkg, skip, data)
+    _, _, _, _, solu, cmn = pkg.initParameters()
+    z = V.fixture()
+    Acquired, eph, sbf, ct, ns = _inputs(pkg, z, skip)
+    runs = [pkg.trackingVT_POS_updated(file, signal, track, cmn, solu, Acquired, V.cnslxyz(pkg), eph, sbf, None, ct,
+                                       ns, ctx=c, nsteps=200) for c in (ctx, mctx)]
+    (t1, n1), (t3, n3) = runs
+    for p in (int(x) for x in z["prns"]):
+        for f in ("P_i", "P_q", "carrFreq", "codeFreq", "absoluteSample", "deltaPr"):
+            assert np.array_equal(getattr(t1(p), f), getattr(t3(p), f)), (p, f)
+    for f in ("usrPos", "usrVel", "clkBias", "clkDrift", "state"):
+        assert np.array_equal(getattr(n1, f), getattr(n3, f)), f
