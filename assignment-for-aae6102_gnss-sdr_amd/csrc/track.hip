@@ -1660,9 +1660,16 @@ __device__ bool sweep_words(const unsigned long long* g, int n, unsigned tag, un
 }
 
 // (16-B granules {lo, tag, hi, tag}, publish16: gnss_internal.h, shared with the VT loop)
+// granule loads a poller keeps in flight per batch: one at a time for E / P / L (2-3 granules a
+// poller, where batching measured 1 % slower), GNSS_SWEEP_BATCH above 3 taps (8-11 a poller: the
+// 11-tap 4-channel launch 49.5 -> 45.9 ms at 4, profiles/r06_ab_sweep_batch.txt)
+#ifndef GNSS_SWEEP_BATCH
+#define GNSS_SWEEP_BATCH 4
+#endif
 
 // Poll n 16-B granules until both tags of each equal `tag`; granule e's words land in
 // dst[2e], dst[2e+1]. Same protocol as sweep_words (pollers pid 0..np-1, n <= 64*np).
+template <int SB>
 __device__ bool sweep16(__amdgpu_buffer_rsrc_t r, int n, unsigned tag, unsigned* dst, int pid, int np,
                         unsigned* err, int base)
 {
@@ -1672,15 +1679,28 @@ __device__ bool sweep16(__amdgpu_buffer_rsrc_t r, int n, unsigned tag, unsigned*
     unsigned long long t0 = 0;
     int late = 0;
     while (todo) {
-        for (int k = 0; (todo >> k) != 0; k++) {
-            if (!((todo >> k) & 1ull)) continue;
-            const int e = pid + k * np;
-            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (base + e) * 16, 0, kPolSc1);
-            if (v.y == tag && v.w == tag) {
-                dst[2 * e] = v.x;
-                dst[2 * e + 1] = v.z;
-                todo &= ~(1ull << k);
+        // a pass over the missing granules, SB loads in flight at a time (each checked only once
+        // all of its batch are issued: one round trip per batch, not per granule; the words land
+        // where they did, so the sums keep their bits)
+        for (unsigned long long rem = todo; rem;) {
+            int ks[SB];
+            u32x4 v[SB];
+#pragma unroll
+            for (int j = 0; j < SB; j++) {
+                ks[j] = rem ? __builtin_ctzll(rem) : -1;
+                if (rem) {
+                    rem &= rem - 1;
+                    v[j] = __builtin_amdgcn_raw_buffer_load_b128(r, (base + pid + ks[j] * np) * 16, 0, kPolSc1);
+                }
             }
+#pragma unroll
+            for (int j = 0; j < SB; j++)
+                if (ks[j] >= 0 && v[j].y == tag && v[j].w == tag) {
+                    const int e = pid + ks[j] * np;
+                    dst[2 * e] = v[j].x;
+                    dst[2 * e + 1] = v[j].z;
+                    todo &= ~(1ull << ks[j]);
+                }
         }
         if (!todo) break;
         if constexpr (GNSS_XCHG_SLEEP > 0) __builtin_amdgcn_s_sleep(GNSS_XCHG_SLEEP);  // (A/B knob)
@@ -2250,7 +2270,9 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
                 np = dsw ? 2 * 64 : 3 * 64;
             }
             if constexpr (!kDefer) {
-                if (!sweep16(pg, bpc * NV, tag0 + s + 1, pw, pid, np, b.run_err, (s & 1) * kMaxBpcRun * NV)) return;
+                if (!sweep16<(NT > 3 ? GNSS_SWEEP_BATCH : 1)>(pg, bpc * NV, tag0 + s + 1, pw, pid, np, b.run_err,
+                                                               (s & 1) * kMaxBpcRun * NV))
+                    return;
             } else {
                 // this step's E / P / L, and the owned B values of the previous step (long published)
                 const int NA = NA_();
