@@ -1185,11 +1185,19 @@ __device__ __forceinline__ void lds_barrier()
 // Block: the NV tap sums of the block's 256 lanes: 8-lane runs, then four runs per lane,
 // then a DPP quad butterfly. Slots are free on entry (caller's barrier); the value is in
 // lanes tid = 4v (v < NV); LDS barriers only (global loads in flight stay so).
-// Taps per pass of the block reduction: all of them at 3 taps; above, two passes of half the
-// taps each, so the reduction's LDS (2 * taps * (T + 32) doubles) fits three 11-tap blocks per
-// CU. Every value is reduced by the same lanes in the same order either way (same bits).
+// Taps per pass of the block reduction (each pass: three barriers): all of them at 3 taps;
+// above, in the per-step kernel, two passes of half the taps each, so the reduction's LDS
+// (2 * taps * (T + 32) doubles) stays small and the one-pass form's extra registers (98 -> 129
+// VGPRs at 11 taps) do not cut that kernel's occupancy. The persistent kernel reduces up to
+// GNSS_RED_ONEPASS taps in one pass: its 11-tap forms run two blocks per CU (their VGPRs),
+// where the one-pass slots still fit (59-71 KB of LDS a block). Every value is reduced by the
+// same lanes in the same order whichever pass it is in (same bits).
+#ifndef GNSS_RED_ONEPASS
+#define GNSS_RED_ONEPASS 11
+#endif
 template <int NT> constexpr int red_taps() { return NT > 3 ? (NT + 1) / 2 : NT; }
-template <int NT> constexpr int red_words() { return 2 * red_taps<NT>() * (kTrkThreads + 32); }
+template <int NT> constexpr int run_red_taps() { return NT <= GNSS_RED_ONEPASS ? NT : red_taps<NT>(); }
+template <int HT> constexpr int red_words() { return 2 * HT * (kTrkThreads + 32); }
 
 // GNSS_RED 1 (round 5, A/B knob, off): each value summed over a wave without LDS -- the DPP
 // butterfly over quads, half rows and rows (every lane of a row ends with the row's sum, the
@@ -1276,12 +1284,12 @@ __device__ __forceinline__ double block_tree(double* s_mem, const double (&oI)[N
     return a;
 }
 
-template <int NT>
+template <int NT, int HT = red_taps<NT>()>
 __device__ __forceinline__ double block_partial(double* s_mem, const double (&oI)[NT],
                                                 const double (&oQ)[NT], int tid)
 {
     if constexpr (GNSS_RED) return block_tree<NT>(s_mem, oI, oQ, tid, (1u << NT) - 1u);
-    constexpr int T = kTrkThreads, HT = red_taps<NT>();
+    constexpr int T = kTrkThreads;
     double* red = s_mem;                 // [2 HT][T]
     double* red2 = s_mem + 2 * HT * T;   // [2 HT][32]
     double a = 0.0;
@@ -1324,17 +1332,16 @@ __device__ __forceinline__ double block_partial(double* s_mem, const double (&oI
 
 // One pass of block_partial over a chosen set of taps (the persistent loop's split of the
 // > 3-tap reduction: the loop's E/P/L first, the other taps after their publication). The
-// taps of bit mask `sel` (at most red_taps<NT>() of them) take part in tap order: the q-th
+// taps of bit mask `sel` (at most HT of them) take part in tap order: the q-th
 // one's I / Q are the pass's values 2q / 2q + 1, reduced by exactly block_partial's lanes and
 // order (8-lane runs, four runs per lane, the DPP quad butterfly), so every value has the bits
 // block_partial gives it. Value w of the pass ends in lanes 4w .. 4w + 3.
-template <int NT>
+template <int NT, int HT>
 __device__ __forceinline__ double block_pass(double* s_mem, const double (&oI)[NT], const double (&oQ)[NT],
                                              int tid, unsigned sel)
 {
     if constexpr (GNSS_RED) return block_tree<NT>(s_mem, oI, oQ, tid, sel);
     constexpr int T = kTrkThreads;
-    constexpr int HT = red_taps<NT>();
     double* red = s_mem;                 // [2 HT][T]
     double* red2 = s_mem + 2 * HT * T;   // [2 HT][32]
 #pragma unroll
@@ -1432,7 +1439,7 @@ __global__ __launch_bounds__(kTrkThreads) void track_step_kernel(const TrkParams
 
     // LDS: running sums slot[8][T], then the block reduction
     constexpr int kSlot = 8 * T * 2;
-    constexpr int kRed = red_words<NT>();
+    constexpr int kRed = red_words<red_taps<NT>()>();
     __shared__ __attribute__((aligned(16))) double s_mem[kSlot > kRed ? kSlot : kRed];
     __shared__ double s_fin[NV];
     __shared__ int s_last;
@@ -1861,7 +1868,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
     const bool io = pblk == 0;
 
     constexpr int kSlot = 8 * T * 2;                  // running sums [8][T] double2
-    constexpr int kRed = red_words<NT>();             // block reduction
+    constexpr int kRed = red_words<run_red_taps<NT>()>();  // block reduction
     constexpr int kPart = run_bpc_cap(NT) * NV;       // everyone's partials (as words)
     // Above 3 taps only E / P / L cross the step's exchange (kDefer, below); GNSS_DEFER 2 (one
     // block of the step per resident block) has one wave reduce the other taps' block partials
@@ -1910,7 +1917,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
     // order (block_pass, channel_sum_l with the whole tap set's lane count), so the records
     // and taps are the bits of the one-exchange form and of the per-step kernel.
     constexpr int CL = chan_lanes<NV>();
-    constexpr int HT = red_taps<NT>();
+    constexpr int HT = run_red_taps<NT>();
     // The configuration lives in LDS and is read where it is used (volatile LDS loads, never
     // hoisted into registers that would live across the step loop: this kernel is at its
     // register budget). selA / selB: the loop's taps / the others; NA: E/P/L values; nBv: B
@@ -2195,13 +2202,13 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
                 if (brow && tid == 0) brow[40 + 256 + vb] = wall_clock64();
                 // block sum in a fixed order, published as granules
                 if constexpr (!kDefer) {
-                    const double bsum = block_partial<NT>(s_mem, oI, oQ, tid);
+                    const double bsum = block_partial<NT, HT>(s_mem, oI, oQ, tid);
                     if (tid < NV * 4 && (tid & 3) == 0)
                         publish16(pg, ((s & 1) * kMaxBpcRun + vb) * NV + (tid >> 2), bsum, tag0 + s + 1);
                 } else {
                     // E / P / L first (region A), then the other taps (region B, slot s mod 4),
                     // reduced while the exchange is in flight
-                    const double ba = block_pass<NT>(s_mem, oI, oQ, tid, (unsigned)dfi(*(const int*)&s_df.selA));
+                    const double ba = block_pass<NT, HT>(s_mem, oI, oQ, tid, (unsigned)dfi(*(const int*)&s_df.selA));
                     const int NA = NA_();
                     if (tid < NA * 4 && (tid & 3) == 0)
                         publish16(pg, ((s & 1) * kMaxBpcRun + vb) * NA + (tid >> 2), ba, tag0 + s + 1);
@@ -2222,7 +2229,7 @@ __global__ __launch_bounds__(kTrkThreads) __attribute__((amdgpu_waves_per_eu(NT 
                         const int hb = dfi(s_df.hb), nB = dfi(s_df.nBv) / 2;
                         for (int ps = 1; (ps - 1) * hb < nB; ps++) {
                             const unsigned sel = sel_pass(ps);
-                            const double bb = block_pass<NT>(s_mem, oI, oQ, tid, sel);
+                            const double bb = block_pass<NT, HT>(s_mem, oI, oQ, tid, sel);
                             if (tid < 2 * __builtin_popcount(sel) * 4 && (tid & 3) == 0)
                                 publish16(pg, gran_region_b(NT) + (s & 3) * gran_slot_b(NT) +
                                                   (2 * (ps - 1) * hb + (tid >> 2)) * bpc + vb,
